@@ -1,0 +1,142 @@
+"""ctypes binding of libmirec.so (the C ABI declared in include/mirec.h).
+
+This is the Python side of the drop-in boundary: every device call goes
+through these entry points with raw device pointers and the current HIP
+stream.  There is no CPU fallback — if the shared library is missing the
+import fails loudly (build it with ``python -c "import __graft_entry__ as g;
+g.build()"`` or ``make -C furusato_recommend_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_float, c_int, c_int32, c_int64,
+                    c_size_t, c_uint64, c_void_p, c_char_p)
+
+import torch  # noqa: F401  (binds libmirec to torch's HIP runtime: same SONAME)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmirec.so")
+
+MIREC_OK = 0
+IN_PRESCALED, IN_RAW, IN_SPARSE, IN_NONE = 0, 1, 2, 3
+SUPPORTED_DIMS = (4, 8, 16, 32, 64, 128, 256)
+
+
+class MirecError(RuntimeError):
+    pass
+
+
+class CSR(Structure):
+    """mirec_csr_t (include/mirec.h)."""
+    _fields_ = [
+        ("rowptr", c_void_p), ("col", c_void_p), ("dinv", c_void_p),
+        ("n_rows", c_int64), ("nnz", c_int64), ("split", c_int32),
+        ("_pad", c_int32), ("n_long", c_int64), ("n_seg", c_int64),
+        ("long_rows", c_void_p), ("long_segptr", c_void_p),
+        ("seg_row", c_void_p), ("seg_beg", c_void_p),
+    ]
+
+
+class AdamH(Structure):
+    """mirec_adam_hparams_t."""
+    _fields_ = [
+        ("one_minus_beta1", c_float), ("beta2", c_float),
+        ("one_minus_beta2", c_float), ("neg_step_size", c_float),
+        ("bc2_sqrt", c_float), ("eps", c_float),
+    ]
+
+
+class Prop(Structure):
+    """mirec_prop_t."""
+    _fields_ = [
+        ("dim", c_int32), ("in_mode", c_int32), ("x_in", c_void_p),
+        ("slot", c_void_p), ("seed_in", c_void_p), ("seed", c_void_p),
+        ("addend", c_void_p), ("seed2", c_void_p), ("divisor", c_float),
+        ("_pad", c_float), ("out", c_void_p), ("xs_out", c_void_p),
+        ("param", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
+        ("adam", AdamH), ("partial", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); the single source of truth for the exports
+# test (tests/test_abi.py checks these against include/mirec.h).
+SIGNATURES = {
+    "mirec_strerror": (c_char_p, [c_int]),
+    "mirec_abi_version": (c_int, []),
+    "mirec_last_hip_error": (c_int, []),
+    "mirec_struct_sizes": (c_int, [POINTER(c_size_t), POINTER(c_size_t), POINTER(c_size_t)]),
+    "mirec_csr_bipartite": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64,
+                                    c_void_p, c_void_p, c_void_p]),
+    "mirec_csr_from_coo": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                   c_void_p, c_void_p]),
+    "mirec_csr_long_rows": (c_int, [c_void_p, c_int64, c_int32, POINTER(c_int64),
+                                    POINTER(c_int64), c_void_p, c_void_p, c_void_p,
+                                    c_void_p]),
+    "mirec_propagate": (c_int, [POINTER(CSR), POINTER(Prop), c_void_p]),
+    "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
+                                  c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mirec_bpr_loss": (c_int, [c_void_p, c_void_p, c_int64, c_float, c_void_p, c_void_p,
+                               c_void_p]),
+    "mirec_bpr_seed_workspace": (c_int, [c_int64, c_int64, POINTER(c_size_t)]),
+    "mirec_bpr_seed": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mirec_bpr_seed_reset": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "mirec_adam_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                 POINTER(AdamH), c_void_p]),
+    "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,
+                                 c_uint64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: the HIP engine is not built. Run "
+            "`make -C furusato_recommend_amd/csrc` (or __graft_entry__.build()). "
+            "There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.mirec_abi_version() != 1:
+        raise ImportError("libmirec.so ABI version mismatch")
+    sizes = [c_size_t(0) for _ in range(3)]
+    lib.mirec_struct_sizes(*(ctypes.byref(x) for x in sizes))
+    want = (ctypes.sizeof(CSR), ctypes.sizeof(Prop), ctypes.sizeof(AdamH))
+    if tuple(x.value for x in sizes) != want:
+        raise ImportError(f"struct layout mismatch: lib {[x.value for x in sizes]} vs {want}")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != MIREC_OK:
+        msg = lib.mirec_strerror(rc).decode()
+        if rc == 3:
+            msg += f" (hipError {lib.mirec_last_hip_error()})"
+        raise MirecError(f"{what}: {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device/host pointer of a tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def adam_hparams(lr: float, beta1: float, beta2: float, eps: float, step: int) -> AdamH:
+    """Per-step scalars of torch.optim.Adam (torch/optim/adam.py:534-547)."""
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    return AdamH(one_minus_beta1=1 - beta1, beta2=beta2, one_minus_beta2=1 - beta2,
+                 neg_step_size=-(lr / bc1), bc2_sqrt=bc2 ** 0.5, eps=eps)

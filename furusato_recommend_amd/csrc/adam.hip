@@ -1,0 +1,67 @@
+// Dense single-pass Adam (torch.optim.Adam, amsgrad=False, weight_decay=0),
+// the optimizer of model/lgcn.py:63 stepped at model/lgcn.py:132.  One pass
+// reads param/grad/m/v and writes param/m/v as float4 (7 x 4 B per element:
+// HBM-bound).  Used by the data-parallel path after the gradient all-reduce;
+// the single-GPU path fuses the same update into the last backward
+// propagation epilogue (prop.hip) and never materialises the gradient.
+#include "common.h"
+
+namespace mirec {
+
+__device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
+                                      const mirec_adam_hparams_t &h) {
+  m = m + h.one_minus_beta1 * (g - m);
+  v = v * h.beta2 + h.one_minus_beta2 * g * g;
+  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
+  p = p + h.neg_step_size * (m / denom);
+}
+
+__global__ __launch_bounds__(256) void adam_dense_kernel(float *__restrict__ param,
+                                                         const float *__restrict__ grad,
+                                                         float *__restrict__ m,
+                                                         float *__restrict__ v, int64_t n4,
+                                                         mirec_adam_hparams_t h) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p = ld4(param + 4 * i), g = ld4(grad + 4 * i), a = ld4(m + 4 * i),
+           b = ld4(v + 4 * i);
+    adam1(p.x, a.x, b.x, g.x, h);
+    adam1(p.y, a.y, b.y, g.y, h);
+    adam1(p.z, a.z, b.z, g.z, h);
+    adam1(p.w, a.w, b.w, g.w, h);
+    st4(param + 4 * i, p);
+    st4(m + 4 * i, a);
+    st4(v + 4 * i, b);
+  }
+}
+
+__global__ void adam_tail_kernel(float *param, const float *grad, float *m, float *v,
+                                 int64_t begin, int64_t n, mirec_adam_hparams_t h) {
+  const int64_t i = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) adam1(param[i], m[i], v[i], grad[i], h);
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_adam_dense(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                                int64_t n, const mirec_adam_hparams_t *h,
+                                mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(param && grad && exp_avg && exp_avg_sq && h && n >= 0);
+  MIREC_CHECK_ARG(((uintptr_t)param | (uintptr_t)grad | (uintptr_t)exp_avg |
+                   (uintptr_t)exp_avg_sq) % 16 == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t n4 = n / 4;
+  if (n4 > 0) {
+    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(adam_dense_kernel, dim3(blocks), dim3(256), 0, st, param, grad, exp_avg,
+                       exp_avg_sq, n4, *h);
+    MIREC_LAUNCH_CHECK();
+  }
+  if (n4 * 4 < n) {
+    hipLaunchKernelGGL(adam_tail_kernel, dim3(1), dim3(64), 0, st, param, grad, exp_avg,
+                       exp_avg_sq, n4 * 4, n, *h);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}

@@ -1,0 +1,83 @@
+// Shared helpers for the gfx950 kernels of libmirec.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mirec.h"
+
+namespace mirec {
+
+// Last HIP error seen by any entry point (exposed by mirec_last_hip_error).
+extern thread_local int g_last_hip_error;
+
+#define MIREC_CHECK_ARG(cond)                                                  \
+  do {                                                                         \
+    if (!(cond)) return MIREC_ERR_ARG;                                         \
+  } while (0)
+
+#define MIREC_LAUNCH_CHECK()                                                   \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess) {                                                    \
+      ::mirec::g_last_hip_error = (int)e_;                                     \
+      return MIREC_ERR_HIP;                                                    \
+    }                                                                          \
+  } while (0)
+
+#define MIREC_HIP(call)                                                        \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      ::mirec::g_last_hip_error = (int)e_;                                     \
+      return MIREC_ERR_HIP;                                                    \
+    }                                                                          \
+  } while (0)
+
+inline bool dim_supported(int d) {
+  return d == 4 || d == 8 || d == 16 || d == 32 || d == 64 || d == 128 ||
+         d == 256;
+}
+
+__device__ __forceinline__ float4 f4_zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float4 f4_add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 f4_sub(float4 a, float4 b) {
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+__device__ __forceinline__ float4 f4_scale(float s, float4 a) {
+  return make_float4(s * a.x, s * a.y, s * a.z, s * a.w);
+}
+__device__ __forceinline__ float4 f4_fma(float s, float4 a, float4 c) {
+  return make_float4(fmaf(s, a.x, c.x), fmaf(s, a.y, c.y), fmaf(s, a.z, c.z),
+                     fmaf(s, a.w, c.w));
+}
+__device__ __forceinline__ float4 f4_div(float4 a, float d) {
+  return make_float4(a.x / d, a.y / d, a.z / d, a.w / d);
+}
+__device__ __forceinline__ float f4_dot(float4 a, float4 b) {
+  return a.x * b.x + a.y * b.y + a.z * b.z + a.w * b.w;
+}
+__device__ __forceinline__ float4 ld4(const float *p) {
+  return *reinterpret_cast<const float4 *>(p);
+}
+__device__ __forceinline__ void st4(float *p, float4 v) {
+  *reinterpret_cast<float4 *>(p) = v;
+}
+__device__ __forceinline__ float4 f4_shfl_xor(float4 v, int m) {
+  return make_float4(__shfl_xor(v.x, m), __shfl_xor(v.y, m),
+                     __shfl_xor(v.z, m), __shfl_xor(v.w, m));
+}
+
+// Sum a float over the LPR-lane group a lane belongs to (groups are
+// contiguous, aligned runs of LPR lanes inside the 64-lane wave).
+template <int LPR>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = 1; m < LPR; m <<= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+}  // namespace mirec

@@ -1,0 +1,287 @@
+// LightGCN propagation on gfx950: CSR segment-gather SpMM with a fused
+// layer epilogue.
+//
+// Replaces PyG LGConv (model/lgcn.py:66,82) / rAdjConv (model/radj.py:28-44):
+//   out[i] = sum_{(j -> i)} x[j] / sqrt(deg_i * deg_j)
+// which the reference evaluates as a [nnz, D] gather, a scale and an atomic
+// scatter-add.  Here one 64-lane wave owns one destination row: the row's
+// column indices are read once, coalesced (64 per load), and broadcast with
+// ds_bpermute; every LPR = D/4 lanes form a group that reads one whole
+// neighbour row as float4s (D=64: 16 lanes x 16 B = one 256-B row), so a wave
+// instruction pulls G = 64/LPR neighbour rows and UNROLL instructions are in
+// flight per lane.  Groups accumulate disjoint neighbour subsets in
+// registers and are combined with a xor-butterfly at the end: no atomics, no
+// LDS, a fixed summation order per row (deterministic).
+//
+// Rows longer than csr->split are cut into segments processed by extra waves
+// of the same launch (partial sums to scratch) and summed in segment order by
+// a finalize launch, so a Zipf-skewed item cannot serialise the grid.
+//
+// Epilogue (per row, LPR lanes): z = dinv_i * sum + seed[slot_i];
+// xs_out = dinv_i * z (next layer's pre-scaled input);
+// o = (z + addend)/divisor + seed2[slot_i]; out = o or Adam(param; grad=o).
+#include "common.h"
+
+namespace mirec {
+
+struct PropK {
+  const int64_t *rowptr;
+  const int32_t *col;
+  const float *dinv;
+  int64_t n_rows;
+  int64_t n_seg;
+  const int32_t *seg_row;
+  const int64_t *seg_beg;
+  int32_t split;
+  const float *x_in;
+  const int32_t *slot;
+  const float *seed_in;
+  const float *seed;
+  const float *addend;
+  const float *seed2;
+  float divisor;
+  float *out;
+  float *xs_out;
+  float *param;
+  float *m;
+  float *v;
+  mirec_adam_hparams_t adam;
+  float *partial;
+};
+
+__device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g,
+                                          const mirec_adam_hparams_t &h) {
+  // torch.optim.Adam single-tensor path (torch/optim/adam.py:457-547):
+  // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+  // denom = sqrt(v)/sqrt(bc2) + eps; p.addcdiv_(m, denom, -lr/bc1)
+  m = m + h.one_minus_beta1 * (g - m);
+  v = v * h.beta2 + h.one_minus_beta2 * g * g;
+  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
+  p = p + h.neg_step_size * (m / denom);
+}
+
+// Sum of the (pre-scaled / raw / sparse) input rows listed in col[beg, end).
+// Returns the per-lane partial (this lane's group's neighbour subset).
+template <int D, int UNROLL, int MODE>
+__device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg,
+                                              int64_t end, int lane) {
+  constexpr int LPR = D / 4;
+  constexpr int G = 64 / LPR;
+  const int grp = lane / LPR;
+  const int sub = lane % LPR;
+  float4 acc = f4_zero();
+  if (MODE == MIREC_IN_NONE) return acc;
+  for (int64_t base = beg; base < end; base += 64) {
+    const int cnt = (int)min((int64_t)64, end - base);
+    int myc = 0;
+    float myw = 1.f;
+    if (lane < cnt) {
+      myc = a.col[base + lane];
+      if (MODE != MIREC_IN_PRESCALED) myw = a.dinv[myc];
+    }
+    if (MODE == MIREC_IN_SPARSE) {
+      // Input is zero except at the (few) seeded rows: test slot[] for all
+      // 64 neighbours at once and gather only the seeded ones.
+      int mys = -1;
+      if (lane < cnt) mys = a.slot[myc];
+      unsigned long long mask = __ballot(mys >= 0);
+      while (mask) {
+        const int b = __ffsll((long long)mask) - 1;
+        mask &= mask - 1;
+        const int s = __shfl(mys, b);
+        const float w = __shfl(myw, b);
+        if (grp == 0) acc = f4_fma(w, ld4(a.seed_in + (int64_t)s * D + sub * 4), acc);
+      }
+      continue;
+    }
+    for (int k = 0; k < cnt; k += G * UNROLL) {
+      float4 v[UNROLL];
+      float w[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int idx = k + u * G + grp;
+        const int j = __shfl(myc, idx & 63);
+        w[u] = (MODE == MIREC_IN_RAW) ? __shfl(myw, idx & 63) : 1.f;
+        if (idx < cnt)
+          v[u] = ld4(a.x_in + (int64_t)j * D + sub * 4);
+        else
+          v[u] = f4_zero();
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (MODE == MIREC_IN_RAW)
+          acc = f4_fma(w[u], v[u], acc);
+        else
+          acc = f4_add(acc, v[u]);
+      }
+    }
+  }
+  return acc;
+}
+
+// Combine the G group partials: afterwards every group holds the row sum.
+template <int D>
+__device__ __forceinline__ float4 combine_groups(float4 s) {
+  constexpr int LPR = D / 4;
+#pragma unroll
+  for (int m = LPR; m < 64; m <<= 1) s = f4_add(s, f4_shfl_xor(s, m));
+  return s;
+}
+
+template <int D>
+__device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4 s,
+                                             int sub) {
+  const float di = a.dinv[row];
+  const int64_t off = row * D + sub * 4;
+  float4 z = f4_scale(di, s);
+  int sl = -1;
+  if (a.slot != nullptr && (a.seed != nullptr || a.seed2 != nullptr)) sl = a.slot[row];
+  if (a.seed != nullptr && sl >= 0) z = f4_add(z, ld4(a.seed + (int64_t)sl * D + sub * 4));
+  if (a.xs_out != nullptr) st4(a.xs_out + off, f4_scale(di, z));
+  if (a.out == nullptr && a.param == nullptr) return;
+  float4 o = z;
+  if (a.addend != nullptr) o = f4_add(o, ld4(a.addend + off));
+  if (a.divisor != 1.f) o = f4_div(o, a.divisor);
+  if (a.seed2 != nullptr && sl >= 0) o = f4_add(o, ld4(a.seed2 + (int64_t)sl * D + sub * 4));
+  if (a.param != nullptr) {
+    float4 p = ld4(a.param + off), m = ld4(a.m + off), v = ld4(a.v + off);
+    adam_elem(p.x, m.x, v.x, o.x, a.adam);
+    adam_elem(p.y, m.y, v.y, o.y, a.adam);
+    adam_elem(p.z, m.z, v.z, o.z, a.adam);
+    adam_elem(p.w, m.w, v.w, o.w, a.adam);
+    st4(a.param + off, p);
+    st4(a.m + off, m);
+    st4(a.v + off, v);
+    if (a.out != nullptr) st4(a.out + off, o);
+  } else {
+    st4(a.out + off, o);
+  }
+}
+
+constexpr int kWavesPerBlock = 4;
+
+// Work item w < n_rows: row w (skipped if long); otherwise segment w-n_rows.
+template <int D, int UNROLL, int MODE>
+__global__ __launch_bounds__(256) void prop_kernel(PropK a) {
+  constexpr int LPR = D / 4;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR;
+  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+  if (w < a.n_rows) {
+    const int64_t beg = a.rowptr[w], end = a.rowptr[w + 1];
+    if (a.split > 0 && end - beg > a.split) return;  // wave-uniform
+    float4 s = gather_rows<D, UNROLL, MODE>(a, beg, end, lane);
+    s = combine_groups<D>(s);
+    if (lane < LPR) row_epilogue<D>(a, w, s, sub);
+  } else {
+    const int64_t sg = w - a.n_rows;
+    if (sg >= a.n_seg) return;
+    const int64_t row = a.seg_row[sg];
+    const int64_t beg = a.seg_beg[sg];
+    const int64_t end = min(beg + (int64_t)a.split, a.rowptr[row + 1]);
+    float4 s = gather_rows<D, UNROLL, MODE>(a, beg, end, lane);
+    s = combine_groups<D>(s);
+    if (lane < LPR) st4(a.partial + sg * D + sub * 4, s);
+  }
+}
+
+// One LPR-lane group per long row: sum its segments in order, then epilogue.
+template <int D>
+__global__ __launch_bounds__(256) void prop_finalize(PropK a, const int32_t *long_rows,
+                                                     const int64_t *long_segptr,
+                                                     int64_t n_long) {
+  constexpr int LPR = D / 4;
+  constexpr int G = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR;
+  const int64_t li = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + lane / LPR;
+  if (li >= n_long) return;
+  const int64_t row = long_rows[li];
+  float4 s = f4_zero();
+  for (int64_t sg = long_segptr[li]; sg < long_segptr[li + 1]; ++sg)
+    s = f4_add(s, ld4(a.partial + sg * D + sub * 4));
+  row_epilogue<D>(a, row, s, sub);
+}
+
+template <int D, int UNROLL>
+static int launch_prop(const mirec_csr_t *c, const PropK &k, int mode, hipStream_t st) {
+  const int64_t work = c->n_rows + c->n_seg;
+  const int64_t blocks = (work + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks > 0) {
+    if (mode == MIREC_IN_PRESCALED)
+      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_PRESCALED>), dim3(blocks), dim3(256), 0, st, k);
+    else if (mode == MIREC_IN_RAW)
+      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_RAW>), dim3(blocks), dim3(256), 0, st, k);
+    else if (mode == MIREC_IN_SPARSE)
+      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_SPARSE>), dim3(blocks), dim3(256), 0, st, k);
+    else
+      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_NONE>), dim3(blocks), dim3(256), 0, st, k);
+    MIREC_LAUNCH_CHECK();
+  }
+  if (c->n_long > 0) {
+    constexpr int G = 64 / (D / 4);
+    const int64_t per_block = (int64_t)kWavesPerBlock * G;
+    const int64_t fb = (c->n_long + per_block - 1) / per_block;
+    hipLaunchKernelGGL((prop_finalize<D>), dim3(fb), dim3(256), 0, st, k, c->long_rows,
+                       c->long_segptr, c->n_long);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
+                               mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(c != nullptr && p != nullptr);
+  MIREC_CHECK_ARG(c->rowptr != nullptr && c->dinv != nullptr && c->n_rows >= 0);
+  MIREC_CHECK_ARG(c->nnz == 0 || c->col != nullptr);
+  if (!dim_supported(p->dim)) return MIREC_ERR_DIM;
+  MIREC_CHECK_ARG(p->in_mode >= 0 && p->in_mode <= 3);
+  if (p->in_mode == MIREC_IN_SPARSE)
+    MIREC_CHECK_ARG(p->slot != nullptr && p->seed_in != nullptr);
+  else if (p->in_mode != MIREC_IN_NONE)
+    MIREC_CHECK_ARG(p->x_in != nullptr);
+  MIREC_CHECK_ARG((p->seed == nullptr && p->seed2 == nullptr) || p->slot != nullptr);
+  MIREC_CHECK_ARG(p->param == nullptr || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr));
+  MIREC_CHECK_ARG(p->divisor != 0.f);
+  if (c->n_seg > 0) {
+    MIREC_CHECK_ARG(c->split > 0 && c->seg_row && c->seg_beg && c->long_rows && c->long_segptr);
+    if (p->partial == nullptr) return MIREC_ERR_WORKSPACE;
+  }
+  PropK k;
+  k.rowptr = c->rowptr;
+  k.col = c->col;
+  k.dinv = c->dinv;
+  k.n_rows = c->n_rows;
+  k.n_seg = c->n_seg;
+  k.seg_row = c->seg_row;
+  k.seg_beg = c->seg_beg;
+  k.split = c->n_seg > 0 ? c->split : 0;
+  k.x_in = p->x_in;
+  k.slot = p->slot;
+  k.seed_in = p->seed_in;
+  k.seed = p->seed;
+  k.addend = p->addend;
+  k.seed2 = p->seed2;
+  k.divisor = p->divisor;
+  k.out = p->out;
+  k.xs_out = p->xs_out;
+  k.param = p->param;
+  k.m = p->exp_avg;
+  k.v = p->exp_avg_sq;
+  k.adam = p->adam;
+  k.partial = p->partial;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (p->dim) {
+    case 4: return launch_prop<4, 1>(c, k, p->in_mode, st);
+    case 8: return launch_prop<8, 1>(c, k, p->in_mode, st);
+    case 16: return launch_prop<16, 1>(c, k, p->in_mode, st);
+    case 32: return launch_prop<32, 2>(c, k, p->in_mode, st);
+    case 64: return launch_prop<64, 4>(c, k, p->in_mode, st);
+    case 128: return launch_prop<128, 4>(c, k, p->in_mode, st);
+    case 256: return launch_prop<256, 8>(c, k, p->in_mode, st);
+  }
+  return MIREC_ERR_DIM;
+}

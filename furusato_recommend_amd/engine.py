@@ -1,0 +1,325 @@
+"""LightGCN propagation + BPR training engine (device side orchestration).
+
+One training step (the reference's ``stageOne``, model/lgcn.py:127-133, on
+top of ``bpr_loss`` :98-118 and ``forward`` :78-86) runs as 3L/2+4 HIP
+launches with no host synchronisation:
+
+  forward  (L launches)   x_l = Â x_{l-1}; acc = x_0 + ... + x_L; out = acc/(L+1)
+                          layer 1 gathers E with per-edge dinv_j (IN_RAW),
+                          layers 2..L gather the pre-scaled x~ = dinv ⊙ x
+                          written by the previous epilogue; the final layer
+                          writes out = acc/(L+1) in place of acc.
+  BPR      (3 + sort)     scores, softplus, loss; sorted (node, occurrence)
+                          pairs → per-node gradient seeds d = dL/d out /(L+1)
+                          and the reg-gradient seed.
+  backward (L launches)   Horner: g_L = d, g_l = d + Â g_{l+1} (Â symmetric:
+                          the backward SpMM is the forward kernel on the
+                          same CSR).  The first backward layer gathers the
+                          sparse seeds (IN_SPARSE); the last one adds the reg
+                          seed and applies Adam to E in its epilogue, so the
+                          dense gradient is never written to HBM.
+  reset    (1)            slot[] back to -1 for the touched nodes.
+
+For data parallelism (dist.py) the last layer writes the dense gradient
+instead and the caller all-reduces it before ``adam_step``.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import (IN_NONE, IN_PRESCALED, IN_RAW, IN_SPARSE, Prop, adam_hparams,
+                   check, lib, ptr)
+from .graph import Graph
+
+
+def prop_launch_bytes(in_mode: int, n_nodes: int, nnz: int, dim: int, *, slot=False,
+                      xs_out=False, addend=False, out=False, adam=False) -> int:
+    """Algorithmic HBM bytes of one mirec_propagate launch:
+    every operand the launch must read or write, each exactly once."""
+    N, D = n_nodes, dim
+    row = N * D * 4
+    b = (N + 1) * 8 + N * 4                       # rowptr (int64), dinv_i
+    if in_mode == IN_PRESCALED:
+        b += nnz * (D * 4 + 4)                    # neighbour rows + col
+    elif in_mode == IN_RAW:
+        b += nnz * (D * 4 + 4 + 4)                # + dinv_j per entry
+    elif in_mode == IN_SPARSE:
+        b += nnz * (4 + 4 + 4)                    # col, dinv_j, slot_j
+    if slot:
+        b += N * 4                                # slot_i
+    b += row * (int(xs_out) + int(addend) + int(out))
+    if adam:
+        b += 6 * row                              # param/m/v read + write
+    return b
+
+
+class AdamState:
+    """torch.optim.Adam state for one dense parameter, in torch's layout."""
+
+    def __init__(self, param: torch.Tensor, lr: float, betas=(0.9, 0.999), eps: float = 1e-8):
+        self.param = param
+        self.lr = float(lr)
+        self.betas = (float(betas[0]), float(betas[1]))
+        self.eps = float(eps)
+        self.n_steps = 0
+        self.exp_avg = torch.zeros_like(param)
+        self.exp_avg_sq = torch.zeros_like(param)
+
+    def next_hparams(self):
+        self.n_steps += 1
+        return adam_hparams(self.lr, self.betas[0], self.betas[1], self.eps, self.n_steps)
+
+    # torch.optim-style surface for the differentiable path (reference
+    # stageOne: optim.zero_grad(); loss.backward(); optim.step()).
+    def zero_grad(self, set_to_none: bool = True):
+        if self.param.grad is not None:
+            if set_to_none:
+                self.param.grad = None
+            else:
+                self.param.grad.zero_()
+
+    @torch.no_grad()
+    def step(self):
+        g = self.param.grad
+        if g is None:
+            return
+        hp = self.next_hparams()
+        check(lib.mirec_adam_dense(self.param.data_ptr(), g.contiguous().data_ptr(),
+                                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                   self.param.numel(), ctypes.byref(hp), _lib.stream_handle()),
+              "adam_dense")
+
+    def state_dict(self, param_id: int = 0) -> dict:
+        """Same structure as torch.optim.Adam.state_dict() for one param."""
+        return {
+            "state": {param_id: {"step": torch.tensor(float(self.n_steps)),
+                                 "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}},
+            "param_groups": [{"lr": self.lr, "betas": self.betas, "eps": self.eps,
+                              "weight_decay": 0, "amsgrad": False, "maximize": False,
+                              "foreach": None, "capturable": False, "differentiable": False,
+                              "fused": None, "params": [param_id]}],
+        }
+
+    def load_state_dict(self, sd: dict) -> None:
+        st = next(iter(sd["state"].values())) if sd["state"] else None
+        if st is not None:
+            self.n_steps = int(float(st["step"]))
+            self.exp_avg.copy_(st["exp_avg"])
+            self.exp_avg_sq.copy_(st["exp_avg_sq"])
+        g = sd["param_groups"][0]
+        self.lr, self.betas, self.eps = float(g["lr"]), tuple(g["betas"]), float(g["eps"])
+
+
+class PropagationEngine:
+    """Owns the per-model scratch buffers and issues the HIP launches."""
+
+    def __init__(self, graph: Graph, dim: int, n_layers: int, max_batch: int):
+        if dim not in _lib.SUPPORTED_DIMS:
+            raise ValueError(f"recdim={dim} not supported by the HIP engine "
+                             f"(supported: {_lib.SUPPORTED_DIMS})")
+        if graph.device.type != "cuda":
+            raise RuntimeError("PropagationEngine needs a HIP device (no CPU fallback)")
+        self.g = graph
+        self.dim = int(dim)
+        self.L = int(n_layers)
+        self.max_batch = int(max_batch)
+        dev = graph.device
+        N, D = graph.n_nodes, self.dim
+        f32 = dict(dtype=torch.float32, device=dev)
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.acc = torch.empty(N, D, **f32)       # layer sum, then out = acc/(L+1)
+        self.xs = [torch.empty(N, D, **f32), torch.empty(N, D, **f32)] if self.L > 1 else \
+            [torch.empty(N, D, **f32)] if self.L == 1 else []
+        self.slot = torch.full((N,), -1, **i32)
+        B3 = 3 * self.max_batch
+        self.seed_p = torch.empty(B3, D, **f32)
+        self.seed_e = torch.empty(B3, D, **f32)
+        self.coef = torch.empty(self.max_batch, **f32)
+        self.softplus = torch.empty(self.max_batch, **f32)
+        self.reg = torch.empty(self.max_batch, **f32)
+        self.keys = torch.empty(B3, **i32)
+        self.vals = torch.empty(B3, **i32)
+        self.keys_sorted = torch.empty(B3, **i32)
+        self.loss = torch.zeros(1, **f32)
+        self.partial = graph.partial_buffer(D)
+        self._ws = None
+        self._ws_bytes = 0
+        self._ensure_ws(self.max_batch)
+        # Optional per-launch timing of the propagation kernel (bench.py).
+        self.prop_events = None
+
+    # ------------------------------------------------------------ internals
+    def _ensure_ws(self, batch: int):
+        nb = ctypes.c_size_t(0)
+        check(lib.mirec_bpr_seed_workspace(batch, self.g.n_nodes, ctypes.byref(nb)),
+              "bpr_seed_workspace")
+        if nb.value > self._ws_bytes:
+            self._ws = torch.empty(nb.value, dtype=torch.uint8, device=self.g.device)
+            self._ws_bytes = nb.value
+
+    def _prop(self, *, in_mode, x_in=None, seed_in=None, seed=None, addend=None, seed2=None,
+              divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None):
+        g = graph or self.g
+        p = Prop()
+        p.dim = self.dim
+        p.in_mode = in_mode
+        p.x_in = ptr(x_in)
+        p.slot = self.slot.data_ptr() if (seed_in is not None or seed is not None
+                                          or seed2 is not None) else None
+        p.seed_in = ptr(seed_in)
+        p.seed = ptr(seed)
+        p.addend = ptr(addend)
+        p.seed2 = ptr(seed2)
+        p.divisor = float(divisor)
+        p.out = ptr(out)
+        p.xs_out = ptr(xs_out)
+        if adam is not None:
+            state, hp = adam
+            p.param = param.data_ptr()
+            p.exp_avg = state.exp_avg.data_ptr()
+            p.exp_avg_sq = state.exp_avg_sq.data_ptr()
+            p.adam = hp
+        part = g.partial_buffer(self.dim)
+        p.partial = ptr(part)
+        ev = self.prop_events
+        if ev is not None:
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+        check(lib.mirec_propagate(g.csr_ptr(), ctypes.byref(p), _lib.stream_handle()),
+              "propagate")
+        if ev is not None:
+            e.record()
+            ev.append((s, e, in_mode, self.launch_bytes(p, g)))
+
+    def launch_bytes(self, p: Prop, g: Graph) -> int:
+        return prop_launch_bytes(p.in_mode, g.n_nodes, g.nnz, self.dim,
+                                 slot=bool(p.slot and (p.seed or p.seed2)),
+                                 xs_out=bool(p.xs_out), addend=bool(p.addend),
+                                 out=bool(p.out), adam=bool(p.param))
+
+    # ------------------------------------------------------------- forward
+    def forward(self, emb: torch.Tensor) -> torch.Tensor:
+        """out = (x_0 + ... + x_L)/(L+1), x_l = Â x_{l-1} (model/lgcn.py:78-86).
+
+        Returns the engine's ``acc`` buffer (valid until the next call)."""
+        L = self.L
+        if L == 0:
+            self.acc.copy_(emb)
+            return self.acc
+        for l in range(1, L + 1):
+            last = l == L
+            self._prop(in_mode=IN_RAW if l == 1 else IN_PRESCALED,
+                       x_in=emb if l == 1 else self.xs[(l - 2) % 2],
+                       addend=emb if l == 1 else self.acc,
+                       divisor=float(L + 1) if last else 1.0,
+                       out=self.acc,
+                       xs_out=None if last else self.xs[(l - 1) % 2])
+        return self.acc
+
+    def propagate_once(self, x: torch.Tensor, out: torch.Tensor, graph: Graph | None = None):
+        """out = Â x (one LGConv call)."""
+        self._prop(in_mode=IN_RAW, x_in=x, out=out, graph=graph)
+
+    def propagate_accumulate(self, g_in: torch.Tensor, addend: torch.Tensor,
+                             out: torch.Tensor, graph: Graph | None = None):
+        """out = Â g_in + addend (generic autograd backward, dense seed)."""
+        self._prop(in_mode=IN_RAW, x_in=g_in, addend=addend, out=out, graph=graph)
+
+    # ------------------------------------------------------------------ BPR
+    def bpr(self, out: torch.Tensor, emb: torch.Tensor, users, pos, neg, decay: float,
+            loss_accum: torch.Tensor | None = None, grad_scale: float = 1.0) -> torch.Tensor:
+        """Loss + gradient seeds for one batch of int32 device triples.
+
+        ``grad_scale`` multiplies the gradient seeds (1/world_size under data
+        parallelism, so a SUM all-reduce yields the union-batch gradient)."""
+        B = int(users.shape[0])
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} > engine max_batch {self.max_batch}")
+        self._ensure_ws(B)
+        st = _lib.stream_handle()
+        g = self.g
+        check(lib.mirec_bpr_forward(out.data_ptr(), emb.data_ptr(), g.n_nodes, g.n_users,
+                                    self.dim, B, users.data_ptr(), pos.data_ptr(),
+                                    neg.data_ptr(), float(grad_scale), self.coef.data_ptr(),
+                                    self.softplus.data_ptr(), self.reg.data_ptr(),
+                                    self.keys.data_ptr(), self.vals.data_ptr(), st),
+              "bpr_forward")
+        check(lib.mirec_bpr_loss(self.softplus.data_ptr(), self.reg.data_ptr(), B,
+                                 float(decay), self.loss.data_ptr(), ptr(loss_accum), st),
+              "bpr_loss")
+        check(lib.mirec_bpr_seed(out.data_ptr(), emb.data_ptr(), g.n_nodes, g.n_users,
+                                 self.dim, B, users.data_ptr(), pos.data_ptr(),
+                                 neg.data_ptr(), self.coef.data_ptr(), self.keys.data_ptr(),
+                                 self.vals.data_ptr(), float(decay), float(grad_scale), self.L,
+                                 self.slot.data_ptr(), self.seed_p.data_ptr(),
+                                 self.seed_e.data_ptr(), self.keys_sorted.data_ptr(),
+                                 self._ws.data_ptr(), self._ws_bytes, st), "bpr_seed")
+        self._last_batch = B
+        return self.loss
+
+    # ------------------------------------------------------------- backward
+    def backward(self, emb: torch.Tensor, adam: AdamState | None = None,
+                 grad_out: torch.Tensor | None = None):
+        """Horner backward from the seeds of the last ``bpr`` call.
+
+        With ``adam`` the last layer applies Adam to ``emb`` in place (fused);
+        otherwise the dense gradient dLoss/dE is written to ``grad_out``."""
+        if (adam is None) == (grad_out is None):
+            raise ValueError("exactly one of adam / grad_out")
+        L = self.L
+        hp = adam.next_hparams() if adam is not None else None
+        final = dict(seed2=self.seed_e)
+        if adam is not None:
+            final.update(adam=(adam, hp), param=emb)
+        else:
+            final.update(out=grad_out)
+        if L == 0:
+            self._prop(in_mode=IN_NONE, seed=self.seed_p, **final)
+        else:
+            for l in range(L - 1, -1, -1):
+                first = l == L - 1
+                kw = dict(in_mode=IN_SPARSE if first else IN_PRESCALED,
+                          seed_in=self.seed_p if first else None,
+                          x_in=None if first else self.xs[(L - 2 - l) % 2],
+                          seed=self.seed_p)
+                if l == 0:
+                    kw.update(final)
+                else:
+                    kw.update(xs_out=self.xs[(L - 1 - l) % 2])
+                self._prop(**kw)
+        check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), self.keys_sorted.data_ptr(),
+                                       3 * self._last_batch, _lib.stream_handle()),
+              "bpr_seed_reset")
+
+    def adam_step(self, param: torch.Tensor, grad: torch.Tensor, adam: AdamState):
+        hp = adam.next_hparams()
+        check(lib.mirec_adam_dense(param.data_ptr(), grad.data_ptr(), adam.exp_avg.data_ptr(),
+                                   adam.exp_avg_sq.data_ptr(), param.numel(), ctypes.byref(hp),
+                                   _lib.stream_handle()), "adam_dense")
+
+    # --------------------------------------------------------------- step
+    def train_step(self, emb: torch.Tensor, adam: AdamState, users, pos, neg, decay: float,
+                   loss_accum: torch.Tensor | None = None) -> torch.Tensor:
+        """stageOne: forward, BPR, backward, fused Adam.  Returns loss (device)."""
+        out = self.forward(emb)
+        loss = self.bpr(out, emb, users, pos, neg, decay, loss_accum)
+        self.backward(emb, adam=adam)
+        return loss
+
+
+def sample_triples(graph: Graph, batch: int, seed: int, offset: int, users, pos, neg, err,
+                   shard: int = 0, n_shards: int = 1):
+    """On-device UniformSample (negative_sample.py:98-134) into int32 buffers."""
+    check(lib.mirec_bpr_sample(graph.csr_ptr(), graph.n_users, graph.m_items, int(batch),
+                               ctypes.c_uint64(seed & (2**64 - 1)),
+                               ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
+                               int(n_shards), users.data_ptr(), pos.data_ptr(),
+                               neg.data_ptr(), err.data_ptr(), _lib.stream_handle()),
+          "bpr_sample")
+
+
+_ = math

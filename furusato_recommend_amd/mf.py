@@ -1,0 +1,92 @@
+"""MF-BPR (model/MF.py:35-112) on the same HIP engine.
+
+Matrix factorisation is LightGCN with zero propagation layers: scores are
+dot products of the ego embeddings and the reg term is taken on the same
+rows.  The two reference tables ``embedding_user`` / ``embedding_item`` are
+views into one [n_users + m_items, d] device table so the fused BPR /
+seed / Adam kernels (one pass over the table) serve both; ``state_dict``
+keeps the reference keys ``embedding_user.weight`` / ``embedding_item.weight``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .engine import AdamState, PropagationEngine
+from .graph import DEFAULT_SPLIT, Graph
+
+
+class MF(nn.Module):
+    def __init__(self, config: dict, dataset):
+        super().__init__()
+        self.config = config
+        self.num_users = int(dataset.n_users)
+        self.num_items = int(dataset.m_items)
+        self.latent_dim = int(config.get("latent_dim_rec", config.get("recdim", 32)))
+        self.device = torch.device(config.get("device", "cuda:0"))
+        if self.device.type != "cuda":
+            raise RuntimeError("MF (furusato_recommend_amd) runs on a HIP device only")
+        # model/MF.py:47-54: default nn.Embedding init, N(0, 1)
+        table = torch.randn(self.num_users + self.num_items, self.latent_dim,
+                            device=self.device)
+        self._table = table
+        self.embedding_user = nn.Embedding(self.num_users, self.latent_dim,
+                                           _weight=table[: self.num_users], device=self.device)
+        self.embedding_item = nn.Embedding(self.num_items, self.latent_dim,
+                                           _weight=table[self.num_users:], device=self.device)
+        self.f = nn.Sigmoid()
+        self.graph = Graph.from_interactions(dataset.trainUser, dataset.trainItem,
+                                             self.num_users, self.num_items, self.device,
+                                             split=int(config.get("csr_split", DEFAULT_SPLIT)))
+        self.optim = AdamState(self._table, lr=config["lr"])
+        self.engine = PropagationEngine(self.graph, self.latent_dim, 0,
+                                        int(config.get("bpr_batch_size", 2048)))
+        self._loss_accum = torch.zeros(1, dtype=torch.float32, device=self.device)
+
+    def load_table(self, user_w: torch.Tensor, item_w: torch.Tensor):
+        with torch.no_grad():
+            self._table[: self.num_users].copy_(user_w)
+            self._table[self.num_users:].copy_(item_w)
+
+    @torch.no_grad()
+    def getUsersRating(self, users):
+        users_emb = self.embedding_user.weight[users.long()]
+        return self.f(users_emb @ self.embedding_item.weight.t())
+
+    def bpr_loss(self, users, pos, neg):
+        users_emb = self.embedding_user(users.long())
+        pos_emb = self.embedding_item(pos.long())
+        neg_emb = self.embedding_item(neg.long())
+        pos_scores = torch.sum(users_emb * pos_emb, dim=1)
+        neg_scores = torch.sum(users_emb * neg_emb, dim=1)
+        loss = torch.mean(nn.functional.softplus(neg_scores - pos_scores))
+        reg = 0.5 * (users_emb.norm(2).pow(2) + pos_emb.norm(2).pow(2)
+                     + neg_emb.norm(2).pow(2)) / float(len(users))
+        return loss, reg
+
+    def forward(self, users, items):
+        u = self.embedding_user(users.long())
+        i = self.embedding_item(items.long())
+        return self.f(torch.sum(u * i, dim=1))
+
+    def _as_i32(self, t):
+        t = torch.as_tensor(t)
+        return t.to(device=self.device, dtype=torch.int32).contiguous()
+
+    @torch.no_grad()
+    def stageOne(self, user, pos, neg, loss_accum=None):
+        return self.engine.train_step(self._table, self.optim, self._as_i32(user),
+                                      self._as_i32(pos), self._as_i32(neg),
+                                      float(self.config["decay"]), loss_accum).clone()
+
+    @torch.no_grad()
+    def OneEpoch(self, user, pos, neg):
+        B = int(self.config["bpr_batch_size"])
+        n = len(user)
+        user, pos, neg = self._as_i32(user), self._as_i32(pos), self._as_i32(neg)
+        self._loss_accum.zero_()
+        for i in range(0, n, B):
+            self.engine.train_step(self._table, self.optim, user[i:i + B], pos[i:i + B],
+                                   neg[i:i + B], float(self.config["decay"]),
+                                   self._loss_accum)
+        return self._loss_accum[0] / (n // B + 1)

@@ -1,0 +1,9 @@
+"""Model registry with the reference's names (main.py:32-56, subset on the
+hot path: 'lgn' = LightGCN, 'mf' = MF)."""
+from .lightgcn import LightGCN
+from .mf import MF
+
+MODELS = {
+    "mf": MF,
+    "lgn": LightGCN,
+}

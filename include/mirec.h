@@ -1,0 +1,238 @@
+/*
+ * mirec.h — C ABI of libmirec.so, the MI355X (gfx950) engine for the
+ * LightGCN propagation + BPR training hot path of
+ * HiromasaYamanishi/furusato_recommend.
+ *
+ * Every entry point is extern "C", takes plain pointers and sizes, returns an
+ * int status (0 = MIREC_OK) and never allocates device memory: the caller
+ * (PyTorch's caching allocator on the Python side) owns every buffer and
+ * passes scratch space explicitly.  Device entry points are stream-ordered on
+ * the hipStream_t passed as `stream` (NULL = the legacy default stream), do
+ * not synchronise the host and are safe to capture into a hipGraph.
+ *
+ * Reference interfaces each group replaces (paths under the reference repo):
+ *   mirec_csr_*            model/lgcn.py:53-61 (symmetric edge list) and the
+ *                          gcn_norm degree pass PyG's LGConv runs per call
+ *                          (called at model/lgcn.py:66,82); restated in-repo
+ *                          by model/radj.py:28-36.
+ *   mirec_propagate        LGConv()(x, edge_index) at model/lgcn.py:82,
+ *                          model/radj.py:39-44 (gather / scale / scatter-sum),
+ *                          the layer mean of model/lgcn.py:78-86 and the
+ *                          autograd backward of both.
+ *   mirec_bpr_*            LightGCN.bpr_loss model/lgcn.py:98-118 + its
+ *                          backward (stageOne, model/lgcn.py:127-133).
+ *   mirec_adam_*           torch.optim.Adam created at model/lgcn.py:63,
+ *                          stepped at model/lgcn.py:132.
+ *   mirec_bpr_sample       UniformSample, negative_sample.py:98-134.
+ */
+#ifndef MIREC_H
+#define MIREC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIREC_ABI_VERSION 1
+
+enum mirec_status {
+  MIREC_OK = 0,
+  MIREC_ERR_ARG = 1,       /* null pointer / negative size / bad enum        */
+  MIREC_ERR_DIM = 2,       /* embedding dim not in {4,8,16,32,64,128,256}    */
+  MIREC_ERR_HIP = 3,       /* a HIP runtime call failed (mirec_last_hip_error) */
+  MIREC_ERR_WORKSPACE = 4, /* caller-provided scratch space too small         */
+  MIREC_ERR_RANGE = 5      /* an index is outside [0, n)                     */
+};
+
+typedef void *mirec_stream_t; /* hipStream_t */
+
+const char *mirec_strerror(int code);
+int mirec_abi_version(void);
+int mirec_last_hip_error(void);
+/* sizeof(mirec_csr_t), sizeof(mirec_prop_t), sizeof(mirec_adam_hparams_t):
+ * lets FFI bindings verify their struct mirrors. */
+int mirec_struct_sizes(size_t *csr, size_t *prop, size_t *adam_hparams);
+
+/* ------------------------------------------------------------------------ */
+/* Graph (host side, once per graph)                                         */
+/* ------------------------------------------------------------------------ */
+
+/* Destination-major CSR of the symmetric user–item graph of
+ * model/lgcn.py:53-61: node ids are users [0, n_users) then items
+ * n_users + [0, m_items).  Row u lists its items in edge order, row
+ * n_users+i lists its users in edge order (stable, duplicates kept as
+ * multi-edges exactly like the reference edge list).  dinv[v] =
+ * deg(v)^-1/2, 0 for isolated nodes (gcn_norm, add_self_loops=False).
+ * rowptr: [n_users+m_items+1], col: [2*n_edges], dinv: [n_users+m_items]. */
+int mirec_csr_bipartite(const int64_t *train_user, const int64_t *train_item,
+                        int64_t n_edges, int64_t n_users, int64_t m_items,
+                        int64_t *rowptr, int32_t *col, float *dinv);
+
+/* Generic stable CSR by destination from a COO edge list (edge_index[0] =
+ * source, edge_index[1] = destination, the LGConv convention).  dinv (may
+ * be NULL) = in-degree^-1/2 of every node (gcn_norm on `col`). */
+int mirec_csr_from_coo(const int64_t *src, const int64_t *dst, int64_t nnz,
+                       int64_t n_nodes, int64_t *rowptr, int32_t *col,
+                       float *dinv);
+
+/* Long-row schedule for load balance: rows with more than `split` entries
+ * are cut into segments of `split` entries.  Call once with NULL outputs
+ * to get the counts, then again with arrays of those sizes:
+ * long_rows[n_long], long_segptr[n_long+1], seg_row[n_seg], seg_beg[n_seg]. */
+int mirec_csr_long_rows(const int64_t *rowptr, int64_t n_rows, int32_t split,
+                        int64_t *n_long, int64_t *n_seg, int32_t *long_rows,
+                        int64_t *long_segptr, int32_t *seg_row,
+                        int64_t *seg_beg);
+
+/* Device-resident CSR descriptor (all pointers are device pointers). */
+typedef struct mirec_csr {
+  const int64_t *rowptr;      /* [n_rows+1] */
+  const int32_t *col;         /* [nnz] source node of each entry */
+  const float *dinv;          /* [n_rows] deg^-1/2 (0 if deg == 0) */
+  int64_t n_rows;
+  int64_t nnz;
+  int32_t split;              /* long-row threshold, 0 = none */
+  int32_t _pad;
+  int64_t n_long;
+  int64_t n_seg;
+  const int32_t *long_rows;   /* [n_long] */
+  const int64_t *long_segptr; /* [n_long+1] */
+  const int32_t *seg_row;     /* [n_seg] */
+  const int64_t *seg_beg;     /* [n_seg] */
+} mirec_csr_t;
+
+/* ------------------------------------------------------------------------ */
+/* Propagation: one LightGCN layer (CSR segment-gather SpMM + epilogue)      */
+/* ------------------------------------------------------------------------ */
+
+enum mirec_in_mode {
+  MIREC_IN_PRESCALED = 0, /* x_in rows are already x~_j = dinv_j * x_j        */
+  MIREC_IN_RAW = 1,       /* x_in rows are x_j; the kernel applies dinv_j     */
+  MIREC_IN_SPARSE = 2,    /* input row j = seed_in[slot[j]] (0 if slot[j]<0),
+                             kernel applies dinv_j                            */
+  MIREC_IN_NONE = 3       /* no gather: y = 0 (epilogue only; L = 0 / MF)    */
+};
+
+typedef struct mirec_adam_hparams {
+  float one_minus_beta1; /* 1 - beta1                      */
+  float beta2;
+  float one_minus_beta2; /* 1 - beta2                      */
+  float neg_step_size;   /* -lr / (1 - beta1^t)            */
+  float bc2_sqrt;        /* sqrt(1 - beta2^t)              */
+  float eps;
+} mirec_adam_hparams_t;
+
+/* For every row i of the CSR:
+ *   y_i   = dinv_i * sum_{j in row i} xin~_j                (Â x, fp32)
+ *   z_i   = y_i + seed[slot_i]               (if seed != NULL and slot_i >= 0)
+ *   xs_out_i = dinv_i * z_i                  (if xs_out != NULL; next layer)
+ *   o_i   = (z_i + addend_i) / divisor + seed2[slot_i]
+ *   out_i = o_i                              (if out != NULL)
+ *   Adam(param_i, exp_avg_i, exp_avg_sq_i; grad = o_i)   (if param != NULL)
+ * `partial` is scratch of csr->n_seg * dim floats (may be NULL if n_seg==0).
+ * Summation order per row is fixed by the CSR: results are deterministic. */
+typedef struct mirec_prop {
+  int32_t dim;
+  int32_t in_mode;
+  const float *x_in;    /* [n_rows, dim] (modes 0/1) */
+  const int32_t *slot;  /* [n_rows] seed slot map, -1 = none */
+  const float *seed_in; /* [*, dim] mode-2 input rows indexed by slot */
+  const float *seed;    /* [*, dim] */
+  const float *addend;  /* [n_rows, dim] */
+  const float *seed2;   /* [*, dim] */
+  float divisor;
+  float _pad;
+  float *out;           /* [n_rows, dim] */
+  float *xs_out;        /* [n_rows, dim] */
+  float *param;         /* fused Adam: [n_rows, dim] each */
+  float *exp_avg;
+  float *exp_avg_sq;
+  mirec_adam_hparams_t adam;
+  float *partial;       /* [n_seg, dim] scratch */
+} mirec_prop_t;
+
+int mirec_propagate(const mirec_csr_t *csr, const mirec_prop_t *p,
+                    mirec_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* BPR (model/lgcn.py:98-133)                                                */
+/* ------------------------------------------------------------------------ */
+
+/* Scores of B triples from the layer-mean embeddings `out` [N, dim] and the
+ * ego embeddings `emb` [N, dim] (users are rows [0, n_users), item ids are
+ * offset by n_users).  Writes, per triple t:
+ *   softplus[t] = softplus(<u,n> - <u,p>)          (torch threshold 20)
+ *   coef[t]     = grad_scale * d mean(softplus) / d(neg - pos)
+ *   reg[t]      = 1/2 (|u0|^2 + |p0|^2 + |n0|^2)
+ * and the 3B seed keys/values (node id, occurrence index) consumed by
+ * mirec_bpr_seed. */
+int mirec_bpr_forward(const float *out, const float *emb, int64_t n_nodes,
+                      int64_t n_users, int32_t dim, int64_t batch,
+                      const int32_t *users, const int32_t *pos,
+                      const int32_t *neg, float grad_scale, float *coef,
+                      float *softplus, float *reg, int32_t *keys,
+                      int32_t *vals, mirec_stream_t stream);
+
+/* loss = mean(softplus) + decay * sum(reg) / B, written to loss_out[0];
+ * if loss_accum != NULL also loss_accum[0] += loss (OneEpoch's aver_loss). */
+int mirec_bpr_loss(const float *softplus, const float *reg, int64_t batch,
+                   float decay, float *loss_out, float *loss_accum,
+                   mirec_stream_t stream);
+
+/* Scratch bytes mirec_bpr_seed needs for a batch of `batch` triples over a
+ * graph of n_nodes nodes. */
+int mirec_bpr_seed_workspace(int64_t batch, int64_t n_nodes, size_t *bytes);
+
+/* Gradient seeds of the backward pass.  Sorts the 3B (node, occurrence)
+ * pairs (stable radix sort), marks the first position q of every distinct
+ * node in `slot` (slot[node] = q; slot must be all -1 on entry) and writes
+ *   seed_p[q] = (sum over the node's occurrences of dLoss/d out_node) / (L+1)
+ *   seed_e[q] = decay * (#occurrences) * emb[node] / B   (reg term)
+ * summed in occurrence order (deterministic).  keys_sorted[3B] keeps the
+ * sorted node ids for mirec_bpr_seed_reset. */
+int mirec_bpr_seed(const float *out, const float *emb, int64_t n_nodes,
+                   int64_t n_users, int32_t dim, int64_t batch,
+                   const int32_t *users, const int32_t *pos,
+                   const int32_t *neg, const float *coef,
+                   const int32_t *keys, const int32_t *vals, float decay,
+                   float grad_scale, int32_t n_layers, int32_t *slot, float *seed_p,
+                   float *seed_e, int32_t *keys_sorted, void *workspace,
+                   size_t workspace_bytes, mirec_stream_t stream);
+
+/* slot[keys_sorted[q]] = -1 for q in [0, n). */
+int mirec_bpr_seed_reset(int32_t *slot, const int32_t *keys_sorted, int64_t n,
+                         mirec_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* Adam (torch.optim.Adam, amsgrad=False, weight_decay=0)                   */
+/* ------------------------------------------------------------------------ */
+
+int mirec_adam_dense(float *param, const float *grad, float *exp_avg,
+                     float *exp_avg_sq, int64_t n,
+                     const mirec_adam_hparams_t *h, mirec_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
+/* On-device BPR sampler (negative_sample.py:98-134 semantics)               */
+/* ------------------------------------------------------------------------ */
+
+/* Draws `batch` triples: u uniform over the users of shard `shard` (users
+ * u with u % n_shards == shard; n_shards = 1 → all users), users with no
+ * positives are redrawn, p uniform over u's CSR row (allPos order), n
+ * uniform over [0, m_items) rejected while n is a positive of u.  Counter-
+ * based: triple t of a call uses stream (seed, offset + t), so a batch is
+ * reproducible and independent of the launch shape.  Item ids are returned
+ * without the n_users offset.  err[0] is set to 1 if a draw exhausted its
+ * retry budget (a user with every item as a positive). */
+int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
+                     int64_t batch, uint64_t seed, uint64_t offset,
+                     int32_t shard, int32_t n_shards, int32_t *users,
+                     int32_t *pos, int32_t *neg, int32_t *err,
+                     mirec_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MIREC_H */

@@ -1,0 +1,209 @@
+"""Generate the golden fixtures by running the REFERENCE's own code.
+
+Run in the build container (the reference is mounted read-only at
+/root/reference; it does not exist on the GPU box, which only reads the
+committed .npz files):
+
+    python tests/golden/make_golden.py
+
+The reference modules are imported unmodified (model/lgcn.py, model/radj.py,
+model/MF.py, negative_sample.py, metric.py, utils.py, world.py).  Two
+third-party packages they import are not installed here and are not pinned
+by the reference (requirements.txt:1-10 lists neither):
+  * torch_scatter.scatter.scatter(src, index, out=, dim=0) — shimmed as the
+    sum scatter it is used as (model/radj.py:43): out.index_add_(0, index, src);
+  * torch_geometric.nn.conv.LGConv — shimmed with PyG's published algorithm:
+    gcn_norm(edge_index, add_self_loops=False) then add-aggregation of
+    x_j * dinv_i * dinv_j.
+The rAdjGCN fixture (r = 0.5) uses only the reference's own arithmetic plus the
+index_add scatter, and pins LGConv's shim (they must agree to ~1e-7).
+Bytecode is not written into the reference tree (sys.dont_write_bytecode).
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def install_shims():
+    ts = types.ModuleType("torch_scatter")
+    tss = types.ModuleType("torch_scatter.scatter")
+
+    def scatter(src, index, dim=0, out=None, reduce="sum", dim_size=None):
+        assert dim == 0 and reduce == "sum"
+        if out is None:
+            n = dim_size if dim_size is not None else int(index.max()) + 1
+            out = torch.zeros((n,) + tuple(src.shape[1:]), dtype=src.dtype)
+        return out.index_add_(0, index, src)
+
+    tss.scatter = scatter
+    ts.scatter = tss
+    pg = types.ModuleType("torch_geometric")
+    pgn = types.ModuleType("torch_geometric.nn")
+    pgc = types.ModuleType("torch_geometric.nn.conv")
+
+    class LGConv(torch.nn.Module):
+        def forward(self, x, edge_index):
+            row, col = edge_index[0], edge_index[1]
+            n = x.size(0)
+            deg = torch.zeros(n, dtype=x.dtype).index_add_(0, col, torch.ones(col.numel(), dtype=x.dtype))
+            dinv = deg.pow(-0.5)
+            dinv.masked_fill_(dinv == float("inf"), 0)
+            w = dinv[row] * dinv[col]
+            return torch.zeros_like(x).index_add_(0, col, x[row] * w.view(-1, 1))
+
+    pgc.LGConv = LGConv
+    pgn.conv = pgc
+    pg.nn = pgn
+    sys.modules.update({"torch_scatter": ts, "torch_scatter.scatter": tss,
+                        "torch_geometric": pg, "torch_geometric.nn": pgn,
+                        "torch_geometric.nn.conv": pgc})
+
+
+class TinyDataset:
+    """Loader protocol (dataloader.py:135-178) for an in-memory graph."""
+
+    def __init__(self, users, items, n_users, m_items):
+        self.trainUser = np.asarray(users, dtype=np.int64)
+        self.trainItem = np.asarray(items, dtype=np.int64)
+        self.n_users, self.m_items = n_users, m_items
+        self.n_user, self.m_item = n_users, m_items
+        self.trainDataSize = len(users)
+        self.allPos = [self.trainItem[self.trainUser == u] for u in range(n_users)]
+
+
+def tiny_graph(seed, n_users=200, m_items=50, n_edges=1000, isolated_item=True):
+    rng = np.random.default_rng(seed)
+    users = np.concatenate([np.arange(n_users), rng.integers(0, n_users, n_edges - n_users)])
+    hi = m_items - 1 if isolated_item else m_items  # last item never appears
+    items = rng.integers(0, hi, n_edges)
+    # force a few duplicate (multi-)edges
+    users[-5:] = users[:5]
+    items[-5:] = items[:5]
+    order = np.argsort(users, kind="stable")  # line-per-user file order
+    return users[order], items[order]
+
+
+def main():
+    sys.dont_write_bytecode = True
+    sys.argv = ["make_golden"]
+    sys.path.insert(0, REF)
+    install_shims()
+    import metric  # noqa: E402  (reference)
+    import negative_sample  # noqa: E402
+    import utils  # noqa: E402
+    from model import MF as ref_mf  # noqa: E402
+    from model import lgcn as ref_lgcn  # noqa: E402
+    from model import radj as ref_radj  # noqa: E402
+
+    torch.manual_seed(0)
+    # ---------------------------------------------------------- LightGCN
+    n_users, m_items = 200, 50
+    u, i = tiny_graph(1)
+    ds = TinyDataset(u, i, n_users, m_items)
+    for dim, L in ((64, 3), (32, 2), (128, 3), (256, 1), (16, 3)):
+        cfg = {"recdim": dim, "layer": L, "lr": 1e-3, "decay": 1e-4, "device": "cpu",
+               "bpr_batch_size": 64, "r": 0.5}
+        g = torch.Generator().manual_seed(dim * 10 + L)
+        E0 = torch.randn(n_users + m_items, dim, generator=g) * 0.1
+        m = ref_lgcn.LightGCN(cfg, ds)
+        m.all_embedding.weight.data.copy_(E0)
+        mr = ref_radj.rAdjGCN(cfg, ds)
+        mr.all_embedding.weight.data.copy_(E0)
+        with torch.no_grad():
+            ou, oi = m.forward()
+            ru, ri = mr.forward()
+            layers = [E0]
+            x = E0
+            for conv in m.layers:
+                x = conv(x, m.train_edge)
+                layers.append(x)
+        B = 64
+        trip = np.stack([
+            np.random.default_rng(7).integers(0, n_users, B),
+            np.random.default_rng(8).integers(0, m_items - 1, B),
+            np.random.default_rng(9).integers(0, m_items - 1, B)], 1)
+        trip[:4, 0] = trip[4:8, 0]  # duplicate users inside the batch
+        tu, tp, tn = (torch.tensor(trip[:, k]) for k in range(3))
+        loss, reg = m.bpr_loss(tu, tp, tn)
+        m.all_embedding.weight.grad = None
+        (loss + cfg["decay"] * reg).backward()
+        grad = m.all_embedding.weight.grad.detach().clone()
+        m.all_embedding.weight.grad = None
+        steps = []
+        step_losses = []
+        for _ in range(2):
+            step_losses.append(float(m.stageOne(tu, tp, tn)))
+            steps.append(m.all_embedding.weight.detach().clone())
+        np.savez_compressed(
+            os.path.join(OUT, f"lgcn_d{dim}_L{L}.npz"),
+            train_user=u, train_item=i, n_users=n_users, m_items=m_items, dim=dim,
+            n_layers=L, lr=cfg["lr"], decay=cfg["decay"], emb0=E0.numpy(),
+            out=torch.cat([ou, oi]).numpy(), out_radj=torch.cat([ru, ri]).numpy(),
+            layers=torch.stack(layers).numpy(), triples=trip, loss=float(loss),
+            reg=float(reg), grad=grad.numpy(), emb_step1=steps[0].numpy(),
+            emb_step2=steps[1].numpy(), step_losses=np.array(step_losses))
+        print("lgcn", dim, L, float(loss), float(reg))
+
+    # ---------------------------------------------------------------- MF
+    cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",
+           "bpr_batch_size": 64}
+    torch.manual_seed(3)
+    mf = ref_mf.MF(cfg, ds)
+    uw0 = mf.embedding_user.weight.detach().clone()
+    iw0 = mf.embedding_item.weight.detach().clone()
+    trip = np.stack([np.random.default_rng(11).integers(0, n_users, 64),
+                     np.random.default_rng(12).integers(0, m_items, 64),
+                     np.random.default_rng(13).integers(0, m_items, 64)], 1)
+    tu, tp, tn = (torch.tensor(trip[:, k]) for k in range(3))
+    l0, r0 = mf.bpr_loss(tu, tp, tn)
+    sl = float(mf.stageOne(tu, tp, tn))
+    with torch.no_grad():
+        rating = mf.getUsersRating(torch.arange(5))
+    np.savez_compressed(os.path.join(OUT, "mf_d32.npz"), train_user=u, train_item=i,
+                        n_users=n_users, m_items=m_items, user_w0=uw0.numpy(),
+                        item_w0=iw0.numpy(), triples=trip, loss=float(l0), reg=float(r0),
+                        step_loss=sl, user_w1=mf.embedding_user.weight.detach().numpy(),
+                        item_w1=mf.embedding_item.weight.detach().numpy(),
+                        rating5=rating.numpy(), lr=cfg["lr"], decay=cfg["decay"])
+    print("mf", float(l0), float(r0), sl)
+
+    # ----------------------------------------------------------- sampler
+    np.random.seed(2020)
+    S = negative_sample.UniformSample(ds)
+    np.savez_compressed(os.path.join(OUT, "sampler.npz"), seed=2020, S=S,
+                        train_user=u, train_item=i, n_users=n_users, m_items=m_items)
+    print("sampler", S.shape)
+
+    # ----------------------------------------------------------- metrics
+    rng = np.random.default_rng(5)
+    n_eval, k = 32, 20
+    pred = np.stack([rng.permutation(m_items)[:k] for _ in range(n_eval)])
+    gt = [list(rng.choice(m_items, size=int(rng.integers(1, 6)), replace=False))
+          for _ in range(n_eval)]
+    gt[0] = list(pred[0, :3])  # guaranteed hits
+    r = utils.getLabel(gt, pred)
+    rows = {}
+    for kk in (10, 20):
+        ret = metric.RecallPrecision_ATk(gt, r, kk)
+        rows[f"recall@{kk}"] = ret["recall"]
+        rows[f"precision@{kk}"] = ret["precision"]
+        rows[f"hr@{kk}"] = ret["hr"]
+        rows[f"ndcg@{kk}"] = metric.NDCGatK_r(gt, r, kk)
+    gt_flat = np.concatenate([np.array(g, dtype=np.int64) for g in gt])
+    gt_len = np.array([len(g) for g in gt], dtype=np.int64)
+    np.savez_compressed(os.path.join(OUT, "metrics.npz"), pred=pred, gt_flat=gt_flat,
+                        gt_len=gt_len, label=r,
+                        **{k.replace("@", "_at_"): v for k, v in rows.items()})
+    print("metrics", rows)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,92 @@
+"""The CPU oracle pinned against fixtures generated from the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import lightgcn_oracle as O
+from tests.conftest import GOLDEN
+
+LGCN = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "lgcn_*.npz")))
+
+
+def rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+@pytest.mark.parametrize("name", LGCN)
+def test_forward_matches_reference(golden, name):
+    f = golden(name)
+    n_users, L = int(f["n_users"]), int(f["n_layers"])
+    ei = O.edge_index(f["train_user"], f["train_item"], n_users)
+    out, layers = O.forward(torch.from_numpy(f["emb0"]), ei, n_users, L, return_layers=True)
+    assert rel(out, f["out_radj"]) < 1e-6          # reference's own formula
+    assert rel(out, f["out"]) < 1e-5               # LGConv (gcn_norm) path
+    for l in range(L + 1):
+        assert rel(layers[l], f["layers"][l]) < 1e-5
+    # The two reference formulations (rAdjConv r=.5 vs LGConv) agree.
+    assert rel(f["out"], f["out_radj"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", LGCN)
+def test_loss_grad_and_adam_match_reference(golden, name):
+    f = golden(name)
+    n_users, m_items = int(f["n_users"]), int(f["m_items"])
+    m = O.OracleLightGCN(f["train_user"], f["train_item"], n_users, m_items, int(f["dim"]),
+                         int(f["n_layers"]), float(f["lr"]), float(f["decay"]),
+                         emb=torch.from_numpy(f["emb0"]))
+    t = f["triples"]
+    loss, reg = m.bpr_loss(t[:, 0], t[:, 1], t[:, 2])
+    assert abs(float(loss) - float(f["loss"])) < 1e-6
+    assert abs(float(reg) - float(f["reg"])) / float(f["reg"]) < 1e-6
+    g = m.grad(t[:, 0], t[:, 1], t[:, 2])
+    assert rel(g, f["grad"]) < 1e-5
+    l1 = m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    assert rel(m.emb.detach(), f["emb_step1"]) < 2e-5
+    l2 = m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    assert rel(m.emb.detach(), f["emb_step2"]) < 2e-5
+    assert np.allclose([l1, l2], f["step_losses"], rtol=1e-6)
+
+
+def test_mf_matches_reference(golden):
+    f = golden("mf_d32.npz")
+    m = O.OracleMF(torch.from_numpy(f["user_w0"]), torch.from_numpy(f["item_w0"]),
+                   float(f["lr"]), float(f["decay"]))
+    t = f["triples"]
+    loss, reg = m.bpr_loss(t[:, 0], t[:, 1], t[:, 2])
+    assert abs(float(loss) - float(f["loss"])) < 1e-5
+    assert abs(float(reg) - float(f["reg"])) / float(f["reg"]) < 1e-6
+    sl = m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    assert abs(sl - float(f["step_loss"])) < 1e-5
+    assert rel(m.user.detach(), f["user_w1"]) < 1e-6
+    assert rel(m.item.detach(), f["item_w1"]) < 1e-6
+
+
+def test_sampler_bit_exact(golden):
+    f = golden("sampler.npz")
+    u, i = f["train_user"], f["train_item"]
+    n_users, m_items = int(f["n_users"]), int(f["m_items"])
+    all_pos = [i[u == k] for k in range(n_users)]
+    np.random.seed(int(f["seed"]))
+    S = O.uniform_sample(n_users, m_items, all_pos, len(u))
+    assert np.array_equal(S, f["S"])
+    for uu, p, n in S:  # the sampler's own invariants
+        assert p in all_pos[uu] and n not in all_pos[uu]
+
+
+def test_metrics_match_reference(golden):
+    f = golden("metrics.npz")
+    gt = np.split(f["gt_flat"], np.cumsum(f["gt_len"])[:-1])
+    gt = [list(g) for g in gt]
+    r = O.get_label(gt, f["pred"])
+    assert np.array_equal(r, f["label"])
+    for k in (10, 20):
+        ret = O.recall_precision_at_k(gt, r, k)
+        assert np.isclose(ret["recall"], f[f"recall_at_{k}"])
+        assert np.isclose(ret["precision"], f[f"precision_at_{k}"])
+        assert ret["hr"] == f[f"hr_at_{k}"]
+        assert np.isclose(O.ndcg_at_k(gt, r, k), f[f"ndcg_at_{k}"])
