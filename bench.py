@@ -3,9 +3,11 @@ d=64 on the synthetic 1M users x 100K items / 20M-edge graph (BASELINE.json
 configs[1]), 1..8 MI355X, user-sharded data parallelism over RCCL.
 
 A step = draw B triples on device (each rank from its user shard) + one
-full training step (full-graph 3-layer forward, fused BPR, full-graph
-backward, Adam) — the reference's UniformSample + stageOne
-(negative_sample.py:98-134, model/lgcn.py:127-133).  `value` = triples
+training step (3-layer forward, fused BPR, 3-layer backward, Adam over the
+whole table) — the reference's UniformSample + stageOne
+(negative_sample.py:98-134, model/lgcn.py:127-133).  With --prune 1
+(default) the layers the loss reads only on the batch's frontier are
+computed there only (engine.py); --prune 0 runs every layer on every row.  `value` = triples
 consumed by all ranks / wall time of the K timed steps (max over ranks),
 inputs resident in HBM.
 
@@ -30,7 +32,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-DOMINANT = "prop_kernel<64, 4, 0>"  # mirec::prop_kernel<D=64, UNROLL=4, IN_PRESCALED>
+# mirec::prop_kernel<D=64, UNROLL=4, IN_PRESCALED, in_mask=false, row_mask=false>
+DOMINANT = "prop_kernel<64, 4, 0, false, false>"
+KIND_NAMES = {0: "prescaled", 1: "raw", 2: "sparse", 3: "none"}
 
 
 def parse():
@@ -48,6 +52,9 @@ def parse():
     ap.add_argument("--cpu-baseline", default="step", choices=["step", "forward", "off"])
     ap.add_argument("--recall", type=int, default=1)
     ap.add_argument("--seed", type=int, default=2020)
+    ap.add_argument("--prune", type=int, default=1,
+                    help="frontier pruning (1) or every layer on every row (0)")
+    ap.add_argument("--dp-mode", default="sparse", choices=["sparse", "dense"])
     return ap.parse_args()
 
 
@@ -111,11 +118,11 @@ def main():
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0, kind=args.kind)
     torch.manual_seed(args.seed)
     cfg = {"recdim": args.dim, "layer": args.layers, "lr": 1e-3, "decay": 1e-4,
-           "device": str(dev), "bpr_batch_size": args.batch}
+           "device": str(dev), "bpr_batch_size": args.batch, "prune": bool(args.prune)}
     model = LightGCN(cfg, ds)
     eng = model.engine
     emb = model.all_embedding.weight.data
-    dp = DataParallel(eng, emb, model.optim) if world > 1 else None
+    dp = DataParallel(eng, emb, model.optim, mode=args.dp_mode) if world > 1 else None
     B = args.batch
     u = torch.empty(B, dtype=torch.int32, device=dev)
     p, n = torch.empty_like(u), torch.empty_like(u)
@@ -153,16 +160,19 @@ def main():
         raise RuntimeError("sampler retry budget exhausted")
 
     # Live per-launch timing of the propagation kernel (HIP events on the
-    # stream it is launched on), by input mode.
-    per_mode = {}
-    for s, e, mode, nbytes in events:
+    # stream it is launched on), by launch kind (in_mode, in_mask, row_mask).
+    # The roofline is quoted for the full (unmasked) pre-scaled launches,
+    # whose algorithmic bytes are exact; masked launches touch data-dependent
+    # subsets and are reported by time only.
+    per_kind = {}
+    for s, e, kind, nbytes in events:
         ms = s.elapsed_time(e)
-        d = per_mode.setdefault(mode, [0, 0.0, 0])
+        d = per_kind.setdefault(kind, [0, 0.0, 0])
         d[0] += 1
         d[1] += ms
         d[2] += nbytes
-    t_prop = sum(v[1] for v in per_mode.values()) / args.steps
-    dom = per_mode.get(0, [1, 1.0, 0])
+    t_prop = sum(v[1] for v in per_kind.values()) / args.steps
+    dom = per_kind.get((0, False, False), [1, 1.0, 0])
     avg_ms = dom[1] / dom[0]
     avg_bytes = dom[2] / dom[0]
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
@@ -171,7 +181,8 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             j = json.load(f)
-        if j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}":
+        if (j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
+                and DOMINANT in j.get("kernel", "")):
             traffic = j.get("hbm_bytes_per_launch")
 
     recall = None
@@ -205,7 +216,8 @@ def main():
                        "users": args.users, "items": args.items, "edges": args.edges,
                        "graph": args.kind, "dim": args.dim, "layers": args.layers,
                        "bpr_batch_per_rank": B, "global_batch": B * world,
-                       "parallelism": f"dp{world} (user-sharded, RCCL all-reduce)"},
+                       "parallelism": f"dp{world} (user-sharded, RCCL {args.dp_mode} "
+                                      f"gradient exchange)"},
             "roofline": {"bound": "hbm", "kernel": DOMINANT,
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -213,7 +225,11 @@ def main():
                          "algorithmic_bytes_per_launch": int(avg_bytes),
                          "launches_per_step": round(dom[0] / args.steps, 2)},
             "propagation_ms_per_step": round(t_prop, 3),
-            "per_mode_ms": {str(k): round(v[1] / v[0], 4) for k, v in sorted(per_mode.items())},
+            "per_launch_kind": {
+                f"{KIND_NAMES[k[0]]}{'+inmask' if k[1] else ''}{'+rowmask' if k[2] else ''}":
+                {"launches_per_step": round(v[0] / args.steps, 2), "avg_ms": round(v[1] / v[0], 4)}
+                for k, v in sorted(per_kind.items())},
+            "prune": bool(args.prune),
             "recall": recall,
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 2),

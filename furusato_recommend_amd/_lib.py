@@ -55,7 +55,8 @@ class Prop(Structure):
         ("addend", c_void_p), ("seed2", c_void_p), ("divisor", c_float),
         ("_pad", c_float), ("out", c_void_p), ("xs_out", c_void_p),
         ("param", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
-        ("adam", AdamH), ("partial", c_void_p),
+        ("adam", AdamH), ("partial", c_void_p), ("row_mask", c_void_p),
+        ("in_mask", c_void_p),
     ]
 
 
@@ -74,6 +75,9 @@ SIGNATURES = {
                                     POINTER(c_int64), c_void_p, c_void_p, c_void_p,
                                     c_void_p]),
     "mirec_propagate": (c_int, [POINTER(CSR), POINTER(Prop), c_void_p]),
+    "mirec_prescale": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "mirec_frontier": (c_int, [POINTER(CSR), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                               c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -85,6 +89,11 @@ SIGNATURES = {
                                c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_bpr_seed_reset": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "mirec_seed_pack": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "mirec_seed_merge_workspace": (c_int, [c_int64, c_int64, POINTER(c_size_t)]),
+    "mirec_seed_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                 c_void_p]),
     "mirec_adam_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                  POINTER(AdamH), c_void_p]),
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,

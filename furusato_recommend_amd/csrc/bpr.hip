@@ -151,7 +151,69 @@ __global__ __launch_bounds__(256) void seed_accum_kernel(
 
 __global__ void seed_reset_kernel(int32_t *slot, const int32_t *keys_sorted, int64_t n) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q < n) slot[keys_sorted[q]] = -1;
+  if (q < n) {
+    const int32_t k = keys_sorted[q];
+    if (k >= 0) slot[k] = -1;
+  }
+}
+
+// Data-parallel seed exchange.  pack: head positions keep their node id,
+// the others get the sentinel n_nodes (sorted last by the merge).
+__global__ void seed_pack_kernel(const int32_t *keys_sorted, int64_t n, int32_t sentinel,
+                                 int32_t *keys_packed) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  const int32_t k = keys_sorted[q];
+  keys_packed[q] = (q == 0 || keys_sorted[q - 1] != k) ? k : sentinel;
+}
+
+// merge heads: slot[node] = q for the first position of each node's run;
+// sentinel positions become -1 (ignored by reset / accumulate).
+__global__ void merge_heads_kernel(int32_t *keys_sorted, int64_t n, int32_t sentinel,
+                                   int32_t *slot) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= n) return;
+  // Sentinels sort last, so a real key's predecessor is never rewritten
+  // concurrently (the sentinel -> -1 rewrite only touches sentinel runs).
+  const int32_t k = keys_sorted[q];
+  const int32_t prev = q > 0 ? keys_sorted[q - 1] : -2;
+  if (k == sentinel) {
+    keys_sorted[q] = -1;
+    return;
+  }
+  if (prev != k) slot[k] = (int32_t)q;
+}
+
+// merged seed row of a node = sum of its gathered rows in gathered order
+// (rank-major: identical on every rank).
+template <int D>
+__global__ __launch_bounds__(256) void merge_accum_kernel(const int32_t *__restrict__ keys_sorted,
+                                                          const int32_t *__restrict__ idx_sorted,
+                                                          int64_t n, const float *__restrict__ rows_p,
+                                                          const float *__restrict__ rows_e,
+                                                          float *seed_p, float *seed_e) {
+  constexpr int LPR = D / 4;
+  constexpr int G = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR;
+  const int64_t q = ((int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6)) * G + lane / LPR;
+  if (q >= n) return;
+  const int32_t node = keys_sorted[q];
+  if (node < 0) return;
+  if (q > 0 && keys_sorted[q - 1] == node) return;
+  float4 ap = f4_zero(), ae = f4_zero();
+  for (int64_t q2 = q; q2 < n && keys_sorted[q2] == node; ++q2) {
+    const int64_t r = idx_sorted[q2];
+    ap = f4_add(ap, ld4(rows_p + r * D + sub * 4));
+    ae = f4_add(ae, ld4(rows_e + r * D + sub * 4));
+  }
+  st4(seed_p + q * D + sub * 4, ap);
+  st4(seed_e + q * D + sub * 4, ae);
+}
+
+__global__ void iota_kernel(int32_t *v, int64_t n) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) v[q] = (int32_t)q;
 }
 
 static int end_bit_for(int64_t n_nodes) {
@@ -298,4 +360,75 @@ extern "C" int mirec_bpr_seed_reset(int32_t *slot, const int32_t *keys_sorted, i
                      reinterpret_cast<hipStream_t>(stream), slot, keys_sorted, n);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
+}
+
+extern "C" int mirec_seed_pack(const int32_t *keys_sorted, int64_t n, int64_t n_nodes,
+                               int32_t *keys_packed, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(keys_sorted && keys_packed && n >= 0 && n_nodes > 0 && n_nodes < INT32_MAX);
+  if (n == 0) return MIREC_OK;
+  hipLaunchKernelGGL(seed_pack_kernel, dim3((n + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), keys_sorted, n, (int32_t)n_nodes,
+                     keys_packed);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_seed_merge_workspace(int64_t n, int64_t n_nodes, size_t *bytes) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(bytes && n > 0 && n_nodes > 0 && n < INT32_MAX);
+  size_t tb = 0;
+  int rc = sort_temp_bytes(n, n_nodes + 1, &tb);
+  if (rc != MIREC_OK) return rc;
+  *bytes = align_up(tb) + 2 * align_up((size_t)n * sizeof(int32_t));
+  return MIREC_OK;
+}
+
+template <int D>
+static int launch_merge_accum(const int32_t *ks, const int32_t *is, int64_t n, const float *rp,
+                              const float *re, float *sp, float *se, hipStream_t st) {
+  using namespace mirec;
+  constexpr int G = 64 / (D / 4);
+  const int64_t per_block = (int64_t)kWaves * G;
+  hipLaunchKernelGGL((merge_accum_kernel<D>), dim3((n + per_block - 1) / per_block), dim3(256), 0,
+                     st, ks, is, n, rp, re, sp, se);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_seed_merge(const int32_t *keys_packed, const float *rows_p,
+                                const float *rows_e, int64_t n, int32_t dim, int64_t n_nodes,
+                                int32_t *slot, float *seed_p, float *seed_e,
+                                int32_t *keys_sorted, void *workspace, size_t workspace_bytes,
+                                mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(keys_packed && rows_p && rows_e && slot && seed_p && seed_e && keys_sorted &&
+                  workspace && n > 0 && n < INT32_MAX && n_nodes > 0 && n_nodes < INT32_MAX);
+  if (!dim_supported(dim)) return MIREC_ERR_DIM;
+  size_t tb = 0;
+  int rc = sort_temp_bytes(n, n_nodes + 1, &tb);
+  if (rc != MIREC_OK) return rc;
+  const size_t need = align_up(tb) + 2 * align_up((size_t)n * sizeof(int32_t));
+  if (workspace_bytes < need) return MIREC_ERR_WORKSPACE;
+  char *ws = static_cast<char *>(workspace);
+  int32_t *idx_in = reinterpret_cast<int32_t *>(ws + align_up(tb));
+  int32_t *idx_sorted = reinterpret_cast<int32_t *>(ws + align_up(tb) + align_up(n * 4));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, idx_in, n);
+  MIREC_LAUNCH_CHECK();
+  size_t tb2 = tb;
+  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws, tb2, keys_packed, keys_sorted, idx_in,
+                                               idx_sorted, (int)n, 0, end_bit_for(n_nodes + 1),
+                                               st));
+  hipLaunchKernelGGL(merge_heads_kernel, dim3((n + 255) / 256), dim3(256), 0, st, keys_sorted, n,
+                     (int32_t)n_nodes, slot);
+  MIREC_LAUNCH_CHECK();
+  switch (dim) {
+#define C(DD) \
+  case DD:    \
+    return launch_merge_accum<DD>(keys_sorted, idx_sorted, n, rows_p, rows_e, seed_p, seed_e, st);
+    C(4) C(8) C(16) C(32) C(64) C(128) C(256)
+#undef C
+  }
+  return MIREC_ERR_DIM;
 }

@@ -13,6 +13,15 @@
 // registers and are combined with a xor-butterfly at the end: no atomics, no
 // LDS, a fixed summation order per row (deterministic).
 //
+// Masks (uint32 bitmaps over nodes, optional):
+//   row_mask  rows whose bit is 0 are skipped entirely (nothing written);
+//   in_mask   neighbours whose bit is 0 contribute exactly 0 and are not
+//             read: the 64 candidates of a chunk are tested at once and the
+//             valid ones compacted to the front with ds_permute.
+// Frontier pruning uses them to compute only the rows the BPR loss depends
+// on; skipped terms are exact zeros, so results equal the dense pass up to
+// fp32 summation order (the compaction regroups the surviving neighbours).
+//
 // Rows longer than csr->split are cut into segments processed by extra waves
 // of the same launch (partial sums to scratch) and summed in segment order by
 // a finalize launch, so a Zipf-skewed item cannot serialise the grid.
@@ -47,7 +56,13 @@ struct PropK {
   float *v;
   mirec_adam_hparams_t adam;
   float *partial;
+  const uint32_t *row_mask;
+  const uint32_t *in_mask;
 };
+
+__device__ __forceinline__ bool bit_set(const uint32_t *bm, int64_t i) {
+  return (bm[i >> 5] >> (i & 31)) & 1u;
+}
 
 __device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g,
                                           const mirec_adam_hparams_t &h) {
@@ -60,39 +75,45 @@ __device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g,
   p = p + h.neg_step_size * (m / denom);
 }
 
-// Sum of the (pre-scaled / raw / sparse) input rows listed in col[beg, end).
-// Returns the per-lane partial (this lane's group's neighbour subset).
-template <int D, int UNROLL, int MODE>
-__device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg,
-                                              int64_t end, int lane) {
+// Sum of the input rows listed in col[beg, end) (pre-scaled / raw x dinv_j /
+// sparse seeds x dinv_j), restricted to in_mask when MASKED.  Returns this
+// lane's group partial (a disjoint subset of the neighbours).
+template <int D, int UNROLL, int MODE, bool MASKED>
+__device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64_t end,
+                                              int lane) {
   constexpr int LPR = D / 4;
   constexpr int G = 64 / LPR;
   const int grp = lane / LPR;
   const int sub = lane % LPR;
   float4 acc = f4_zero();
   if (MODE == MIREC_IN_NONE) return acc;
+  const float *src = (MODE == MIREC_IN_SPARSE) ? a.seed_in : a.x_in;
   for (int64_t base = beg; base < end; base += 64) {
-    const int cnt = (int)min((int64_t)64, end - base);
-    int myc = 0;
+    int cnt = (int)min((int64_t)64, end - base);
+    int myc = lane < cnt ? a.col[base + lane] : 0;
+    if (MASKED) {
+      const bool ok = lane < cnt && bit_set(a.in_mask, myc);
+      const unsigned long long m = __ballot(ok);
+      const int nv = __popcll(m);
+      if (nv == 0) continue;  // wave-uniform
+      if (nv < cnt) {
+        const int below = __popcll(m & ((1ull << lane) - 1ull));
+        const int dst = ok ? below : nv + (lane - below);
+        myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
+      }
+      cnt = nv;
+    }
     float myw = 1.f;
-    if (lane < cnt) {
-      myc = a.col[base + lane];
-      if (MODE != MIREC_IN_PRESCALED) myw = a.dinv[myc];
+    int myr = myc;
+    if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
+      if (lane < cnt) myw = a.dinv[myc];
     }
     if (MODE == MIREC_IN_SPARSE) {
-      // Input is zero except at the (few) seeded rows: test slot[] for all
-      // 64 neighbours at once and gather only the seeded ones.
-      int mys = -1;
-      if (lane < cnt) mys = a.slot[myc];
-      unsigned long long mask = __ballot(mys >= 0);
-      while (mask) {
-        const int b = __ffsll((long long)mask) - 1;
-        mask &= mask - 1;
-        const int s = __shfl(mys, b);
-        const float w = __shfl(myw, b);
-        if (grp == 0) acc = f4_fma(w, ld4(a.seed_in + (int64_t)s * D + sub * 4), acc);
+      myr = lane < cnt ? a.slot[myc] : 0;
+      if (myr < 0) {  // defensive: a masked-in node without a seed row
+        myr = 0;
+        myw = 0.f;
       }
-      continue;
     }
     for (int k = 0; k < cnt; k += G * UNROLL) {
       float4 v[UNROLL];
@@ -100,16 +121,16 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg,
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
         const int idx = k + u * G + grp;
-        const int j = __shfl(myc, idx & 63);
-        w[u] = (MODE == MIREC_IN_RAW) ? __shfl(myw, idx & 63) : 1.f;
+        const int j = __shfl(myr, idx & 63);
+        w[u] = (MODE != MIREC_IN_PRESCALED) ? __shfl(myw, idx & 63) : 1.f;
         if (idx < cnt)
-          v[u] = ld4(a.x_in + (int64_t)j * D + sub * 4);
+          v[u] = ld4(src + (int64_t)j * D + sub * 4);
         else
           v[u] = f4_zero();
       }
 #pragma unroll
       for (int u = 0; u < UNROLL; ++u) {
-        if (MODE == MIREC_IN_RAW)
+        if (MODE != MIREC_IN_PRESCALED)
           acc = f4_fma(w[u], v[u], acc);
         else
           acc = f4_add(acc, v[u]);
@@ -129,15 +150,14 @@ __device__ __forceinline__ float4 combine_groups(float4 s) {
 }
 
 template <int D>
-__device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4 s,
-                                             int sub) {
+__device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4 s, int sub) {
   const float di = a.dinv[row];
   const int64_t off = row * D + sub * 4;
   float4 z = f4_scale(di, s);
   int sl = -1;
   if (a.slot != nullptr && (a.seed != nullptr || a.seed2 != nullptr)) sl = a.slot[row];
   if (a.seed != nullptr && sl >= 0) z = f4_add(z, ld4(a.seed + (int64_t)sl * D + sub * 4));
-  if (a.xs_out != nullptr) st4(a.xs_out + off, f4_scale(di, z));
+  if (a.xs_out != nullptr && a.param == nullptr) st4(a.xs_out + off, f4_scale(di, z));
   if (a.out == nullptr && a.param == nullptr) return;
   float4 o = z;
   if (a.addend != nullptr) o = f4_add(o, ld4(a.addend + off));
@@ -153,6 +173,8 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
     st4(a.m + off, m);
     st4(a.v + off, v);
     if (a.out != nullptr) st4(a.out + off, o);
+    // with Adam, xs_out receives the pre-scaled UPDATED parameter
+    if (a.xs_out != nullptr) st4(a.xs_out + off, f4_scale(di, p));
   } else {
     st4(a.out + off, o);
   }
@@ -161,25 +183,29 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
 constexpr int kWavesPerBlock = 4;
 
 // Work item w < n_rows: row w (skipped if long); otherwise segment w-n_rows.
-template <int D, int UNROLL, int MODE>
+// MASKED = in_mask filter on neighbours, ROWMASK = row_mask filter on rows
+// (separate instantiations so profiles tell full and pruned launches apart).
+template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
 __global__ __launch_bounds__(256) void prop_kernel(PropK a) {
   constexpr int LPR = D / 4;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR;
   const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
   if (w < a.n_rows) {
+    if (ROWMASK && !bit_set(a.row_mask, w)) return;  // wave-uniform
     const int64_t beg = a.rowptr[w], end = a.rowptr[w + 1];
-    if (a.split > 0 && end - beg > a.split) return;  // wave-uniform
-    float4 s = gather_rows<D, UNROLL, MODE>(a, beg, end, lane);
+    if (a.split > 0 && end - beg > a.split) return;
+    float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, beg, end, lane);
     s = combine_groups<D>(s);
     if (lane < LPR) row_epilogue<D>(a, w, s, sub);
   } else {
     const int64_t sg = w - a.n_rows;
     if (sg >= a.n_seg) return;
     const int64_t row = a.seg_row[sg];
+    if (ROWMASK && !bit_set(a.row_mask, row)) return;
     const int64_t beg = a.seg_beg[sg];
     const int64_t end = min(beg + (int64_t)a.split, a.rowptr[row + 1]);
-    float4 s = gather_rows<D, UNROLL, MODE>(a, beg, end, lane);
+    float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, beg, end, lane);
     s = combine_groups<D>(s);
     if (lane < LPR) st4(a.partial + sg * D + sub * 4, s);
   }
@@ -188,8 +214,7 @@ __global__ __launch_bounds__(256) void prop_kernel(PropK a) {
 // One LPR-lane group per long row: sum its segments in order, then epilogue.
 template <int D>
 __global__ __launch_bounds__(256) void prop_finalize(PropK a, const int32_t *long_rows,
-                                                     const int64_t *long_segptr,
-                                                     int64_t n_long) {
+                                                     const int64_t *long_segptr, int64_t n_long) {
   constexpr int LPR = D / 4;
   constexpr int G = 64 / LPR;
   const int lane = threadIdx.x & 63;
@@ -197,25 +222,40 @@ __global__ __launch_bounds__(256) void prop_finalize(PropK a, const int32_t *lon
   const int64_t li = ((int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * G + lane / LPR;
   if (li >= n_long) return;
   const int64_t row = long_rows[li];
+  if (a.row_mask != nullptr && !bit_set(a.row_mask, row)) return;
   float4 s = f4_zero();
   for (int64_t sg = long_segptr[li]; sg < long_segptr[li + 1]; ++sg)
     s = f4_add(s, ld4(a.partial + sg * D + sub * 4));
   row_epilogue<D>(a, row, s, sub);
 }
 
+template <int D, int UNROLL, int MODE, bool MASKED>
+static void launch_main(dim3 grid, hipStream_t st, const PropK &k) {
+  if (k.row_mask != nullptr)
+    hipLaunchKernelGGL((prop_kernel<D, UNROLL, MODE, MASKED, true>), grid, dim3(256), 0, st, k);
+  else
+    hipLaunchKernelGGL((prop_kernel<D, UNROLL, MODE, MASKED, false>), grid, dim3(256), 0, st, k);
+}
+
 template <int D, int UNROLL>
 static int launch_prop(const mirec_csr_t *c, const PropK &k, int mode, hipStream_t st) {
   const int64_t work = c->n_rows + c->n_seg;
   const int64_t blocks = (work + kWavesPerBlock - 1) / kWavesPerBlock;
+  const bool masked = k.in_mask != nullptr;
   if (blocks > 0) {
-    if (mode == MIREC_IN_PRESCALED)
-      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_PRESCALED>), dim3(blocks), dim3(256), 0, st, k);
+    const dim3 g((unsigned)blocks);
+    if (mode == MIREC_IN_PRESCALED && !masked)
+      launch_main<D, UNROLL, MIREC_IN_PRESCALED, false>(g, st, k);
+    else if (mode == MIREC_IN_PRESCALED)
+      launch_main<D, UNROLL, MIREC_IN_PRESCALED, true>(g, st, k);
+    else if (mode == MIREC_IN_RAW && !masked)
+      launch_main<D, UNROLL, MIREC_IN_RAW, false>(g, st, k);
     else if (mode == MIREC_IN_RAW)
-      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_RAW>), dim3(blocks), dim3(256), 0, st, k);
+      launch_main<D, UNROLL, MIREC_IN_RAW, true>(g, st, k);
     else if (mode == MIREC_IN_SPARSE)
-      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_SPARSE>), dim3(blocks), dim3(256), 0, st, k);
+      launch_main<D, UNROLL, MIREC_IN_SPARSE, true>(g, st, k);
     else
-      hipLaunchKernelGGL((prop_kernel<D, UNROLL, MIREC_IN_NONE>), dim3(blocks), dim3(256), 0, st, k);
+      launch_main<D, UNROLL, MIREC_IN_NONE, false>(g, st, k);
     MIREC_LAUNCH_CHECK();
   }
   if (c->n_long > 0) {
@@ -229,6 +269,15 @@ static int launch_prop(const mirec_csr_t *c, const PropK &k, int mode, hipStream
   return MIREC_OK;
 }
 
+// x~ = dinv ⊙ x (row scale), float4.
+__global__ __launch_bounds__(256) void prescale_kernel(const float *__restrict__ x,
+                                                       const float *__restrict__ dinv, int64_t n4,
+                                                       int32_t d4, float *__restrict__ out) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    st4(out + 4 * i, f4_scale(dinv[i / d4], ld4(x + 4 * i)));
+}
+
 }  // namespace mirec
 
 extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
@@ -240,9 +289,10 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   if (!dim_supported(p->dim)) return MIREC_ERR_DIM;
   MIREC_CHECK_ARG(p->in_mode >= 0 && p->in_mode <= 3);
   if (p->in_mode == MIREC_IN_SPARSE)
-    MIREC_CHECK_ARG(p->slot != nullptr && p->seed_in != nullptr);
+    MIREC_CHECK_ARG(p->slot != nullptr && p->seed_in != nullptr && p->in_mask != nullptr);
   else if (p->in_mode != MIREC_IN_NONE)
     MIREC_CHECK_ARG(p->x_in != nullptr);
+  MIREC_CHECK_ARG(p->in_mode != MIREC_IN_NONE || p->in_mask == nullptr);
   MIREC_CHECK_ARG((p->seed == nullptr && p->seed2 == nullptr) || p->slot != nullptr);
   MIREC_CHECK_ARG(p->param == nullptr || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr));
   MIREC_CHECK_ARG(p->divisor != 0.f);
@@ -273,6 +323,8 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   k.v = p->exp_avg_sq;
   k.adam = p->adam;
   k.partial = p->partial;
+  k.row_mask = p->row_mask;
+  k.in_mask = p->in_mask;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (p->dim) {
     case 4: return launch_prop<4, 1>(c, k, p->in_mode, st);
@@ -284,4 +336,18 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
     case 256: return launch_prop<256, 8>(c, k, p->in_mode, st);
   }
   return MIREC_ERR_DIM;
+}
+
+extern "C" int mirec_prescale(const float *x, const float *dinv, int64_t n_rows, int32_t dim,
+                              float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(x && dinv && out && n_rows >= 0);
+  if (!dim_supported(dim)) return MIREC_ERR_DIM;
+  const int64_t n4 = n_rows * dim / 4;
+  if (n4 == 0) return MIREC_OK;
+  const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(prescale_kernel, dim3(blocks), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, dinv, n4, dim / 4, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
 }

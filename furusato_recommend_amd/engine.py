@@ -1,23 +1,26 @@
 """LightGCN propagation + BPR training engine (device side orchestration).
 
 One training step (the reference's ``stageOne``, model/lgcn.py:127-133, on
-top of ``bpr_loss`` :98-118 and ``forward`` :78-86) runs as 3L/2+4 HIP
+top of ``bpr_loss`` :98-118 and ``forward`` :78-86) runs as ~2L+8 HIP
 launches with no host synchronisation:
 
-  forward  (L launches)   x_l = Â x_{l-1}; acc = x_0 + ... + x_L; out = acc/(L+1)
-                          layer 1 gathers E with per-edge dinv_j (IN_RAW),
-                          layers 2..L gather the pre-scaled x~ = dinv ⊙ x
-                          written by the previous epilogue; the final layer
-                          writes out = acc/(L+1) in place of acc.
+  frontier (1-2)          S = batch nodes, F1 = S ∪ N(S) as bitmaps
+  forward  (1 + L)        x~_0 = dinv ⊙ E, then x_l = Â x_{l-1};
+                          acc = x_0 + ... + x_L; out = acc/(L+1).  Every
+                          layer gathers pre-scaled rows x~ = dinv ⊙ x written
+                          by the previous epilogue; layer L runs on S only,
+                          layer L-1 on F1 only (pruning).
   BPR      (3 + sort)     scores, softplus, loss; sorted (node, occurrence)
                           pairs → per-node gradient seeds d = dL/d out /(L+1)
                           and the reg-gradient seed.
   backward (L launches)   Horner: g_L = d, g_l = d + Â g_{l+1} (Â symmetric:
                           the backward SpMM is the forward kernel on the
-                          same CSR).  The first backward layer gathers the
-                          sparse seeds (IN_SPARSE); the last one adds the reg
-                          seed and applies Adam to E in its epilogue, so the
-                          dense gradient is never written to HBM.
+                          same CSR).  The first backward layer gathers only
+                          the seeded neighbours (IN_SPARSE, S bitmap) and is
+                          written on F1 only; the second skips neighbours
+                          outside F1; the last one adds the reg seed and
+                          applies Adam to E in its epilogue, so the dense
+                          gradient is never written to HBM.
   reset    (1)            slot[] back to -1 for the touched nodes.
 
 For data parallelism (dist.py) the last layer writes the dense gradient
@@ -115,9 +118,17 @@ class AdamState:
 
 
 class PropagationEngine:
-    """Owns the per-model scratch buffers and issues the HIP launches."""
+    """Owns the per-model scratch buffers and issues the HIP launches.
 
-    def __init__(self, graph: Graph, dim: int, n_layers: int, max_batch: int):
+    ``prune`` (default on) enables frontier pruning: with S the batch's
+    nodes and F1 = S ∪ N(S) (mirec_frontier), forward layer L is computed on
+    S only and layer L-1 on F1 only (the loss reads the layer mean only on
+    S), and the first two backward layers skip the rows / neighbours that
+    are exactly zero.  Loss, gradient and update are the dense pass's up to
+    fp32 summation order; ``prune=False`` runs every layer on every row."""
+
+    def __init__(self, graph: Graph, dim: int, n_layers: int, max_batch: int,
+                 prune: bool = True):
         if dim not in _lib.SUPPORTED_DIMS:
             raise ValueError(f"recdim={dim} not supported by the HIP engine "
                              f"(supported: {_lib.SUPPORTED_DIMS})")
@@ -127,14 +138,20 @@ class PropagationEngine:
         self.dim = int(dim)
         self.L = int(n_layers)
         self.max_batch = int(max_batch)
+        self.prune = bool(prune)
         dev = graph.device
         N, D = graph.n_nodes, self.dim
         f32 = dict(dtype=torch.float32, device=dev)
         i32 = dict(dtype=torch.int32, device=dev)
         self.acc = torch.empty(N, D, **f32)       # layer sum, then out = acc/(L+1)
+        self.x0s = torch.empty(N, D, **f32) if self.L > 0 else None  # dinv ⊙ E
         self.xs = [torch.empty(N, D, **f32), torch.empty(N, D, **f32)] if self.L > 1 else \
             [torch.empty(N, D, **f32)] if self.L == 1 else []
         self.slot = torch.full((N,), -1, **i32)
+        words = (N + 31) // 32
+        self.bm_self = torch.zeros(words, **i32)  # S  (uint32 bitmap)
+        self.bm_hop = torch.zeros(words, **i32)   # S ∪ N(S)
+        self._masks_ready = False
         B3 = 3 * self.max_batch
         self.seed_p = torch.empty(B3, D, **f32)
         self.seed_e = torch.empty(B3, D, **f32)
@@ -149,8 +166,11 @@ class PropagationEngine:
         self._ws = None
         self._ws_bytes = 0
         self._ensure_ws(self.max_batch)
-        # Optional per-launch timing of the propagation kernel (bench.py).
+        # Optional per-launch timing of the propagation kernel (bench.py):
+        # list of (start, end, (in_mode, in_masked, row_masked), bytes).
         self.prop_events = None
+        self._seeds = None
+        self._merged = None
 
     # ------------------------------------------------------------ internals
     def _ensure_ws(self, batch: int):
@@ -162,7 +182,8 @@ class PropagationEngine:
             self._ws_bytes = nb.value
 
     def _prop(self, *, in_mode, x_in=None, seed_in=None, seed=None, addend=None, seed2=None,
-              divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None):
+              divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None,
+              row_mask=None, in_mask=None):
         g = graph or self.g
         p = Prop()
         p.dim = self.dim
@@ -185,6 +206,8 @@ class PropagationEngine:
             p.adam = hp
         part = g.partial_buffer(self.dim)
         p.partial = ptr(part)
+        p.row_mask = ptr(row_mask)
+        p.in_mask = ptr(in_mask)
         ev = self.prop_events
         if ev is not None:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -193,7 +216,8 @@ class PropagationEngine:
               "propagate")
         if ev is not None:
             e.record()
-            ev.append((s, e, in_mode, self.launch_bytes(p, g)))
+            kind = (in_mode, in_mask is not None, row_mask is not None)
+            ev.append((s, e, kind, self.launch_bytes(p, g)))
 
     def launch_bytes(self, p: Prop, g: Graph) -> int:
         return prop_launch_bytes(p.in_mode, g.n_nodes, g.nnz, self.dim,
@@ -201,23 +225,50 @@ class PropagationEngine:
                                  xs_out=bool(p.xs_out), addend=bool(p.addend),
                                  out=bool(p.out), adam=bool(p.param))
 
+    def compute_frontier(self, users=None, pos=None, neg=None, keys=None, n_keys: int = 0):
+        """bm_self = S, bm_hop = S ∪ N(S) for a triple batch or a key list."""
+        g = self.g
+        if keys is not None:
+            check(lib.mirec_frontier(g.csr_ptr(), keys.data_ptr(), int(n_keys), None, None, None,
+                                     0, g.n_users, self.bm_self.data_ptr(),
+                                     self.bm_hop.data_ptr(), _lib.stream_handle()), "frontier")
+        else:
+            check(lib.mirec_frontier(g.csr_ptr(), None, 0, users.data_ptr(), pos.data_ptr(),
+                                     neg.data_ptr(), int(users.shape[0]), g.n_users,
+                                     self.bm_self.data_ptr(), self.bm_hop.data_ptr(),
+                                     _lib.stream_handle()), "frontier")
+        self._masks_ready = True
+
+    def prescale(self, x: torch.Tensor, out: torch.Tensor):
+        check(lib.mirec_prescale(x.data_ptr(), self.g.dinv.data_ptr(), self.g.n_nodes, self.dim,
+                                 out.data_ptr(), _lib.stream_handle()), "prescale")
+
     # ------------------------------------------------------------- forward
-    def forward(self, emb: torch.Tensor) -> torch.Tensor:
+    def forward(self, emb: torch.Tensor, pruned: bool = False) -> torch.Tensor:
         """out = (x_0 + ... + x_L)/(L+1), x_l = Â x_{l-1} (model/lgcn.py:78-86).
 
-        Returns the engine's ``acc`` buffer (valid until the next call)."""
+        ``pruned`` (after compute_frontier): rows outside the frontier are not
+        computed (valid only on S).  Returns the engine's ``acc`` buffer
+        (valid until the next call)."""
         L = self.L
         if L == 0:
             self.acc.copy_(emb)
             return self.acc
+        if pruned and not self._masks_ready:
+            raise RuntimeError("forward(pruned=True) needs compute_frontier() first")
+        self.prescale(emb, self.x0s)
         for l in range(1, L + 1):
             last = l == L
-            self._prop(in_mode=IN_RAW if l == 1 else IN_PRESCALED,
-                       x_in=emb if l == 1 else self.xs[(l - 2) % 2],
+            rm = None
+            if pruned:
+                rm = self.bm_self if l == L else (self.bm_hop if l == L - 1 else None)
+            self._prop(in_mode=IN_PRESCALED,
+                       x_in=self.x0s if l == 1 else self.xs[(l - 2) % 2],
                        addend=emb if l == 1 else self.acc,
                        divisor=float(L + 1) if last else 1.0,
                        out=self.acc,
-                       xs_out=None if last else self.xs[(l - 1) % 2])
+                       xs_out=None if last else self.xs[(l - 1) % 2],
+                       row_mask=rm)
         return self.acc
 
     def propagate_once(self, x: torch.Tensor, out: torch.Tensor, graph: Graph | None = None):
@@ -235,10 +286,13 @@ class PropagationEngine:
         """Loss + gradient seeds for one batch of int32 device triples.
 
         ``grad_scale`` multiplies the gradient seeds (1/world_size under data
-        parallelism, so a SUM all-reduce yields the union-batch gradient)."""
+        parallelism, so the exchanged seeds / gradients sum to the union
+        batch's)."""
         B = int(users.shape[0])
         if B > self.max_batch:
             raise ValueError(f"batch {B} > engine max_batch {self.max_batch}")
+        if not self._masks_ready:
+            self.compute_frontier(users, pos, neg)  # the seed set S for the backward
         self._ensure_ws(B)
         st = _lib.stream_handle()
         g = self.g
@@ -258,42 +312,89 @@ class PropagationEngine:
                                  self.slot.data_ptr(), self.seed_p.data_ptr(),
                                  self.seed_e.data_ptr(), self.keys_sorted.data_ptr(),
                                  self._ws.data_ptr(), self._ws_bytes, st), "bpr_seed")
-        self._last_batch = B
+        self._seeds = (self.seed_p, self.seed_e, self.keys_sorted, 3 * B)
         return self.loss
+
+    # ----------------------------------------------- data-parallel exchange
+    def export_seeds(self):
+        """Local seeds as fixed-size rows for an all-gather: (keys [3B] int32,
+        seed_p [3B, D], seed_e [3B, D]); non-head rows carry key = n_nodes.
+        Clears the local slot map (the merged seeds replace it)."""
+        seed_p, seed_e, ks, n = self._seeds
+        st = _lib.stream_handle()
+        packed = self.keys[:n]  # bpr_forward's keys are no longer needed
+        check(lib.mirec_seed_pack(ks.data_ptr(), n, self.g.n_nodes, packed.data_ptr(), st),
+              "seed_pack")
+        check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), ks.data_ptr(), n, st),
+              "bpr_seed_reset")
+        self._masks_ready = False
+        return packed, seed_p[:n], seed_e[:n]
+
+    def import_seeds(self, keys, rows_p, rows_e):
+        """Merge gathered seeds (rank-major order) into this engine's slot map
+        and rebuild the frontier of the union seed set."""
+        n = int(keys.shape[0])
+        if self._merged is None or self._merged[0].shape[0] < n:
+            dev, D = self.g.device, self.dim
+            self._merged = (torch.empty(n, D, dtype=torch.float32, device=dev),
+                            torch.empty(n, D, dtype=torch.float32, device=dev),
+                            torch.empty(n, dtype=torch.int32, device=dev))
+        mp, me, mk = self._merged
+        nb = ctypes.c_size_t(0)
+        check(lib.mirec_seed_merge_workspace(n, self.g.n_nodes, ctypes.byref(nb)),
+              "seed_merge_workspace")
+        if nb.value > self._ws_bytes:
+            self._ws = torch.empty(nb.value, dtype=torch.uint8, device=self.g.device)
+            self._ws_bytes = nb.value
+        check(lib.mirec_seed_merge(keys.data_ptr(), rows_p.data_ptr(), rows_e.data_ptr(), n,
+                                   self.dim, self.g.n_nodes, self.slot.data_ptr(), mp.data_ptr(),
+                                   me.data_ptr(), mk.data_ptr(), self._ws.data_ptr(),
+                                   self._ws_bytes, _lib.stream_handle()), "seed_merge")
+        self.compute_frontier(keys=mk, n_keys=n)
+        self._seeds = (mp, me, mk, n)
 
     # ------------------------------------------------------------- backward
     def backward(self, emb: torch.Tensor, adam: AdamState | None = None,
                  grad_out: torch.Tensor | None = None):
-        """Horner backward from the seeds of the last ``bpr`` call.
+        """Horner backward from the current seeds (g_L = d, g_l = d + Â g_{l+1}).
 
         With ``adam`` the last layer applies Adam to ``emb`` in place (fused);
         otherwise the dense gradient dLoss/dE is written to ``grad_out``."""
         if (adam is None) == (grad_out is None):
             raise ValueError("exactly one of adam / grad_out")
+        if self._seeds is None or not self._masks_ready:
+            raise RuntimeError("backward() needs bpr() (or import_seeds()) first")
         L = self.L
+        seed_p, seed_e, keys_sorted, n_keys = self._seeds
         hp = adam.next_hparams() if adam is not None else None
-        final = dict(seed2=self.seed_e)
+        final = dict(seed2=seed_e)
         if adam is not None:
             final.update(adam=(adam, hp), param=emb)
         else:
             final.update(out=grad_out)
         if L == 0:
-            self._prop(in_mode=IN_NONE, seed=self.seed_p, **final)
+            self._prop(in_mode=IN_NONE, seed=seed_p, **final)
         else:
             for l in range(L - 1, -1, -1):
                 first = l == L - 1
-                kw = dict(in_mode=IN_SPARSE if first else IN_PRESCALED,
-                          seed_in=self.seed_p if first else None,
-                          x_in=None if first else self.xs[(L - 2 - l) % 2],
-                          seed=self.seed_p)
+                if first:
+                    # input g_L = d lives on S only; with pruning its output
+                    # g_{L-1} is written only on F1 = S ∪ N(S) (zero elsewhere)
+                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p, in_mask=self.bm_self,
+                              row_mask=self.bm_hop if (self.prune and l > 0) else None)
+                else:
+                    kw = dict(in_mode=IN_PRESCALED, x_in=self.xs[(L - 2 - l) % 2],
+                              in_mask=self.bm_hop if (self.prune and l == L - 2) else None)
+                kw["seed"] = seed_p
                 if l == 0:
                     kw.update(final)
                 else:
                     kw.update(xs_out=self.xs[(L - 1 - l) % 2])
                 self._prop(**kw)
-        check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), self.keys_sorted.data_ptr(),
-                                       3 * self._last_batch, _lib.stream_handle()),
-              "bpr_seed_reset")
+        check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), keys_sorted.data_ptr(), n_keys,
+                                       _lib.stream_handle()), "bpr_seed_reset")
+        self._seeds = None
+        self._masks_ready = False
 
     def adam_step(self, param: torch.Tensor, grad: torch.Tensor, adam: AdamState):
         hp = adam.next_hparams()
@@ -302,10 +403,15 @@ class PropagationEngine:
                                    _lib.stream_handle()), "adam_dense")
 
     # --------------------------------------------------------------- step
+    def forward_for_batch(self, emb: torch.Tensor, users, pos, neg) -> torch.Tensor:
+        """Frontier of the batch, then the (pruned if enabled) forward."""
+        self.compute_frontier(users, pos, neg)
+        return self.forward(emb, pruned=self.prune)
+
     def train_step(self, emb: torch.Tensor, adam: AdamState, users, pos, neg, decay: float,
                    loss_accum: torch.Tensor | None = None) -> torch.Tensor:
         """stageOne: forward, BPR, backward, fused Adam.  Returns loss (device)."""
-        out = self.forward(emb)
+        out = self.forward_for_batch(emb, users, pos, neg)
         loss = self.bpr(out, emb, users, pos, neg, decay, loss_accum)
         self.backward(emb, adam=adam)
         return loss

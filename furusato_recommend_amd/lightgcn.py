@@ -73,7 +73,8 @@ class LightGCN(nn.Module):
         self.__init_weight()
         self.optim = AdamState(self.all_embedding.weight, lr=config["lr"])
         self.engine = PropagationEngine(self.graph, self.latent_dim, self.num_layers,
-                                        int(config.get("bpr_batch_size", 2048)))
+                                        int(config.get("bpr_batch_size", 2048)),
+                                        prune=bool(config.get("prune", True)))
         self._loss_accum = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.test_item_emb = None
 

@@ -130,7 +130,8 @@ typedef struct mirec_adam_hparams {
  *   xs_out_i = dinv_i * z_i                  (if xs_out != NULL; next layer)
  *   o_i   = (z_i + addend_i) / divisor + seed2[slot_i]
  *   out_i = o_i                              (if out != NULL)
- *   Adam(param_i, exp_avg_i, exp_avg_sq_i; grad = o_i)   (if param != NULL)
+ *   Adam(param_i, exp_avg_i, exp_avg_sq_i; grad = o_i)   (if param != NULL;
+ *       then xs_out_i = dinv_i * param_i after the update)
  * `partial` is scratch of csr->n_seg * dim floats (may be NULL if n_seg==0).
  * Summation order per row is fixed by the CSR: results are deterministic. */
 typedef struct mirec_prop {
@@ -151,10 +152,28 @@ typedef struct mirec_prop {
   float *exp_avg_sq;
   mirec_adam_hparams_t adam;
   float *partial;       /* [n_seg, dim] scratch */
+  const uint32_t *row_mask; /* [ceil(n_rows/32)] bitmap: rows with bit 0 are
+                               skipped (nothing written); NULL = all rows */
+  const uint32_t *in_mask;  /* bitmap over source nodes: only neighbours with
+                               bit 1 contribute (others are exact zeros);
+                               required for MIREC_IN_SPARSE; NULL = all */
 } mirec_prop_t;
 
 int mirec_propagate(const mirec_csr_t *csr, const mirec_prop_t *p,
                     mirec_stream_t stream);
+
+/* out = dinv ⊙ x row-wise (the pre-scaled layer-0 input x~_0). */
+int mirec_prescale(const float *x, const float *dinv, int64_t n_rows,
+                   int32_t dim, float *out, mirec_stream_t stream);
+
+/* Frontier bitmaps of a key set S (keys[n_keys], entries outside [0, n_rows)
+ * ignored; or, if keys == NULL, the 3*batch nodes of the triples users[b],
+ * n_users+pos[b], n_users+neg[b]):  bm_self = S, bm_hop = S ∪ N(S).  Both
+ * bitmaps are [ceil(n_rows/32)] uint32 and are cleared first. */
+int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
+                   const int32_t *users, const int32_t *pos, const int32_t *neg,
+                   int64_t batch, int64_t n_users, uint32_t *bm_self,
+                   uint32_t *bm_hop, mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */
@@ -201,9 +220,30 @@ int mirec_bpr_seed(const float *out, const float *emb, int64_t n_nodes,
                    float *seed_e, int32_t *keys_sorted, void *workspace,
                    size_t workspace_bytes, mirec_stream_t stream);
 
-/* slot[keys_sorted[q]] = -1 for q in [0, n). */
+/* slot[keys_sorted[q]] = -1 for q in [0, n) (negative keys are skipped). */
 int mirec_bpr_seed_reset(int32_t *slot, const int32_t *keys_sorted, int64_t n,
                          mirec_stream_t stream);
+
+/* Data-parallel sparse gradient exchange (dist.py).  The backward pass is
+ * linear in the seeds, so the union batch's gradient is the backward of the
+ * SUM of every rank's seeds: ranks all-gather their (node, seed_p, seed_e)
+ * rows (3B each) instead of all-reducing the dense [N, D] gradient.
+ * pack: keys_packed[q] = keys_sorted[q] at head positions, n_nodes elsewhere. */
+int mirec_seed_pack(const int32_t *keys_sorted, int64_t n, int64_t n_nodes,
+                    int32_t *keys_packed, mirec_stream_t stream);
+
+int mirec_seed_merge_workspace(int64_t n, int64_t n_nodes, size_t *bytes);
+
+/* merge: n gathered (key, row_p, row_e) entries (key == n_nodes: empty) →
+ * per distinct node the sum of its rows in gathered order (deterministic,
+ * identical on every rank), written at the node's first sorted position q;
+ * slot[node] = q (slot must be all -1 on entry); keys_sorted[n] keeps the
+ * sorted keys (-1 for empty entries) for mirec_bpr_seed_reset. */
+int mirec_seed_merge(const int32_t *keys_packed, const float *rows_p,
+                     const float *rows_e, int64_t n, int32_t dim,
+                     int64_t n_nodes, int32_t *slot, float *seed_p,
+                     float *seed_e, int32_t *keys_sorted, void *workspace,
+                     size_t workspace_bytes, mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Adam (torch.optim.Adam, amsgrad=False, weight_decay=0)                   */

@@ -34,11 +34,12 @@ class DS:
         self.testDict = {}
 
 
-def lgcn_from(f, split=None, batch=64):
+def lgcn_from(f, split=None, batch=64, prune=True):
     from furusato_recommend_amd import LightGCN
     ds = DS(f["train_user"], f["train_item"], f["n_users"], f["m_items"])
     cfg = {"recdim": int(f["dim"]), "layer": int(f["n_layers"]), "lr": float(f["lr"]),
-           "decay": float(f["decay"]), "device": "cuda:0", "bpr_batch_size": batch}
+           "decay": float(f["decay"]), "device": "cuda:0", "bpr_batch_size": batch,
+           "prune": prune}
     if split is not None:
         cfg["csr_split"] = split
     m = LightGCN(cfg, ds)
@@ -64,11 +65,12 @@ def test_forward(golden, name, split):
     assert rel(y, f["layers"][1]) < TOL
 
 
+@pytest.mark.parametrize("prune", [True, False])
 @pytest.mark.parametrize("split", [None, 4])
 @pytest.mark.parametrize("name", LGCN)
-def test_train_steps(golden, name, split):
+def test_train_steps(golden, name, split, prune):
     f = golden(name)
-    m = lgcn_from(f, split)
+    m = lgcn_from(f, split, prune=prune)
     t = torch.from_numpy(f["triples"])
     l1 = float(m.stageOne(t[:, 0], t[:, 1], t[:, 2]))
     assert rel(m.all_embedding.weight, f["emb_step1"]) < TOL
@@ -228,3 +230,81 @@ def test_zipf_long_rows_match_unsplit():
         e = PropagationEngine(g, 64, 3, 64)
         outs.append(e.forward(x).clone())
     assert rel(outs[0], outs[1]) < 1e-5
+
+
+def test_seed_exchange_two_ranks_in_one_process(golden):
+    """The DP sparse exchange (pack -> concatenate as an all-gather would ->
+    merge) for 2 simulated ranks == the reference gradient of the union."""
+    f = golden("lgcn_d64_L3.npz")
+    m = lgcn_from(f)
+    t = torch.from_numpy(f["triples"]).cuda().int()
+    eng, w = m.engine, m.all_embedding.weight
+    out = eng.forward(w)
+    parts = []
+    for half in (t[:32], t[32:]):
+        eng.bpr(out, w, half[:, 0].contiguous(), half[:, 1].contiguous(),
+                half[:, 2].contiguous(), float(f["decay"]), grad_scale=0.5)
+        parts.append([x.clone() for x in eng.export_seeds()])
+    assert int((eng.slot != -1).sum()) == 0
+    eng.import_seeds(*(torch.cat([parts[0][i], parts[1][i]]) for i in range(3)))
+    g = torch.empty_like(w)
+    eng.backward(w, grad_out=g)
+    assert rel(g, f["grad"]) < TOL
+    assert int((eng.slot != -1).sum()) == 0
+
+
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_data_parallel_rccl_world1(golden, mode):
+    """dist.DataParallel through real RCCL collectives (world_size 1) ==
+    the reference's stageOne."""
+    import socket
+
+    import torch.distributed as dist
+
+    from furusato_recommend_amd.dist import DataParallel
+    f = golden("lgcn_d64_L3.npz")
+    m = lgcn_from(f)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        dp = DataParallel(m.engine, m.all_embedding.weight.data, m.optim, mode=mode)
+        t = torch.from_numpy(f["triples"]).cuda().int()
+        for k in (1, 2):
+            dp.step(t[:, 0].contiguous(), t[:, 1].contiguous(), t[:, 2].contiguous(),
+                    float(f["decay"]))
+            assert rel(m.all_embedding.weight, f[f"emb_step{k}"]) < TOL
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pruned_step_equals_dense_step_full_size():
+    """C2 size: the frontier-pruned training step (only the rows the loss
+    depends on) updates E exactly like the full-graph step (fp32 summation
+    order aside), for several steps with different batches."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.engine import AdamState, PropagationEngine, sample_triples
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(1_000_000, 100_000, 20_000_000, seed=0, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    torch.manual_seed(0)
+    e0 = torch.randn(g.n_nodes, 64, device="cuda") * 0.1
+    res = []
+    for prune in (True, False):
+        eng = PropagationEngine(g, 64, 3, 2048, prune=prune)
+        e = e0.clone()
+        adam = AdamState(e, 1e-3)
+        u = torch.empty(2048, dtype=torch.int32, device="cuda")
+        p, n = torch.empty_like(u), torch.empty_like(u)
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        losses = []
+        for step in range(3):
+            sample_triples(g, 2048, 7, step * 2048, u, p, n, err)
+            losses.append(float(eng.train_step(e, adam, u, p, n, 1e-4)))
+        res.append((e, losses))
+    assert rel(res[0][0], res[1][0]) < 1e-5
+    assert np.allclose(res[0][1], res[1][1], rtol=1e-5)
+    assert not torch.equal(res[0][0], e0)

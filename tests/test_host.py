@@ -71,22 +71,67 @@ def test_algorithmic_bytes_c2():
 
 # ------------------------------------------------------- data parallel (gloo)
 class OracleEngine:
-    """CPU stand-in with the PropagationEngine interface used by dist.py."""
+    """CPU stand-in with the PropagationEngine interface used by dist.py:
+    dense mode via autograd; sparse mode via explicit seeds dL/d out (and
+    the reg-gradient rows) + the linear backward sum_l Â^l d."""
 
-    def __init__(self, o: O.OracleLightGCN):
+    def __init__(self, o: O.OracleLightGCN, batch: int):
         self.o = o
+        self.B3 = 3 * batch
 
     def forward(self, emb):
+        return None
+
+    def forward_for_batch(self, emb, users, pos, neg):
         return None
 
     def bpr(self, out, emb, users, pos, neg, decay, loss_accum=None, grad_scale=1.0):
         self._batch = (users, pos, neg)
         self._scale = grad_scale
-        return torch.zeros(1)
+        o = self.o
+        N = o.emb.shape[0]
+        e = o.emb.detach().clone().requires_grad_(True)
+        out = O.forward(e, o.ei, o.n_users, o.L, o.div)
+        out = torch.cat(out).detach().requires_grad_(True)
+        u, p, n = (torch.as_tensor(x).long() for x in (users, pos, neg))
+        us, ps, ns = out[u], out[p + o.n_users], out[n + o.n_users]
+        loss = torch.mean(torch.nn.functional.softplus((us * ns).sum(1) - (us * ps).sum(1)))
+        reg = 0.5 * (e[u].norm(2).pow(2) + e[p + o.n_users].norm(2).pow(2)
+                     + e[n + o.n_users].norm(2).pow(2)) / float(len(u))
+        (loss + decay * reg).backward()
+        self._d = out.grad * grad_scale / (o.L + 1)
+        self._e = e.grad * grad_scale
+        self._N = N
+        return loss.detach()
+
+    def export_seeds(self):
+        rows = torch.nonzero((self._d != 0).any(1) | (self._e != 0).any(1)).flatten()
+        assert len(rows) <= self.B3
+        keys = torch.full((self.B3,), self._N, dtype=torch.int32)
+        rp = torch.zeros(self.B3, self._d.shape[1])
+        re = torch.zeros_like(rp)
+        keys[:len(rows)] = rows.int()
+        rp[:len(rows)] = self._d[rows]
+        re[:len(rows)] = self._e[rows]
+        return keys, rp, re
+
+    def import_seeds(self, keys, rows_p, rows_e):
+        d = torch.zeros(self._N, rows_p.shape[1])
+        e = torch.zeros_like(d)
+        ok = keys < self._N
+        d.index_add_(0, keys[ok].long(), rows_p[ok])
+        e.index_add_(0, keys[ok].long(), rows_e[ok])
+        self._d, self._e = d, e
 
     def backward(self, emb, adam=None, grad_out=None):
-        g = self.o.grad(*self._batch)
-        grad_out.copy_(g * self._scale)
+        if grad_out is not None:
+            grad_out.copy_(self.o.grad(*self._batch) * self._scale)
+            return
+        g, x = self._d.clone(), self._d
+        for _ in range(self.o.L):
+            x = O.lgconv(x, self.o.ei, self.o.div)
+            g = g + x
+        self.adam_step(emb, g + self._e, adam)
 
     def adam_step(self, param, grad, adam):
         self.o.emb.grad = grad.clone()
@@ -102,7 +147,7 @@ def _free_port():
     return port
 
 
-def _dp_worker(rank, world, port, fpath, q):
+def _dp_worker(rank, world, port, fpath, q, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from furusato_recommend_amd.dist import DataParallel
@@ -110,9 +155,10 @@ def _dp_worker(rank, world, port, fpath, q):
     o = O.OracleLightGCN(f["train_user"], f["train_item"], int(f["n_users"]), int(f["m_items"]),
                          64, 3, float(f["lr"]), float(f["decay"]),
                          emb=torch.from_numpy(f["emb0"]) + (0.5 if rank else 0.0))
-    dp = DataParallel(OracleEngine(o), o.emb.data, None)  # broadcast fixes rank 1's init
     t = f["triples"]
     half = len(t) // world
+    # the broadcast in DataParallel fixes rank 1's perturbed init
+    dp = DataParallel(OracleEngine(o, half), o.emb.data, None, mode=mode)
     for step in range(2):
         mine = t[rank * half:(rank + 1) * half]
         dp.step(mine[:, 0], mine[:, 1], mine[:, 2], float(f["decay"]))
@@ -120,15 +166,17 @@ def _dp_worker(rank, world, port, fpath, q):
     dist.destroy_process_group()
 
 
-def test_data_parallel_equals_union_batch(golden):
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_data_parallel_equals_union_batch(golden, mode):
     """2 ranks on disjoint halves == one process on the union batch (the
-    reference's own stageOne on all 64 triples = emb_step1/2)."""
+    reference's own stageOne on all 64 triples = emb_step1/2), for both the
+    sparse-seed all-gather and the dense-gradient all-reduce exchange."""
     from tests.conftest import GOLDEN
     fpath = os.path.join(GOLDEN, "lgcn_d64_L3.npz")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, fpath, q)) for r in range(2)]
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, fpath, q, mode)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=120) for _ in range(2))

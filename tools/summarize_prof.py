@@ -48,7 +48,8 @@ for k, d in per.items():
     kern[k] = {"dispatches": len(d["FETCH_SIZE"]), "FETCH_SIZE_KiB": fs, "WRITE_SIZE_KiB": ws,
                "read_bytes": 2 * fs * 1024, "write_bytes": ws * 1024,
                "hbm_bytes_per_launch": 2 * fs * 1024 + ws * 1024}
-dom = "void mirec::prop_kernel<64, 4, 0>(mirec::PropK)"
+dom = sys.argv[4] if len(sys.argv) > 4 else \
+    "void mirec::prop_kernel<64, 4, 0, false, false>(mirec::PropK)"
 out = {"workload": workload, "tag": tag, "kernel": dom,
        "hbm_bytes_per_launch": kern.get(dom, {}).get("hbm_bytes_per_launch"),
        "correction": "read = 2*FETCH_SIZE*1024 (gfx950 wide-read undercount), write = WRITE_SIZE*1024",
