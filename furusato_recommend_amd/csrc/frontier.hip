@@ -17,8 +17,9 @@ namespace mirec {
 
 constexpr int kWaves = 4;
 
-__device__ __forceinline__ void set_bit(uint32_t *bm, int64_t i) {
-  atomicOr(bm + (i >> 5), 1u << (i & 31));
+__device__ __forceinline__ bool set_bit(uint32_t *bm, int64_t i) {
+  const uint32_t b = 1u << (i & 31);
+  return (atomicOr(bm + (i >> 5), b) & b) == 0u;  // true if this call set it
 }
 
 __global__ __launch_bounds__(256) void frontier_keys_kernel(
@@ -26,7 +27,7 @@ __global__ __launch_bounds__(256) void frontier_keys_kernel(
     int32_t split, const int32_t *__restrict__ keys, int64_t n_keys,
     const int32_t *__restrict__ users, const int32_t *__restrict__ pos,
     const int32_t *__restrict__ neg, int64_t batch, int64_t n_users, uint32_t *bm_self,
-    uint32_t *bm_hop) {
+    uint32_t *bm_hop, int32_t *self_list, int32_t *self_count) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   int64_t node;
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(256) void frontier_keys_kernel(
   }
   if (node < 0 || node >= n_rows) return;  // empty / sentinel entries
   if (lane == 0) {
-    set_bit(bm_self, node);
+    if (set_bit(bm_self, node) && self_list != nullptr)
+      self_list[atomicAdd(self_count, 1)] = (int32_t)node;
     set_bit(bm_hop, node);
   }
   const int64_t beg = rowptr[node], end = rowptr[node + 1];
@@ -67,7 +69,8 @@ __global__ __launch_bounds__(256) void frontier_segments_kernel(
 extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t n_keys,
                               const int32_t *users, const int32_t *pos, const int32_t *neg,
                               int64_t batch, int64_t n_users, uint32_t *bm_self,
-                              uint32_t *bm_hop, mirec_stream_t stream) {
+                              uint32_t *bm_hop, int32_t *self_list, int32_t *self_count,
+                              mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(c && c->rowptr && c->col && bm_self && bm_hop);
   MIREC_CHECK_ARG(keys != nullptr || (users && pos && neg && batch >= 0 && n_users >= 0));
@@ -75,11 +78,13 @@ extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t
   const size_t words = (size_t)((c->n_rows + 31) / 32);
   MIREC_HIP(hipMemsetAsync(bm_self, 0, words * 4, st));
   MIREC_HIP(hipMemsetAsync(bm_hop, 0, words * 4, st));
+  MIREC_CHECK_ARG(self_list == nullptr || self_count != nullptr);
+  if (self_count != nullptr) MIREC_HIP(hipMemsetAsync(self_count, 0, 4, st));
   const int64_t n = keys != nullptr ? n_keys : 3 * batch;
   if (n > 0) {
     hipLaunchKernelGGL(frontier_keys_kernel, dim3((n + kWaves - 1) / kWaves), dim3(256), 0, st,
                        c->rowptr, c->col, c->n_rows, c->n_seg > 0 ? c->split : 0, keys, n_keys,
-                       users, pos, neg, batch, n_users, bm_self, bm_hop);
+                       users, pos, neg, batch, n_users, bm_self, bm_hop, self_list, self_count);
     MIREC_LAUNCH_CHECK();
   }
   if (c->n_seg > 0 && n > 0) {

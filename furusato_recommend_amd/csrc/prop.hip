@@ -58,6 +58,10 @@ struct PropK {
   float *partial;
   const uint32_t *row_mask;
   const uint32_t *in_mask;
+  const int32_t *row_list;   // rows to process (deduplicated), or NULL = all rows
+  const int32_t *row_count;  // device count of row_list entries
+  int64_t row_waves;         // waves of the row phase (host upper bound)
+  int32_t narrow_max;        // rows up to this degree are gathered group-per-row
 };
 
 __device__ __forceinline__ bool bit_set(const uint32_t *bm, int64_t i) {
@@ -140,6 +144,77 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64
   return acc;
 }
 
+// Group-per-row gather (short rows): each LPR-lane group owns one row and
+// walks its neighbours LPR at a time (one coalesced col load per chunk),
+// UNROLL float4 row loads in flight per lane.  G rows progress per wave, so
+// latency-bound short rows get G x the memory-level parallelism of the
+// wave-per-row path.  Control flow is group-uniform; shuffles stay inside
+// the group.
+template <int D, int UNROLL, int MODE, bool MASKED>
+__device__ __forceinline__ float4 gather_narrow(const PropK &a, int64_t beg, int64_t end,
+                                                int lane) {
+  constexpr int LPR = D / 4;
+  const int grp = lane / LPR;
+  const int sub = lane % LPR;
+  const int gbase = grp * LPR;
+  float4 acc = f4_zero();
+  if (MODE == MIREC_IN_NONE) return acc;
+  const float *src = (MODE == MIREC_IN_SPARSE) ? a.seed_in : a.x_in;
+  for (int64_t c = beg; c < end; c += LPR) {
+    int cnt = (int)min((int64_t)LPR, end - c);
+    int myc = sub < cnt ? a.col[c + sub] : 0;
+    if (MASKED) {
+      const bool ok = sub < cnt && bit_set(a.in_mask, myc);
+      const unsigned long long bal = __ballot(ok);
+      const unsigned long long gm =
+          (LPR == 64) ? bal : ((bal >> gbase) & ((1ull << LPR) - 1ull));
+      const int nv = __popcll(gm);
+      if (nv == 0) continue;  // group-uniform
+      if (nv < cnt) {
+        const int below = __popcll(gm & ((1ull << sub) - 1ull));
+        const int dst = gbase + (ok ? below : nv + (sub - below));
+        myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
+      }
+      cnt = nv;
+    }
+    float myw = 1.f;
+    int myr = myc;
+    if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
+      if (sub < cnt) myw = a.dinv[myc];
+    }
+    if (MODE == MIREC_IN_SPARSE) {
+      myr = sub < cnt ? a.slot[myc] : 0;
+      if (myr < 0) {
+        myr = 0;
+        myw = 0.f;
+      }
+    }
+    for (int k = 0; k < cnt; k += UNROLL) {
+      float4 v[UNROLL];
+      float w[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const int idx = k + u;
+        const int srcl = gbase + (idx & (LPR - 1));
+        const int j = __shfl(myr, srcl);
+        w[u] = (MODE != MIREC_IN_PRESCALED) ? __shfl(myw, srcl) : 1.f;
+        if (idx < cnt)
+          v[u] = ld4(src + (int64_t)j * D + sub * 4);
+        else
+          v[u] = f4_zero();
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (MODE != MIREC_IN_PRESCALED)
+          acc = f4_fma(w[u], v[u], acc);
+        else
+          acc = f4_add(acc, v[u]);
+      }
+    }
+  }
+  return acc;
+}
+
 // Combine the G group partials: afterwards every group holds the row sum.
 template <int D>
 __device__ __forceinline__ float4 combine_groups(float4 s) {
@@ -182,24 +257,54 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
 
 constexpr int kWavesPerBlock = 4;
 
-// Work item w < n_rows: row w (skipped if long); otherwise segment w-n_rows.
+// Row phase: wave w takes the G rows w*G .. w*G+G-1 (of the row list if
+// given).  If all of them have degree <= narrow_max each group gathers its
+// own row (gather_narrow); otherwise the wave walks them one by one with the
+// whole wave per row (gather_rows).  Segment phase: wave row_waves + s
+// gathers segment s of a long row into `partial`.
 // MASKED = in_mask filter on neighbours, ROWMASK = row_mask filter on rows
 // (separate instantiations so profiles tell full and pruned launches apart).
 template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
 __global__ __launch_bounds__(256) void prop_kernel(PropK a) {
   constexpr int LPR = D / 4;
+  constexpr int G = 64 / LPR;
+  constexpr int NARROW_UNROLL = UNROLL < 4 ? 4 : UNROLL;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR;
+  const int grp = lane / LPR;
   const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (w < a.n_rows) {
-    if (ROWMASK && !bit_set(a.row_mask, w)) return;  // wave-uniform
-    const int64_t beg = a.rowptr[w], end = a.rowptr[w + 1];
-    if (a.split > 0 && end - beg > a.split) return;
-    float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, beg, end, lane);
-    s = combine_groups<D>(s);
-    if (lane < LPR) row_epilogue<D>(a, w, s, sub);
+  if (w < a.row_waves) {
+    const int64_t nrows = a.row_list != nullptr ? (int64_t)*a.row_count : a.n_rows;
+    const int64_t idx = w * G + grp;
+    bool have = idx < nrows;
+    int32_t row = 0;
+    if (have) row = a.row_list != nullptr ? a.row_list[idx] : (int32_t)idx;
+    if (ROWMASK && have) have = bit_set(a.row_mask, row);
+    int64_t beg = 0, end = 0;
+    if (have) {
+      beg = a.rowptr[row];
+      end = a.rowptr[row + 1];
+      if (a.split > 0 && end - beg > a.split) have = false;  // segments handle it
+    }
+    const int64_t deg = have ? end - beg : 0;
+    if (G > 1 && __ballot(deg > a.narrow_max) == 0ull) {
+      float4 s = gather_narrow<D, NARROW_UNROLL, MODE, MASKED>(a, beg, end, lane);
+      if (have) row_epilogue<D>(a, row, s, sub);
+      return;
+    }
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+      const int src = g * LPR;
+      if (!__shfl((int)have, src)) continue;  // wave-uniform
+      const int32_t r = __shfl(row, src);
+      const int64_t rb = __shfl((long long)beg, src);
+      const int64_t re = __shfl((long long)end, src);
+      float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, rb, re, lane);
+      s = combine_groups<D>(s);
+      if (lane < LPR) row_epilogue<D>(a, r, s, sub);
+    }
   } else {
-    const int64_t sg = w - a.n_rows;
+    const int64_t sg = w - a.row_waves;
     if (sg >= a.n_seg) return;
     const int64_t row = a.seg_row[sg];
     if (ROWMASK && !bit_set(a.row_mask, row)) return;
@@ -238,8 +343,12 @@ static void launch_main(dim3 grid, hipStream_t st, const PropK &k) {
 }
 
 template <int D, int UNROLL>
-static int launch_prop(const mirec_csr_t *c, const PropK &k, int mode, hipStream_t st) {
-  const int64_t work = c->n_rows + c->n_seg;
+static int launch_prop(const mirec_csr_t *c, PropK k, int64_t list_cap, int mode,
+                       hipStream_t st) {
+  constexpr int G = 64 / (D / 4);
+  const int64_t rows = k.row_list != nullptr ? list_cap : c->n_rows;
+  k.row_waves = (rows + G - 1) / G;
+  const int64_t work = k.row_waves + c->n_seg;
   const int64_t blocks = (work + kWavesPerBlock - 1) / kWavesPerBlock;
   const bool masked = k.in_mask != nullptr;
   if (blocks > 0) {
@@ -296,6 +405,8 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   MIREC_CHECK_ARG((p->seed == nullptr && p->seed2 == nullptr) || p->slot != nullptr);
   MIREC_CHECK_ARG(p->param == nullptr || (p->exp_avg != nullptr && p->exp_avg_sq != nullptr));
   MIREC_CHECK_ARG(p->divisor != 0.f);
+  MIREC_CHECK_ARG(p->row_list == nullptr ||
+                  (p->row_count != nullptr && p->row_list_cap >= 0 && p->row_mask != nullptr));
   if (c->n_seg > 0) {
     MIREC_CHECK_ARG(c->split > 0 && c->seg_row && c->seg_beg && c->long_rows && c->long_segptr);
     if (p->partial == nullptr) return MIREC_ERR_WORKSPACE;
@@ -325,15 +436,20 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   k.partial = p->partial;
   k.row_mask = p->row_mask;
   k.in_mask = p->in_mask;
+  k.row_list = p->row_list;
+  k.row_count = p->row_count;
+  k.row_waves = 0;
+  k.narrow_max = p->narrow_max;
+  const int64_t cap = p->row_list_cap;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (p->dim) {
-    case 4: return launch_prop<4, 1>(c, k, p->in_mode, st);
-    case 8: return launch_prop<8, 1>(c, k, p->in_mode, st);
-    case 16: return launch_prop<16, 1>(c, k, p->in_mode, st);
-    case 32: return launch_prop<32, 2>(c, k, p->in_mode, st);
-    case 64: return launch_prop<64, 4>(c, k, p->in_mode, st);
-    case 128: return launch_prop<128, 4>(c, k, p->in_mode, st);
-    case 256: return launch_prop<256, 8>(c, k, p->in_mode, st);
+    case 4: return launch_prop<4, 1>(c, k, cap, p->in_mode, st);
+    case 8: return launch_prop<8, 1>(c, k, cap, p->in_mode, st);
+    case 16: return launch_prop<16, 1>(c, k, cap, p->in_mode, st);
+    case 32: return launch_prop<32, 2>(c, k, cap, p->in_mode, st);
+    case 64: return launch_prop<64, 4>(c, k, cap, p->in_mode, st);
+    case 128: return launch_prop<128, 4>(c, k, cap, p->in_mode, st);
+    case 256: return launch_prop<256, 8>(c, k, cap, p->in_mode, st);
   }
   return MIREC_ERR_DIM;
 }

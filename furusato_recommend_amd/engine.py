@@ -151,7 +151,12 @@ class PropagationEngine:
         words = (N + 31) // 32
         self.bm_self = torch.zeros(words, **i32)  # S  (uint32 bitmap)
         self.bm_hop = torch.zeros(words, **i32)   # S ∪ N(S)
+        self.self_list = torch.zeros(3 * self.max_batch, **i32)  # S, deduplicated
+        self.self_count = torch.zeros(1, **i32)
+        self._self_cap = 0
         self._masks_ready = False
+        # rows of degree <= narrow_max are gathered one per lane group
+        self.narrow_max = 64
         B3 = 3 * self.max_batch
         self.seed_p = torch.empty(B3, D, **f32)
         self.seed_e = torch.empty(B3, D, **f32)
@@ -183,7 +188,7 @@ class PropagationEngine:
 
     def _prop(self, *, in_mode, x_in=None, seed_in=None, seed=None, addend=None, seed2=None,
               divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None,
-              row_mask=None, in_mask=None):
+              row_mask=None, in_mask=None, row_list=None, row_count=None, row_list_cap=0):
         g = graph or self.g
         p = Prop()
         p.dim = self.dim
@@ -208,6 +213,10 @@ class PropagationEngine:
         p.partial = ptr(part)
         p.row_mask = ptr(row_mask)
         p.in_mask = ptr(in_mask)
+        p.row_list = ptr(row_list)
+        p.row_count = ptr(row_count)
+        p.row_list_cap = int(row_list_cap)
+        p.narrow_max = int(self.narrow_max)
         ev = self.prop_events
         if ev is not None:
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -231,12 +240,19 @@ class PropagationEngine:
         if keys is not None:
             check(lib.mirec_frontier(g.csr_ptr(), keys.data_ptr(), int(n_keys), None, None, None,
                                      0, g.n_users, self.bm_self.data_ptr(),
-                                     self.bm_hop.data_ptr(), _lib.stream_handle()), "frontier")
-        else:
-            check(lib.mirec_frontier(g.csr_ptr(), None, 0, users.data_ptr(), pos.data_ptr(),
-                                     neg.data_ptr(), int(users.shape[0]), g.n_users,
-                                     self.bm_self.data_ptr(), self.bm_hop.data_ptr(),
+                                     self.bm_hop.data_ptr(), None, None,
                                      _lib.stream_handle()), "frontier")
+            self._self_cap = 0  # no S list for key sets
+        else:
+            B = int(users.shape[0])
+            if B > self.max_batch:
+                raise ValueError(f"batch {B} > engine max_batch {self.max_batch}")
+            check(lib.mirec_frontier(g.csr_ptr(), None, 0, users.data_ptr(), pos.data_ptr(),
+                                     neg.data_ptr(), B, g.n_users,
+                                     self.bm_self.data_ptr(), self.bm_hop.data_ptr(),
+                                     self.self_list.data_ptr(), self.self_count.data_ptr(),
+                                     _lib.stream_handle()), "frontier")
+            self._self_cap = 3 * B
         self._masks_ready = True
 
     def prescale(self, x: torch.Tensor, out: torch.Tensor):
@@ -259,16 +275,21 @@ class PropagationEngine:
         self.prescale(emb, self.x0s)
         for l in range(1, L + 1):
             last = l == L
-            rm = None
-            if pruned:
-                rm = self.bm_self if l == L else (self.bm_hop if l == L - 1 else None)
+            rows = {}
+            if pruned and l == L:      # S: the deduplicated batch-node list
+                rows = dict(row_mask=self.bm_self)
+                if self._self_cap:
+                    rows.update(row_list=self.self_list, row_count=self.self_count,
+                                row_list_cap=self._self_cap)
+            elif pruned and l == L - 1:
+                rows = dict(row_mask=self.bm_hop)
             self._prop(in_mode=IN_PRESCALED,
                        x_in=self.x0s if l == 1 else self.xs[(l - 2) % 2],
                        addend=emb if l == 1 else self.acc,
                        divisor=float(L + 1) if last else 1.0,
                        out=self.acc,
                        xs_out=None if last else self.xs[(l - 1) % 2],
-                       row_mask=rm)
+                       **rows)
         return self.acc
 
     def propagate_once(self, x: torch.Tensor, out: torch.Tensor, graph: Graph | None = None):

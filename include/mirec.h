@@ -157,6 +157,15 @@ typedef struct mirec_prop {
   const uint32_t *in_mask;  /* bitmap over source nodes: only neighbours with
                                bit 1 contribute (others are exact zeros);
                                required for MIREC_IN_SPARSE; NULL = all */
+  const int32_t *row_list;  /* optional deduplicated row list (device); the
+                               rows processed are row_list[0 .. *row_count);
+                               needs row_mask = the same set (long rows) */
+  const int32_t *row_count; /* device pointer to the list length */
+  int64_t row_list_cap;     /* host upper bound of *row_count (grid size) */
+  int32_t narrow_max;       /* rows of degree <= narrow_max are gathered one
+                               per lane group (latency-bound short rows);
+                               longer ones one per wave.  0 = always wave */
+  int32_t _pad2;
 } mirec_prop_t;
 
 int mirec_propagate(const mirec_csr_t *csr, const mirec_prop_t *p,
@@ -169,11 +178,14 @@ int mirec_prescale(const float *x, const float *dinv, int64_t n_rows,
 /* Frontier bitmaps of a key set S (keys[n_keys], entries outside [0, n_rows)
  * ignored; or, if keys == NULL, the 3*batch nodes of the triples users[b],
  * n_users+pos[b], n_users+neg[b]):  bm_self = S, bm_hop = S ∪ N(S).  Both
- * bitmaps are [ceil(n_rows/32)] uint32 and are cleared first. */
+ * bitmaps are [ceil(n_rows/32)] uint32 and are cleared first.  If self_list
+ * is given it receives the distinct nodes of S (in no particular order) and
+ * *self_count their number (capacity: n_keys or 3*batch). */
 int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    const int32_t *users, const int32_t *pos, const int32_t *neg,
                    int64_t batch, int64_t n_users, uint32_t *bm_self,
-                   uint32_t *bm_hop, mirec_stream_t stream);
+                   uint32_t *bm_hop, int32_t *self_list, int32_t *self_count,
+                   mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */

@@ -48,11 +48,13 @@ def lgcn_from(f, split=None, batch=64, prune=True):
     return m
 
 
+@pytest.mark.parametrize("narrow_max", [0, 64, 1 << 30])
 @pytest.mark.parametrize("split", [None, 4])
 @pytest.mark.parametrize("name", LGCN)
-def test_forward(golden, name, split):
+def test_forward(golden, name, split, narrow_max):
     f = golden(name)
     m = lgcn_from(f, split)
+    m.engine.narrow_max = narrow_max  # 0: wave-per-row only; huge: group-per-row only
     if split is not None:
         assert m.graph.n_long > 0  # long-row segments exercised
     out = m.propagated()
@@ -65,12 +67,14 @@ def test_forward(golden, name, split):
     assert rel(y, f["layers"][1]) < TOL
 
 
+@pytest.mark.parametrize("narrow_max", [0, 64])
 @pytest.mark.parametrize("prune", [True, False])
 @pytest.mark.parametrize("split", [None, 4])
 @pytest.mark.parametrize("name", LGCN)
-def test_train_steps(golden, name, split, prune):
+def test_train_steps(golden, name, split, prune, narrow_max):
     f = golden(name)
     m = lgcn_from(f, split, prune=prune)
+    m.engine.narrow_max = narrow_max
     t = torch.from_numpy(f["triples"])
     l1 = float(m.stageOne(t[:, 0], t[:, 1], t[:, 2]))
     assert rel(m.all_embedding.weight, f["emb_step1"]) < TOL
@@ -183,7 +187,8 @@ def test_sampler_invariants():
     assert np.all(us.cpu().numpy() % 4 == 1)
 
 
-def test_full_size_properties():
+@pytest.mark.parametrize("narrow_max", [0, 64])
+def test_full_size_properties(narrow_max):
     """BASELINE C2 size (1M users x 100K items, 20M edges): size-independent
     checks — sqrt(deg) is a fixed point of Â, sampled rows vs float64 host
     sums, adjointness <x, Ây> = <Âx, y>."""
@@ -192,6 +197,7 @@ def test_full_size_properties():
     ds = SyntheticBipartite(1_000_000, 100_000, 20_000_000, seed=0, test_frac=0)
     g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
     eng = PropagationEngine(g, 64, 3, 2048)
+    eng.narrow_max = narrow_max
     N = g.n_nodes
     deg = torch.from_numpy(g.degree().astype(np.float32)).cuda()
     x = torch.randn(N, 64, device="cuda") * 0.1
