@@ -56,7 +56,8 @@ class Prop(Structure):
         ("_pad", c_float), ("out", c_void_p), ("xs_out", c_void_p),
         ("param", c_void_p), ("exp_avg", c_void_p), ("exp_avg_sq", c_void_p),
         ("adam", AdamH), ("partial", c_void_p), ("row_mask", c_void_p),
-        ("in_mask", c_void_p), ("row_list", c_void_p), ("row_count", c_void_p),
+        ("in_mask", c_void_p), ("out_mask", c_void_p), ("row_list", c_void_p),
+        ("row_count", c_void_p),
         ("row_list_cap", c_int64), ("narrow_max", c_int32), ("_pad2", c_int32),
     ]
 

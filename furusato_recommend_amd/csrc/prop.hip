@@ -13,9 +13,9 @@
 // registers and are combined with a xor-butterfly at the end: no atomics, no
 // LDS, a fixed summation order per row (deterministic).
 //
-// Masks (uint32 bitmaps over nodes, optional):
-//   row_mask  rows whose bit is 0 are skipped entirely (nothing written);
-//   in_mask   neighbours whose bit is 0 contribute exactly 0 and are not
+// Masks (byte maps over nodes, optional; 1.1 MB at C2, L2-resident):
+//   row_mask  rows whose byte is 0 are skipped entirely (nothing written);
+//   in_mask   neighbours whose byte is 0 contribute exactly 0 and are not
 //             read: the 64 candidates of a chunk are tested at once and the
 //             valid ones compacted to the front with ds_permute.
 // Frontier pruning uses them to compute only the rows the BPR loss depends
@@ -56,17 +56,16 @@ struct PropK {
   float *v;
   mirec_adam_hparams_t adam;
   float *partial;
-  const uint32_t *row_mask;
-  const uint32_t *in_mask;
+  const uint8_t *row_mask;
+  const uint8_t *in_mask;
+  const uint8_t *out_mask;   // rows whose `out` (and addend read) is skipped when 0
   const int32_t *row_list;   // rows to process (deduplicated), or NULL = all rows
   const int32_t *row_count;  // device count of row_list entries
   int64_t row_waves;         // waves of the row phase (host upper bound)
   int32_t narrow_max;        // rows up to this degree are gathered group-per-row
 };
 
-__device__ __forceinline__ bool bit_set(const uint32_t *bm, int64_t i) {
-  return (bm[i >> 5] >> (i & 31)) & 1u;
-}
+__device__ __forceinline__ bool bit_set(const uint8_t *bm, int64_t i) { return bm[i] != 0; }
 
 __device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g,
                                           const mirec_adam_hparams_t &h) {
@@ -234,6 +233,7 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
   if (a.seed != nullptr && sl >= 0) z = f4_add(z, ld4(a.seed + (int64_t)sl * D + sub * 4));
   if (a.xs_out != nullptr && a.param == nullptr) st4(a.xs_out + off, f4_scale(di, z));
   if (a.out == nullptr && a.param == nullptr) return;
+  if (a.out_mask != nullptr && a.param == nullptr && a.out_mask[row] == 0) return;
   float4 o = z;
   if (a.addend != nullptr) o = f4_add(o, ld4(a.addend + off));
   if (a.divisor != 1.f) o = f4_div(o, a.divisor);
@@ -436,6 +436,7 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   k.partial = p->partial;
   k.row_mask = p->row_mask;
   k.in_mask = p->in_mask;
+  k.out_mask = p->out_mask;
   k.row_list = p->row_list;
   k.row_count = p->row_count;
   k.row_waves = 0;

@@ -4,7 +4,7 @@ One training step (the reference's ``stageOne``, model/lgcn.py:127-133, on
 top of ``bpr_loss`` :98-118 and ``forward`` :78-86) runs as ~2L+8 HIP
 launches with no host synchronisation:
 
-  frontier (1-2)          S = batch nodes, F1 = S ∪ N(S) as bitmaps
+  frontier (1-2)          S = batch nodes, F1 = S ∪ N(S) as byte maps
   forward  (1 + L)        x~_0 = dinv ⊙ E, then x_l = Â x_{l-1};
                           acc = x_0 + ... + x_L; out = acc/(L+1).  Every
                           layer gathers pre-scaled rows x~ = dinv ⊙ x written
@@ -16,7 +16,7 @@ launches with no host synchronisation:
   backward (L launches)   Horner: g_L = d, g_l = d + Â g_{l+1} (Â symmetric:
                           the backward SpMM is the forward kernel on the
                           same CSR).  The first backward layer gathers only
-                          the seeded neighbours (IN_SPARSE, S bitmap) and is
+                          the seeded neighbours (IN_SPARSE, S byte map) and is
                           written on F1 only; the second skips neighbours
                           outside F1; the last one adds the reg seed and
                           applies Adam to E in its epilogue, so the dense
@@ -148,9 +148,9 @@ class PropagationEngine:
         self.xs = [torch.empty(N, D, **f32), torch.empty(N, D, **f32)] if self.L > 1 else \
             [torch.empty(N, D, **f32)] if self.L == 1 else []
         self.slot = torch.full((N,), -1, **i32)
-        words = (N + 31) // 32
-        self.bm_self = torch.zeros(words, **i32)  # S  (uint32 bitmap)
-        self.bm_hop = torch.zeros(words, **i32)   # S ∪ N(S)
+        words = (N + 3) // 4
+        self.bm_self = torch.zeros(words, **i32)  # S          (byte map, int32-backed)
+        self.bm_hop = torch.zeros(words, **i32)   # S ∪ N(S)   (byte map)
         self.self_list = torch.zeros(3 * self.max_batch, **i32)  # S, deduplicated
         self.self_count = torch.zeros(1, **i32)
         self._self_cap = 0
@@ -188,7 +188,8 @@ class PropagationEngine:
 
     def _prop(self, *, in_mode, x_in=None, seed_in=None, seed=None, addend=None, seed2=None,
               divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None,
-              row_mask=None, in_mask=None, row_list=None, row_count=None, row_list_cap=0):
+              row_mask=None, in_mask=None, row_list=None, row_count=None, row_list_cap=0,
+              out_mask=None):
         g = graph or self.g
         p = Prop()
         p.dim = self.dim
@@ -213,6 +214,7 @@ class PropagationEngine:
         p.partial = ptr(part)
         p.row_mask = ptr(row_mask)
         p.in_mask = ptr(in_mask)
+        p.out_mask = ptr(out_mask)
         p.row_list = ptr(row_list)
         p.row_count = ptr(row_count)
         p.row_list_cap = int(row_list_cap)
@@ -283,6 +285,9 @@ class PropagationEngine:
                                 row_list_cap=self._self_cap)
             elif pruned and l == L - 1:
                 rows = dict(row_mask=self.bm_hop)
+            if pruned and l == L - 2:
+                # the layer sum is read next by layer L-1, on F1 rows only
+                rows["out_mask"] = self.bm_hop
             self._prop(in_mode=IN_PRESCALED,
                        x_in=self.x0s if l == 1 else self.xs[(l - 2) % 2],
                        addend=emb if l == 1 else self.acc,

@@ -129,7 +129,7 @@ typedef struct mirec_adam_hparams {
  *   z_i   = y_i + seed[slot_i]               (if seed != NULL and slot_i >= 0)
  *   xs_out_i = dinv_i * z_i                  (if xs_out != NULL; next layer)
  *   o_i   = (z_i + addend_i) / divisor + seed2[slot_i]
- *   out_i = o_i                              (if out != NULL)
+ *   out_i = o_i                 (if out != NULL and out_mask_i != 0)
  *   Adam(param_i, exp_avg_i, exp_avg_sq_i; grad = o_i)   (if param != NULL;
  *       then xs_out_i = dinv_i * param_i after the update)
  * `partial` is scratch of csr->n_seg * dim floats (may be NULL if n_seg==0).
@@ -152,11 +152,14 @@ typedef struct mirec_prop {
   float *exp_avg_sq;
   mirec_adam_hparams_t adam;
   float *partial;       /* [n_seg, dim] scratch */
-  const uint32_t *row_mask; /* [ceil(n_rows/32)] bitmap: rows with bit 0 are
+  const uint8_t *row_mask;  /* [n_rows] byte map: rows with byte 0 are
                                skipped (nothing written); NULL = all rows */
-  const uint32_t *in_mask;  /* bitmap over source nodes: only neighbours with
-                               bit 1 contribute (others are exact zeros);
-                               required for MIREC_IN_SPARSE; NULL = all */
+  const uint8_t *in_mask;   /* byte map over source nodes: only neighbours
+                               with byte != 0 contribute (others are exact
+                               zeros); required for MIREC_IN_SPARSE */
+  const uint8_t *out_mask;  /* byte map: rows with byte 0 skip the `out`
+                               write and the addend read (their xs_out is
+                               still written); ignored with fused Adam */
   const int32_t *row_list;  /* optional deduplicated row list (device); the
                                rows processed are row_list[0 .. *row_count);
                                needs row_mask = the same set (long rows) */
@@ -178,13 +181,13 @@ int mirec_prescale(const float *x, const float *dinv, int64_t n_rows,
 /* Frontier bitmaps of a key set S (keys[n_keys], entries outside [0, n_rows)
  * ignored; or, if keys == NULL, the 3*batch nodes of the triples users[b],
  * n_users+pos[b], n_users+neg[b]):  bm_self = S, bm_hop = S ∪ N(S).  Both
- * bitmaps are [ceil(n_rows/32)] uint32 and are cleared first.  If self_list
+ * are byte maps of ceil(n_rows/4)*4 bytes (4-byte aligned), cleared first.  If self_list
  * is given it receives the distinct nodes of S (in no particular order) and
  * *self_count their number (capacity: n_keys or 3*batch). */
 int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    const int32_t *users, const int32_t *pos, const int32_t *neg,
-                   int64_t batch, int64_t n_users, uint32_t *bm_self,
-                   uint32_t *bm_hop, int32_t *self_list, int32_t *self_count,
+                   int64_t batch, int64_t n_users, uint8_t *bm_self,
+                   uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
                    mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
