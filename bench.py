@@ -164,10 +164,17 @@ def main():
     # The roofline is quoted for the full (unmasked) pre-scaled launches,
     # whose algorithmic bytes are exact; masked launches touch data-dependent
     # subsets and are reported by time only.
+    # A launch with an out_mask (forward layer 1 under pruning: layer sum
+    # kept on F1 only) moves 2·|F1|·D·4 more bytes than launch_bytes counts;
+    # |F1| is taken from the last step's mask (it varies by <0.5 % per step).
+    f1_rows = int((eng.bm_hop.view(torch.uint8)[: model.graph.n_nodes] != 0).sum())
     per_kind = {}
     for s, e, kind, nbytes in events:
         ms = s.elapsed_time(e)
-        d = per_kind.setdefault(kind, [0, 0.0, 0])
+        if kind[3]:
+            nbytes += 2 * f1_rows * args.dim * 4
+        key = kind[:3]  # one rocprof kernel per (mode, in_mask, row_mask)
+        d = per_kind.setdefault(key, [0, 0.0, 0])
         d[0] += 1
         d[1] += ms
         d[2] += nbytes
@@ -230,6 +237,7 @@ def main():
                 {"launches_per_step": round(v[0] / args.steps, 2), "avg_ms": round(v[1] / v[0], 4)}
                 for k, v in sorted(per_kind.items())},
             "prune": bool(args.prune),
+            "frontier_F1_rows": f1_rows,
             "recall": recall,
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 2),

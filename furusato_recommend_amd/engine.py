@@ -227,14 +227,18 @@ class PropagationEngine:
               "propagate")
         if ev is not None:
             e.record()
-            kind = (in_mode, in_mask is not None, row_mask is not None)
+            kind = (in_mode, in_mask is not None, row_mask is not None, out_mask is not None)
             ev.append((s, e, kind, self.launch_bytes(p, g)))
 
     def launch_bytes(self, p: Prop, g: Graph) -> int:
+        """Algorithmic bytes of a launch over every row.  With an out_mask the
+        `out`/addend streams are excluded (the caller adds 2·|mask|·D·4 from
+        the measured mask size)."""
+        om = bool(p.out_mask)
         return prop_launch_bytes(p.in_mode, g.n_nodes, g.nnz, self.dim,
                                  slot=bool(p.slot and (p.seed or p.seed2)),
-                                 xs_out=bool(p.xs_out), addend=bool(p.addend),
-                                 out=bool(p.out), adam=bool(p.param))
+                                 xs_out=bool(p.xs_out), addend=bool(p.addend) and not om,
+                                 out=bool(p.out) and not om, adam=bool(p.param))
 
     def compute_frontier(self, users=None, pos=None, neg=None, keys=None, n_keys: int = 0):
         """bm_self = S, bm_hop = S ∪ N(S) for a triple batch or a key list."""

@@ -121,6 +121,14 @@ class LightGCN(nn.Module):
         items_emb = out[self.num_users:]
         return torch.matmul(users_emb, items_emb.t())
 
+    @torch.no_grad()
+    def eval_ratings(self):
+        """users -> rating rows [len(users), m_items] with ONE propagation for
+        the whole evaluation (getUsersRating semantics, model/lgcn.py:120-125)."""
+        out = self.propagated()
+        items = out[self.num_users:]
+        return lambda users: out[users.long()] @ items.t()
+
     def _as_i32(self, t):
         if not torch.is_tensor(t):
             t = torch.as_tensor(t)

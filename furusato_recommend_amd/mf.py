@@ -53,6 +53,27 @@ class MF(nn.Module):
         users_emb = self.embedding_user.weight[users.long()]
         return self.f(users_emb @ self.embedding_item.weight.t())
 
+    @torch.no_grad()
+    def eval_ratings(self):
+        """users -> sigmoid(U Iᵀ) rows (model/MF.py:56-60)."""
+        items = self.embedding_item.weight
+        return lambda users: self.f(self.embedding_user.weight[users.long()] @ items.t())
+
+    @torch.no_grad()
+    def propagated(self) -> torch.Tensor:
+        return self._table
+
+    def sample(self, n_triples: int, seed: int, offset: int = 0, shard: int = 0,
+               n_shards: int = 1):
+        """On-device UniformSample: int32 (users, pos, neg) device tensors."""
+        from .engine import sample_triples
+        u = torch.empty(n_triples, dtype=torch.int32, device=self.device)
+        p, n = torch.empty_like(u), torch.empty_like(u)
+        err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        sample_triples(self.graph, n_triples, seed, offset, u, p, n, err, shard, n_shards)
+        self._sample_err = err
+        return u, p, n
+
     def bpr_loss(self, users, pos, neg):
         users_emb = self.embedding_user(users.long())
         pos_emb = self.embedding_item(pos.long())

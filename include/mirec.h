@@ -286,6 +286,21 @@ int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
                      int32_t *pos, int32_t *neg, int32_t *err,
                      mirec_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* Evaluation (trainer.py:130-138)                                           */
+/* ------------------------------------------------------------------------ */
+
+/* scores [n_eval, m_items] row-major (a GEMM of user and item embeddings,
+ * model/lgcn.py:124).  If csr != NULL, row b's train positives (the CSR row
+ * of user users[b]: node ids n_users + item) are set to -1024 in place
+ * (trainer.py:132-137).  Then the k best items of every row (score
+ * descending, ties to the lower item id) go to topk_idx[b*k ..] and, if
+ * topk_val != NULL, their scores to topk_val.  1 <= k <= 64. */
+int mirec_topk_masked(float *scores, int64_t n_eval, int64_t m_items,
+                      const int32_t *users, const mirec_csr_t *csr,
+                      int64_t n_users, int32_t k, int32_t *topk_idx,
+                      float *topk_val, mirec_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -314,3 +314,93 @@ def test_pruned_step_equals_dense_step_full_size():
     assert rel(res[0][0], res[1][0]) < 1e-5
     assert np.allclose(res[0][1], res[1][1], rtol=1e-5)
     assert not torch.equal(res[0][0], e0)
+
+
+@pytest.mark.parametrize("L", [1, 2, 3, 4, 5])
+def test_pruned_equals_dense_any_depth(L):
+    """Frontier pruning's layer/row bookkeeping for every depth: pruned and
+    dense steps give the same parameters, loss and layer-mean embeddings."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.engine import AdamState, PropagationEngine, sample_triples
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(5000, 800, 60_000, seed=4, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    torch.manual_seed(1)
+    e0 = torch.randn(g.n_nodes, 32, device="cuda") * 0.1
+    res = []
+    for prune in (True, False):
+        eng = PropagationEngine(g, 32, L, 256, prune=prune)
+        e = e0.clone()
+        adam = AdamState(e, 1e-2)
+        u = torch.empty(256, dtype=torch.int32, device="cuda")
+        p, n = torch.empty_like(u), torch.empty_like(u)
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        losses = []
+        for step in range(3):
+            sample_triples(g, 256, 3, step * 256, u, p, n, err)
+            losses.append(float(eng.train_step(e, adam, u, p, n, 1e-4)))
+        res.append((e, losses))
+    assert rel(res[0][0], res[1][0]) < 1e-5
+    assert np.allclose(res[0][1], res[1][1], rtol=1e-5)
+
+
+def test_topk_masked_matches_torch():
+    """mirec_topk_masked == rating[train positives] = -1024; torch.topk
+    (trainer.py:132-138) on random scores (no ties)."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.evaluate import topk_masked
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(3000, 1500, 40_000, seed=5, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    users = torch.arange(0, 3000, 7, device="cuda")
+    rating = torch.randn(len(users), ds.m_items, device="cuda")
+    ref = rating.clone()
+    for r, u in enumerate(users.tolist()):
+        ref[r, torch.from_numpy(ds.allPos[u]).cuda()] = -(1 << 10)
+    for k in (1, 20, 50, 64):
+        rv, ri = torch.topk(ref, k=k)
+        val, idx = topk_masked(rating.clone(), users, g, k)
+        assert torch.equal(idx.long(), ri)
+        assert torch.equal(val, rv)
+
+
+def test_evaluate_matches_oracle():
+    """Recall/Precision/NDCG/HR@{10,20} of evaluate() == the oracle's
+    restatement of Trainer.test on the same propagated embeddings."""
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from furusato_recommend_amd.evaluate import evaluate
+    from oracle.lightgcn_oracle import OracleLightGCN
+    from oracle.lightgcn_oracle import evaluate as oracle_evaluate
+    ds = SyntheticBipartite(4000, 900, 50_000, seed=6, test_frac=0.3)
+    m = LightGCN({"recdim": 32, "layer": 2, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+                  "bpr_batch_size": 512}, ds)
+    for _ in range(3):
+        m.OneEpoch(*m.sample(2048, seed=1))
+    res, top = evaluate(m, ds.testDict, (10, 20), batch=1000, return_topk=True)
+    o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, 32, 2, 1e-3, 1e-4,
+                       emb=m.all_embedding.weight.detach().cpu())
+    out = o.propagated()
+    ref = oracle_evaluate(out[:ds.n_users], out[ds.n_users:], ds.testDict, ds.allPos, (10, 20))
+    for k in res:
+        assert np.allclose(res[k], ref[k], rtol=1e-6, atol=1e-9), (k, res[k], ref[k])
+
+
+def test_trainer_epochs_and_checkpoint(tmp_path):
+    """Trainer surface: train / test / train_epoch; a reference-style
+    state_dict round-trips (key all_embedding.weight)."""
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from furusato_recommend_amd.trainer import Trainer
+    ds = SyntheticBipartite(3000, 500, 30_000, seed=7, test_frac=0.2)
+    cfg = {"recdim": 64, "layer": 3, "lr": 1e-2, "decay": 1e-4, "device": "cuda:0",
+           "bpr_batch_size": 1024, "test_span": 1, "checkpoint_path": str(tmp_path / "m.pth")}
+    m = LightGCN(cfg, ds)
+    t = Trainer(cfg, ds, m)
+    hist = t.train_epoch(epochs=3)
+    losses = [h["loss"] for h in hist if "loss" in h]
+    assert len(losses) == 3 and losses[-1] < losses[0]
+    sd = torch.load(tmp_path / "m.pth", weights_only=True)
+    assert list(sd.keys()) == ["all_embedding.weight"]
+    assert sd["all_embedding.weight"].shape == (3500, 64)
+    m2 = LightGCN(cfg, ds)
+    m2.load_state_dict(sd)
+    assert torch.equal(m2.all_embedding.weight.cpu(), sd["all_embedding.weight"].cpu())
