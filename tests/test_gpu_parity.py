@@ -380,9 +380,13 @@ def test_evaluate_matches_oracle():
     o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, 32, 2, 1e-3, 1e-4,
                        emb=m.all_embedding.weight.detach().cpu())
     out = o.propagated()
+    assert rel(m.propagated(), out) < TOL
     ref = oracle_evaluate(out[:ds.n_users], out[ds.n_users:], ds.testDict, ds.allPos, (10, 20))
+    # CPU vs GPU fp32 scores may swap a near-tie at the k-th place: allow one
+    # such flip (1/|test users| on recall/precision/ndcg sums per user).
+    n = len(ds.testDict)
     for k in res:
-        assert np.allclose(res[k], ref[k], rtol=1e-6, atol=1e-9), (k, res[k], ref[k])
+        assert np.all(np.abs(res[k] - ref[k]) <= 1.5 / n + 1e-9), (k, res[k], ref[k])
 
 
 def test_trainer_epochs_and_checkpoint(tmp_path):
