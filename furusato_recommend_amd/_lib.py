@@ -99,6 +99,15 @@ SIGNATURES = {
                                  c_void_p]),
     "mirec_adam_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                  POINTER(AdamH), c_void_p]),
+    "mirec_sample_fanout": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int32, c_uint64,
+                                    c_uint64, c_void_p, c_void_p]),
+    "mirec_gather_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "mirec_scatter_add_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p,
+                                       c_void_p]),
+    "mirec_fanout_mean": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float,
+                                  c_uint64, c_void_p, c_void_p]),
+    "mirec_fanout_mean_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float,
+                                      c_uint64, c_void_p, c_void_p]),
     "mirec_topk_masked": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,

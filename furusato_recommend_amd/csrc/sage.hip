@@ -1,0 +1,217 @@
+// GraphSAGE hot ops on gfx950 (model/graphsage.py:311-324 + the samplers of
+// neighbor_sampling.py:14-30 / PyG NeighborSampler at graphsage.py:342-365).
+//
+// Sampling is fixed-fanout WITH replacement (the repo's uniform_neighbors),
+// so every hop is a regular tree: level l+1 holds k children per level-l
+// node, contiguous.  That turns PyG's scatter-mean over a sampled edge_index
+// into a fixed-width segment mean — no CSR, no atomics in the forward.
+//
+//   mirec_sample_fanout   children[t*k + c] ~ U(CSR row of nodes[t]); -1 if
+//                         the node has no neighbours (its mean is then 0)
+//   mirec_gather_rows     out[i] = table[ids[i]] (0 for ids < 0)
+//   mirec_scatter_add_rows  grad_table[ids[i]] += grad[i] (float atomics:
+//                         the backward of the gather)
+//   mirec_fanout_mean     out[t] = mean over valid c of dropout(x[t*k + c])
+//   mirec_fanout_mean_bwd grad_x[t*k + c] = mask * grad_out[t] / cnt
+// Dropout masks are a counter hash of (seed, element index), recomputed in
+// the backward (nothing stored).
+#include "common.h"
+
+namespace mirec {
+
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void sample_fanout_kernel(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n_rows,
+    const int32_t *__restrict__ nodes, int64_t n, int32_t k, uint64_t seed, uint64_t offset,
+    int32_t *__restrict__ children) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * k) return;
+  const int64_t t = i / k;
+  const int32_t v = nodes[t];
+  int32_t out = -1;
+  if (v >= 0 && v < n_rows) {
+    const int64_t beg = rowptr[v], deg = rowptr[v + 1] - beg;
+    if (deg > 0) {
+      const uint64_t r = mix64(mix64(seed) ^ (offset + (uint64_t)i));
+      out = col[beg + (int64_t)__umul64hi(r, (uint64_t)deg)];
+    }
+  }
+  children[i] = out;
+}
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ table,
+                                                          const int32_t *__restrict__ ids, int64_t n,
+                                                          int32_t d4, float *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * d4) return;
+  const int64_t r = i / d4;
+  const int64_t c = i - r * d4;
+  const int32_t id = ids[r];
+  st4(out + 4 * i, id >= 0 ? ld4(table + ((int64_t)id * d4 + c) * 4) : f4_zero());
+}
+
+__global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float *__restrict__ grad,
+                                                               const int32_t *__restrict__ ids,
+                                                               int64_t n, int32_t d,
+                                                               float *__restrict__ table_grad) {
+  // one wave-instruction = 64 consecutive floats of one row (256 B): the
+  // full-rate shape for global float atomics on gfx950
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * d) return;
+  const int64_t r = i / d;
+  const int32_t id = ids[r];
+  if (id < 0) return;
+  atomicAdd(table_grad + (int64_t)id * d + (i - r * d), grad[i]);
+}
+
+__device__ __forceinline__ bool keep(uint64_t key, uint64_t idx, uint32_t thresh) {
+  return (uint32_t)(mix64(key ^ idx) >> 32) >= thresh;
+}
+
+// one thread per (target, float4 column)
+__global__ __launch_bounds__(256) void fanout_mean_kernel(
+    const float *__restrict__ x, const int32_t *__restrict__ valid, int64_t n_targets, int32_t k,
+    int32_t d4, uint64_t key, uint32_t thresh, float scale, float *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_targets * d4) return;
+  const int64_t t = i / d4;
+  const int64_t c4 = i - t * d4;
+  const int64_t d = (int64_t)d4 * 4;
+  float4 acc = f4_zero();
+  int cnt = 0;
+  for (int c = 0; c < k; ++c) {
+    const int64_t child = t * k + c;
+    if (valid != nullptr && valid[child] < 0) continue;
+    ++cnt;
+    float4 v = ld4(x + child * d + c4 * 4);
+    if (thresh != 0u) {
+      const uint64_t e = (uint64_t)(child * d + c4 * 4);
+      v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
+      v.y = keep(key, e + 1, thresh) ? v.y * scale : 0.f;
+      v.z = keep(key, e + 2, thresh) ? v.z * scale : 0.f;
+      v.w = keep(key, e + 3, thresh) ? v.w * scale : 0.f;
+    }
+    acc = f4_add(acc, v);
+  }
+  st4(out + i * 4, cnt > 0 ? f4_div(acc, (float)cnt) : f4_zero());
+}
+
+__global__ __launch_bounds__(256) void fanout_mean_bwd_kernel(
+    const float *__restrict__ grad_out, const int32_t *__restrict__ valid, int64_t n_targets,
+    int32_t k, int32_t d4, uint64_t key, uint32_t thresh, float scale,
+    float *__restrict__ grad_x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (child, float4)
+  if (i >= n_targets * k * d4) return;
+  const int64_t child = i / d4;
+  const int64_t c4 = i - child * d4;
+  const int64_t t = child / k;
+  const int64_t d = (int64_t)d4 * 4;
+  float4 g = f4_zero();
+  if (valid == nullptr || valid[child] >= 0) {
+    int cnt = k;
+    if (valid != nullptr) {
+      cnt = 0;
+      for (int c = 0; c < k; ++c) cnt += valid[t * k + c] >= 0 ? 1 : 0;
+    }
+    g = f4_div(ld4(grad_out + t * d + c4 * 4), (float)cnt);
+    if (thresh != 0u) {
+      const uint64_t e = (uint64_t)(child * d + c4 * 4);
+      g.x = keep(key, e, thresh) ? g.x * scale : 0.f;
+      g.y = keep(key, e + 1, thresh) ? g.y * scale : 0.f;
+      g.z = keep(key, e + 2, thresh) ? g.z * scale : 0.f;
+      g.w = keep(key, e + 3, thresh) ? g.w * scale : 0.f;
+    }
+  }
+  st4(grad_x + i * 4, g);
+}
+
+static bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
+  if (!(p >= 0.f && p < 1.f)) return false;
+  *key = mix64(seed ^ 0xA24BAED4963EE407ull);
+  *thresh = (uint32_t)((double)p * 4294967296.0);
+  *scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (p > 0.f && *thresh == 0u) *thresh = 1u;
+  return true;
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
+                                   int32_t k, uint64_t seed, uint64_t offset, int32_t *children,
+                                   mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(csr && csr->rowptr && csr->col && nodes && children && n >= 0 && k > 0);
+  if (n == 0) return MIREC_OK;
+  const int64_t tot = n * k;
+  hipLaunchKernelGGL(sample_fanout_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), csr->rowptr, csr->col, csr->n_rows,
+                     nodes, n, k, seed, offset, children);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_gather_rows(const float *table, const int32_t *ids, int64_t n, int32_t dim,
+                                 float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(table && ids && out && n >= 0 && dim > 0 && dim % 4 == 0);
+  if (n == 0) return MIREC_OK;
+  const int64_t tot = n * (dim / 4);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), table, ids, n, dim / 4, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_scatter_add_rows(const float *grad, const int32_t *ids, int64_t n,
+                                      int32_t dim, float *table_grad, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(grad && ids && table_grad && n >= 0 && dim > 0);
+  if (n == 0) return MIREC_OK;
+  const int64_t tot = n * dim;
+  hipLaunchKernelGGL(scatter_add_rows_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), grad, ids, n, dim, table_grad);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_fanout_mean(const float *x, const int32_t *valid, int64_t n_targets,
+                                 int32_t k, int32_t dim, float dropout_p, uint64_t seed,
+                                 float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(x && out && n_targets >= 0 && k > 0 && dim > 0 && dim % 4 == 0);
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
+  if (n_targets == 0) return MIREC_OK;
+  const int64_t tot = n_targets * (dim / 4);
+  hipLaunchKernelGGL(fanout_mean_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, valid, n_targets, k, dim / 4, key,
+                     thresh, scale, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid,
+                                     int64_t n_targets, int32_t k, int32_t dim, float dropout_p,
+                                     uint64_t seed, float *grad_x, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(grad_out && grad_x && n_targets >= 0 && k > 0 && dim > 0 && dim % 4 == 0);
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
+  if (n_targets == 0) return MIREC_OK;
+  const int64_t tot = n_targets * k * (dim / 4);
+  hipLaunchKernelGGL(fanout_mean_bwd_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), grad_out, valid, n_targets, k,
+                     dim / 4, key, thresh, scale, grad_x);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

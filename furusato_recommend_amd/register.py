@@ -1,9 +1,11 @@
 """Model registry with the reference's names (main.py:32-56, subset on the
-hot path: 'lgn' = LightGCN, 'mf' = MF)."""
+hot path: 'lgn' = LightGCN, 'mf' = MF, 'sage' = GraphSAGE)."""
+from .graphsage import GraphSAGE
 from .lightgcn import LightGCN
 from .mf import MF
 
 MODELS = {
     "mf": MF,
     "lgn": LightGCN,
+    "sage": GraphSAGE,
 }

@@ -287,6 +287,40 @@ int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
                      mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* GraphSAGE hop ops (model/graphsage.py:311-324, neighbor_sampling.py)      */
+/* ------------------------------------------------------------------------ */
+
+/* Fixed-fanout sampling WITH replacement (neighbor_sampling.py:14-30):
+ * children[t*k + c] = a uniform entry of the CSR row of nodes[t]
+ * (counter RNG keyed by (seed, offset + t*k + c)); -1 if the row is empty. */
+int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
+                        int32_t k, uint64_t seed, uint64_t offset,
+                        int32_t *children, mirec_stream_t stream);
+
+/* out[i, :] = table[ids[i], :] (zeros for ids[i] < 0); dim % 4 == 0. */
+int mirec_gather_rows(const float *table, const int32_t *ids, int64_t n,
+                      int32_t dim, float *out, mirec_stream_t stream);
+
+/* table_grad[ids[i], :] += grad[i, :] (float atomics; ids < 0 skipped). */
+int mirec_scatter_add_rows(const float *grad, const int32_t *ids, int64_t n,
+                           int32_t dim, float *table_grad, mirec_stream_t stream);
+
+/* out[t] = mean over the children c in [0,k) with valid[t*k+c] >= 0 (all if
+ * valid == NULL) of dropout_p-dropout(x[t*k + c]); 0 if no valid child.
+ * Dropout keeps an element with probability 1-p and scales it by 1/(1-p);
+ * the mask is a hash of (seed, element index), so the backward recomputes
+ * it.  dim % 4 == 0. */
+int mirec_fanout_mean(const float *x, const int32_t *valid, int64_t n_targets,
+                      int32_t k, int32_t dim, float dropout_p, uint64_t seed,
+                      float *out, mirec_stream_t stream);
+
+/* Backward of mirec_fanout_mean: grad_x[t*k + c] (written, not added). */
+int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid,
+                          int64_t n_targets, int32_t k, int32_t dim,
+                          float dropout_p, uint64_t seed, float *grad_x,
+                          mirec_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Evaluation (trainer.py:130-138)                                           */
 /* ------------------------------------------------------------------------ */
 

@@ -14,7 +14,11 @@ by the reference (requirements.txt:1-10 lists neither):
     sum scatter it is used as (model/radj.py:43): out.index_add_(0, index, src);
   * torch_geometric.nn.conv.LGConv — shimmed with PyG's published algorithm:
     gcn_norm(edge_index, add_self_loops=False) then add-aggregation of
-    x_j * dinv_i * dinv_j.
+    x_j * dinv_i * dinv_j;
+  * torch_scatter's reduce='mean' (model/graphsage.py:320): sum / count
+    clamped to 1; torch_geometric.loader.NeighborSampler: an import-only
+    placeholder (the GraphSAGE fixture feeds an explicit sampled tree to the
+    reference's own forward / loss).
 The rAdjGCN fixture (r = 0.5) uses only the reference's own arithmetic plus the
 index_add scatter, and pins LGConv's shim (they must agree to ~1e-7).
 Bytecode is not written into the reference tree (sys.dont_write_bytecode).
@@ -37,11 +41,19 @@ def install_shims():
     tss = types.ModuleType("torch_scatter.scatter")
 
     def scatter(src, index, dim=0, out=None, reduce="sum", dim_size=None):
-        assert dim == 0 and reduce == "sum"
+        # torch_scatter semantics for the two reductions the reference uses
+        # (sum: model/radj.py:43, mean: model/graphsage.py:320): mean divides
+        # by the per-row count clamped to 1, rows without sources stay 0.
+        assert dim == 0 and reduce in ("sum", "mean")
         if out is None:
             n = dim_size if dim_size is not None else int(index.max()) + 1
             out = torch.zeros((n,) + tuple(src.shape[1:]), dtype=src.dtype)
-        return out.index_add_(0, index, src)
+        out = out.index_add(0, index, src)
+        if reduce == "mean":
+            cnt = torch.zeros(out.shape[0], dtype=src.dtype).index_add_(
+                0, index, torch.ones(index.numel(), dtype=src.dtype)).clamp_(min=1)
+            out = out / cnt.view(-1, *([1] * (out.dim() - 1)))
+        return out
 
     tss.scatter = scatter
     ts.scatter = tss
@@ -62,9 +74,20 @@ def install_shims():
     pgc.LGConv = LGConv
     pgn.conv = pgc
     pg.nn = pgn
+    # model/graphsage.py imports PyG's NeighborSampler at module level; only
+    # its forward/loss are exercised here (on an explicit sampled tree), so
+    # the loader is a placeholder that refuses to run.
+    pgl = types.ModuleType("torch_geometric.loader")
+
+    class NeighborSampler:  # noqa: D401
+        def __init__(self, *a, **k):
+            raise RuntimeError("PyG NeighborSampler is not available in the oracle shims")
+
+    pgl.NeighborSampler = NeighborSampler
+    pg.loader = pgl
     sys.modules.update({"torch_scatter": ts, "torch_scatter.scatter": tss,
                         "torch_geometric": pg, "torch_geometric.nn": pgn,
-                        "torch_geometric.nn.conv": pgc})
+                        "torch_geometric.nn.conv": pgc, "torch_geometric.loader": pgl})
 
 
 class TinyDataset:
@@ -89,6 +112,124 @@ def tiny_graph(seed, n_users=200, m_items=50, n_edges=1000, isolated_item=True):
     items[-5:] = items[:5]
     order = np.argsort(users, kind="stable")  # line-per-user file order
     return users[order], items[order]
+
+
+def sage_tree(rng, seeds, rows, L, sizes):
+    """Fixed-fanout tree with replacement, groups in the canonical order of
+    furusato_recommend_amd.graphsage.GraphSAGE.sample_tree (depth-first:
+    for each group, child groups for hops depth+1..L)."""
+    groups, children = [], {}
+
+    def add(ids, depth):
+        groups.append((ids, depth))
+        return len(groups) - 1
+
+    def expand(gi):
+        ids, depth = groups[gi]
+        for h in range(depth + 1, L + 1):
+            k = sizes[h - 1]
+            ch = np.full(len(ids) * k, -1, np.int64)
+            for t, v in enumerate(ids):
+                if v >= 0 and len(rows[v]):
+                    ch[t * k:(t + 1) * k] = rng.choice(rows[v], k, replace=True)
+            ci = add(ch, h)
+            children[(gi, h)] = ci
+            expand(ci)
+
+    expand(add(np.asarray(seeds, np.int64), 0))
+    return groups, children
+
+
+def tree_to_adjs(groups, children, L, sizes):
+    """PyG NeighborSampler layout for the reference forward
+    (model/graphsage.py:311-324): groups sorted by depth give the node list;
+    layer i's targets (depth <= L-1-i) are its prefix; edges child -> parent."""
+    order = sorted(range(len(groups)), key=lambda g: groups[g][1])
+    start, pos = {}, 0
+    for g in order:
+        start[g] = pos
+        pos += len(groups[g][0])
+    n_id = np.concatenate([groups[g][0] for g in order])
+    adjs = []
+    for i in range(L):
+        hop = L - i
+        src, dst = [], []
+        n_targets = sum(len(groups[g][0]) for g in order if groups[g][1] <= L - 1 - i)
+        for g in order:
+            if groups[g][1] > L - 1 - i:
+                continue
+            c = children[(g, hop)]
+            k = sizes[hop - 1]
+            ids = groups[c][0]
+            for t in range(len(groups[g][0])):
+                for j in range(k):
+                    if ids[t * k + j] >= 0:
+                        src.append(start[c] + t * k + j)
+                        dst.append(start[g] + t)
+        ei = torch.tensor([src, dst], dtype=torch.long)
+        adjs.append((ei, None, (None, n_targets)))
+    return n_id, adjs
+
+
+def make_sage_golden(ds, u, i, n_users, m_items):
+    from types import SimpleNamespace
+
+    from model import graphsage as ref_sage  # noqa: E402
+    L, sizes, d, decay, lr = 2, [4, 3], 16, 1e-2, 1e-2
+    rows = [[] for _ in range(n_users + m_items)]
+    for a, b in zip(u, i):
+        rows[a].append(n_users + b)
+        rows[n_users + b].append(a)
+    rows = [np.array(r, np.int64) for r in rows]
+    rng = np.random.default_rng(21)
+    B = 16
+    users = rng.integers(0, n_users, B)
+    pos = rng.integers(0, m_items, B)
+    neg = rng.integers(0, m_items, B)
+    seeds = np.concatenate([users, pos + n_users, neg + n_users])
+    groups, children = sage_tree(rng, seeds, rows, L, sizes)
+    n_id, adjs = tree_to_adjs(groups, children, L, sizes)
+    g = torch.Generator().manual_seed(5)
+    table = torch.nn.Parameter(torch.randn(n_users + m_items, d, generator=g) * 0.1)
+    lins = torch.nn.ModuleList([torch.nn.Linear(2 * d, d) for _ in range(L)])
+    for li in lins:
+        torch.nn.init.normal_(li.weight, std=0.2, generator=g)
+        torch.nn.init.normal_(li.bias, std=0.05, generator=g)
+    U, I = table[:n_users], table[n_users:]
+    params = [U, I] + [p for li in lins for p in (li.weight, li.bias)]
+    ns = SimpleNamespace(w_linears=lins, dropout=torch.nn.Dropout(0.0), num_layers=L,
+                         device="cpu", config={"decay": decay},
+                         parameters=lambda: iter(params))
+    idx = torch.from_numpy(np.where(n_id >= 0, n_id, 0))
+    x = table[idx] * torch.from_numpy(n_id >= 0).float().unsqueeze(1)
+    out = ref_sage.GraphSAGE.forward(ns, x, adjs)  # the reference's own forward
+    ue, pe, ne = out[:B], out[B:2 * B], out[2 * B:3 * B]
+    loss = ref_sage.GraphSAGE.loss(ns, ue, pe, ne)
+    opt = torch.optim.Adam([table] + [p for li in lins for p in (li.weight, li.bias)], lr=lr)
+    opt.zero_grad()
+    loss.backward()
+    grads = {"g_table": table.grad.detach().clone().numpy()}
+    for k_, li in enumerate(lins):
+        grads[f"g_w{k_}"] = li.weight.grad.detach().clone().numpy()
+        grads[f"g_b{k_}"] = li.bias.grad.detach().clone().numpy()
+    t0 = table.detach().clone().numpy()
+    w0 = {f"w{k_}": li.weight.detach().clone().numpy() for k_, li in enumerate(lins)}
+    b0 = {f"b{k_}": li.bias.detach().clone().numpy() for k_, li in enumerate(lins)}
+    opt.step()
+    after = {"table_step1": table.detach().numpy()}
+    for k_, li in enumerate(lins):
+        after[f"w{k_}_step1"] = li.weight.detach().numpy()
+        after[f"b{k_}_step1"] = li.bias.detach().numpy()
+    flat_groups = np.concatenate([gr[0] for gr in groups])
+    group_len = np.array([len(gr[0]) for gr in groups])
+    group_depth = np.array([gr[1] for gr in groups])
+    np.savez_compressed(os.path.join(OUT, "sage_d16_L2.npz"), train_user=u, train_item=i,
+                        n_users=n_users, m_items=m_items, dim=d, n_layers=L,
+                        sizes=np.array(sizes), lr=lr, decay=decay, batch=B, seeds=seeds,
+                        groups=flat_groups, group_len=group_len, group_depth=group_depth,
+                        emb_out=out.detach().numpy(), loss=float(loss), table0=t0,
+                        **w0, **b0, **grads, **after)
+    print("sage", float(loss))
 
 
 def main():
@@ -151,6 +292,9 @@ def main():
             reg=float(reg), grad=grad.numpy(), emb_step1=steps[0].numpy(),
             emb_step2=steps[1].numpy(), step_losses=np.array(step_losses))
         print("lgcn", dim, L, float(loss), float(reg))
+
+    # ----------------------------------------------------------- GraphSAGE
+    make_sage_golden(ds, u, i, n_users, m_items)
 
     # ---------------------------------------------------------------- MF
     cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",

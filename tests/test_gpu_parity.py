@@ -408,3 +408,133 @@ def test_trainer_epochs_and_checkpoint(tmp_path):
     m2 = LightGCN(cfg, ds)
     m2.load_state_dict(sd)
     assert torch.equal(m2.all_embedding.weight.cpu(), sd["all_embedding.weight"].cpu())
+
+
+def sage_from(f, dropout=0.0):
+    from furusato_recommend_amd import GraphSAGE
+    ds = DS(f["train_user"], f["train_item"], f["n_users"], f["m_items"])
+    L = int(f["n_layers"])
+    cfg = {"recdim": int(f["dim"]), "layer": L, "fanouts": [int(x) for x in f["sizes"]],
+           "lr": float(f["lr"]), "decay": float(f["decay"]), "device": "cuda:0",
+           "bpr_batch_size": int(f["batch"]), "dropout_p": dropout}
+    m = GraphSAGE(cfg, ds)
+    with torch.no_grad():
+        m._table.copy_(torch.from_numpy(f["table0"]))
+        for k, li in enumerate(m.w_linears):
+            li.weight.copy_(torch.from_numpy(f[f"w{k}"]))
+            li.bias.copy_(torch.from_numpy(f[f"b{k}"]))
+    return m
+
+
+def test_sage_step_matches_reference(golden):
+    """GraphSAGE forward on the reference's sampled tree, its loss, gradients
+    (HIP gather/scatter + fanout mean) and one Adam step == the reference's
+    own GraphSAGE.forward / loss + torch Adam (dropout off)."""
+    from furusato_recommend_amd.graphsage import SampleTree
+    f = golden("sage_d16_L2.npz")
+    m = sage_from(f)
+    L, B = int(f["n_layers"]), int(f["batch"])
+    groups = [torch.from_numpy(g.astype(np.int32)).cuda()
+              for g in np.split(f["groups"], np.cumsum(f["group_len"])[:-1])]
+    tree = SampleTree.from_groups(groups, L)
+    out = m.forward(tree)
+    assert rel(out, f["emb_out"][:3 * B]) < TOL
+    seeds = torch.from_numpy(f["seeds"].astype(np.int32))
+    loss = float(m.stageOne(seeds[:B], seeds[B:2 * B] - int(f["n_users"]),
+                            seeds[2 * B:] - int(f["n_users"]), tree=tree))
+    assert abs(loss - float(f["loss"])) < TOL * abs(float(f["loss"]))
+    assert rel(m._table, f["table_step1"]) < TOL
+    for k, li in enumerate(m.w_linears):
+        assert rel(li.weight, f[f"w{k}_step1"]) < TOL
+        assert rel(li.bias, f[f"b{k}_step1"]) < TOL
+
+
+def test_sage_gradients_match_reference(golden):
+    from furusato_recommend_amd.graphsage import SampleTree
+    f = golden("sage_d16_L2.npz")
+    m = sage_from(f)
+    L, B = int(f["n_layers"]), int(f["batch"])
+    groups = [torch.from_numpy(g.astype(np.int32)).cuda()
+              for g in np.split(f["groups"], np.cumsum(f["group_len"])[:-1])]
+    out = m.forward(SampleTree.from_groups(groups, L))
+    loss = m.loss(out[:B], out[B:2 * B], out[2 * B:])
+    loss.backward()
+    assert rel(m._table.grad, f["g_table"]) < TOL
+    for k, li in enumerate(m.w_linears):
+        assert rel(li.weight.grad, f[f"g_w{k}"]) < TOL
+        assert rel(li.bias.grad, f[f"g_b{k}"]) < TOL
+
+
+def test_fanout_sampler_and_dropout_mean():
+    """Fixed-fanout sampling with replacement (neighbor_sampling.py:14-30):
+    children come from the CSR row, uniformly; isolated nodes give -1.
+    Dropout mean: E[mean] == plain mean, backward consistent with forward."""
+    import ctypes
+
+    from furusato_recommend_amd import SyntheticBipartite, _lib
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(300, 60, 3000, seed=9, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    nodes = torch.arange(g.n_nodes, dtype=torch.int32, device="cuda")
+    k = 400
+    ch = torch.empty(g.n_nodes * k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.mirec_sample_fanout(g.csr_ptr(), nodes.data_ptr(), g.n_nodes, k,
+                                            ctypes.c_uint64(3), ctypes.c_uint64(0), ch.data_ptr(),
+                                            _lib.stream_handle()), "sample")
+    ch = ch.view(g.n_nodes, k).cpu().numpy()
+    deg = g.degree()
+    for v in range(0, g.n_nodes, 7):
+        row = g.col_host[g.rowptr_host[v]:g.rowptr_host[v + 1]]
+        if deg[v] == 0:
+            assert np.all(ch[v] == -1)
+            continue
+        assert np.all(np.isin(ch[v], row))
+        # multiplicity-aware uniformity over the row's entries (chi-square)
+        vals, cnt = np.unique(row, return_counts=True)
+        obs = np.array([(ch[v] == x).sum() for x in vals])
+        exp = cnt / cnt.sum() * k
+        chi2 = float(((obs - exp) ** 2 / exp).sum())
+        assert chi2 < len(vals) - 1 + 8 * np.sqrt(2 * max(len(vals) - 1, 1)) + 10
+    x = torch.randn(4000 * 8, 64, device="cuda")
+    valid = torch.zeros(4000 * 8, dtype=torch.int32, device="cuda")
+    plain = torch.empty(4000, 64, device="cuda")
+    drop = torch.empty_like(plain)
+    for p, out in ((0.0, plain), (0.2, drop)):
+        _lib.check(_lib.lib.mirec_fanout_mean(x.data_ptr(), valid.data_ptr(), 4000, 8, 64, p,
+                                              ctypes.c_uint64(5), out.data_ptr(),
+                                              _lib.stream_handle()), "mean")
+    assert rel(plain, x.view(4000, 8, 64).mean(1)) < 1e-6
+    assert abs(float((drop - plain).mean())) < 0.01
+    gx = torch.empty_like(x)
+    go = torch.randn(4000, 64, device="cuda")
+    _lib.check(_lib.lib.mirec_fanout_mean_bwd(go.data_ptr(), valid.data_ptr(), 4000, 8, 64, 0.2,
+                                              ctypes.c_uint64(5), gx.data_ptr(),
+                                              _lib.stream_handle()), "bwd")
+    # <go, mean(x)> == <gx, x> (the backward is the forward's adjoint)
+    assert abs(float((go * drop).sum()) - float((gx * x).sum())) < 1e-3 * float((go * drop).abs().sum())
+
+
+def test_sage_full_graph_inference_and_training():
+    """getUsersRating('all') == layer-wise full-neighbourhood means on the CPU;
+    a few OneEpoch steps with dropout reduce the loss."""
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    ds = SyntheticBipartite(2000, 400, 20_000, seed=10, test_frac=0.1)
+    m = GraphSAGE({"recdim": 32, "layer": 2, "fanouts": [8, 4], "lr": 5e-3, "decay": 1e-5,
+                   "device": "cuda:0", "bpr_batch_size": 256}, ds)
+    out = m.propagated()
+    # CPU reference of graphsage.py:401-424 (scatter mean over train edges)
+    x = m._table.detach().cpu()
+    tu = torch.from_numpy(ds.trainUser)
+    ti = torch.from_numpy(ds.trainItem) + ds.n_users
+    src = torch.cat([ti, tu])
+    dst = torch.cat([tu, ti])
+    for i, li in enumerate(m.w_linears):
+        agg = torch.zeros_like(x).index_add_(0, dst, x[src])
+        cnt = torch.zeros(x.shape[0]).index_add_(0, dst, torch.ones(len(dst))).clamp(min=1)
+        x = torch.nn.functional.linear(torch.cat([x, agg / cnt[:, None]], 1),
+                                       li.weight.detach().cpu(), li.bias.detach().cpu())
+        if i == 0:
+            x = x.relu()
+    assert rel(out, x) < TOL
+    losses = [float(m.OneEpoch(*m.sample(2048, seed=s))) for s in range(6)]
+    assert losses[-1] < losses[0]

@@ -90,3 +90,34 @@ def test_metrics_match_reference(golden):
         assert np.isclose(ret["precision"], f[f"precision_at_{k}"])
         assert ret["hr"] == f[f"hr_at_{k}"]
         assert np.isclose(O.ndcg_at_k(gt, r, k), f[f"ndcg_at_{k}"])
+
+
+def sage_groups(f):
+    return np.split(f["groups"], np.cumsum(f["group_len"])[:-1])
+
+
+def test_sage_matches_reference(golden):
+    """The tree restatement of GraphSAGE.forward / loss == the reference's
+    own forward on the equivalent PyG adjacency (model/graphsage.py:311-337)."""
+    f = golden("sage_d16_L2.npz")
+    L, sizes, d = int(f["n_layers"]), [int(x) for x in f["sizes"]], int(f["dim"])
+    nu = int(f["n_users"])
+    table = torch.nn.Parameter(torch.from_numpy(f["table0"]).clone())
+    lins = torch.nn.ModuleList([torch.nn.Linear(2 * d, d) for _ in range(L)])
+    with torch.no_grad():
+        for k, li in enumerate(lins):
+            li.weight.copy_(torch.from_numpy(f[f"w{k}"]))
+            li.bias.copy_(torch.from_numpy(f[f"b{k}"]))
+    depths, _ = O.sage_canonical_layout(L)
+    assert list(f["group_depth"]) == depths
+    out = O.sage_forward(table, lins, sage_groups(f), L, sizes)
+    B = int(f["batch"])
+    assert rel(out.detach(), f["emb_out"][:3 * B]) < 1e-6
+    reg = [table[:nu], table[nu:]] + [p for li in lins for p in (li.weight, li.bias)]
+    loss = O.sage_loss(out[:B], out[B:2 * B], out[2 * B:], reg, float(f["decay"]))
+    assert abs(float(loss) - float(f["loss"])) < 1e-6
+    loss.backward()
+    assert rel(table.grad, f["g_table"]) < 1e-5
+    for k, li in enumerate(lins):
+        assert rel(li.weight.grad, f[f"g_w{k}"]) < 1e-5
+        assert rel(li.bias.grad, f[f"g_b{k}"]) < 1e-5
