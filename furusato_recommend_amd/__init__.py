@@ -9,9 +9,10 @@ CPU fallback.
 from ._lib import LIB_PATH, MirecError  # noqa: F401  (fails loudly if not built)
 from .dataloader import FiveCore, Loader, SyntheticBipartite  # noqa: F401
 from .graph import Graph  # noqa: F401
+from .graphsage import GraphSAGE  # noqa: F401
 from .lightgcn import LightGCN  # noqa: F401
 from .mf import MF  # noqa: F401
 from .register import MODELS  # noqa: F401
 
-__all__ = ["LightGCN", "MF", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
+__all__ = ["LightGCN", "MF", "GraphSAGE", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
            "MirecError", "LIB_PATH"]
