@@ -84,3 +84,36 @@ class DataParallel:
                 dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.group)
             eng.adam_step(self.emb, self.grad, self.adam)
         return loss
+
+
+class DenseGradDataParallel:
+    """Data parallelism for models trained through autograd (GraphSAGE;
+    replaces ddp_sage.py:754-878, which like ddp_lgcn.py never synchronised
+    gradients).  Every rank samples its own user shard; the loss is scaled by
+    1/world_size and the gradients of all parameters are SUM-all-reduced over
+    RCCL as one flattened bucket between backward and the (HIP) Adam step."""
+
+    def __init__(self, model, group=None):
+        self.model = model
+        self.group = group
+        self.distributed = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        if self.world > 1:
+            for p in model.parameters():
+                dist.broadcast(p.data, src=0, group=group)
+
+    def _allreduce(self):
+        if not self.distributed:
+            return
+        grads = [p.grad for p in self.model.parameters() if p.grad is not None]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+        off = 0
+        for g in grads:
+            g.copy_(flat[off: off + g.numel()].view_as(g))
+            off += g.numel()
+
+    def step(self, users, pos, neg):
+        return self.model.stageOne(users, pos, neg, grad_hook=self._allreduce,
+                                   loss_scale=1.0 / self.world)
