@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # mirec::prop_kernel<D=64, UNROLL=4, IN_PRESCALED, in_mask=false, row_mask=false>
-DOMINANT = "prop_kernel<64, 4, 0, false, false>"
+DOMINANT = "prop_kernel<D, UNROLL, 0, false, false>"
 KIND_NAMES = {0: "prescaled", 1: "raw", 2: "sparse", 3: "none"}
 
 
@@ -56,6 +56,10 @@ def parse():
                     help="frontier pruning (1) or every layer on every row (0)")
     ap.add_argument("--dp-mode", default="sparse", choices=["sparse", "dense"])
     return ap.parse_args()
+
+
+def c2_workload(args) -> bool:
+    return (args.users, args.items, args.edges) == (1_000_000, 100_000, 20_000_000)
 
 
 def cpu_model():
@@ -188,8 +192,9 @@ def main():
     if os.path.exists(pmc):
         with open(pmc) as f:
             j = json.load(f)
-        if (j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
-                and DOMINANT in j.get("kernel", "")):
+        kname = f"prop_kernel<{args.dim}, {({32: 2, 64: 4, 128: 4, 256: 8}).get(args.dim, 1)}, 0, false, false>"
+        if (c2_workload(args) and j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
+                and kname in j.get("kernel", "")):
             traffic = j.get("hbm_bytes_per_launch")
 
     recall = None
@@ -205,8 +210,14 @@ def main():
 
     if rank == 0:
         value = world * args.steps * B / dt
+        c2 = (args.users, args.items, args.edges, args.dim, args.layers) == \
+            (1_000_000, 100_000, 20_000_000, 64, 3)
+        wl = ("C2" if c2 else "custom") + (
+            f": LightGCN {args.layers}-layer d={args.dim}, synthetic {args.users} users x "
+            f"{args.items} items / {args.edges} edges ({args.kind})")
         line = {
-            "metric": "BPR positive-edges/sec (LightGCN-3 d=64, 1M x 100K / 20M edges)",
+            "metric": f"BPR positive-edges/sec (LightGCN-{args.layers} d={args.dim}, "
+                      f"{args.users} x {args.items} / {args.edges} edges)",
             "value": round(value, 1),
             "unit": "positive-edges/s",
             "n_gpus": world,
@@ -218,14 +229,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (SURVEY §8d C2 recipe, seed 0), random-init N(0, 0.1) weights",
-            "config": {"workload": "C2: LightGCN 3-layer d=64, synthetic 1M users x 100K items"
-                                   " / 20M edges, full-graph propagation per step",
+            "config": {"workload": wl,
                        "users": args.users, "items": args.items, "edges": args.edges,
                        "graph": args.kind, "dim": args.dim, "layers": args.layers,
                        "bpr_batch_per_rank": B, "global_batch": B * world,
                        "parallelism": f"dp{world} (user-sharded, RCCL {args.dp_mode} "
                                       f"gradient exchange)"},
-            "roofline": {"bound": "hbm", "kernel": DOMINANT,
+            "roofline": {"bound": "hbm",
+                         "kernel": DOMINANT.replace("D, UNROLL", f"{args.dim}, "
+                                                    f"{ {32: 2, 64: 4, 128: 4, 256: 8}.get(args.dim, 1)}"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "avg_launch_ms": round(avg_ms, 4),

@@ -12,7 +12,8 @@ from .graph import Graph  # noqa: F401
 from .graphsage import GraphSAGE  # noqa: F401
 from .lightgcn import LightGCN  # noqa: F401
 from .mf import MF  # noqa: F401
+from .sasrec import SASRec  # noqa: F401
 from .register import MODELS  # noqa: F401
 
-__all__ = ["LightGCN", "MF", "GraphSAGE", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
+__all__ = ["LightGCN", "MF", "GraphSAGE", "SASRec", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
            "MirecError", "LIB_PATH"]

@@ -108,6 +108,10 @@ SIGNATURES = {
                                   c_uint64, c_void_p, c_void_p]),
     "mirec_fanout_mean_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float,
                                       c_uint64, c_void_p, c_void_p]),
+    "mirec_attention_fwd": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
+                                    c_void_p]),
+    "mirec_attention_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,
+                                    c_void_p, c_void_p]),
     "mirec_topk_masked": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,

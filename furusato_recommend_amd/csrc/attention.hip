@@ -1,0 +1,255 @@
+// SASRec causal self-attention core on gfx950 MFMA (model/sasrec.py:385-397:
+// torch.nn.MultiheadAttention with a causal mask, T <= 50).
+//
+// One 256-thread workgroup (4 waves) per (sequence b, head h).  The T <= 64
+// rows of Q, K, V for the head are staged in LDS (row stride dh+1: no bank
+// conflicts on column reads), then every product is a handful of 32x32 tiles
+// of v_mfma_f32_32x32x2_f32 — exact f32 FMAs (bitwise a k-ordered fmaf
+// chain), so the 1e-4 fp32 parity holds without any reduced precision:
+//   S = Q Kᵀ · 1/sqrt(dh) (+ causal -inf)   4 tiles, one per wave
+//   P = softmax_rows(S)                     4 lanes per row, in LDS
+//   O = P V                                 2 x dh/32 tiles
+// Backward (recomputes S, P): dV = Pᵀ dO, dP = dO Vᵀ,
+// dS = P ⊙ (dP − rowsum(dP ⊙ P)) / sqrt(dh), dQ = dS K, dK = dSᵀ Q.
+// q/k/v are read straight from the packed in-projection output [B, T, 3d]
+// (head h = columns h*dh .. h*dh+dh of each third) and O / dQKV are written
+// in the same packed layouts, so the surrounding Linear layers are plain
+// library GEMMs.  dh ∈ {16, 32, 64}: dh = 16 is zero-padded to 32 in LDS.
+#include "common.h"
+
+namespace mirec {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kT = 64;  // padded sequence tile
+
+// 32x32 tile D += A·B over K (multiple of 2) with operands in LDS:
+//   A(i, k) = TA ? A[k*lda + i] : A[i*lda + k]
+//   B(k, j) = TB ? B[j*ldb + k] : B[k*ldb + j]
+// lane l feeds A(i=l&31, k=2s+(l>>5)) and B(k=2s+(l>>5), j=l&31).
+template <bool TA, bool TB>
+__device__ __forceinline__ f32x16 mfma_tile(const float *A, int lda, const float *B, int ldb,
+                                            int K, f32x16 acc, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+  for (int s = 0; s < K; s += 2) {
+    const int k = s + h;
+    const float a = TA ? A[k * lda + r] : A[r * lda + k];
+    const float b = TB ? B[r * ldb + k] : B[k * ldb + r];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+__device__ __forceinline__ int acc_row(int reg, int lane) {
+  return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// Load rows [0, T) of one head of a packed [B, T, 3d] (or [B, T, d]) tensor
+// into an LDS tile [kT][ld] (zero rows T..kT-1 and columns dh..dpad-1).
+__device__ __forceinline__ void load_head(float *dst, int ld, const float *src, int64_t row_stride,
+                                          int T, int dh, int dpad) {
+  for (int e = threadIdx.x; e < kT * dpad; e += blockDim.x) {
+    const int i = e / dpad, c = e - (e / dpad) * dpad;
+    dst[i * ld + c] = (i < T && c < dh) ? src[(int64_t)i * row_stride + c] : 0.f;
+  }
+}
+
+// S = scale * Q Kᵀ with the causal mask, written to sS [kT][kT+1]; then
+// row softmax in place (P).  Rows >= T are computed too (finite, unused).
+__device__ void scores_softmax(const float *sQ, const float *sK, int ld, float *sS, int dpad,
+                               float scale) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int qi = w >> 1, qj = w & 1;
+  f32x16 acc = mfma_tile<false, true>(sQ + 32 * qi * ld, ld, sK + 32 * qj * ld, ld, dpad,
+                                      zero16(), lane);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int i = 32 * qi + acc_row(r, lane), j = 32 * qj + (lane & 31);
+    sS[i * (kT + 1) + j] = j > i ? -INFINITY : acc[r] * scale;
+  }
+  __syncthreads();
+  // 4 lanes per row, 16 columns each
+  const int row = threadIdx.x >> 2, part = threadIdx.x & 3;
+  float *srow = sS + row * (kT + 1) + part * 16;
+  float m = -INFINITY;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) m = fmaxf(m, srow[c]);
+  m = fmaxf(m, __shfl_xor(m, 1));
+  m = fmaxf(m, __shfl_xor(m, 2));
+  float e[16], sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    e[c] = expf(srow[c] - m);
+    sum += e[c];
+  }
+  sum += __shfl_xor(sum, 1);
+  sum += __shfl_xor(sum, 2);
+  const float inv = 1.f / sum;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) srow[c] = e[c] * inv;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__ qkv,
+                                                       float *__restrict__ out, int T, int H,
+                                                       int dh, int dpad, float scale) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ld = dpad + 1;
+  float *sQ = smem, *sK = sQ + kT * ld, *sV = sK + kT * ld, *sS = sV + kT * ld;
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int d = H * dh;
+  const int64_t rs = 3 * (int64_t)d;
+  const float *base = qkv + (int64_t)b * T * rs + h * dh;
+  load_head(sQ, ld, base, rs, T, dh, dpad);
+  load_head(sK, ld, base + d, rs, T, dh, dpad);
+  load_head(sV, ld, base + 2 * d, rs, T, dh, dpad);
+  __syncthreads();
+  scores_softmax(sQ, sK, ld, sS, dpad, scale);
+  // O = P V: tiles (oi, oj) over 2 x dpad/32, strided over the 4 waves
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ntiles = 2 * (dpad / 32);
+  for (int t = w; t < ntiles; t += 4) {
+    const int oi = t & 1, oj = t >> 1;
+    f32x16 acc = mfma_tile<false, false>(sS + 32 * oi * (kT + 1), kT + 1, sV + 32 * oj, ld, kT,
+                                         zero16(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * oi + acc_row(r, lane), c = 32 * oj + (lane & 31);
+      if (i < T && c < dh) out[((int64_t)b * T + i) * d + h * dh + c] = acc[r];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__ qkv,
+                                                       const float *__restrict__ dout,
+                                                       float *__restrict__ dqkv, int T, int H,
+                                                       int dh, int dpad, float scale) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int ld = dpad + 1;
+  float *sQ = smem, *sK = sQ + kT * ld, *sV = sK + kT * ld, *sO = sV + kT * ld;
+  float *sP = sO + kT * ld, *sD = sP + kT * (kT + 1);
+  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int d = H * dh;
+  const int64_t rs = 3 * (int64_t)d;
+  const float *base = qkv + (int64_t)b * T * rs + h * dh;
+  load_head(sQ, ld, base, rs, T, dh, dpad);
+  load_head(sK, ld, base + d, rs, T, dh, dpad);
+  load_head(sV, ld, base + 2 * d, rs, T, dh, dpad);
+  load_head(sO, ld, dout + (int64_t)b * T * d + h * dh, d, T, dh, dpad);  // dO
+  __syncthreads();
+  scores_softmax(sQ, sK, ld, sP, dpad, scale);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float *gbase = dqkv + (int64_t)b * T * rs + h * dh;
+  // dV = Pᵀ dO  (rows j, cols c; K = i)
+  const int ntiles = 2 * (dpad / 32);
+  for (int t = w; t < ntiles; t += 4) {
+    const int ti = t & 1, tj = t >> 1;
+    f32x16 acc = mfma_tile<true, false>(sP + 32 * ti, kT + 1, sO + 32 * tj, ld, kT, zero16(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int j = 32 * ti + acc_row(r, lane), c = 32 * tj + (lane & 31);
+      if (j < T && c < dh) gbase[(int64_t)j * rs + 2 * d + c] = acc[r];
+    }
+  }
+  // dP = dO Vᵀ (K = dpad) -> sD, one 32x32 tile per wave
+  {
+    const int qi = w >> 1, qj = w & 1;
+    f32x16 acc = mfma_tile<false, true>(sO + 32 * qi * ld, ld, sV + 32 * qj * ld, ld, dpad,
+                                        zero16(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * qi + acc_row(r, lane), j = 32 * qj + (lane & 31);
+      sD[i * (kT + 1) + j] = acc[r];
+    }
+  }
+  __syncthreads();
+  // dS = P ⊙ (dP − Σ_j dP P) · scale, in place in sD (4 lanes per row)
+  {
+    const int row = threadIdx.x >> 2, part = threadIdx.x & 3;
+    float *prow = sP + row * (kT + 1) + part * 16;
+    float *drow = sD + row * (kT + 1) + part * 16;
+    float dot = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) dot += prow[c] * drow[c];
+    dot += __shfl_xor(dot, 1);
+    dot += __shfl_xor(dot, 2);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) drow[c] = prow[c] * (drow[c] - dot) * scale;
+  }
+  __syncthreads();
+  for (int t = w; t < 2 * ntiles; t += 4) {
+    const bool is_q = t < ntiles;
+    const int tt = is_q ? t : t - ntiles;
+    const int ti = tt & 1, tj = tt >> 1;
+    f32x16 acc;
+    if (is_q)  // dQ = dS K: rows i, cols k, K = j
+      acc = mfma_tile<false, false>(sD + 32 * ti * (kT + 1), kT + 1, sK + 32 * tj, ld, kT,
+                                    zero16(), lane);
+    else  // dK = dSᵀ Q: rows j, cols k, K = i
+      acc = mfma_tile<true, false>(sD + 32 * ti, kT + 1, sQ + 32 * tj, ld, kT, zero16(), lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = 32 * ti + acc_row(r, lane), c = 32 * tj + (lane & 31);
+      if (i < T && c < dh) gbase[(int64_t)i * rs + (is_q ? 0 : d) + c] = acc[r];
+    }
+  }
+}
+
+// Dynamic LDS above 64 KiB needs an explicit opt-in per kernel (once).
+static int allow_big_lds() {
+  static int rc = -1;
+  if (rc < 0) {
+    rc = 0;
+    if (hipFuncSetAttribute((const void *)attn_fwd_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
+        hipFuncSetAttribute((const void *)attn_bwd_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      rc = 1;
+  }
+  return rc;
+}
+
+static int attn_smem(int dpad, bool bwd) {
+  const int ld = dpad + 1;
+  return (int)sizeof(float) * (bwd ? (4 * kT * ld + 2 * kT * (kT + 1)) : (3 * kT * ld + kT * (kT + 1)));
+}
+
+}  // namespace mirec
+
+extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, int32_t heads,
+                                   int32_t head_dim, float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && out && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
+  MIREC_CHECK_ARG(head_dim == 16 || head_dim == 32 || head_dim == 64);
+  if (batch == 0) return MIREC_OK;
+  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
+  const int dpad = head_dim < 32 ? 32 : head_dim;
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
+                     attn_smem(dpad, false), reinterpret_cast<hipStream_t>(stream), qkv, out, T,
+                     heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t batch, int32_t T,
+                                   int32_t heads, int32_t head_dim, float *dqkv,
+                                   mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && dout && dqkv && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
+  MIREC_CHECK_ARG(head_dim == 16 || head_dim == 32 || head_dim == 64);
+  if (batch == 0) return MIREC_OK;
+  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
+  const int dpad = head_dim < 32 ? 32 : head_dim;
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
+                     attn_smem(dpad, true), reinterpret_cast<hipStream_t>(stream), qkv, dout,
+                     dqkv, T, heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

@@ -321,6 +321,22 @@ int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid,
                           mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
+/* SASRec causal self-attention (model/sasrec.py:385-397), f32 MFMA          */
+/* ------------------------------------------------------------------------ */
+
+/* qkv: the packed in-projection output [batch, T, 3*heads*head_dim] (q | k |
+ * v, head h = columns h*head_dim ..); out: [batch, T, heads*head_dim] =
+ * softmax(q kᵀ / sqrt(head_dim) + causal mask) v per head.  T <= 64,
+ * head_dim ∈ {16, 32, 64}. */
+int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, int32_t heads,
+                        int32_t head_dim, float *out, mirec_stream_t stream);
+
+/* Backward: dqkv [batch, T, 3*heads*head_dim] (written) from dout. */
+int mirec_attention_bwd(const float *qkv, const float *dout, int64_t batch, int32_t T,
+                        int32_t heads, int32_t head_dim, float *dqkv,
+                        mirec_stream_t stream);
+
+/* ------------------------------------------------------------------------ */
 /* Evaluation (trainer.py:130-138)                                           */
 /* ------------------------------------------------------------------------ */
 

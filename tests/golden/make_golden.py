@@ -232,6 +232,59 @@ def make_sage_golden(ds, u, i, n_users, m_items):
     print("sage", float(loss))
 
 
+def make_sasrec_golden():
+    """The reference's own SASRec.oneblock / forward_user (model/sasrec.py:
+    385-413) with nn.MultiheadAttention, on padded sequences; dropout off."""
+    from types import SimpleNamespace
+
+    from torch.nn.utils.rnn import pad_sequence
+
+    from model import sasrec as ref_sas  # noqa: E402
+    for d, heads, L in ((64, 8, 2), (128, 2, 2)):
+        torch.manual_seed(100 + heads)
+        ns = SimpleNamespace(
+            num_layers=L, device="cpu", dropout=torch.nn.Dropout(0.0),
+            attn_layers=torch.nn.ModuleList(
+                [torch.nn.MultiheadAttention(d, heads, batch_first=True) for _ in range(L)]),
+            attn_norm_layers=torch.nn.ModuleList([torch.nn.LayerNorm(d) for _ in range(L)]),
+            ffn_norm_layers=torch.nn.ModuleList([torch.nn.LayerNorm(d) for _ in range(L)]),
+            ffn_layers=torch.nn.ModuleList([torch.nn.Linear(d, d) for _ in range(L)]))
+        with torch.no_grad():  # non-trivial LN / bias parameters
+            for mods in (ns.attn_norm_layers, ns.ffn_norm_layers):
+                for m in mods:
+                    m.weight.normal_(1.0, 0.1)
+                    m.bias.normal_(0.0, 0.1)
+            for m in ns.attn_layers:
+                m.in_proj_bias.normal_(0.0, 0.05)
+                m.out_proj.bias.normal_(0.0, 0.05)
+        ns.oneblock = lambda x, layer, ns=ns: ref_sas.SASRec.oneblock(ns, x, layer)
+        lengths = [50, 1, 17, 33, 8, 50]
+        seqs = [torch.randn(l, d) for l in lengths]
+        x = pad_sequence(seqs, batch_first=True).requires_grad_(True)
+        length = torch.tensor(lengths).unsqueeze(0)  # DataLoader-batched shape [1, B]
+        out = ref_sas.SASRec.forward_user(ns, x, length)
+        wts = torch.randn_like(out)
+        (out * wts).sum().backward()
+        params = {}
+        for li in range(L):
+            a = ns.attn_layers[li]
+            params.update({f"in_w{li}": a.in_proj_weight, f"in_b{li}": a.in_proj_bias,
+                           f"out_w{li}": a.out_proj.weight, f"out_b{li}": a.out_proj.bias,
+                           f"ln1_w{li}": ns.attn_norm_layers[li].weight,
+                           f"ln1_b{li}": ns.attn_norm_layers[li].bias,
+                           f"ln2_w{li}": ns.ffn_norm_layers[li].weight,
+                           f"ln2_b{li}": ns.ffn_norm_layers[li].bias,
+                           f"ffn_w{li}": ns.ffn_layers[li].weight,
+                           f"ffn_b{li}": ns.ffn_layers[li].bias})
+        arrs = {k: v.detach().numpy() for k, v in params.items()}
+        arrs.update({f"g_{k}": v.grad.detach().numpy() for k, v in params.items()})
+        np.savez_compressed(os.path.join(OUT, f"sasrec_d{d}_h{heads}.npz"), d=d, heads=heads,
+                            L=L, lengths=np.array(lengths), x=x.detach().numpy(),
+                            out=out.detach().numpy(), wts=wts.numpy(),
+                            g_x=x.grad.detach().numpy(), **arrs)
+        print("sasrec", d, heads, float(out.abs().mean()))
+
+
 def main():
     sys.dont_write_bytecode = True
     sys.argv = ["make_golden"]
@@ -295,6 +348,8 @@ def main():
 
     # ----------------------------------------------------------- GraphSAGE
     make_sage_golden(ds, u, i, n_users, m_items)
+
+    make_sasrec_golden()
 
     # ---------------------------------------------------------------- MF
     cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",

@@ -121,3 +121,20 @@ def test_sage_matches_reference(golden):
     for k, li in enumerate(lins):
         assert rel(li.weight.grad, f[f"g_w{k}"]) < 1e-5
         assert rel(li.bias.grad, f[f"g_b{k}"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", ["sasrec_d64_h8.npz", "sasrec_d128_h2.npz"])
+def test_sasrec_block_matches_reference(golden, name):
+    """Written-out causal MHA + block + masked mean == the reference's
+    SASRec.forward_user over torch.nn.MultiheadAttention (dropout off)."""
+    f = golden(name)
+    L, heads = int(f["L"]), int(f["heads"])
+    p = {k: torch.from_numpy(v).requires_grad_(True) for k, v in f.items()
+         if not k.startswith("g_") and k not in ("d", "heads", "L", "lengths", "x", "out", "wts")}
+    x = torch.from_numpy(f["x"]).requires_grad_(True)
+    out = O.sasrec_forward_user(x, f["lengths"], p, heads, L)
+    assert rel(out.detach(), f["out"]) < 1e-5
+    (out * torch.from_numpy(f["wts"])).sum().backward()
+    assert rel(x.grad, f["g_x"]) < 1e-5
+    for k, v in p.items():
+        assert rel(v.grad, f["g_" + k]) < 1e-4, k
