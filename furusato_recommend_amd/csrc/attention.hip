@@ -14,7 +14,7 @@
 // q/k/v are read straight from the packed in-projection output [B, T, 3d]
 // (head h = columns h*dh .. h*dh+dh of each third) and O / dQKV are written
 // in the same packed layouts, so the surrounding Linear layers are plain
-// library GEMMs.  dh ∈ {16, 32, 64}: dh = 16 is zero-padded to 32 in LDS.
+// library GEMMs.  Any head dim <= 64: it is zero-padded to 32 or 64 in LDS.
 #include "common.h"
 
 namespace mirec {
@@ -227,10 +227,10 @@ extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, i
                                    int32_t head_dim, float *out, mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && out && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
-  MIREC_CHECK_ARG(head_dim == 16 || head_dim == 32 || head_dim == 64);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
   if (batch == 0) return MIREC_OK;
   if (allow_big_lds() != 0) return MIREC_ERR_HIP;
-  const int dpad = head_dim < 32 ? 32 : head_dim;
+  const int dpad = head_dim <= 32 ? 32 : 64;
   hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
                      attn_smem(dpad, false), reinterpret_cast<hipStream_t>(stream), qkv, out, T,
                      heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));
@@ -243,10 +243,10 @@ extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t 
                                    mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && dout && dqkv && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
-  MIREC_CHECK_ARG(head_dim == 16 || head_dim == 32 || head_dim == 64);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
   if (batch == 0) return MIREC_OK;
   if (allow_big_lds() != 0) return MIREC_ERR_HIP;
-  const int dpad = head_dim < 32 ? 32 : head_dim;
+  const int dpad = head_dim <= 32 ? 32 : 64;
   hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
                      attn_smem(dpad, true), reinterpret_cast<hipStream_t>(stream), qkv, dout,
                      dqkv, T, heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));

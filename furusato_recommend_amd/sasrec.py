@@ -57,8 +57,8 @@ class CausalSelfAttention(nn.Module):
 
     def __init__(self, d: int, heads: int, device=None):
         super().__init__()
-        if d % heads or (d // heads) not in (16, 32, 64):
-            raise ValueError("head_dim = d / heads must be 16, 32 or 64")
+        if d % heads or not 1 <= d // heads <= 64:
+            raise ValueError("head_dim = d / heads must be an integer <= 64")
         self.heads = heads
         self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d, device=device))
         self.in_proj_bias = nn.Parameter(torch.zeros(3 * d, device=device))

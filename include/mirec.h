@@ -327,7 +327,7 @@ int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid,
 /* qkv: the packed in-projection output [batch, T, 3*heads*head_dim] (q | k |
  * v, head h = columns h*head_dim ..); out: [batch, T, heads*head_dim] =
  * softmax(q kᵀ / sqrt(head_dim) + causal mask) v per head.  T <= 64,
- * head_dim ∈ {16, 32, 64}. */
+ * 1 <= head_dim <= 64. */
 int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, int32_t heads,
                         int32_t head_dim, float *out, mirec_stream_t stream);
 

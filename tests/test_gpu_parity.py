@@ -597,7 +597,7 @@ def test_sasrec_attention_kernel_vs_torch_sdpa():
 
     from furusato_recommend_amd.sasrec import _CausalAttention
     torch.manual_seed(0)
-    for heads, dh, T in ((8, 16, 50), (2, 64, 64), (4, 32, 7), (1, 64, 1)):
+    for heads, dh, T in ((8, 16, 50), (2, 64, 64), (4, 32, 7), (1, 64, 1), (8, 8, 33), (3, 48, 20)):
         d = heads * dh
         qkv = torch.randn(5, T, 3 * d, device="cuda", requires_grad=True)
         out = _CausalAttention.apply(qkv, heads)
