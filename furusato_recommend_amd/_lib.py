@@ -16,7 +16,8 @@ from ctypes import (POINTER, Structure, c_float, c_int, c_int32, c_int64,
 import torch  # noqa: F401  (binds libmirec to torch's HIP runtime: same SONAME)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmirec.so")
+# MIREC_LIB selects an alternative build for A/B timing (tools/bench_variants.py)
+LIB_PATH = os.environ.get("MIREC_LIB") or os.path.join(_HERE, "libmirec.so")
 
 MIREC_OK = 0
 IN_PRESCALED, IN_RAW, IN_SPARSE, IN_NONE = 0, 1, 2, 3
@@ -59,6 +60,7 @@ class Prop(Structure):
         ("in_mask", c_void_p), ("out_mask", c_void_p), ("row_list", c_void_p),
         ("row_count", c_void_p),
         ("row_list_cap", c_int64), ("narrow_max", c_int32), ("_pad2", c_int32),
+        ("wide_list", c_void_p), ("wide_count", c_void_p),
     ]
 
 
@@ -81,6 +83,8 @@ SIGNATURES = {
     "mirec_frontier": (c_int, [POINTER(CSR), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p]),
+    "mirec_mask_compact": (c_int, [POINTER(CSR), c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -8,11 +8,13 @@
 // two byte maps (1 byte per node, 1.1 MB at C2: L2-resident) from a key list
 // or directly from the triples:
 //   bm_self = S,  bm_hop = S ∪ N(S)
-// One wave per key expands its CSR row with plain byte stores (idempotent:
-// no atomics); S membership is set with one 32-bit atomicOr per key so the
-// first setter can append the node to the deduplicated S list.  Rows longer
-// than the CSR split are expanded by one wave per segment (second kernel),
-// so a hot item does not serialise the launch.
+// One lane per key sets S membership with a 32-bit atomicOr, so the first
+// setter appends the node to the deduplicated S list (one list atomic per
+// block); then one wave per S node expands its CSR row with plain byte stores
+// (idempotent: no atomics).  Rows longer than the CSR split are expanded by
+// one wave per segment, so a hot item does not serialise the launch.
+// mirec_mask_compact turns a byte map (F1) into a row list for the masked
+// propagation launches.
 #include "common.h"
 
 namespace mirec {
@@ -25,31 +27,92 @@ __device__ __forceinline__ bool test_and_set(uint8_t *bm, int64_t i) {
   return (atomicOr(reinterpret_cast<uint32_t *>(bm) + (i >> 2), b) & b) == 0u;
 }
 
+// Reserves c list entries for this thread in a 256-thread block: one
+// atomicAdd per block on `count` (not one per entry: same-address atomics
+// serialise in one L2 channel).  Returns this thread's first offset; entries
+// keep thread order inside the block.  Every thread of the block must call.
+__device__ __forceinline__ int32_t block_reserve(int c, int32_t *count) {
+  __shared__ int wsum[kWaves];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();  // a previous call's readers are done with wsum / base
+  int incl = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int t = __shfl_up(incl, d);
+    if (lane >= d) incl += t;
+  }
+  if (lane == 63) wsum[wid] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) t += wsum[k];
+    base = t > 0 ? atomicAdd(count, t) : 0;
+  }
+  __syncthreads();
+  int off = base + incl - c;
+  for (int k = 0; k < wid; ++k) off += wsum[k];
+  return off;
+}
+
+__device__ __forceinline__ int64_t key_node(int64_t i, const int32_t *keys, int64_t n_keys,
+                                            const int32_t *users, const int32_t *pos,
+                                            const int32_t *neg, int64_t batch, int64_t n_users) {
+  if (keys != nullptr) return i < n_keys ? (int64_t)keys[i] : -1;
+  if (i >= 3 * batch) return -1;
+  return i < batch ? (int64_t)users[i]
+                   : (i < 2 * batch ? n_users + pos[i - batch] : n_users + neg[i - 2 * batch]);
+}
+
+// One lane per key: S membership (first setter appends the node to the
+// deduplicated S list) and the node's own bm_hop byte.
+__global__ __launch_bounds__(256) void frontier_self_kernel(
+    int64_t n_rows, const int32_t *__restrict__ keys, int64_t n_keys,
+    const int32_t *__restrict__ users, const int32_t *__restrict__ pos,
+    const int32_t *__restrict__ neg, int64_t batch, int64_t n_users, uint8_t *bm_self,
+    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t node = key_node(i, keys, n_keys, users, pos, neg, batch, n_users);
+  const bool valid = node >= 0 && node < n_rows;  // empty / sentinel entries
+  const bool first = valid && test_and_set(bm_self, node);
+  if (valid) bm_hop[node] = 1;
+  const int32_t off = block_reserve(first ? 1 : 0, self_count);
+  if (first) self_list[off] = (int32_t)node;
+}
+
+// One wave per S node: its CSR row's neighbours into bm_hop with plain byte
+// stores (idempotent, no atomics).
+__global__ __launch_bounds__(256) void frontier_expand_kernel(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int32_t split,
+    const int32_t *__restrict__ self_list, const int32_t *__restrict__ self_count,
+    uint8_t *bm_hop) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (i >= *self_count) return;
+  const int64_t node = self_list[i];
+  const int64_t beg = rowptr[node], end = rowptr[node + 1];
+  if (split > 0 && end - beg > split) return;  // expanded per segment
+  for (int64_t e = beg + lane; e < end; e += 64) bm_hop[col[e]] = 1;
+}
+
+// Without an S list: one wave per key does both (duplicates re-expand).
 __global__ __launch_bounds__(256) void frontier_keys_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n_rows,
     int32_t split, const int32_t *__restrict__ keys, int64_t n_keys,
     const int32_t *__restrict__ users, const int32_t *__restrict__ pos,
     const int32_t *__restrict__ neg, int64_t batch, int64_t n_users, uint8_t *bm_self,
-    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count) {
+    uint8_t *bm_hop) {
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
-  int64_t node;
-  if (keys != nullptr) {
-    if (i >= n_keys) return;
-    node = keys[i];
-  } else {
-    if (i >= 3 * batch) return;
-    node = i < batch ? (int64_t)users[i]
-                     : (i < 2 * batch ? n_users + pos[i - batch] : n_users + neg[i - 2 * batch]);
-  }
-  if (node < 0 || node >= n_rows) return;  // empty / sentinel entries
+  const int64_t node = key_node(i, keys, n_keys, users, pos, neg, batch, n_users);
+  if (node < 0 || node >= n_rows) return;
   if (lane == 0) {
-    if (test_and_set(bm_self, node) && self_list != nullptr)
-      self_list[atomicAdd(self_count, 1)] = (int32_t)node;
+    bm_self[node] = 1;
     bm_hop[node] = 1;
   }
   const int64_t beg = rowptr[node], end = rowptr[node + 1];
-  if (split > 0 && end - beg > split) return;  // expanded per segment
+  if (split > 0 && end - beg > split) return;
   for (int64_t e = beg + lane; e < end; e += 64) bm_hop[col[e]] = 1;
 }
 
@@ -67,6 +130,41 @@ __global__ __launch_bounds__(256) void frontier_segments_kernel(
   for (int64_t e = beg + lane; e < end; e += 64) bm_hop[col[e]] = 1;
 }
 
+// Byte map -> row lists (narrow / wide by degree), ascending within a block.
+// Each thread tests 16 bytes (one 16-B load of four map words).
+__global__ __launch_bounds__(256) void mask_compact_kernel(
+    const uint8_t *__restrict__ bm, const int64_t *__restrict__ rowptr, int64_t n,
+    int32_t narrow_max, int32_t *list, int32_t *count, int32_t *wide_list,
+    int32_t *wide_count) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t b0 = t * 16;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  if (b0 + 16 <= n) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(bm + b0);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else if (b0 < n) {
+    for (int k = 0; b0 + k < n; ++k)
+      if (bm[b0 + k]) w[k >> 2] |= 1u << (8 * (k & 3));
+  }
+  uint32_t set = 0u, wide = 0u;  // bit k: byte k set / node k goes wide
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if ((w[k >> 2] >> (8 * (k & 3))) & 0xffu) {
+      set |= 1u << k;
+      if (wide_list != nullptr && rowptr[b0 + k + 1] - rowptr[b0 + k] > narrow_max)
+        wide |= 1u << k;
+    }
+  }
+  const uint32_t narrow = set & ~wide;
+  int32_t off = block_reserve(__popc(narrow), count);
+  int32_t woff = wide_list != nullptr ? block_reserve(__popc(wide), wide_count) : 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if ((narrow >> k) & 1u) list[off++] = (int32_t)(b0 + k);
+    if ((wide >> k) & 1u) wide_list[woff++] = (int32_t)(b0 + k);
+  }
+}
+
 }  // namespace mirec
 
 extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t n_keys,
@@ -77,23 +175,53 @@ extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t
   using namespace mirec;
   MIREC_CHECK_ARG(c && c->rowptr && c->col && bm_self && bm_hop);
   MIREC_CHECK_ARG(keys != nullptr || (users && pos && neg && batch >= 0 && n_users >= 0));
+  MIREC_CHECK_ARG(self_list == nullptr || self_count != nullptr);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const size_t bytes = (size_t)((c->n_rows + 3) / 4) * 4;  // whole words (test_and_set)
   MIREC_HIP(hipMemsetAsync(bm_self, 0, bytes, st));
   MIREC_HIP(hipMemsetAsync(bm_hop, 0, bytes, st));
-  MIREC_CHECK_ARG(self_list == nullptr || self_count != nullptr);
-  if (self_count != nullptr) MIREC_HIP(hipMemsetAsync(self_count, 0, 4, st));
   const int64_t n = keys != nullptr ? n_keys : 3 * batch;
-  if (n > 0) {
+  const int32_t split = c->n_seg > 0 ? c->split : 0;
+  if (self_list != nullptr) {
+    MIREC_HIP(hipMemsetAsync(self_count, 0, 4, st));
+    if (n > 0) {
+      hipLaunchKernelGGL(frontier_self_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c->n_rows,
+                         keys, n_keys, users, pos, neg, batch, n_users, bm_self, bm_hop,
+                         self_list, self_count);
+      MIREC_LAUNCH_CHECK();
+      hipLaunchKernelGGL(frontier_expand_kernel, dim3((n + kWaves - 1) / kWaves), dim3(256), 0,
+                         st, c->rowptr, c->col, split, self_list, self_count, bm_hop);
+      MIREC_LAUNCH_CHECK();
+    }
+  } else if (n > 0) {
     hipLaunchKernelGGL(frontier_keys_kernel, dim3((n + kWaves - 1) / kWaves), dim3(256), 0, st,
-                       c->rowptr, c->col, c->n_rows, c->n_seg > 0 ? c->split : 0, keys, n_keys,
-                       users, pos, neg, batch, n_users, bm_self, bm_hop, self_list, self_count);
+                       c->rowptr, c->col, c->n_rows, split, keys, n_keys, users, pos, neg, batch,
+                       n_users, bm_self, bm_hop);
     MIREC_LAUNCH_CHECK();
   }
   if (c->n_seg > 0 && n > 0) {
     hipLaunchKernelGGL(frontier_segments_kernel, dim3((c->n_seg + kWaves - 1) / kWaves), dim3(256),
                        0, st, c->rowptr, c->col, c->seg_row, c->seg_beg, c->n_seg, c->split,
                        bm_self, bm_hop);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
+
+extern "C" int mirec_mask_compact(const mirec_csr_t *c, const uint8_t *bm, int32_t narrow_max,
+                                  int32_t *list, int32_t *count, int32_t *wide_list,
+                                  int32_t *wide_count, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(c && c->rowptr && bm && list && count && c->n_rows >= 0);
+  MIREC_CHECK_ARG(wide_list == nullptr || wide_count != nullptr);
+  MIREC_CHECK_ARG(((uintptr_t)bm & 15u) == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  MIREC_HIP(hipMemsetAsync(count, 0, 4, st));
+  if (wide_count != nullptr) MIREC_HIP(hipMemsetAsync(wide_count, 0, 4, st));
+  const int64_t threads = (c->n_rows + 15) / 16;
+  if (threads > 0) {
+    hipLaunchKernelGGL(mask_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, bm,
+                       c->rowptr, c->n_rows, narrow_max, list, count, wide_list, wide_count);
     MIREC_LAUNCH_CHECK();
   }
   return MIREC_OK;

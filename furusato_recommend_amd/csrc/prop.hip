@@ -63,6 +63,8 @@ struct PropK {
   const int32_t *row_count;  // device count of row_list entries
   int64_t row_waves;         // waves of the row phase (host upper bound)
   int32_t narrow_max;        // rows up to this degree are gathered group-per-row
+  const int32_t *wide_list;  // rows gathered by a whole workgroup each (list mode)
+  const int32_t *wide_count;
 };
 
 __device__ __forceinline__ bool bit_set(const uint8_t *bm, int64_t i) { return bm[i] != 0; }
@@ -94,8 +96,11 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64
   for (int64_t base = beg; base < end; base += 64) {
     int cnt = (int)min((int64_t)64, end - base);
     int myc = lane < cnt ? a.col[base + lane] : 0;
+    // SPARSE: the seed-row slot itself is the filter (slot >= 0 <=> node in
+    // S), one dependent load less than a byte-map test followed by the slot.
+    int myr = (MODE == MIREC_IN_SPARSE) ? (lane < cnt ? a.slot[myc] : -1) : myc;
     if (MASKED) {
-      const bool ok = lane < cnt && bit_set(a.in_mask, myc);
+      const bool ok = lane < cnt && (MODE == MIREC_IN_SPARSE ? myr >= 0 : bit_set(a.in_mask, myc));
       const unsigned long long m = __ballot(ok);
       const int nv = __popcll(m);
       if (nv == 0) continue;  // wave-uniform
@@ -103,20 +108,14 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64
         const int below = __popcll(m & ((1ull << lane) - 1ull));
         const int dst = ok ? below : nv + (lane - below);
         myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
+        if (MODE == MIREC_IN_SPARSE) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
       }
       cnt = nv;
     }
+    if (MODE != MIREC_IN_SPARSE) myr = myc;
     float myw = 1.f;
-    int myr = myc;
     if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
       if (lane < cnt) myw = a.dinv[myc];
-    }
-    if (MODE == MIREC_IN_SPARSE) {
-      myr = lane < cnt ? a.slot[myc] : 0;
-      if (myr < 0) {  // defensive: a masked-in node without a seed row
-        myr = 0;
-        myw = 0.f;
-      }
     }
     for (int k = 0; k < cnt; k += G * UNROLL) {
       float4 v[UNROLL];
@@ -162,8 +161,9 @@ __device__ __forceinline__ float4 gather_narrow(const PropK &a, int64_t beg, int
   for (int64_t c = beg; c < end; c += LPR) {
     int cnt = (int)min((int64_t)LPR, end - c);
     int myc = sub < cnt ? a.col[c + sub] : 0;
+    int myr = (MODE == MIREC_IN_SPARSE) ? (sub < cnt ? a.slot[myc] : -1) : myc;
     if (MASKED) {
-      const bool ok = sub < cnt && bit_set(a.in_mask, myc);
+      const bool ok = sub < cnt && (MODE == MIREC_IN_SPARSE ? myr >= 0 : bit_set(a.in_mask, myc));
       const unsigned long long bal = __ballot(ok);
       const unsigned long long gm =
           (LPR == 64) ? bal : ((bal >> gbase) & ((1ull << LPR) - 1ull));
@@ -173,20 +173,14 @@ __device__ __forceinline__ float4 gather_narrow(const PropK &a, int64_t beg, int
         const int below = __popcll(gm & ((1ull << sub) - 1ull));
         const int dst = gbase + (ok ? below : nv + (sub - below));
         myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
+        if (MODE == MIREC_IN_SPARSE) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
       }
       cnt = nv;
     }
+    if (MODE != MIREC_IN_SPARSE) myr = myc;
     float myw = 1.f;
-    int myr = myc;
     if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
       if (sub < cnt) myw = a.dinv[myc];
-    }
-    if (MODE == MIREC_IN_SPARSE) {
-      myr = sub < cnt ? a.slot[myc] : 0;
-      if (myr < 0) {
-        myr = 0;
-        myw = 0.f;
-      }
     }
     for (int k = 0; k < cnt; k += UNROLL) {
       float4 v[UNROLL];
@@ -262,23 +256,25 @@ constexpr int kWavesPerBlock = 4;
 // own row (gather_narrow); otherwise the wave walks them one by one with the
 // whole wave per row (gather_rows).  Segment phase: wave row_waves + s
 // gathers segment s of a long row into `partial`.
+// With a row list the list length is known only on the device: the grid is
+// capped (kListBlocks) and blocks stride over the list's work items, so a
+// short list does not pay for its host-side capacity in empty waves.
 // MASKED = in_mask filter on neighbours, ROWMASK = row_mask filter on rows
 // (separate instantiations so profiles tell full and pruned launches apart).
 template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
-__global__ __launch_bounds__(256) void prop_kernel(PropK a) {
+__device__ __forceinline__ void prop_work(const PropK &a, int64_t w, int64_t nrows,
+                                          int64_t row_waves) {
   constexpr int LPR = D / 4;
   constexpr int G = 64 / LPR;
   constexpr int NARROW_UNROLL = UNROLL < 4 ? 4 : UNROLL;
   const int lane = threadIdx.x & 63;
   const int sub = lane % LPR;
   const int grp = lane / LPR;
-  const int64_t w = (int64_t)blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
-  if (w < a.row_waves) {
-    const int64_t nrows = a.row_list != nullptr ? (int64_t)*a.row_count : a.n_rows;
+  if (w < row_waves) {
     const int64_t idx = w * G + grp;
     bool have = idx < nrows;
     int32_t row = 0;
-    if (have) row = a.row_list != nullptr ? a.row_list[idx] : (int32_t)idx;
+    if (have) row = (ROWMASK && a.row_list != nullptr) ? a.row_list[idx] : (int32_t)idx;
     if (ROWMASK && have) have = bit_set(a.row_mask, row);
     int64_t beg = 0, end = 0;
     if (have) {
@@ -304,7 +300,7 @@ __global__ __launch_bounds__(256) void prop_kernel(PropK a) {
       if (lane < LPR) row_epilogue<D>(a, r, s, sub);
     }
   } else {
-    const int64_t sg = w - a.row_waves;
+    const int64_t sg = w - row_waves;
     if (sg >= a.n_seg) return;
     const int64_t row = a.seg_row[sg];
     if (ROWMASK && !bit_set(a.row_mask, row)) return;
@@ -313,6 +309,97 @@ __global__ __launch_bounds__(256) void prop_kernel(PropK a) {
     float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, beg, end, lane);
     s = combine_groups<D>(s);
     if (lane < LPR) st4(a.partial + sg * D + sub * 4, s);
+  }
+}
+
+// One row gathered by the whole 256-thread workgroup: wave q takes the q-th
+// quarter of the row's entries, the four wave sums are added in wave order
+// through LDS (deterministic), wave 0 runs the epilogue.  Block-uniform
+// control flow (contains barriers).
+template <int D, int UNROLL, int MODE, bool MASKED>
+__device__ __forceinline__ void block_row(const PropK &a, int32_t row) {
+  constexpr int LPR = D / 4;
+  __shared__ float4 red[kWavesPerBlock - 1][LPR];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int sub = lane % LPR;
+  const int64_t beg = a.rowptr[row], end = a.rowptr[row + 1];
+  if (a.split > 0 && end - beg > a.split) return;  // segments handle it (uniform)
+  const int64_t q = (end - beg + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int64_t wb = min(beg + wid * q, end), we = min(wb + q, end);
+  float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, wb, we, lane);
+  s = combine_groups<D>(s);
+  if (wid > 0 && lane < LPR) red[wid - 1][sub] = s;
+  __syncthreads();
+  if (wid == 0 && lane < LPR) {
+#pragma unroll
+    for (int k = 0; k < kWavesPerBlock - 1; ++k) s = f4_add(s, red[k][sub]);
+    row_epilogue<D>(a, row, s, sub);
+  }
+  __syncthreads();  // red[] is reused by the block's next row
+}
+
+// One row gathered by one wave.
+template <int D, int UNROLL, int MODE, bool MASKED>
+__device__ __forceinline__ void wave_row(const PropK &a, int32_t row) {
+  constexpr int LPR = D / 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t beg = a.rowptr[row], end = a.rowptr[row + 1];
+  if (a.split > 0 && end - beg > a.split) return;  // segments handle it
+  float4 s = gather_rows<D, UNROLL, MODE, MASKED>(a, beg, end, lane);
+  s = combine_groups<D>(s);
+  if (lane < LPR) row_epilogue<D>(a, row, s, lane % LPR);
+}
+
+constexpr int64_t kListBlocks = 4096;  // 2 x the waves resident at 8/SIMD
+
+#ifndef MIREC_PROP_MIN_WAVES
+#define MIREC_PROP_MIN_WAVES 7
+#endif
+// Occupancy floor (waves per SIMD): keeps the register allocator at <= 72
+// VGPRs so 7-8 waves per SIMD keep enough gathers in flight.
+template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIREC_PROP_MIN_WAVES, 8)))
+void prop_kernel(PropK a) {
+  constexpr int G = 64 / (D / 4);
+  // wave index made provably uniform (SGPR): loop control stays scalar
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if constexpr (!ROWMASK) {
+    prop_work<D, UNROLL, MODE, MASKED, ROWMASK>(a, (int64_t)blockIdx.x * kWavesPerBlock + wid,
+                                                a.n_rows, a.row_waves);
+  } else {
+    if (a.row_list == nullptr) {
+      prop_work<D, UNROLL, MODE, MASKED, ROWMASK>(a, (int64_t)blockIdx.x * kWavesPerBlock + wid,
+                                                  a.n_rows, a.row_waves);
+      return;
+    }
+    // List mode: the list lengths are known only on the device, so the grid
+    // is capped (kListBlocks) and blocks stride over the work: first one
+    // block per wide row, then G rows per wave of the narrow list, then the
+    // long-row segments.
+    // SPARSE launches mostly scan indices (few seeded neighbours): a wave
+    // per wide row is enough there; gathering launches use a workgroup.
+    constexpr int WPB = (MODE == MIREC_IN_SPARSE) ? kWavesPerBlock : 1;  // wide rows / block
+    const int64_t n_wide = a.wide_list != nullptr ? (int64_t)*a.wide_count : 0;
+    const int64_t wide_blocks = (n_wide + WPB - 1) / WPB;
+    const int64_t nrows = *a.row_count;
+    const int64_t row_waves = (nrows + G - 1) / G;
+    const int64_t waves = row_waves + a.n_seg;
+    const int64_t total = wide_blocks + (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+#pragma unroll 1
+    for (int64_t b = blockIdx.x; b < total; b += gridDim.x) {
+      if (b < wide_blocks) {
+        if constexpr (WPB == 1) {
+          block_row<D, UNROLL, MODE, MASKED>(a, a.wide_list[b]);
+        } else {
+          const int64_t i = b * WPB + wid;
+          if (i < n_wide) wave_row<D, UNROLL, MODE, MASKED>(a, a.wide_list[i]);
+        }
+      } else {
+        const int64_t w = (b - wide_blocks) * kWavesPerBlock + wid;
+        if (w < waves) prop_work<D, UNROLL, MODE, MASKED, ROWMASK>(a, w, nrows, row_waves);
+      }
+    }
   }
 }
 
@@ -349,7 +436,11 @@ static int launch_prop(const mirec_csr_t *c, PropK k, int64_t list_cap, int mode
   const int64_t rows = k.row_list != nullptr ? list_cap : c->n_rows;
   k.row_waves = (rows + G - 1) / G;
   const int64_t work = k.row_waves + c->n_seg;
-  const int64_t blocks = (work + kWavesPerBlock - 1) / kWavesPerBlock;
+  int64_t blocks = (work + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (k.row_list != nullptr) {
+    if (k.wide_list != nullptr) blocks += list_cap;
+    blocks = std::min(blocks, kListBlocks);
+  }
   const bool masked = k.in_mask != nullptr;
   if (blocks > 0) {
     const dim3 g((unsigned)blocks);
@@ -361,7 +452,7 @@ static int launch_prop(const mirec_csr_t *c, PropK k, int64_t list_cap, int mode
       launch_main<D, UNROLL, MIREC_IN_RAW, false>(g, st, k);
     else if (mode == MIREC_IN_RAW)
       launch_main<D, UNROLL, MIREC_IN_RAW, true>(g, st, k);
-    else if (mode == MIREC_IN_SPARSE)
+    else if (mode == MIREC_IN_SPARSE)  // always filtered (by slot >= 0)
       launch_main<D, UNROLL, MIREC_IN_SPARSE, true>(g, st, k);
     else
       launch_main<D, UNROLL, MIREC_IN_NONE, false>(g, st, k);
@@ -398,7 +489,7 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   if (!dim_supported(p->dim)) return MIREC_ERR_DIM;
   MIREC_CHECK_ARG(p->in_mode >= 0 && p->in_mode <= 3);
   if (p->in_mode == MIREC_IN_SPARSE)
-    MIREC_CHECK_ARG(p->slot != nullptr && p->seed_in != nullptr && p->in_mask != nullptr);
+    MIREC_CHECK_ARG(p->slot != nullptr && p->seed_in != nullptr);
   else if (p->in_mode != MIREC_IN_NONE)
     MIREC_CHECK_ARG(p->x_in != nullptr);
   MIREC_CHECK_ARG(p->in_mode != MIREC_IN_NONE || p->in_mask == nullptr);
@@ -407,6 +498,7 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   MIREC_CHECK_ARG(p->divisor != 0.f);
   MIREC_CHECK_ARG(p->row_list == nullptr ||
                   (p->row_count != nullptr && p->row_list_cap >= 0 && p->row_mask != nullptr));
+  MIREC_CHECK_ARG(p->wide_list == nullptr || (p->row_list != nullptr && p->wide_count != nullptr));
   if (c->n_seg > 0) {
     MIREC_CHECK_ARG(c->split > 0 && c->seg_row && c->seg_beg && c->long_rows && c->long_segptr);
     if (p->partial == nullptr) return MIREC_ERR_WORKSPACE;
@@ -441,6 +533,8 @@ extern "C" int mirec_propagate(const mirec_csr_t *c, const mirec_prop_t *p,
   k.row_count = p->row_count;
   k.row_waves = 0;
   k.narrow_max = p->narrow_max;
+  k.wide_list = p->wide_list;
+  k.wide_count = p->wide_count;
   const int64_t cap = p->row_list_cap;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (p->dim) {

@@ -4,8 +4,10 @@ One training step (the reference's ``stageOne``, model/lgcn.py:127-133, on
 top of ``bpr_loss`` :98-118 and ``forward`` :78-86) runs as ~2L+8 HIP
 launches with no host synchronisation:
 
-  frontier (1-2)          S = batch nodes, F1 = S ∪ N(S) as byte maps
-  forward  (1 + L)        x~_0 = dinv ⊙ E, then x_l = Â x_{l-1};
+  frontier (3-4)          S = batch nodes, F1 = S ∪ N(S) as byte maps and
+                          row lists
+  forward  (L [+1])       x~_0 = dinv ⊙ E (skipped when the previous step's
+                          fused update already wrote it), x_l = Â x_{l-1};
                           acc = x_0 + ... + x_L; out = acc/(L+1).  Every
                           layer gathers pre-scaled rows x~ = dinv ⊙ x written
                           by the previous epilogue; layer L runs on S only,
@@ -16,15 +18,17 @@ launches with no host synchronisation:
   backward (L launches)   Horner: g_L = d, g_l = d + Â g_{l+1} (Â symmetric:
                           the backward SpMM is the forward kernel on the
                           same CSR).  The first backward layer gathers only
-                          the seeded neighbours (IN_SPARSE, S byte map) and is
-                          written on F1 only; the second skips neighbours
+                          the seeded neighbours (IN_SPARSE: slot[j] >= 0) and
+                          is written on F1 only; the second skips neighbours
                           outside F1; the last one adds the reg seed and
                           applies Adam to E in its epilogue, so the dense
-                          gradient is never written to HBM.
+                          gradient is never written to HBM; it also writes
+                          dinv ⊙ E_new, the next step's x~_0.
   reset    (1)            slot[] back to -1 for the touched nodes.
 
-For data parallelism (dist.py) the last layer writes the dense gradient
-instead and the caller all-reduces it before ``adam_step``.
+For data parallelism (dist.py) the ranks exchange their gradient seeds
+before the backward (sparse mode), or the last layer writes the dense
+gradient and the caller all-reduces it before ``adam_step`` (dense mode).
 """
 from __future__ import annotations
 
@@ -60,6 +64,16 @@ def prop_launch_bytes(in_mode: int, n_nodes: int, nnz: int, dim: int, *, slot=Fa
     return b
 
 
+# Generation counter of raw-pointer writes to parameter tables (kernels do
+# not bump torch's version counter); part of the engine's prescale token.
+_raw_writes = 0
+
+
+def _note_raw_write():
+    global _raw_writes
+    _raw_writes += 1
+
+
 class AdamState:
     """torch.optim.Adam state for one dense parameter, in torch's layout."""
 
@@ -91,6 +105,7 @@ class AdamState:
         if g is None:
             return
         hp = self.next_hparams()
+        _note_raw_write()
         check(lib.mirec_adam_dense(self.param.data_ptr(), g.contiguous().data_ptr(),
                                    self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
                                    self.param.numel(), ctypes.byref(hp), _lib.stream_handle()),
@@ -154,6 +169,15 @@ class PropagationEngine:
         self.self_list = torch.zeros(3 * self.max_batch, **i32)  # S, deduplicated
         self.self_count = torch.zeros(1, **i32)
         self._self_cap = 0
+        # S and F1 as row lists split by degree (narrow: <= narrow_max,
+        # gathered G rows per wave; wide: one workgroup per row)
+        cap = N if self.prune else 1
+        self.s_lists = (torch.zeros(cap, **i32), torch.zeros(cap, **i32))
+        self.hop_lists = (torch.zeros(cap, **i32), torch.zeros(cap, **i32))
+        self.list_counts = torch.zeros(4, **i32)  # S narrow, S wide, F1 narrow, F1 wide
+        # tuning switches (tools/bench_variants.py)
+        self.use_hop_list = True      # F1 launches walk hop_list (else: byte map)
+        self.reuse_prescaled = True   # fused update writes the next x~_0
         self._masks_ready = False
         # rows of degree <= narrow_max are gathered one per lane group
         self.narrow_max = 64
@@ -176,6 +200,10 @@ class PropagationEngine:
         self.prop_events = None
         self._seeds = None
         self._merged = None
+        # (data_ptr, _version) of the table x0s = dinv ⊙ E was last written
+        # for by a fused-Adam backward (which emits it for free); forward()
+        # skips the prescale pass when the table is unchanged since.
+        self._x0s_token = None
 
     # ------------------------------------------------------------ internals
     def _ensure_ws(self, batch: int):
@@ -189,7 +217,7 @@ class PropagationEngine:
     def _prop(self, *, in_mode, x_in=None, seed_in=None, seed=None, addend=None, seed2=None,
               divisor=1.0, out=None, xs_out=None, adam=None, param=None, graph=None,
               row_mask=None, in_mask=None, row_list=None, row_count=None, row_list_cap=0,
-              out_mask=None):
+              out_mask=None, wide_list=None, wide_count=None):
         g = graph or self.g
         p = Prop()
         p.dim = self.dim
@@ -218,6 +246,8 @@ class PropagationEngine:
         p.row_list = ptr(row_list)
         p.row_count = ptr(row_count)
         p.row_list_cap = int(row_list_cap)
+        p.wide_list = ptr(wide_list)
+        p.wide_count = ptr(wide_count)
         p.narrow_max = int(self.narrow_max)
         ev = self.prop_events
         if ev is not None:
@@ -241,14 +271,19 @@ class PropagationEngine:
                                  out=bool(p.out) and not om, adam=bool(p.param))
 
     def compute_frontier(self, users=None, pos=None, neg=None, keys=None, n_keys: int = 0):
-        """bm_self = S, bm_hop = S ∪ N(S) for a triple batch or a key list."""
+        """bm_self = S, bm_hop = S ∪ N(S) for a triple batch or a key list;
+        self_list = S deduplicated, hop_list = F1 as a row list (pruning)."""
         g = self.g
         if keys is not None:
-            check(lib.mirec_frontier(g.csr_ptr(), keys.data_ptr(), int(n_keys), None, None, None,
+            n = int(n_keys)
+            if self.self_list.shape[0] < n:
+                self.self_list = torch.zeros(n, dtype=torch.int32, device=g.device)
+            check(lib.mirec_frontier(g.csr_ptr(), keys.data_ptr(), n, None, None, None,
                                      0, g.n_users, self.bm_self.data_ptr(),
-                                     self.bm_hop.data_ptr(), None, None,
-                                     _lib.stream_handle()), "frontier")
-            self._self_cap = 0  # no S list for key sets
+                                     self.bm_hop.data_ptr(), self.self_list.data_ptr(),
+                                     self.self_count.data_ptr(), _lib.stream_handle()),
+                  "frontier")
+            self._self_cap = n
         else:
             B = int(users.shape[0])
             if B > self.max_batch:
@@ -259,7 +294,39 @@ class PropagationEngine:
                                      self.self_list.data_ptr(), self.self_count.data_ptr(),
                                      _lib.stream_handle()), "frontier")
             self._self_cap = 3 * B
+        if self.prune and self.use_hop_list:
+            c = self.list_counts
+            for k, (bm, (nl, wl)) in enumerate(((self.bm_self, self.s_lists),
+                                                (self.bm_hop, self.hop_lists))):
+                check(lib.mirec_mask_compact(g.csr_ptr(), bm.data_ptr(), int(self.narrow_max),
+                                             nl.data_ptr(), c[2 * k].data_ptr(),
+                                             wl.data_ptr(), c[2 * k + 1].data_ptr(),
+                                             _lib.stream_handle()), "mask_compact")
         self._masks_ready = True
+
+    def _lists(self, k, bm, lists, cap):
+        if not self.use_hop_list:
+            return dict(row_mask=bm)
+        c = self.list_counts
+        return dict(row_mask=bm, row_list=lists[0], row_count=c[2 * k], row_list_cap=cap,
+                    wide_list=lists[1], wide_count=c[2 * k + 1])
+
+    def _self_rows(self):
+        return self._lists(0, self.bm_self, self.s_lists, min(self._self_cap, self.g.n_nodes))
+
+    def _hop_rows(self):
+        return self._lists(1, self.bm_hop, self.hop_lists, self.g.n_nodes)
+
+    @staticmethod
+    def _token(emb: torch.Tensor):
+        return (emb.data_ptr(), emb._version, _raw_writes)
+
+    def invalidate_prescaled(self):
+        """Forget the cached dinv ⊙ E.  Needed only after writing the table
+        through ``.data`` (invisible to the tensor's version counter) between
+        training steps; in-place torch ops, ``load_state_dict`` and
+        re-assignment are detected."""
+        self._x0s_token = None
 
     def prescale(self, x: torch.Tensor, out: torch.Tensor):
         check(lib.mirec_prescale(x.data_ptr(), self.g.dinv.data_ptr(), self.g.n_nodes, self.dim,
@@ -278,17 +345,16 @@ class PropagationEngine:
             return self.acc
         if pruned and not self._masks_ready:
             raise RuntimeError("forward(pruned=True) needs compute_frontier() first")
-        self.prescale(emb, self.x0s)
+        if self._x0s_token != self._token(emb):
+            self.prescale(emb, self.x0s)
+            self._x0s_token = self._token(emb)
         for l in range(1, L + 1):
             last = l == L
             rows = {}
             if pruned and l == L:      # S: the deduplicated batch-node list
-                rows = dict(row_mask=self.bm_self)
-                if self._self_cap:
-                    rows.update(row_list=self.self_list, row_count=self.self_count,
-                                row_list_cap=self._self_cap)
-            elif pruned and l == L - 1:
-                rows = dict(row_mask=self.bm_hop)
+                rows = self._self_rows()
+            elif pruned and l == L - 1:  # F1 = S ∪ N(S)
+                rows = self._hop_rows()
             if pruned and l == L - 2:
                 # the layer sum is read next by layer L-1, on F1 rows only
                 rows["out_mask"] = self.bm_hop
@@ -400,6 +466,8 @@ class PropagationEngine:
         final = dict(seed2=seed_e)
         if adam is not None:
             final.update(adam=(adam, hp), param=emb)
+            if L > 0 and self.reuse_prescaled:  # the update also emits the next x~_0
+                final.update(xs_out=self.x0s)
         else:
             final.update(out=grad_out)
         if L == 0:
@@ -410,8 +478,8 @@ class PropagationEngine:
                 if first:
                     # input g_L = d lives on S only; with pruning its output
                     # g_{L-1} is written only on F1 = S ∪ N(S) (zero elsewhere)
-                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p, in_mask=self.bm_self,
-                              row_mask=self.bm_hop if (self.prune and l > 0) else None)
+                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p,
+                              **(self._hop_rows() if (self.prune and l > 0) else {}))
                 else:
                     kw = dict(in_mode=IN_PRESCALED, x_in=self.xs[(L - 2 - l) % 2],
                               in_mask=self.bm_hop if (self.prune and l == L - 2) else None)
@@ -425,8 +493,11 @@ class PropagationEngine:
                                        _lib.stream_handle()), "bpr_seed_reset")
         self._seeds = None
         self._masks_ready = False
+        self._x0s_token = self._token(emb) if (adam is not None and L > 0
+                                               and self.reuse_prescaled) else None
 
     def adam_step(self, param: torch.Tensor, grad: torch.Tensor, adam: AdamState):
+        _note_raw_write()  # the table changes behind its version counter
         hp = adam.next_hparams()
         check(lib.mirec_adam_dense(param.data_ptr(), grad.data_ptr(), adam.exp_avg.data_ptr(),
                                    adam.exp_avg_sq.data_ptr(), param.numel(), ctypes.byref(hp),

@@ -156,7 +156,8 @@ typedef struct mirec_prop {
                                skipped (nothing written); NULL = all rows */
   const uint8_t *in_mask;   /* byte map over source nodes: only neighbours
                                with byte != 0 contribute (others are exact
-                               zeros); required for MIREC_IN_SPARSE */
+                               zeros); ignored by MIREC_IN_SPARSE, which
+                               filters by slot[j] >= 0 itself */
   const uint8_t *out_mask;  /* byte map: rows with byte 0 skip the `out`
                                write and the addend read (their xs_out is
                                still written); ignored with fused Adam */
@@ -169,6 +170,12 @@ typedef struct mirec_prop {
                                per lane group (latency-bound short rows);
                                longer ones one per wave.  0 = always wave */
   int32_t _pad2;
+  const int32_t *wide_list; /* optional second list (with row_list): rows
+                               wide_list[0 .. *wide_count) are gathered by a
+                               whole 256-thread workgroup each (4 waves split
+                               the row, combined in LDS in a fixed order), so
+                               a short list of long rows is not latency-bound */
+  const int32_t *wide_count;
 } mirec_prop_t;
 
 int mirec_propagate(const mirec_csr_t *csr, const mirec_prop_t *p,
@@ -189,6 +196,18 @@ int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    int64_t batch, int64_t n_users, uint8_t *bm_self,
                    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
                    mirec_stream_t stream);
+
+/* Row lists of the nodes whose byte in the byte map bm[csr->n_rows] is
+ * non-zero (16-byte aligned map): nodes of degree <= narrow_max (or all, if
+ * wide_list is NULL) go to list[0 .. *count), the others to
+ * wide_list[0 .. *wide_count); each list is ascending within runs of 4096
+ * nodes, runs in no particular order (the result of a propagation does not
+ * depend on list order).  Capacity: n_rows each.  Feeds the row_list /
+ * wide_list of mirec_prop_t for the frontier-pruned launches. */
+int mirec_mask_compact(const mirec_csr_t *csr, const uint8_t *bm,
+                       int32_t narrow_max, int32_t *list, int32_t *count,
+                       int32_t *wide_list, int32_t *wide_count,
+                       mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */

@@ -161,6 +161,91 @@ def test_deterministic(golden):
     assert torch.equal(res[0][1], res[1][1])
 
 
+def test_prescale_reuse_tracks_table_writes(golden):
+    """The fused update emits the next step's dinv ⊙ E; the engine reuses it
+    only while the table is untouched (version counter, raw kernel writes)."""
+    f = golden("lgcn_d64_L3.npz")
+    t = torch.from_numpy(f["triples"])
+    tc = t.cuda()
+
+    def run(force):
+        m = lgcn_from(f)
+        w = m.all_embedding.weight
+
+        def step():
+            if force:
+                m.engine.invalidate_prescaled()
+            m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+        step()
+        step()
+        with torch.no_grad():
+            w.mul_(0.5)                      # torch in-place: version bump
+        step()
+        m.optim.zero_grad()
+        loss, reg = m.bpr_loss(tc[:, 0], tc[:, 1], tc[:, 2])
+        (loss + float(f["decay"]) * reg).backward()
+        m.optim.step()                       # HIP Adam kernel: raw write
+        step()
+        w.data.add_(0.01)                    # invisible to the version counter
+        m.engine.invalidate_prescaled()
+        step()
+        return w.detach().clone()
+    assert torch.equal(run(False), run(True))
+
+
+@pytest.mark.parametrize("split", [None, 64])
+def test_frontier_sets_and_lists(split):
+    """S / F1 byte maps, the deduplicated S list and the F1 row list vs host
+    set arithmetic (triples and key-list forms, sentinel keys, long rows)."""
+    from furusato_recommend_amd import Graph
+    from furusato_recommend_amd.engine import PropagationEngine
+    rng = np.random.default_rng(3)
+    n_users, m_items, E = 5000, 700, 60000
+    u = rng.integers(0, n_users, E)
+    i = np.minimum(rng.zipf(1.3, E) - 1, m_items - 1)  # hot items -> long rows
+    g = Graph.from_interactions(u, i, n_users, m_items, device="cuda:0",
+                                **({} if split is None else {"split": split}))
+    if split is not None:
+        assert g.n_long > 0
+    eng = PropagationEngine(g, 32, 3, max_batch=700, prune=True)
+    rowptr = g.rowptr.cpu().numpy()
+    col = g.col.cpu().numpy()
+    N = g.n_nodes
+
+    def check_sets(S):
+        S = set(int(x) for x in S)
+        F1 = set(S)
+        for x in S:
+            F1.update(int(c) for c in col[rowptr[x]:rowptr[x + 1]])
+        bs = eng.bm_self.view(torch.uint8)[:N].cpu().numpy()
+        bh = eng.bm_hop.view(torch.uint8)[:N].cpu().numpy()
+        assert set(np.nonzero(bs)[0].tolist()) == S
+        assert set(np.nonzero(bh)[0].tolist()) == F1
+        ns = int(eng.self_count.item())
+        sl = eng.self_list[:ns].cpu().numpy()
+        assert ns == len(S) and set(sl.tolist()) == S
+        deg = np.diff(rowptr)
+        cnt = eng.list_counts.cpu().numpy()
+        for k, (want, lists) in enumerate(((S, eng.s_lists), (F1, eng.hop_lists))):
+            nl = lists[0][:cnt[2 * k]].cpu().numpy()
+            wl = lists[1][:cnt[2 * k + 1]].cpu().numpy()
+            both = np.concatenate([nl, wl])
+            assert len(both) == len(want) and set(both.tolist()) == want
+            assert (deg[nl] <= eng.narrow_max).all() and (deg[wl] > eng.narrow_max).all()
+
+    B = 700
+    us = torch.from_numpy(rng.integers(0, n_users, B)).int().cuda()
+    ps = torch.from_numpy(rng.integers(0, m_items, B)).int().cuda()
+    ns_ = torch.from_numpy(rng.integers(0, m_items, B)).int().cuda()
+    eng.compute_frontier(us, ps, ns_)
+    S = np.concatenate([us.cpu().numpy(), n_users + ps.cpu().numpy(),
+                        n_users + ns_.cpu().numpy()])
+    check_sets(S)
+    keys = np.concatenate([rng.integers(0, N, 3000), [N, N, -1]]).astype(np.int32)
+    eng.compute_frontier(keys=torch.from_numpy(keys).cuda(), n_keys=len(keys))
+    check_sets(keys[(keys >= 0) & (keys < N)])
+
+
 def test_sampler_invariants():
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     ds = SyntheticBipartite(500, 300, 6000, seed=3, test_frac=0)
