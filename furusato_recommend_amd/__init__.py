@@ -10,10 +10,11 @@ from ._lib import LIB_PATH, MirecError  # noqa: F401  (fails loudly if not built
 from .dataloader import FiveCore, Loader, SyntheticBipartite  # noqa: F401
 from .graph import Graph  # noqa: F401
 from .graphsage import GraphSAGE  # noqa: F401
+from .lgconv import LGConv  # noqa: F401
 from .lightgcn import LightGCN  # noqa: F401
 from .mf import MF  # noqa: F401
 from .sasrec import SASRec  # noqa: F401
 from .register import MODELS  # noqa: F401
 
-__all__ = ["LightGCN", "MF", "GraphSAGE", "SASRec", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
+__all__ = ["LGConv", "LightGCN", "MF", "GraphSAGE", "SASRec", "Graph", "Loader", "SyntheticBipartite", "FiveCore", "MODELS",
            "MirecError", "LIB_PATH"]

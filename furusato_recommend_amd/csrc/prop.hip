@@ -97,10 +97,13 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64
     int cnt = (int)min((int64_t)64, end - base);
     int myc = lane < cnt ? a.col[base + lane] : 0;
     // SPARSE: the seed-row slot itself is the filter (slot >= 0 <=> node in
-    // S), one dependent load less than a byte-map test followed by the slot.
-    int myr = (MODE == MIREC_IN_SPARSE) ? (lane < cnt ? a.slot[myc] : -1) : myc;
+    // S), one dependent load less than a byte-map test followed by the slot
+    // (with an in_mask, SPARSE tests the byte map first and reads the slot
+    // of the hits only: fewer slot reads when many neighbours are seeded)
+    const bool slot_filter = MODE == MIREC_IN_SPARSE && a.in_mask == nullptr;
+    int myr = slot_filter ? (lane < cnt ? a.slot[myc] : -1) : myc;
     if (MASKED) {
-      const bool ok = lane < cnt && (MODE == MIREC_IN_SPARSE ? myr >= 0 : bit_set(a.in_mask, myc));
+      const bool ok = lane < cnt && (slot_filter ? myr >= 0 : bit_set(a.in_mask, myc));
       const unsigned long long m = __ballot(ok);
       const int nv = __popcll(m);
       if (nv == 0) continue;  // wave-uniform
@@ -108,14 +111,19 @@ __device__ __forceinline__ float4 gather_rows(const PropK &a, int64_t beg, int64
         const int below = __popcll(m & ((1ull << lane) - 1ull));
         const int dst = ok ? below : nv + (lane - below);
         myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
-        if (MODE == MIREC_IN_SPARSE) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
+        if (slot_filter) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
       }
       cnt = nv;
     }
     if (MODE != MIREC_IN_SPARSE) myr = myc;
+    else if (!slot_filter) myr = lane < cnt ? a.slot[myc] : 0;
     float myw = 1.f;
     if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
       if (lane < cnt) myw = a.dinv[myc];
+    }
+    if (MODE == MIREC_IN_SPARSE && myr < 0) {  // byte map set without a seed row
+      myr = 0;
+      myw = 0.f;
     }
     for (int k = 0; k < cnt; k += G * UNROLL) {
       float4 v[UNROLL];
@@ -161,9 +169,10 @@ __device__ __forceinline__ float4 gather_narrow(const PropK &a, int64_t beg, int
   for (int64_t c = beg; c < end; c += LPR) {
     int cnt = (int)min((int64_t)LPR, end - c);
     int myc = sub < cnt ? a.col[c + sub] : 0;
-    int myr = (MODE == MIREC_IN_SPARSE) ? (sub < cnt ? a.slot[myc] : -1) : myc;
+    const bool slot_filter = MODE == MIREC_IN_SPARSE && a.in_mask == nullptr;
+    int myr = slot_filter ? (sub < cnt ? a.slot[myc] : -1) : myc;
     if (MASKED) {
-      const bool ok = sub < cnt && (MODE == MIREC_IN_SPARSE ? myr >= 0 : bit_set(a.in_mask, myc));
+      const bool ok = sub < cnt && (slot_filter ? myr >= 0 : bit_set(a.in_mask, myc));
       const unsigned long long bal = __ballot(ok);
       const unsigned long long gm =
           (LPR == 64) ? bal : ((bal >> gbase) & ((1ull << LPR) - 1ull));
@@ -173,14 +182,19 @@ __device__ __forceinline__ float4 gather_narrow(const PropK &a, int64_t beg, int
         const int below = __popcll(gm & ((1ull << sub) - 1ull));
         const int dst = gbase + (ok ? below : nv + (sub - below));
         myc = __builtin_amdgcn_ds_permute(dst << 2, myc);
-        if (MODE == MIREC_IN_SPARSE) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
+        if (slot_filter) myr = __builtin_amdgcn_ds_permute(dst << 2, myr);
       }
       cnt = nv;
     }
     if (MODE != MIREC_IN_SPARSE) myr = myc;
+    else if (!slot_filter) myr = sub < cnt ? a.slot[myc] : 0;
     float myw = 1.f;
     if (MODE == MIREC_IN_RAW || MODE == MIREC_IN_SPARSE) {
       if (sub < cnt) myw = a.dinv[myc];
+    }
+    if (MODE == MIREC_IN_SPARSE && myr < 0) {  // byte map set without a seed row
+      myr = 0;
+      myw = 0.f;
     }
     for (int k = 0; k < cnt; k += UNROLL) {
       float4 v[UNROLL];

@@ -178,6 +178,10 @@ class PropagationEngine:
         # tuning switches (tools/bench_variants.py)
         self.use_hop_list = True      # F1 launches walk hop_list (else: byte map)
         self.reuse_prescaled = True   # fused update writes the next x~_0
+        # first backward layer's neighbour filter: "slot" (one dependent load;
+        # best for one batch), "bytemap" (S byte map, then the slot of the
+        # hits; best for the union of many ranks' seeds) or "auto"
+        self.sparse_filter = "auto"
         self._masks_ready = False
         # rows of degree <= narrow_max are gathered one per lane group
         self.narrow_max = 64
@@ -310,6 +314,12 @@ class PropagationEngine:
         c = self.list_counts
         return dict(row_mask=bm, row_list=lists[0], row_count=c[2 * k], row_list_cap=cap,
                     wide_list=lists[1], wide_count=c[2 * k + 1])
+
+    def _sparse_filter(self):
+        f = self.sparse_filter
+        if f == "auto":
+            f = "bytemap" if self._self_cap > 3 * self.max_batch else "slot"
+        return self.bm_self if f == "bytemap" else None
 
     def _self_rows(self):
         return self._lists(0, self.bm_self, self.s_lists, min(self._self_cap, self.g.n_nodes))
@@ -478,7 +488,7 @@ class PropagationEngine:
                 if first:
                     # input g_L = d lives on S only; with pruning its output
                     # g_{L-1} is written only on F1 = S ∪ N(S) (zero elsewhere)
-                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p,
+                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p, in_mask=self._sparse_filter(),
                               **(self._hop_rows() if (self.prune and l > 0) else {}))
                 else:
                     kw = dict(in_mode=IN_PRESCALED, x_in=self.xs[(L - 2 - l) % 2],
@@ -516,6 +526,27 @@ class PropagationEngine:
         loss = self.bpr(out, emb, users, pos, neg, decay, loss_accum)
         self.backward(emb, adam=adam)
         return loss
+
+
+def propagate(graph: Graph, x: torch.Tensor, out: torch.Tensor):
+    """out = Â x on ``graph`` (one LGConv call; x, out: contiguous fp32
+    [n_nodes, D] device tensors, D in SUPPORTED_DIMS)."""
+    n, D = x.shape
+    if D not in _lib.SUPPORTED_DIMS or n != graph.n_nodes or out.shape != x.shape:
+        raise ValueError(f"propagate: x {tuple(x.shape)}, out {tuple(out.shape)}, "
+                         f"graph of {graph.n_nodes} nodes")
+    if x.dtype != torch.float32 or not (x.is_contiguous() and out.is_contiguous()):
+        raise ValueError("propagate: contiguous float32 tensors required")
+    p = Prop()
+    p.dim = D
+    p.in_mode = IN_RAW
+    p.x_in = x.data_ptr()
+    p.divisor = 1.0
+    p.out = out.data_ptr()
+    p.partial = ptr(graph.partial_buffer(D))
+    p.narrow_max = 64
+    check(lib.mirec_propagate(graph.csr_ptr(), ctypes.byref(p), _lib.stream_handle()),
+          "propagate")
 
 
 def sample_triples(graph: Graph, batch: int, seed: int, offset: int, users, pos, neg, err,

@@ -89,8 +89,10 @@ class Graph:
 
     @classmethod
     def from_edge_index(cls, edge_index, n_nodes: int, device,
-                        split: int = DEFAULT_SPLIT) -> "Graph":
-        """Generic LGConv graph: edge_index[0] = source, [1] = target."""
+                        split: int = DEFAULT_SPLIT, normalize: bool = True) -> "Graph":
+        """Generic LGConv graph: edge_index[0] = source, [1] = target (PyG
+        flow source_to_target; degree = in-degree at the target, multi-edges
+        counted).  ``normalize=False``: plain neighbour sum (dinv = 1)."""
         ei = np.ascontiguousarray(np.asarray(edge_index, dtype=np.int64))
         src, dst = np.ascontiguousarray(ei[0]), np.ascontiguousarray(ei[1])
         nnz = src.shape[0]
@@ -100,6 +102,8 @@ class Graph:
         check(lib.mirec_csr_from_coo(src.ctypes.data, dst.ctypes.data, nnz, n_nodes,
                                      rowptr.ctypes.data, col.ctypes.data, dinv.ctypes.data),
               "csr_from_coo")
+        if not normalize:
+            dinv[:] = 1.0
         # Is the edge multiset symmetric?  Then Âᵀ = Â (same CSR for backward).
         fwd = np.sort(src * n_nodes + dst)
         bwd = np.sort(dst * n_nodes + src)

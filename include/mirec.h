@@ -156,8 +156,11 @@ typedef struct mirec_prop {
                                skipped (nothing written); NULL = all rows */
   const uint8_t *in_mask;   /* byte map over source nodes: only neighbours
                                with byte != 0 contribute (others are exact
-                               zeros); ignored by MIREC_IN_SPARSE, which
-                               filters by slot[j] >= 0 itself */
+                               zeros).  MIREC_IN_SPARSE filters by
+                               slot[j] >= 0 when in_mask is NULL, else by
+                               the byte map first (must cover the seeded
+                               nodes; fewer slot reads when many neighbours
+                               are seeded) */
   const uint8_t *out_mask;  /* byte map: rows with byte 0 skip the `out`
                                write and the addend read (their xs_out is
                                still written); ignored with fused Adam */

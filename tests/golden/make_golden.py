@@ -62,9 +62,15 @@ def install_shims():
     pgc = types.ModuleType("torch_geometric.nn.conv")
 
     class LGConv(torch.nn.Module):
+        def __init__(self, normalize: bool = True):
+            super().__init__()
+            self.normalize = normalize
+
         def forward(self, x, edge_index):
             row, col = edge_index[0], edge_index[1]
             n = x.size(0)
+            if not self.normalize:
+                return torch.zeros_like(x).index_add_(0, col, x[row])
             deg = torch.zeros(n, dtype=x.dtype).index_add_(0, col, torch.ones(col.numel(), dtype=x.dtype))
             dinv = deg.pow(-0.5)
             dinv.masked_fill_(dinv == float("inf"), 0)
@@ -232,6 +238,57 @@ def make_sage_golden(ds, u, i, n_users, m_items):
     print("sage", float(loss))
 
 
+def skewed_graph(seed, n, m_per_node, directed):
+    """Cora-like (2708 nodes, ~5.3 K undirected edges, hub degree ~170)
+    preferential-attachment graph with duplicate edges and isolated nodes
+    (stands in for notebooks/Cora/raw/ind.cora.graph, which is a pickle and is
+    not loaded)."""
+    rng = np.random.default_rng(seed)
+    src, dst = [], []
+    targets = [0, 1]
+    for v in range(2, n - 2):  # the last two nodes stay isolated
+        k = min(m_per_node, len(targets))
+        picks = rng.choice(len(targets), size=k, replace=True)
+        for t in picks:
+            src.append(v)
+            dst.append(targets[t])
+        targets.extend([targets[t] for t in picks] + [v] * k)
+    src, dst = np.array(src), np.array(dst)
+    if directed:
+        flip = rng.random(src.size) < 0.3
+        src, dst = np.where(flip, dst, src), np.where(flip, src, dst)
+        return np.stack([src, dst])
+    return np.concatenate([np.stack([src, dst]), np.stack([dst, src])], 1)
+
+
+def make_graph_op_golden():
+    """Operator-level fixtures: LGConv(x, edge_index) on non-bipartite graphs
+    (PyG semantics, model/lgcn.py:66,82), its input gradient, and the
+    normalize=False variant."""
+    from torch_geometric.nn.conv import LGConv  # the shim (PyG algorithm)
+    out = {}
+    cases = {"sym": (2708, 2, False, (16, 48)), "dir": (500, 3, True, (64, 256))}
+    for name, (n, mper, directed, dims) in cases.items():
+        ei = skewed_graph(17 if directed else 16, n, mper, directed)
+        out[f"{name}_edge_index"] = ei
+        out[f"{name}_n"] = n
+        eit = torch.from_numpy(ei)
+        for d in dims:
+            g = torch.Generator().manual_seed(1000 + d)
+            x = torch.randn(n, d, generator=g).requires_grad_(True)
+            # the cotangent is regenerated by the tests from this seed
+            ybar = torch.randn(n, d, generator=torch.Generator().manual_seed(2000 + d))
+            y = LGConv()(x, eit)
+            (y * ybar).sum().backward()
+            out[f"{name}_d{d}_x"] = x.detach().numpy()
+            out[f"{name}_d{d}_y"] = y.detach().numpy()
+            out[f"{name}_d{d}_xbar"] = x.grad.numpy()
+            if d == dims[0]:
+                out[f"{name}_d{d}_y_sum"] = LGConv(normalize=False)(x.detach(), eit).numpy()
+    np.savez_compressed(os.path.join(OUT, "lgconv_graphs.npz"), **out)
+    print("lgconv graphs", {k: v.shape for k, v in out.items() if k.endswith("edge_index")})
+
+
 def make_sasrec_golden():
     """The reference's own SASRec.oneblock / forward_user (model/sasrec.py:
     385-413) with nn.MultiheadAttention, on padded sequences; dropout off."""
@@ -350,6 +407,8 @@ def main():
     make_sage_golden(ds, u, i, n_users, m_items)
 
     make_sasrec_golden()
+
+    make_graph_op_golden()
 
     # ---------------------------------------------------------------- MF
     cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",

@@ -713,3 +713,30 @@ def test_sasrec_trains():
         sample_triples(g, 2048, s, 0, u, p, n, err)
         losses.append(float(m.OneEpoch(u, p, n)))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("split", [None, 32])
+@pytest.mark.parametrize("name,d", [("sym", 16), ("sym", 48), ("dir", 64), ("dir", 256)])
+def test_lgconv_operator_matches_fixture(golden, name, d, split):
+    """LGConv()(x, edge_index) on non-bipartite (skewed, duplicate edges,
+    isolated nodes) and directed graphs: forward, input gradient (Âᵀ on the
+    transposed CSR), normalize=False; odd widths are padded."""
+    from furusato_recommend_amd import LGConv
+    from tests.test_oracle import lgconv_case
+    f = golden("lgconv_graphs.npz")
+    ei, x, y, ybar, xbar, ysum = lgconv_case(f, name, d)
+    conv = LGConv(split=split)
+    eic = ei.cuda()
+    xg = x.cuda().requires_grad_(True)
+    yg = conv(xg, eic)
+    if split is not None:
+        assert conv._graph.n_long > 0
+    assert conv._graph.symmetric == (name == "sym")
+    assert rel(yg, y) < TOL
+    (yg * ybar.cuda()).sum().backward()
+    assert rel(xg.grad, xbar) < TOL
+    g0 = conv._graph
+    conv(xg.detach(), eic)
+    assert conv._graph is g0          # CSR cached per edge_index
+    if ysum is not None:
+        assert rel(LGConv(normalize=False)(x.cuda(), eic), ysum) < TOL
