@@ -15,6 +15,8 @@
 // (head h = columns h*dh .. h*dh+dh of each third) and O / dQKV are written
 // in the same packed layouts, so the surrounding Linear layers are plain
 // library GEMMs.  Any head dim <= 64: it is zero-padded to 32 or 64 in LDS.
+#include <algorithm>
+
 #include "common.h"
 
 namespace mirec {
@@ -51,24 +53,65 @@ __device__ __forceinline__ f32x16 zero16() {
   return z;
 }
 
-// Load rows [0, T) of one head of a packed [B, T, 3d] (or [B, T, d]) tensor
-// into an LDS tile [kT][ld] (zero rows T..kT-1 and columns dh..dpad-1).
-__device__ __forceinline__ void load_head(float *dst, int ld, const float *src, int64_t row_stride,
-                                          int T, int dh, int dpad) {
-  for (int e = threadIdx.x; e < kT * dpad; e += blockDim.x) {
-    const int i = e / dpad, c = e - (e / dpad) * dpad;
-    dst[i * ld + c] = (i < T && c < dh) ? src[(int64_t)i * row_stride + c] : 0.f;
+// Load rows [0, T) of NT heads (packed [B, T, *] tensors with row strides
+// rs[t]) into LDS tiles [kT][ld] (zero rows T..kT-1 and columns dh..DPAD-1).
+// Every load of all NT tiles is issued before the first LDS store, so the
+// workgroup pays one HBM latency, not one per element.  float4 loads when
+// dh % 4 == 0 (then rows are 16-byte aligned), scalar otherwise.
+template <int DPAD, int NT>
+__device__ __forceinline__ void load_heads(float *const (&dst)[NT], const float *const (&src)[NT],
+                                           const int64_t (&rs)[NT], int ld, int T, int dh) {
+  if ((dh & 3) == 0) {
+    constexpr int C4 = DPAD / 4;
+    constexpr int PER = kT * C4 / 256;
+    float4 v[NT][PER];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * 256, i = e / C4, c = e % C4;
+        v[t][q] = (i < T && 4 * c < dh) ? ld4(src[t] + (int64_t)i * rs[t] + 4 * c) : f4_zero();
+      }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * 256, i = e / C4, c = e % C4;
+        float *d = dst[t] + i * ld + 4 * c;
+        d[0] = v[t][q].x;
+        d[1] = v[t][q].y;
+        d[2] = v[t][q].z;
+        d[3] = v[t][q].w;
+      }
+  } else {
+    constexpr int PER = kT * DPAD / 256;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      float v[PER];
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * 256, i = e / DPAD, c = e % DPAD;
+        v[q] = (i < T && c < dh) ? src[t][(int64_t)i * rs[t] + c] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int e = threadIdx.x + q * 256, i = e / DPAD, c = e % DPAD;
+        dst[t][i * ld + c] = v[q];
+      }
+    }
   }
 }
 
 // S = scale * Q Kᵀ with the causal mask, written to sS [kT][kT+1]; then
 // row softmax in place (P).  Rows >= T are computed too (finite, unused).
+// sS may alias sQ (the products are in registers before it is written).
 __device__ void scores_softmax(const float *sQ, const float *sK, int ld, float *sS, int dpad,
                                float scale) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int qi = w >> 1, qj = w & 1;
   f32x16 acc = mfma_tile<false, true>(sQ + 32 * qi * ld, ld, sK + 32 * qj * ld, ld, dpad,
                                       zero16(), lane);
+  if ((const float *)sS == sQ) __syncthreads();  // every wave is done reading sQ
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int i = 32 * qi + acc_row(r, lane), j = 32 * qj + (lane & 31);
@@ -97,24 +140,30 @@ __device__ void scores_softmax(const float *sQ, const float *sK, int ld, float *
   __syncthreads();
 }
 
+template <int DPAD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__ qkv,
                                                        float *__restrict__ out, int T, int H,
-                                                       int dh, int dpad, float scale) {
+                                                       int dh, float scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int ld = dpad + 1;
-  float *sQ = smem, *sK = sQ + kT * ld, *sV = sK + kT * ld, *sS = sV + kT * ld;
+  constexpr int ld = DPAD + 1;
+  // P overwrites Q: [sQ | sS] [sK] [sV]
+  constexpr int qs = kT * ld > kT * (kT + 1) ? kT * ld : kT * (kT + 1);
+  float *sQ = smem, *sS = smem, *sK = smem + qs, *sV = sK + kT * ld;
   const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   const float *base = qkv + (int64_t)b * T * rs + h * dh;
-  load_head(sQ, ld, base, rs, T, dh, dpad);
-  load_head(sK, ld, base + d, rs, T, dh, dpad);
-  load_head(sV, ld, base + 2 * d, rs, T, dh, dpad);
+  {
+    float *const dst[3] = {sQ, sK, sV};
+    const float *const src[3] = {base, base + d, base + 2 * d};
+    const int64_t strides[3] = {rs, rs, rs};
+    load_heads<DPAD, 3>(dst, src, strides, ld, T, dh);
+  }
   __syncthreads();
-  scores_softmax(sQ, sK, ld, sS, dpad, scale);
-  // O = P V: tiles (oi, oj) over 2 x dpad/32, strided over the 4 waves
+  scores_softmax(sQ, sK, ld, sS, DPAD, scale);
+  // O = P V: tiles (oi, oj) over 2 x DPAD/32, strided over the 4 waves
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ntiles = 2 * (dpad / 32);
+  constexpr int ntiles = 2 * (DPAD / 32);
   for (int t = w; t < ntiles; t += 4) {
     const int oi = t & 1, oj = t >> 1;
     f32x16 acc = mfma_tile<false, false>(sS + 32 * oi * (kT + 1), kT + 1, sV + 32 * oj, ld, kT,
@@ -127,28 +176,32 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__
   }
 }
 
+template <int DPAD>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__ qkv,
                                                        const float *__restrict__ dout,
                                                        float *__restrict__ dqkv, int T, int H,
-                                                       int dh, int dpad, float scale) {
+                                                       int dh, float scale) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int ld = dpad + 1;
+  constexpr int dpad = DPAD;
+  constexpr int ld = DPAD + 1;
   float *sQ = smem, *sK = sQ + kT * ld, *sV = sK + kT * ld, *sO = sV + kT * ld;
   float *sP = sO + kT * ld, *sD = sP + kT * (kT + 1);
   const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   const float *base = qkv + (int64_t)b * T * rs + h * dh;
-  load_head(sQ, ld, base, rs, T, dh, dpad);
-  load_head(sK, ld, base + d, rs, T, dh, dpad);
-  load_head(sV, ld, base + 2 * d, rs, T, dh, dpad);
-  load_head(sO, ld, dout + (int64_t)b * T * d + h * dh, d, T, dh, dpad);  // dO
+  {
+    float *const dst[4] = {sQ, sK, sV, sO};
+    const float *const src[4] = {base, base + d, base + 2 * d, dout + (int64_t)b * T * d + h * dh};
+    const int64_t strides[4] = {rs, rs, rs, (int64_t)d};  // sO = dO
+    load_heads<DPAD, 4>(dst, src, strides, ld, T, dh);
+  }
   __syncthreads();
   scores_softmax(sQ, sK, ld, sP, dpad, scale);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float *gbase = dqkv + (int64_t)b * T * rs + h * dh;
   // dV = Pᵀ dO  (rows j, cols c; K = i)
-  const int ntiles = 2 * (dpad / 32);
+  constexpr int ntiles = 2 * (dpad / 32);
   for (int t = w; t < ntiles; t += 4) {
     const int ti = t & 1, tj = t >> 1;
     f32x16 acc = mfma_tile<true, false>(sP + 32 * ti, kT + 1, sO + 32 * tj, ld, kT, zero16(), lane);
@@ -207,18 +260,20 @@ static int allow_big_lds() {
   static int rc = -1;
   if (rc < 0) {
     rc = 0;
-    if (hipFuncSetAttribute((const void *)attn_fwd_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess ||
-        hipFuncSetAttribute((const void *)attn_bwd_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
-      rc = 1;
+    const void *fns[4] = {(const void *)attn_fwd_kernel<32>, (const void *)attn_fwd_kernel<64>,
+                          (const void *)attn_bwd_kernel<32>, (const void *)attn_bwd_kernel<64>};
+    for (const void *f : fns)
+      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+          hipSuccess)
+        rc = 1;
   }
   return rc;
 }
 
 static int attn_smem(int dpad, bool bwd) {
   const int ld = dpad + 1;
-  return (int)sizeof(float) * (bwd ? (4 * kT * ld + 2 * kT * (kT + 1)) : (3 * kT * ld + kT * (kT + 1)));
+  const int qs = std::max(kT * ld, kT * (kT + 1));  // forward: P overwrites Q
+  return (int)sizeof(float) * (bwd ? (4 * kT * ld + 2 * kT * (kT + 1)) : (qs + 2 * kT * ld));
 }
 
 }  // namespace mirec
@@ -231,9 +286,15 @@ extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, i
   if (batch == 0) return MIREC_OK;
   if (allow_big_lds() != 0) return MIREC_ERR_HIP;
   const int dpad = head_dim <= 32 ? 32 : 64;
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
-                     attn_smem(dpad, false), reinterpret_cast<hipStream_t>(stream), qkv, out, T,
-                     heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));
+  const float scale = 1.f / sqrtf((float)head_dim);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)(batch * heads));
+  if (dpad == 32)
+    hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), attn_smem(32, false), st, qkv, out,
+                       T, heads, head_dim, scale);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), attn_smem(64, false), st, qkv, out,
+                       T, heads, head_dim, scale);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -247,9 +308,15 @@ extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t 
   if (batch == 0) return MIREC_OK;
   if (allow_big_lds() != 0) return MIREC_ERR_HIP;
   const int dpad = head_dim <= 32 ? 32 : 64;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3((unsigned)(batch * heads)), dim3(256),
-                     attn_smem(dpad, true), reinterpret_cast<hipStream_t>(stream), qkv, dout,
-                     dqkv, T, heads, head_dim, dpad, 1.f / sqrtf((float)head_dim));
+  const float scale = 1.f / sqrtf((float)head_dim);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const dim3 grid((unsigned)(batch * heads));
+  if (dpad == 32)
+    hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), attn_smem(32, true), st, qkv, dout,
+                       dqkv, T, heads, head_dim, scale);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), attn_smem(64, true), st, qkv, dout,
+                       dqkv, T, heads, head_dim, scale);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

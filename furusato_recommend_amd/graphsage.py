@@ -32,30 +32,10 @@ from . import _lib
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
+from .rows import _GatherRows  # noqa: F401  (used below)
 
 
 # ----------------------------------------------------------------- autograd
-class _GatherRows(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, table, ids):
-        n, d = ids.numel(), table.shape[1]
-        out = torch.empty(n, d, dtype=table.dtype, device=table.device)
-        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
-                                    _lib.stream_handle()), "gather_rows")
-        ctx.save_for_backward(ids)
-        ctx.shape = table.shape
-        return out
-
-    @staticmethod
-    def backward(ctx, grad):
-        (ids,) = ctx.saved_tensors
-        g = torch.zeros(ctx.shape, dtype=grad.dtype, device=grad.device)
-        check(lib.mirec_scatter_add_rows(grad.contiguous().data_ptr(), ids.data_ptr(),
-                                         ids.numel(), ctx.shape[1], g.data_ptr(),
-                                         _lib.stream_handle()), "scatter_add_rows")
-        return g, None
-
-
 class _FanoutMean(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, valid, k, p, seed):

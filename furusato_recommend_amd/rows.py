@@ -1,0 +1,45 @@
+"""Row gather with an atomic scatter-add backward (libmirec): the embedding
+lookup of the GraphSAGE hop path and of SASRec's sequence / item inputs.
+
+``gather_rows(table, ids)`` = ``table[ids]`` with ids < 0 giving zero rows
+(and no gradient).  Its backward adds each gradient row into the table
+gradient with float atomics (one 256-B wave instruction per 64 floats), in
+place of torch's sort-based embedding/index backward.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, ids):
+        n, d = ids.numel(), table.shape[1]
+        out = torch.empty(n, d, dtype=table.dtype, device=table.device)
+        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
+                                    _lib.stream_handle()), "gather_rows")
+        ctx.save_for_backward(ids)
+        ctx.shape = table.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (ids,) = ctx.saved_tensors
+        g = torch.zeros(ctx.shape, dtype=grad.dtype, device=grad.device)
+        check(lib.mirec_scatter_add_rows(grad.contiguous().data_ptr(), ids.data_ptr(),
+                                         ids.numel(), ctx.shape[1], g.data_ptr(),
+                                         _lib.stream_handle()), "scatter_add_rows")
+        return g, None
+
+
+def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """table[ids] for int32 ids of any shape (-1 = zero row); differentiable
+    w.r.t. ``table``.  Returns [*ids.shape, table.shape[1]]."""
+    if table.dtype != torch.float32 or table.dim() != 2 or table.shape[1] % 4:
+        raise ValueError("gather_rows: float32 [n, d] table with d % 4 == 0")
+    flat = ids.reshape(-1).to(torch.int32).contiguous()
+    out = _GatherRows.apply(table.contiguous(), flat)
+    return out.view(*ids.shape, table.shape[1])

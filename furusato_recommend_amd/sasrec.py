@@ -23,6 +23,24 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import check, lib
 from .engine import AdamState
+from .rows import gather_rows
+
+
+# Optional per-launch timing (tools/bench_sasrec.py): a list receiving
+# (kind, start_event, end_event, (B, T, heads, head_dim)).
+ATTN_EVENTS = None
+
+
+def _timed(kind, shape, launch):
+    ev = ATTN_EVENTS
+    if ev is None:
+        return launch()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    r = launch()
+    e.record()
+    ev.append((kind, s, e, shape))
+    return r
 
 
 class _CausalAttention(torch.autograd.Function):
@@ -32,8 +50,9 @@ class _CausalAttention(torch.autograd.Function):
         d = d3 // 3
         qkv = qkv.contiguous()
         out = torch.empty(B, T, d, dtype=qkv.dtype, device=qkv.device)
-        check(lib.mirec_attention_fwd(qkv.data_ptr(), B, T, heads, d // heads, out.data_ptr(),
-                                      _lib.stream_handle()), "attention_fwd")
+        _timed("fwd", (B, T, heads, d // heads), lambda: check(lib.mirec_attention_fwd(
+            qkv.data_ptr(), B, T, heads, d // heads, out.data_ptr(), _lib.stream_handle()),
+            "attention_fwd"))
         ctx.save_for_backward(qkv)
         ctx.heads = heads
         return out
@@ -42,10 +61,12 @@ class _CausalAttention(torch.autograd.Function):
     def backward(ctx, dout):
         (qkv,) = ctx.saved_tensors
         B, T, d3 = qkv.shape
+        dh = d3 // 3 // ctx.heads
         dqkv = torch.empty_like(qkv)
-        check(lib.mirec_attention_bwd(qkv.data_ptr(), dout.contiguous().data_ptr(), B, T,
-                                      ctx.heads, d3 // 3 // ctx.heads, dqkv.data_ptr(),
-                                      _lib.stream_handle()), "attention_bwd")
+        dout = dout.contiguous()
+        _timed("bwd", (B, T, ctx.heads, dh), lambda: check(lib.mirec_attention_bwd(
+            qkv.data_ptr(), dout.data_ptr(), B, T, ctx.heads, dh, dqkv.data_ptr(),
+            _lib.stream_handle()), "attention_bwd"))
         return dqkv, None
 
 
@@ -154,12 +175,15 @@ class SASRec(nn.Module):
         return self.item_last_proj(x)
 
     def sequence_input(self, users):
+        """Padded item-embedding sequences [B, T, d] (zero past `length`,
+        pad_sequence in OneEpoch, sasrec.py:449-455) and lengths.  The lookup
+        is one row gather whose backward scatter-adds into the table."""
         items = self.seq.items[users.long()]
         length = self.seq.length[users.long()]
         T = self.seq.max_len
         mask = (torch.arange(T, device=items.device)[None, :] < length[:, None])
-        x = self.item_id_embedding(items.long()) * mask.unsqueeze(2).to(torch.float32)
-        return x, length
+        ids = torch.where(mask, items, torch.full_like(items, -1))
+        return gather_rows(self.item_id_embedding.weight, ids), length
 
     def loss(self, user_emb, pos_emb, neg_emb):
         """sasrec.py:423-435 (norm of every 'emb' parameter, accumulated by
@@ -181,8 +205,8 @@ class SASRec(nn.Module):
         x, length = self.sequence_input(users)
         u = self.forward_user(x, length)
         item_w = self.item_id_embedding.weight
-        pe = self.forward_item(item_w[pos])
-        ne = self.forward_item(item_w[neg])
+        pe = self.forward_item(gather_rows(item_w, pos))
+        ne = self.forward_item(gather_rows(item_w, neg))
         loss = self.loss(u, pe, ne)
         loss.backward()
         with torch.no_grad():

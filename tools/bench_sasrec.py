@@ -1,0 +1,121 @@
+"""Config C4 (BASELINE.json configs[3]): SASRec L=2 heads=2 d=128 maxlen=50,
+1M users with synthetic sequences of length U[5, 50] over 100K items, one
+MI355X.  A step is one stageOne (model/sasrec.py:437-474 per batch): B
+sequences through two attention blocks + pooling, the item tower on the
+positive and negative items, BPR + norm loss, backward, Adam.  Prints one
+JSON line: positive-edges/s and the attention kernels' roofline (live HIP
+events on their launch stream).
+
+Algorithmic work of one attention launch over B sequences x h heads (dense
+T x T scores, as torch's masked MHA computes them):
+  forward : 4 T^2 dh FLOP per (sequence, head); reads qkv (B T 3d 4 B),
+            writes out (B T d 4 B)
+  backward: 10 T^2 dh FLOP (S recomputed, dV, dP, dQ, dK); reads qkv and dO,
+            writes dqkv
+The bound is whichever of HBM (8 TB/s) and f32 MFMA (157.3 TFLOP/s,
+MI355X_MICROARCH.md) takes longer for that work.
+
+    python tools/bench_sasrec.py [--steps K --warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12
+F32_MFMA_PEAK = 157.3e12
+
+
+class _DS:
+    def __init__(self, n_users, m_items):
+        self.n_users, self.m_items = n_users, m_items
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=2048)
+    ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--heads", type=int, default=2)
+    ap.add_argument("--layers", type=int, default=2)
+    ap.add_argument("--maxlen", type=int, default=50)
+    ap.add_argument("--users", type=int, default=1_000_000)
+    ap.add_argument("--items", type=int, default=100_000)
+    args = ap.parse_args()
+    from furusato_recommend_amd import SASRec, sasrec as S
+    from furusato_recommend_amd.sasrec import SequenceData
+    dev = torch.device("cuda:0")
+    torch.manual_seed(2020)
+    seq = SequenceData.synthetic(args.users, args.items, dev, max_len=args.maxlen, min_len=5,
+                                 seed=0)
+    m = SASRec({"recdim": args.dim, "layer": args.layers, "heads": args.heads, "lr": 1e-3,
+                "decay": 1e-4, "device": "cuda:0", "bpr_batch_size": args.batch,
+                "dropout_p": 0.2}, _DS(args.users, args.items), sequences=seq)
+    B = args.batch
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def batch():
+        # users uniform; positive = a random element of the user's sequence;
+        # negative uniform (timing workload: no rejection of positives)
+        u = torch.randint(0, args.users, (B,), device=dev, generator=g)
+        ln = seq.length[u]
+        k = (torch.rand(B, device=dev, generator=g) * ln).long()
+        p = seq.items[u, k].long()
+        n = torch.randint(0, args.items, (B,), device=dev, generator=g)
+        return u, p, n
+
+    for _ in range(args.warmup):
+        m.stageOne(*batch())
+    torch.cuda.synchronize()
+    S.ATTN_EVENTS = []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.stageOne(*batch())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ev, S.ATTN_EVENTS = S.ATTN_EVENTS, None
+
+    kinds = {}
+    for kind, s, e, (b, T, h, dh) in ev:
+        d = h * dh
+        if kind == "fwd":
+            fl = 4.0 * T * T * dh * b * h
+            by = 4.0 * b * T * (3 * d + d)
+        else:
+            fl = 10.0 * T * T * dh * b * h
+            by = 4.0 * b * T * (3 * d + d + 3 * d)
+        k = kinds.setdefault(kind, [0, 0.0, fl, by])
+        k[0] += 1
+        k[1] += s.elapsed_time(e)
+    roof = {}
+    for kind, (cnt, ms, fl, by) in kinds.items():
+        t = ms / cnt * 1e-3
+        t_hbm, t_mfma = by / HBM_PEAK, fl / F32_MFMA_PEAK
+        if t_hbm >= t_mfma:
+            roof[kind] = {"bound": "hbm", "achieved": round(by / t / 1e9, 1), "peak": 8000.0,
+                          "unit": "GB/s", "frac": round(t_hbm / t, 4)}
+        else:
+            roof[kind] = {"bound": "mfma", "achieved": round(fl / t / 1e12, 2), "peak": 157.3,
+                          "unit": "TFLOP/s", "frac": round(t_mfma / t, 4)}
+        roof[kind].update(avg_launch_ms=round(ms / cnt, 4), launches_per_step=cnt / args.steps,
+                          flop_per_launch=fl, bytes_per_launch=by)
+    print(json.dumps({
+        "metric": "SASRec BPR positive-edges/sec (C4)",
+        "value": round(args.steps * B / dt, 1), "unit": "positive-edges/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
+        "dtype": "f32", "data": "synthetic sequences U[5,%d], random-init weights" % args.maxlen,
+        "config": {"workload": "C4: SASRec L=%d heads=%d d=%d maxlen=%d, %d users x %d items"
+                   % (args.layers, args.heads, args.dim, args.maxlen, args.users, args.items),
+                   "bpr_batch": B},
+        "attention_roofline": roof}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
