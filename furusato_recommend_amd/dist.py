@@ -93,6 +93,8 @@ class DenseGradDataParallel:
     1/world_size and the gradients of all parameters are SUM-all-reduced over
     RCCL as one flattened bucket between backward and the (HIP) Adam step."""
 
+    BUCKET_MIN = 1 << 20  # elements: gradients this large are reduced in place
+
     def __init__(self, model, group=None):
         self.model = model
         self.group = group
@@ -107,12 +109,19 @@ class DenseGradDataParallel:
         if not self.distributed:
             return
         grads = [p.grad for p in self.model.parameters() if p.grad is not None]
-        flat = torch.cat([g.reshape(-1) for g in grads])
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-        off = 0
-        for g in grads:
-            g.copy_(flat[off: off + g.numel()].view_as(g))
-            off += g.numel()
+        # large gradients (the id table) are reduced in place; the small ones
+        # share one flattened bucket
+        big = [g for g in grads if g.numel() >= self.BUCKET_MIN and g.is_contiguous()]
+        small = [g for g in grads if not (g.numel() >= self.BUCKET_MIN and g.is_contiguous())]
+        for g in big:
+            dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
+        if small:
+            flat = torch.cat([g.reshape(-1) for g in small])
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off = 0
+            for g in small:
+                g.copy_(flat[off: off + g.numel()].view_as(g))
+                off += g.numel()
 
     def step(self, users, pos, neg):
         return self.model.stageOne(users, pos, neg, grad_hook=self._allreduce,

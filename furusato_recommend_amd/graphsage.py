@@ -32,10 +32,48 @@ from . import _lib
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
-from .rows import _GatherRows  # noqa: F401  (used below)
 
 
 # ----------------------------------------------------------------- autograd
+class _TableTerms(torch.autograd.Function):
+    """Everything the loss takes from the [N, d] id table in one node:
+    rows = table[ids] (the tree's gathered rows) and the norms of the user
+    and item slices (graphsage.py:326-337 regularisation).  The backward
+    writes the table gradient once — [g_u u/|u| ; g_i i/|i|] as one dense
+    pass — and scatter-adds the row gradients into it, instead of autograd
+    materialising and summing three full-size tensors (slice backward
+    zeros + copies, the gather's zeros, their sums)."""
+
+    @staticmethod
+    def forward(ctx, table, ids, n_user: int):
+        n, d = ids.numel(), table.shape[1]
+        rows = torch.empty(n, d, dtype=table.dtype, device=table.device)
+        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, rows.data_ptr(),
+                                    _lib.stream_handle()), "gather_rows")
+        nu = table[:n_user].norm(2)
+        ni = table[n_user:].norm(2)
+        ctx.save_for_backward(table, ids, nu, ni)
+        ctx.n_user = n_user
+        return rows, nu, ni
+
+    @staticmethod
+    def backward(ctx, g_rows, g_nu, g_ni):
+        table, ids, nu, ni = ctx.saved_tensors
+        k = ctx.n_user
+        grad = torch.empty_like(table)
+        zero = torch.zeros_like(nu)
+        # d|x|/dx = x/|x| (0 for a zero slice, as torch's norm backward)
+        cu = zero if g_nu is None else torch.where(nu > 0, g_nu / nu, zero)
+        ci = zero if g_ni is None else torch.where(ni > 0, g_ni / ni, zero)
+        torch.mul(table[:k], cu, out=grad[:k])
+        torch.mul(table[k:], ci, out=grad[k:])
+        if g_rows is not None:
+            check(lib.mirec_scatter_add_rows(g_rows.contiguous().data_ptr(), ids.data_ptr(),
+                                             ids.numel(), table.shape[1], grad.data_ptr(),
+                                             _lib.stream_handle()), "scatter_add_rows")
+        return grad, None, None
+
+
 class _FanoutMean(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, valid, k, p, seed):
@@ -197,7 +235,8 @@ class GraphSAGE(nn.Module):
         L = self.num_layers
         p = self.dropout_p if (self.training and dropout_seed is not None) else 0.0
         ids = torch.cat([g[0] for g in tree.groups])
-        rows = _GatherRows.apply(self._table, ids)
+        rows, nu, ni = _TableTerms.apply(self._table, ids, self.n_user)
+        self._slice_norms = (nu, ni)  # consumed by loss()
         h, off = [], 0
         for g, _ in tree.groups:
             h.append(rows[off: off + g.numel()])
@@ -231,8 +270,12 @@ class GraphSAGE(nn.Module):
         pos_scores = torch.sum(user_emb * pos_emb, dim=1)
         neg_scores = torch.sum(user_emb * neg_emb, dim=1)
         all_param = 0
-        for prm in self.reg_parameters():
-            all_param = all_param + all_param + prm.norm(2)
+        norms = getattr(self, "_slice_norms", None)
+        self._slice_norms = None
+        for k, prm in enumerate(self.reg_parameters()):
+            # the two table slices' norms come from the forward's fused node
+            nrm = norms[k] if (k < 2 and norms is not None) else prm.norm(2)
+            all_param = all_param + all_param + nrm
         all_param = all_param / user_emb.size(0)
         loss = torch.mean(F.softplus(neg_scores - pos_scores))
         return loss + all_param * self.config["decay"]

@@ -186,3 +186,44 @@ def test_data_parallel_equals_union_batch(golden, mode):
     assert np.array_equal(res[0], res[1])  # replicas stay identical
     ref = f["emb_step2"]
     assert np.max(np.abs(res[0] - ref)) / np.max(np.abs(ref)) < 2e-5
+
+
+def _dense_dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from furusato_recommend_amd.dist import DenseGradDataParallel
+
+    class M(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            g = torch.Generator().manual_seed(rank)  # replicas start different
+            self.table = torch.nn.Parameter(torch.randn(1 << 20 | 8, 4, generator=g))
+            self.lin = torch.nn.Linear(4, 3)
+
+    m = M()
+    dp = DenseGradDataParallel(m)
+    for k, p in enumerate(m.parameters()):
+        p.grad = torch.full_like(p, float(rank + 1) * (k + 1))
+    dp._allreduce()
+    q.put((rank, [p.detach().clone() for p in m.parameters()],
+           [p.grad.clone() for p in m.parameters()]))
+    dist.destroy_process_group()
+
+
+def test_dense_grad_data_parallel_gloo():
+    """DenseGradDataParallel (GraphSAGE / SASRec DP): rank-0 broadcast of the
+    parameters, SUM all-reduce of every gradient (the big table in place, the
+    small ones through the flattened bucket)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dense_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: (ps, gs) for r, ps, gs in (q.get(timeout=120) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    for k, (a, b) in enumerate(zip(res[0][1], res[1][1])):
+        assert torch.equal(a, b) and torch.all(a == 3.0 * (k + 1))
