@@ -140,10 +140,21 @@ __device__ void scores_softmax(const float *sQ, const float *sK, int ld, float *
   __syncthreads();
 }
 
+// Rows of sequence b: [row0, row0 + T) — uniform (b*T, T) or from offsets.
+__device__ __forceinline__ void seq_rows(const int32_t *offsets, int b, int &T, int64_t &row0) {
+  if (offsets == nullptr) {
+    row0 = (int64_t)b * T;
+  } else {
+    row0 = offsets[b];
+    T = min(offsets[b + 1] - offsets[b], kT);
+  }
+}
+
 template <int DPAD>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__ qkv,
                                                        float *__restrict__ out, int T, int H,
-                                                       int dh, float scale) {
+                                                       int dh, float scale,
+                                                       const int32_t *__restrict__ offsets) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int ld = DPAD + 1;
   // P overwrites Q: [sQ | sS] [sK] [sV]
@@ -152,7 +163,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__
   const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
-  const float *base = qkv + (int64_t)b * T * rs + h * dh;
+  int64_t row0;
+  seq_rows(offsets, b, T, row0);
+  const float *base = qkv + row0 * rs + h * dh;
   {
     float *const dst[3] = {sQ, sK, sV};
     const float *const src[3] = {base, base + d, base + 2 * d};
@@ -171,7 +184,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int i = 32 * oi + acc_row(r, lane), c = 32 * oj + (lane & 31);
-      if (i < T && c < dh) out[((int64_t)b * T + i) * d + h * dh + c] = acc[r];
+      if (i < T && c < dh) out[(row0 + i) * d + h * dh + c] = acc[r];
     }
   }
 }
@@ -180,7 +193,8 @@ template <int DPAD>
 __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__ qkv,
                                                        const float *__restrict__ dout,
                                                        float *__restrict__ dqkv, int T, int H,
-                                                       int dh, float scale) {
+                                                       int dh, float scale,
+                                                       const int32_t *__restrict__ offsets) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int dpad = DPAD;
   constexpr int ld = DPAD + 1;
@@ -189,17 +203,19 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__
   const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
-  const float *base = qkv + (int64_t)b * T * rs + h * dh;
+  int64_t row0;
+  seq_rows(offsets, b, T, row0);
+  const float *base = qkv + row0 * rs + h * dh;
   {
     float *const dst[4] = {sQ, sK, sV, sO};
-    const float *const src[4] = {base, base + d, base + 2 * d, dout + (int64_t)b * T * d + h * dh};
+    const float *const src[4] = {base, base + d, base + 2 * d, dout + row0 * d + h * dh};
     const int64_t strides[4] = {rs, rs, rs, (int64_t)d};  // sO = dO
     load_heads<DPAD, 4>(dst, src, strides, ld, T, dh);
   }
   __syncthreads();
   scores_softmax(sQ, sK, ld, sP, dpad, scale);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float *gbase = dqkv + (int64_t)b * T * rs + h * dh;
+  float *gbase = dqkv + row0 * rs + h * dh;
   // dV = Pᵀ dO  (rows j, cols c; K = i)
   constexpr int ntiles = 2 * (dpad / 32);
   for (int t = w; t < ntiles; t += 4) {
@@ -276,6 +292,39 @@ static int attn_smem(int dpad, bool bwd) {
   return (int)sizeof(float) * (bwd ? (4 * kT * ld + 2 * kT * (kT + 1)) : (qs + 2 * kT * ld));
 }
 
+static int launch_fwd(const float *qkv, const int32_t *offsets, int64_t batch, int T,
+                      int heads, int head_dim, float *out, hipStream_t st) {
+  if (batch == 0) return MIREC_OK;
+  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
+  const float scale = 1.f / sqrtf((float)head_dim);
+  const dim3 grid((unsigned)(batch * heads));
+  if (head_dim <= 32)
+    hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), attn_smem(32, false), st, qkv, out,
+                       T, heads, head_dim, scale, offsets);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), attn_smem(64, false), st, qkv, out,
+                       T, heads, head_dim, scale, offsets);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+static int launch_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                      int64_t batch, int T, int heads, int head_dim, float *dqkv,
+                      hipStream_t st) {
+  if (batch == 0) return MIREC_OK;
+  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
+  const float scale = 1.f / sqrtf((float)head_dim);
+  const dim3 grid((unsigned)(batch * heads));
+  if (head_dim <= 32)
+    hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), attn_smem(32, true), st, qkv, dout,
+                       dqkv, T, heads, head_dim, scale, offsets);
+  else
+    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), attn_smem(64, true), st, qkv, dout,
+                       dqkv, T, heads, head_dim, scale, offsets);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
 }  // namespace mirec
 
 extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, int32_t heads,
@@ -283,20 +332,8 @@ extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, i
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && out && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  if (batch == 0) return MIREC_OK;
-  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
-  const int dpad = head_dim <= 32 ? 32 : 64;
-  const float scale = 1.f / sqrtf((float)head_dim);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)(batch * heads));
-  if (dpad == 32)
-    hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), attn_smem(32, false), st, qkv, out,
-                       T, heads, head_dim, scale);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), attn_smem(64, false), st, qkv, out,
-                       T, heads, head_dim, scale);
-  MIREC_LAUNCH_CHECK();
-  return MIREC_OK;
+  return launch_fwd(qkv, nullptr, batch, T, heads, head_dim, out,
+                    reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t batch, int32_t T,
@@ -305,18 +342,26 @@ extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t 
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && dout && dqkv && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  if (batch == 0) return MIREC_OK;
-  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
-  const int dpad = head_dim <= 32 ? 32 : 64;
-  const float scale = 1.f / sqrtf((float)head_dim);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const dim3 grid((unsigned)(batch * heads));
-  if (dpad == 32)
-    hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), attn_smem(32, true), st, qkv, dout,
-                       dqkv, T, heads, head_dim, scale);
-  else
-    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), attn_smem(64, true), st, qkv, dout,
-                       dqkv, T, heads, head_dim, scale);
-  MIREC_LAUNCH_CHECK();
-  return MIREC_OK;
+  return launch_bwd(qkv, dout, nullptr, batch, T, heads, head_dim, dqkv,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mirec_attention_varlen_fwd(const float *qkv, const int32_t *offsets,
+                                          int64_t batch, int32_t heads, int32_t head_dim,
+                                          float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && offsets && out && batch >= 0 && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
+  return launch_fwd(qkv, offsets, batch, kT, heads, head_dim, out,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mirec_attention_varlen_bwd(const float *qkv, const float *dout,
+                                          const int32_t *offsets, int64_t batch, int32_t heads,
+                                          int32_t head_dim, float *dqkv, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && dout && offsets && dqkv && batch >= 0 && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
+  return launch_bwd(qkv, dout, offsets, batch, kT, heads, head_dim, dqkv,
+                    reinterpret_cast<hipStream_t>(stream));
 }

@@ -27,11 +27,12 @@ from .rows import gather_rows
 
 
 # Optional per-launch timing (tools/bench_sasrec.py): a list receiving
-# (kind, start_event, end_event, (B, T, heads, head_dim)).
+# (kind, start_event, end_event, (B, T, heads, head_dim), offsets or None);
+# packed launches have T = -1 and their int32 offsets.
 ATTN_EVENTS = None
 
 
-def _timed(kind, shape, launch):
+def _timed(kind, shape, launch, offsets=None):
     ev = ATTN_EVENTS
     if ev is None:
         return launch()
@@ -39,7 +40,7 @@ def _timed(kind, shape, launch):
     s.record()
     r = launch()
     e.record()
-    ev.append((kind, s, e, shape))
+    ev.append((kind, s, e, shape, offsets))
     return r
 
 
@@ -70,6 +71,38 @@ class _CausalAttention(torch.autograd.Function):
         return dqkv, None
 
 
+class _CausalAttentionVarlen(torch.autograd.Function):
+    """Packed sequences: qkv [n_tok, 3d], sequence b = rows offsets[b] ..
+    offsets[b+1]-1 (mirec_attention_varlen_*)."""
+
+    @staticmethod
+    def forward(ctx, qkv, offsets, heads: int):
+        n, d3 = qkv.shape
+        d = d3 // 3
+        B = offsets.numel() - 1
+        qkv = qkv.contiguous()
+        out = torch.empty(n, d, dtype=qkv.dtype, device=qkv.device)
+        _timed("fwd", (B, -1, heads, d // heads), lambda: check(lib.mirec_attention_varlen_fwd(
+            qkv.data_ptr(), offsets.data_ptr(), B, heads, d // heads, out.data_ptr(),
+            _lib.stream_handle()), "attention_varlen_fwd"), offsets)
+        ctx.save_for_backward(qkv, offsets)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, offsets = ctx.saved_tensors
+        n, d3 = qkv.shape
+        B = offsets.numel() - 1
+        dh = d3 // 3 // ctx.heads
+        dqkv = torch.empty_like(qkv)
+        dout = dout.contiguous()
+        _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(lib.mirec_attention_varlen_bwd(
+            qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), B, ctx.heads, dh,
+            dqkv.data_ptr(), _lib.stream_handle()), "attention_varlen_bwd"), offsets)
+        return dqkv, None, None
+
+
 class CausalSelfAttention(nn.Module):
     """nn.MultiheadAttention(d, heads, batch_first=True) called as
     attn(x, x, x, attn_mask=causal)[0] — same parameter names
@@ -87,9 +120,15 @@ class CausalSelfAttention(nn.Module):
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
 
-    def forward(self, x):
+    def forward(self, x, offsets=None):
+        """x [B, T, d] (padded), or packed [n_tok, d] with int32 ``offsets``
+        [B+1] (sequence b = rows offsets[b] .. offsets[b+1]-1)."""
         qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
-        return self.out_proj(_CausalAttention.apply(qkv, self.heads))
+        if offsets is None:
+            att = _CausalAttention.apply(qkv, self.heads)
+        else:
+            att = _CausalAttentionVarlen.apply(qkv, offsets, self.heads)
+        return self.out_proj(att)
 
 
 class SequenceData:
@@ -106,7 +145,13 @@ class SequenceData:
             lens[u] = len(s)
         self.items = torch.from_numpy(items).to(device)
         self.length = torch.from_numpy(lens).to(device)
+        self.length_host = lens
         self.max_len = max_len
+        self._check()
+
+    def _check(self):
+        if self.max_len > 64:
+            raise ValueError("SASRec attention supports sequences of at most 64 items")
 
     @classmethod
     def synthetic(cls, n_users, m_items, device, max_len=50, min_len=5, seed=0):
@@ -116,6 +161,8 @@ class SequenceData:
         items = torch.randint(0, m_items, (n_users, max_len), generator=g, dtype=torch.int32)
         items[torch.arange(max_len)[None, :] >= lens[:, None]] = 0
         obj.items, obj.length, obj.max_len = items.to(device), lens.to(device), max_len
+        obj.length_host = lens.numpy()
+        obj._check()
         return obj
 
 
@@ -147,11 +194,12 @@ class SASRec(nn.Module):
         self.optims = [AdamState(p, lr=config["lr"]) for p in self.parameters()]
 
     # ------------------------------------------------------------- blocks
-    def oneblock(self, x, layer):
-        """sasrec.py:385-397."""
+    def oneblock(self, x, layer, offsets=None):
+        """sasrec.py:385-397 (padded [B, T, d], or packed [n_tok, d] with
+        ``offsets``: every other op of the block is per position)."""
         init_x = x
         x = self.attn_norm_layers[layer](x)
-        x = self.attn_layers[layer](x)
+        x = self.attn_layers[layer](x, offsets)
         x = self.dropout(x)
         x = (init_x + x).relu()
         init_x = x
@@ -167,6 +215,38 @@ class SASRec(nn.Module):
         T = x.shape[1]
         mask = (torch.arange(T, device=x.device)[None, :] < length[:, None]).to(x.dtype)
         return (x * mask.unsqueeze(2)).sum(1) / length.to(x.dtype).unsqueeze(1)
+
+    def forward_user_packed(self, x, offsets, seg, length):
+        """forward_user on packed sequences: x [n_tok, d], ``seg`` [n_tok]
+        the sequence of every row.  Padding positions never reach a real
+        position under the causal mask and are excluded from the pool, so
+        this equals forward_user on the padded batch while skipping them."""
+        for i in range(self.num_layers):
+            x = self.oneblock(x, i, offsets)
+        pooled = torch.zeros(length.numel(), x.shape[1], dtype=x.dtype, device=x.device)
+        pooled = pooled.index_add(0, seg, x)
+        return pooled / length.to(x.dtype).unsqueeze(1)
+
+    def packed_input(self, users):
+        """(x [n_tok, d], offsets [B+1] int32, seg [n_tok], length [B]) of the
+        users' sequences.  The token count is taken from the host copy of
+        the lengths (host ``users``: no device synchronisation)."""
+        if torch.is_tensor(users) and users.is_cuda:
+            u_host = users.cpu().numpy()
+        else:
+            u_host = np.asarray(users)
+        lens_h = self.seq.length_host[u_host]
+        n_tok = int(lens_h.sum())
+        dev = self.device
+        u = torch.as_tensor(u_host, device=dev).long()
+        length = self.seq.length[u]
+        offsets = torch.zeros(len(u_host) + 1, dtype=torch.int32, device=dev)
+        offsets[1:] = torch.cumsum(length, 0).to(torch.int32)
+        seg = torch.repeat_interleave(torch.arange(len(u_host), device=dev), length,
+                                      output_size=n_tok)
+        pos = torch.arange(n_tok, device=dev) - offsets[seg].long()
+        ids = self.seq.items[u[seg], pos]
+        return gather_rows(self.item_id_embedding.weight, ids), offsets, seg, length
 
     def forward_item(self, x):
         """sasrec.py:415-421."""
@@ -201,9 +281,9 @@ class SASRec(nn.Module):
     def stageOne(self, users, pos, neg):
         for p in self.parameters():
             p.grad = None
-        users, pos, neg = (torch.as_tensor(t).to(self.device).long() for t in (users, pos, neg))
-        x, length = self.sequence_input(users)
-        u = self.forward_user(x, length)
+        pos, neg = (torch.as_tensor(t).to(self.device).long() for t in (pos, neg))
+        x, offsets, seg, length = self.packed_input(users)
+        u = self.forward_user_packed(x, offsets, seg, length)
         item_w = self.item_id_embedding.weight
         pe = self.forward_item(gather_rows(item_w, pos))
         ne = self.forward_item(gather_rows(item_w, neg))
@@ -217,6 +297,8 @@ class SASRec(nn.Module):
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])
         n = len(user)
+        # users on the host: the packed batches are sized without a sync
+        user = user.cpu().numpy() if torch.is_tensor(user) else np.asarray(user)
         acc = torch.zeros((), device=self.device)
         for i in range(0, n, B):
             acc += self.stageOne(user[i:i + B], pos[i:i + B], neg[i:i + B])

@@ -358,6 +358,20 @@ int mirec_attention_bwd(const float *qkv, const float *dout, int64_t batch, int3
                         int32_t heads, int32_t head_dim, float *dqkv,
                         mirec_stream_t stream);
 
+/* Packed (variable-length) form: sequence b is rows offsets[b] ..
+ * offsets[b+1]-1 of qkv [n_tok, 3*heads*head_dim] / out / dout / dqkv
+ * [n_tok, ...]; offsets (device, int32, batch+1 entries, non-decreasing)
+ * with every length <= 64 (longer sequences are cut to their first 64
+ * rows).  Padding positions past a sequence's length never influence its
+ * earlier positions under the causal mask, so the padded and the packed
+ * forms agree on every real row; the packed one skips the padding. */
+int mirec_attention_varlen_fwd(const float *qkv, const int32_t *offsets, int64_t batch,
+                               int32_t heads, int32_t head_dim, float *out,
+                               mirec_stream_t stream);
+int mirec_attention_varlen_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                               int64_t batch, int32_t heads, int32_t head_dim,
+                               float *dqkv, mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Evaluation (trainer.py:130-138)                                           */
 /* ------------------------------------------------------------------------ */

@@ -697,6 +697,56 @@ def test_sasrec_attention_kernel_vs_torch_sdpa():
         assert rel(g1, g2) < TOL
 
 
+def test_sasrec_varlen_attention_matches_padded():
+    """Packed (varlen) kernels == padded kernels on every real row, fwd and
+    bwd (padding rows carry zero output gradient, as under the pooled loss),
+    incl. lengths 1 and 64 and a zero-length sequence."""
+    from furusato_recommend_amd.sasrec import _CausalAttention, _CausalAttentionVarlen
+    torch.manual_seed(1)
+    for heads, dh in ((2, 64), (8, 16), (3, 20)):
+        d, T = heads * dh, 64
+        lens = torch.tensor([1, 64, 17, 0, 50, 33])
+        B = lens.numel()
+        qkv = torch.randn(B, T, 3 * d, device="cuda")
+        mask = (torch.arange(T)[None, :] < lens[:, None]).cuda()
+        go = torch.randn(B, T, d, device="cuda") * mask.unsqueeze(2)
+        qp = qkv.clone().requires_grad_(True)
+        out_p = _CausalAttention.apply(qp, heads)
+        gp, = torch.autograd.grad(out_p, qp, go)
+        offsets = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+        offsets[1:] = torch.cumsum(lens.cuda(), 0).int()
+        qv = qkv[mask].clone().requires_grad_(True)
+        out_v = _CausalAttentionVarlen.apply(qv, offsets, heads)
+        gv, = torch.autograd.grad(out_v, qv, go[mask])
+        assert rel(out_v, out_p[mask]) < TOL
+        assert rel(gv, gp[mask]) < TOL
+
+
+def test_sasrec_packed_path_equals_padded():
+    """The training path (packed sequences) gives the padded path's user
+    embeddings and parameter gradients (dropout off)."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    ds = SyntheticBipartite(600, 300, 12_000, seed=5)
+    torch.manual_seed(0)
+    m = SASRec({"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+                "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0}, ds)
+    u_h = np.random.default_rng(0).integers(0, 600, 128)
+    x, offs, seg, length = m.packed_input(u_h)
+    up = m.forward_user_packed(x, offs, seg, length)
+    xp, lp = m.sequence_input(torch.as_tensor(u_h, device="cuda"))
+    ud = m.forward_user(xp, lp)
+    assert rel(up, ud) < TOL
+    w = torch.randn_like(up)
+    params = [p for p in m.parameters() if p.requires_grad]
+    g1 = torch.autograd.grad((up * w).sum(), params, allow_unused=True)
+    g2 = torch.autograd.grad((ud * w).sum(), params, allow_unused=True)
+    for a, b in zip(g1, g2):
+        if b is None:
+            assert a is None or float(a.abs().max()) == 0.0
+        else:
+            assert rel(a, b) < TOL
+
+
 def test_sasrec_trains():
     from furusato_recommend_amd import SASRec, SyntheticBipartite
     ds = SyntheticBipartite(3000, 500, 40_000, seed=11, test_frac=0.1)

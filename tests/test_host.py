@@ -205,8 +205,10 @@ def _dense_dp_worker(rank, world, port, q):
     for k, p in enumerate(m.parameters()):
         p.grad = torch.full_like(p, float(rank + 1) * (k + 1))
     dp._allreduce()
-    q.put((rank, [p.detach().clone() for p in m.parameters()],
-           [p.grad.clone() for p in m.parameters()]))
+    # numpy, not tensors: torch shares tensor storage through a file
+    # descriptor that dies with this process
+    q.put((rank, [p.detach().numpy().copy() for p in m.parameters()],
+           [p.grad.numpy().copy() for p in m.parameters()]))
     dist.destroy_process_group()
 
 
@@ -224,6 +226,6 @@ def test_dense_grad_data_parallel_gloo():
     for p in procs:
         p.join(timeout=60)
     for a, b in zip(res[0][0], res[1][0]):
-        assert torch.equal(a, b)
+        assert np.array_equal(a, b)
     for k, (a, b) in enumerate(zip(res[0][1], res[1][1])):
-        assert torch.equal(a, b) and torch.all(a == 3.0 * (k + 1))
+        assert np.array_equal(a, b) and np.all(a == 3.0 * (k + 1))

@@ -6,12 +6,13 @@ positive and negative items, BPR + norm loss, backward, Adam.  Prints one
 JSON line: positive-edges/s and the attention kernels' roofline (live HIP
 events on their launch stream).
 
-Algorithmic work of one attention launch over B sequences x h heads (dense
-T x T scores, as torch's masked MHA computes them):
-  forward : 4 T^2 dh FLOP per (sequence, head); reads qkv (B T 3d 4 B),
-            writes out (B T d 4 B)
-  backward: 10 T^2 dh FLOP (S recomputed, dV, dP, dQ, dK); reads qkv and dO,
-            writes dqkv
+Training runs on packed sequences (only the real positions; padding never
+reaches them under the causal mask).  Algorithmic work of one attention
+launch over B sequences of lengths T_b x h heads (dense T_b x T_b scores):
+  forward : 4 T_b^2 dh FLOP per (sequence, head); reads qkv (T_b 3d 4 B),
+            writes out (T_b d 4 B)
+  backward: 10 T_b^2 dh FLOP (S recomputed, dV, dP, dQ, dK); reads qkv and
+            dO, writes dqkv
 The bound is whichever of HBM (8 TB/s) and f32 MFMA (157.3 TFLOP/s,
 MI355X_MICROARCH.md) takes longer for that work.
 
@@ -23,6 +24,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -61,15 +63,20 @@ def main():
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(7)
 
+    rng = np.random.default_rng(7)
+
     def batch():
-        # users uniform; positive = a random element of the user's sequence;
-        # negative uniform (timing workload: no rejection of positives)
-        u = torch.randint(0, args.users, (B,), device=dev, generator=g)
+        # users uniform, drawn on the host like the reference's UniformSample
+        # (so the packed batch is sized without a device sync); positive = a
+        # random element of the user's sequence; negative uniform (timing
+        # workload: no rejection of positives)
+        u_h = rng.integers(0, args.users, B)
+        u = torch.from_numpy(u_h).to(dev, non_blocking=True)
         ln = seq.length[u]
         k = (torch.rand(B, device=dev, generator=g) * ln).long()
         p = seq.items[u, k].long()
         n = torch.randint(0, args.items, (B,), device=dev, generator=g)
-        return u, p, n
+        return u_h, p, n
 
     for _ in range(args.warmup):
         m.stageOne(*batch())
@@ -83,20 +90,28 @@ def main():
     ev, S.ATTN_EVENTS = S.ATTN_EVENTS, None
 
     kinds = {}
-    for kind, s, e, (b, T, h, dh) in ev:
+    for kind, s, e, (b, T, h, dh), offs in ev:
         d = h * dh
-        if kind == "fwd":
-            fl = 4.0 * T * T * dh * b * h
-            by = 4.0 * b * T * (3 * d + d)
+        if offs is not None:  # packed: sum over the real sequence lengths
+            lens = np.diff(offs.cpu().numpy().astype(np.int64))
+            t2, t1 = float((lens * lens).sum()), float(lens.sum())
         else:
-            fl = 10.0 * T * T * dh * b * h
-            by = 4.0 * b * T * (3 * d + d + 3 * d)
-        k = kinds.setdefault(kind, [0, 0.0, fl, by])
+            t2, t1 = float(b) * T * T, float(b) * T
+        if kind == "fwd":
+            fl = 4.0 * t2 * dh * h
+            by = 4.0 * t1 * (3 * d + d)
+        else:
+            fl = 10.0 * t2 * dh * h
+            by = 4.0 * t1 * (3 * d + d + 3 * d)
+        k = kinds.setdefault(kind, [0, 0.0, 0.0, 0.0])
         k[0] += 1
         k[1] += s.elapsed_time(e)
+        k[2] += fl
+        k[3] += by
     roof = {}
     for kind, (cnt, ms, fl, by) in kinds.items():
         t = ms / cnt * 1e-3
+        fl, by = fl / cnt, by / cnt  # per launch
         t_hbm, t_mfma = by / HBM_PEAK, fl / F32_MFMA_PEAK
         if t_hbm >= t_mfma:
             roof[kind] = {"bound": "hbm", "achieved": round(by / t / 1e9, 1), "peak": 8000.0,
