@@ -278,7 +278,10 @@ class SASRec(nn.Module):
         loss = torch.mean(F.softplus(neg_scores - pos_scores))
         return loss + all_param * self.config["decay"]
 
-    def stageOne(self, users, pos, neg):
+    def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0):
+        """One BPR step on packed sequences.  ``loss_scale`` scales the
+        gradient (1/world_size under data parallelism); ``grad_hook`` runs
+        between backward and Adam (DenseGradDataParallel's all-reduce)."""
         for p in self.parameters():
             p.grad = None
         pos, neg = (torch.as_tensor(t).to(self.device).long() for t in (pos, neg))
@@ -288,7 +291,9 @@ class SASRec(nn.Module):
         pe = self.forward_item(gather_rows(item_w, pos))
         ne = self.forward_item(gather_rows(item_w, neg))
         loss = self.loss(u, pe, ne)
-        loss.backward()
+        (loss * loss_scale if loss_scale != 1.0 else loss).backward()
+        if grad_hook is not None:
+            grad_hook()
         with torch.no_grad():
             for opt in self.optims:
                 opt.step()
