@@ -115,13 +115,18 @@ class SyntheticBipartite(_Base):
 
     ``kind='uniform'``: users = cat(arange(n_users), randint(n_users, E - n_users)),
     items uniform (item degree ≈ Poisson(E/m)); ``kind='zipf'``: item
-    popularity ∝ 1/rank^alpha (load-balance stress).  Multi-edges are kept.
+    popularity ∝ 1/rank^alpha (load-balance stress); ``kind='cluster'``:
+    user u and item i belong to community u % n_clusters / i % n_clusters,
+    and an edge picks an item of its user's community with probability
+    p_in, else a uniform item (a graph with something to learn: Recall@20
+    moves far above chance).  Multi-edges are kept.
     ``test_frac`` of the users (with ≥ 2 edges) have their guaranteed edge
     moved to the test split.
     """
 
     def __init__(self, n_users: int, m_items: int, n_edges: int, seed: int = 0,
-                 kind: str = "uniform", alpha: float = 1.0, test_frac: float = 0.1):
+                 kind: str = "uniform", alpha: float = 1.0, test_frac: float = 0.1,
+                 n_clusters: int = 20, p_in: float = 0.9):
         super().__init__()
         if n_edges < n_users:
             raise ValueError("need n_edges >= n_users (every user has a train edge)")
@@ -133,6 +138,17 @@ class SyntheticBipartite(_Base):
         elif kind == "zipf":
             w = 1.0 / torch.arange(1, m_items + 1, dtype=torch.float64) ** alpha
             items = torch.multinomial(w, n_edges, replacement=True, generator=g)
+        elif kind == "cluster":
+            K = int(n_clusters)
+            if m_items < K:
+                raise ValueError("need m_items >= n_clusters")
+            per = (m_items - 1 - torch.arange(K)) // K + 1  # items i with i % K == c
+            c = users % K
+            r = torch.rand(n_edges, generator=g)
+            slot = (torch.rand(n_edges, generator=g) * per[c]).long()
+            inside = c + K * slot
+            items = torch.where(r < p_in, inside, torch.randint(0, m_items, (n_edges,),
+                                                                generator=g))
         else:
             raise ValueError(kind)
         users = users.numpy().astype(np.int64)
