@@ -238,7 +238,7 @@ class SASRec(nn.Module):
         lens_h = self.seq.length_host[u_host]
         n_tok = int(lens_h.sum())
         dev = self.device
-        u = torch.as_tensor(u_host, device=dev).long()
+        u = self._upload(u_host)
         length = self.seq.length[u]
         offsets = torch.zeros(len(u_host) + 1, dtype=torch.int32, device=dev)
         offsets[1:] = torch.cumsum(length, 0).to(torch.int32)
@@ -247,6 +247,30 @@ class SASRec(nn.Module):
         pos = torch.arange(n_tok, device=dev) - offsets[seg].long()
         ids = self.seq.items[u[seg], pos]
         return gather_rows(self.item_id_embedding.weight, ids), offsets, seg, length
+
+    def _upload(self, host_ids) -> torch.Tensor:
+        """int64 host ids -> device without a stream sync: a pageable H2D copy
+        blocks until the stream drains, so the ids go through one of two
+        pinned staging buffers (each reused only after its previous copy's
+        event completed)."""
+        n = len(host_ids)
+        st = getattr(self, "_stage", None)
+        if st is None or st[0][0].numel() < n:
+            st = ([torch.empty(max(n, 4096), dtype=torch.int64).pin_memory() for _ in range(2)],
+                  [None, None], [0])
+            self._stage = st
+        bufs, events, turn = st
+        k = turn[0]
+        turn[0] ^= 1
+        if events[k] is not None:
+            events[k].synchronize()
+        buf = bufs[k][:n]
+        buf.numpy()[:] = np.asarray(host_ids, dtype=np.int64)
+        out = buf.to(self.device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        events[k] = ev
+        return out
 
     def forward_item(self, x):
         """sasrec.py:415-421."""

@@ -71,7 +71,7 @@ def main():
         # random element of the user's sequence; negative uniform (timing
         # workload: no rejection of positives)
         u_h = rng.integers(0, args.users, B)
-        u = torch.from_numpy(u_h).to(dev, non_blocking=True)
+        u = m._upload(u_h)  # pinned staging: no stream sync
         ln = seq.length[u]
         k = (torch.rand(B, device=dev, generator=g) * ln).long()
         p = seq.items[u, k].long()
