@@ -112,6 +112,10 @@ SIGNATURES = {
                                   c_uint64, c_void_p, c_void_p]),
     "mirec_fanout_mean_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_float,
                                       c_uint64, c_void_p, c_void_p]),
+    "mirec_fanout_mean_gather": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                         c_float, c_uint64, c_void_p, c_void_p]),
+    "mirec_fanout_mean_gather_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                             c_float, c_uint64, c_void_p, c_void_p]),
     "mirec_attention_fwd": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
                                     c_void_p]),
     "mirec_attention_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,

@@ -13,6 +13,9 @@
 //                         the backward of the gather)
 //   mirec_fanout_mean     out[t] = mean over valid c of dropout(x[t*k + c])
 //   mirec_fanout_mean_bwd grad_x[t*k + c] = mask * grad_out[t] / cnt
+//   mirec_fanout_mean_gather(_bwd)  the same with child rows gathered from
+//                         the table by id (leaf hop: no materialised rows;
+//                         backward scatter-adds into the table gradient)
 // Dropout masks are a counter hash of (seed, element index), recomputed in
 // the backward (nothing stored).
 #include "common.h"
@@ -74,7 +77,9 @@ __device__ __forceinline__ bool keep(uint64_t key, uint64_t idx, uint32_t thresh
   return (uint32_t)(mix64(key ^ idx) >> 32) >= thresh;
 }
 
-// one thread per (target, float4 column)
+// one thread per (target, float4 column).  GATHER: child rows are
+// table[valid[child]] (fused row gather, nothing materialised), else x rows.
+template <bool GATHER>
 __global__ __launch_bounds__(256) void fanout_mean_kernel(
     const float *__restrict__ x, const int32_t *__restrict__ valid, int64_t n_targets, int32_t k,
     int32_t d4, uint64_t key, uint32_t thresh, float scale, float *__restrict__ out) {
@@ -89,7 +94,8 @@ __global__ __launch_bounds__(256) void fanout_mean_kernel(
     const int64_t child = t * k + c;
     if (valid != nullptr && valid[child] < 0) continue;
     ++cnt;
-    float4 v = ld4(x + child * d + c4 * 4);
+    const int64_t row = GATHER ? (int64_t)valid[child] : child;
+    float4 v = ld4(x + row * d + c4 * 4);
     if (thresh != 0u) {
       const uint64_t e = (uint64_t)(child * d + c4 * 4);
       v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
@@ -129,6 +135,27 @@ __global__ __launch_bounds__(256) void fanout_mean_bwd_kernel(
     }
   }
   st4(grad_x + i * 4, g);
+}
+
+// Backward of the fused gather + mean: table_grad[ids[child]] += mask *
+// grad_out[t] / cnt.  One thread per (child, float): a wave-instruction adds
+// 64 consecutive floats of one row (the full-rate atomic shape).
+__global__ __launch_bounds__(256) void fanout_mean_gather_bwd_kernel(
+    const float *__restrict__ grad_out, const int32_t *__restrict__ ids, int64_t n_targets,
+    int32_t k, int32_t d, uint64_t key, uint32_t thresh, float scale,
+    float *__restrict__ table_grad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (child, column)
+  if (i >= n_targets * k * d) return;
+  const int64_t child = i / d;
+  const int64_t col = i - child * d;
+  const int32_t id = ids[child];
+  if (id < 0) return;
+  const int64_t t = child / k;
+  int cnt = 0;
+  for (int c = 0; c < k; ++c) cnt += ids[t * k + c] >= 0 ? 1 : 0;
+  float g = grad_out[t * d + col] / (float)cnt;
+  if (thresh != 0u) g = keep(key, (uint64_t)i, thresh) ? g * scale : 0.f;
+  atomicAdd(table_grad + (int64_t)id * d + col, g);
 }
 
 static bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
@@ -191,7 +218,7 @@ extern "C" int mirec_fanout_mean(const float *x, const int32_t *valid, int64_t n
   MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
   if (n_targets == 0) return MIREC_OK;
   const int64_t tot = n_targets * (dim / 4);
-  hipLaunchKernelGGL(fanout_mean_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+  hipLaunchKernelGGL(fanout_mean_kernel<false>, dim3((tot + 255) / 256), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), x, valid, n_targets, k, dim / 4, key,
                      thresh, scale, out);
   MIREC_LAUNCH_CHECK();
@@ -212,6 +239,44 @@ extern "C" int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid
   hipLaunchKernelGGL(fanout_mean_bwd_kernel, dim3((tot + 255) / 256), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), grad_out, valid, n_targets, k,
                      dim / 4, key, thresh, scale, grad_x);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_fanout_mean_gather(const float *table, const int32_t *ids, int64_t n_targets,
+                                        int32_t k, int32_t dim, float dropout_p, uint64_t seed,
+                                        float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(table && ids && out && n_targets >= 0 && k > 0 && dim > 0 && dim % 4 == 0);
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
+  if (n_targets == 0) return MIREC_OK;
+  const int64_t tot = n_targets * (dim / 4);
+  hipLaunchKernelGGL(fanout_mean_kernel<true>, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), table, ids, n_targets, k, dim / 4,
+                     key, thresh, scale, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_fanout_mean_gather_bwd(const float *grad_out, const int32_t *ids,
+                                            int64_t n_targets, int32_t k, int32_t dim,
+                                            float dropout_p, uint64_t seed, float *table_grad,
+                                            mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(grad_out && ids && table_grad && n_targets >= 0 && k > 0 && dim > 0 &&
+                  dim % 4 == 0);
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
+  if (n_targets == 0) return MIREC_OK;
+  const int64_t tot = n_targets * k * dim;
+  hipLaunchKernelGGL(fanout_mean_gather_bwd_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), grad_out, ids, n_targets, k, dim,
+                     key, thresh, scale, table_grad);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -37,29 +37,47 @@ from .graph import DEFAULT_SPLIT, Graph
 # ----------------------------------------------------------------- autograd
 class _TableTerms(torch.autograd.Function):
     """Everything the loss takes from the [N, d] id table in one node:
-    rows = table[ids] (the tree's gathered rows) and the norms of the user
-    and item slices (graphsage.py:326-337 regularisation).  The backward
-    writes the table gradient once — [g_u u/|u| ; g_i i/|i|] as one dense
-    pass — and scatter-adds the row gradients into it, instead of autograd
-    materialising and summing three full-size tensors (slice backward
-    zeros + copies, the gather's zeros, their sums)."""
+      * rows = table[ids] for the tree's inner groups (their raw rows feed
+        layer 0 as self features),
+      * for every leaf group (depth L: only ever averaged by its parent at
+        layer 0) the parent's dropout-mean over its children's table rows,
+        gathered and averaged in one pass (mirec_fanout_mean_gather) — the
+        leaf rows, ~90 % of a [25, 10] tree, are never materialised,
+      * the norms of the user and item slices (graphsage.py:326-337).
+    The backward writes the table gradient once — [g_u u/|u| ; g_i i/|i|] as
+    one dense pass — and scatter-adds the inner row gradients and the leaf
+    means' gradients into it (float atomics), instead of autograd
+    materialising and summing full-size tensors.
+    ``leaves`` = ((ids, k, dropout p, seed), ...)."""
 
     @staticmethod
-    def forward(ctx, table, ids, n_user: int):
+    def forward(ctx, table, ids, n_user: int, leaves):
         n, d = ids.numel(), table.shape[1]
+        st = _lib.stream_handle()
         rows = torch.empty(n, d, dtype=table.dtype, device=table.device)
-        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, rows.data_ptr(),
-                                    _lib.stream_handle()), "gather_rows")
+        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, rows.data_ptr(), st),
+              "gather_rows")
+        aggrs = []
+        for lid, k, p, seed in leaves:
+            n_t = lid.numel() // k
+            out = torch.empty(n_t, d, dtype=table.dtype, device=table.device)
+            check(lib.mirec_fanout_mean_gather(table.data_ptr(), lid.data_ptr(), n_t, k, d,
+                                               float(p), ctypes.c_uint64(seed), out.data_ptr(),
+                                               st), "fanout_mean_gather")
+            aggrs.append(out)
         nu = table[:n_user].norm(2)
         ni = table[n_user:].norm(2)
-        ctx.save_for_backward(table, ids, nu, ni)
+        ctx.save_for_backward(table, ids, nu, ni, *[l[0] for l in leaves])
+        ctx.leaf_cfg = [(k, p, seed) for _, k, p, seed in leaves]
         ctx.n_user = n_user
-        return rows, nu, ni
+        return (rows, nu, ni, *aggrs)
 
     @staticmethod
-    def backward(ctx, g_rows, g_nu, g_ni):
-        table, ids, nu, ni = ctx.saved_tensors
+    def backward(ctx, g_rows, g_nu, g_ni, *g_aggrs):
+        table, ids, nu, ni, *leaf_ids = ctx.saved_tensors
         k = ctx.n_user
+        d = table.shape[1]
+        st = _lib.stream_handle()
         grad = torch.empty_like(table)
         zero = torch.zeros_like(nu)
         # d|x|/dx = x/|x| (0 for a zero slice, as torch's norm backward)
@@ -69,9 +87,16 @@ class _TableTerms(torch.autograd.Function):
         torch.mul(table[k:], ci, out=grad[k:])
         if g_rows is not None:
             check(lib.mirec_scatter_add_rows(g_rows.contiguous().data_ptr(), ids.data_ptr(),
-                                             ids.numel(), table.shape[1], grad.data_ptr(),
-                                             _lib.stream_handle()), "scatter_add_rows")
-        return grad, None, None
+                                             ids.numel(), d, grad.data_ptr(), st),
+                  "scatter_add_rows")
+        for g, lid, (kk, p, seed) in zip(g_aggrs, leaf_ids, ctx.leaf_cfg):
+            if g is None:
+                continue
+            check(lib.mirec_fanout_mean_gather_bwd(g.contiguous().data_ptr(), lid.data_ptr(),
+                                                   lid.numel() // kk, kk, d, float(p),
+                                                   ctypes.c_uint64(seed), grad.data_ptr(), st),
+                  "fanout_mean_gather_bwd")
+        return grad, None, None, None
 
 
 class _FanoutMean(torch.autograd.Function):
@@ -234,23 +259,39 @@ class GraphSAGE(nn.Module):
         """Seed embeddings h^(L) for a sampled tree (graphsage.py:311-324)."""
         L = self.num_layers
         p = self.dropout_p if (self.training and dropout_seed is not None) else 0.0
-        ids = torch.cat([g[0] for g in tree.groups])
-        rows, nu, ni = _TableTerms.apply(self._table, ids, self.n_user)
+        groups = tree.groups
+        parent = {ci: gi for (gi, _), ci in tree.children.items()}
+
+        def seed_of(gi, i):
+            return 0 if p == 0.0 else (dropout_seed * 1_000_003 + gi * 131 + i)
+
+        # leaves (depth L) are only averaged by their parents at layer 0:
+        # fused gather + mean inside the table node
+        inner = [gi for gi, (_, dep) in enumerate(groups) if dep < L]
+        leaf = [ci for ci, (_, dep) in enumerate(groups) if dep == L]
+        leaves = tuple((groups[ci][0], self.sizes[L - 1], p, seed_of(parent[ci], 0))
+                       for ci in leaf)
+        ids = torch.cat([groups[gi][0] for gi in inner])
+        rows, nu, ni, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves)
         self._slice_norms = (nu, ni)  # consumed by loss()
-        h, off = [], 0
-        for g, _ in tree.groups:
-            h.append(rows[off: off + g.numel()])
-            off += g.numel()
+        # one split node: its backward concatenates the group gradients once
+        # (per-slice views would each materialise a full-size zero tensor)
+        h = [None] * len(groups)
+        for gi, part in zip(inner, torch.split(rows, [groups[gi][0].numel() for gi in inner])):
+            h[gi] = part
+        leaf_aggr = {parent[ci]: a for ci, a in zip(leaf, aggrs)}
         for i in range(L):
             hop = L - i
             new = list(h)
-            for gi, (g, depth) in enumerate(tree.groups):
+            for gi, (g, depth) in enumerate(groups):
                 if depth > L - 1 - i:
                     continue
                 ci = tree.children[(gi, hop)]
                 k = self.sizes[hop - 1]
-                s = 0 if p == 0.0 else (dropout_seed * 1_000_003 + gi * 131 + i)
-                aggr = _FanoutMean.apply(h[ci], tree.groups[ci][0], k, p, s)
+                if i == 0:
+                    aggr = leaf_aggr[gi]  # children at hop L are leaves
+                else:
+                    aggr = _FanoutMean.apply(h[ci], groups[ci][0], k, p, seed_of(gi, i))
                 x = self.w_linears[i](torch.cat([h[gi], aggr], dim=1))
                 new[gi] = x.relu() if i != L - 1 else x
             h = new

@@ -821,3 +821,33 @@ def test_lgconv_operator_matches_fixture(golden, name, d, split):
     assert conv._graph is g0          # CSR cached per edge_index
     if ysum is not None:
         assert rel(LGConv(normalize=False)(x.cuda(), eic), ysum) < TOL
+
+
+def test_fused_leaf_gather_mean_equals_unfused():
+    """mirec_fanout_mean_gather(_bwd) == row gather + mirec_fanout_mean (and
+    its backward scattered into the table), dropout on, isolated children."""
+    import ctypes
+
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd._lib import check, lib
+    from furusato_recommend_amd.graphsage import _FanoutMean
+    from furusato_recommend_amd.rows import gather_rows
+    torch.manual_seed(4)
+    N, d, n_t, k, p, seed = 500, 32, 300, 5, 0.3, 123
+    table = torch.randn(N, d, device="cuda", requires_grad=True)
+    ids = torch.randint(0, N, (n_t * k,), device="cuda", dtype=torch.int32)
+    ids[::7] = -1
+    ids[:k] = -1  # a target with no valid child
+    go = torch.randn(n_t, d, device="cuda")
+    rows = gather_rows(table, ids)
+    ref = _FanoutMean.apply(rows, ids, k, p, seed)
+    gref, = torch.autograd.grad(ref, table, go)
+    out = torch.empty(n_t, d, device="cuda")
+    st = _lib.stream_handle()
+    check(lib.mirec_fanout_mean_gather(table.data_ptr(), ids.data_ptr(), n_t, k, d, p,
+                                       ctypes.c_uint64(seed), out.data_ptr(), st), "fmg")
+    g = torch.zeros(N, d, device="cuda")
+    check(lib.mirec_fanout_mean_gather_bwd(go.data_ptr(), ids.data_ptr(), n_t, k, d, p,
+                                           ctypes.c_uint64(seed), g.data_ptr(), st), "fmg_bwd")
+    assert torch.equal(out, ref.detach())
+    assert rel(g, gref) < TOL
