@@ -75,6 +75,9 @@ SIGNATURES = {
                                     c_void_p, c_void_p, c_void_p]),
     "mirec_csr_from_coo": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                    c_void_p, c_void_p]),
+    "mirec_parse_interactions": (c_int, [c_void_p, c_int64, c_int64, c_int32, POINTER(c_int64),
+                                         POINTER(c_int64), POINTER(c_int64), POINTER(c_int64),
+                                         c_void_p, c_void_p, c_void_p]),
     "mirec_csr_long_rows": (c_int, [c_void_p, c_int64, c_int32, POINTER(c_int64),
                                     POINTER(c_int64), c_void_p, c_void_p, c_void_p,
                                     c_void_p]),

@@ -54,60 +54,97 @@ class _Base:
         return [self.allPos[int(u)] for u in users]
 
 
+def parse_interactions(path: str, stop_uid: int = -1, n_threads: int | None = None):
+    """Native parse of a ``uid i1 i2 ...`` file (mirec_parse_interactions):
+    (line_uid [L], line_off [L+1], items [I], max_uid, max_item), file order."""
+    import ctypes
+
+    from ._lib import check, lib
+    data = np.fromfile(path, dtype=np.uint8)
+    nt = int(n_threads or min(16, os.cpu_count() or 1))
+    L, I = ctypes.c_int64(0), ctypes.c_int64(0)
+    mu, mi = ctypes.c_int64(0), ctypes.c_int64(0)
+    ptr = data.ctypes.data if data.size else None
+    check(lib.mirec_parse_interactions(ptr, data.size, int(stop_uid), nt, ctypes.byref(L),
+                                       ctypes.byref(I), ctypes.byref(mu), ctypes.byref(mi),
+                                       None, None, None), f"parse {path}")
+    line_uid = np.empty(L.value, np.int64)
+    line_off = np.empty(L.value + 1, np.int64)
+    items = np.empty(I.value, np.int64)
+    check(lib.mirec_parse_interactions(ptr, data.size, int(stop_uid), nt, ctypes.byref(L),
+                                       ctypes.byref(I), ctypes.byref(mu), ctypes.byref(mi),
+                                       line_uid.ctypes.data, line_off.ctypes.data,
+                                       items.ctypes.data), f"parse {path}")
+    return line_uid, line_off, items, mu.value, mi.value
+
+
+class _LineIndexed(list):
+    """allPos built lazily from the parsed offsets: element k is line k's
+    items (a view), as the reference's line-indexed list."""
+
+    def __init__(self, items, off):
+        super().__init__()
+        self._items, self._off = items, off
+        self._n = len(off) - 1
+
+    def _fill(self):
+        if self._n and not super().__len__():
+            self.extend(np.split(self._items, self._off[1:-1]))
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            self._fill()
+            return super().__getitem__(k)
+        k = int(k)
+        if k < 0:
+            k += self._n
+        if not 0 <= k < self._n:
+            raise IndexError(k)
+        return self._items[self._off[k]:self._off[k + 1]]
+
+    def __iter__(self):
+        for k in range(self._n):
+            yield self[k]
+
+
 class Loader(_Base):
-    """Text-file loader with dataloader.py:73-173 semantics."""
+    """Text-file loader with dataloader.py:73-173 semantics, parsed by the
+    native multi-threaded reader (the reference's Python loop runs ~1e5
+    lines/s; tools/bench_ingest.py times both)."""
 
     def __init__(self, config: dict | None = None, path: str = "./data/cf"):
         super().__init__()
         config = config or {}
         suffix = config.get("suffix", "")
-        test_mode = bool(config.get("test", False))
+        stop = 100 if bool(config.get("test", False)) else -1
         train_file = os.path.join(path, suffix, f"train{suffix}.txt")
         test_file = os.path.join(path, suffix, f"test{suffix}.txt")
-        tu, ti, allpos = [], [], []
-        self.n_user = 0
-        self.m_item = 0
-        with open(train_file) as f:
-            for line in f:
-                parts = line.strip("\n").split(" ")
-                if len(parts) < 1 or parts[0] == "":
-                    continue
-                uid = int(parts[0])
-                items = [int(x) for x in parts[1:] if x != ""]
-                tu.extend([uid] * len(items))
-                ti.extend(items)
-                allpos.append(np.array(items, dtype=np.int64))
-                if items:
-                    self.m_item = max(self.m_item, max(items))
-                self.n_user = max(self.n_user, uid)
-                if uid == 100 and test_mode:
-                    break
-        test_u, test_i = [], []
-        if os.path.exists(test_file):
-            with open(test_file) as f:
-                for line in f:
-                    parts = line.strip("\n").split(" ")
-                    if len(parts) < 1 or parts[0] == "":
-                        continue
-                    uid = int(parts[0])
-                    items = [int(x) for x in parts[1:] if x != ""]
-                    test_u.extend([uid] * len(items))
-                    test_i.extend(items)
-                    if items:
-                        self.m_item = max(self.m_item, max(items))
-                    self.n_user = max(self.n_user, uid)
-                    if uid == 100 and test_mode:
-                        break
-        self.m_item += 1
-        self.n_user += 1
-        self.trainUser = np.array(tu, dtype=np.int64)
-        self.trainItem = np.array(ti, dtype=np.int64)
-        self._allPos = allpos  # indexed by train-file line, as the reference
-        self.testUser = np.array(test_u, dtype=np.int64)
-        self.testItem = np.array(test_i, dtype=np.int64)
+        uid, off, items, mu, mi = parse_interactions(train_file, stop)
+        counts = np.diff(off)
+        self.trainUser = np.repeat(uid, counts)
+        self.trainItem = items
+        self._allPos = _LineIndexed(items, off)  # indexed by train-file line
+        n_user, m_item = mu, mi
         self._testDict = {}
-        for u, i in zip(test_u, test_i):
-            self._testDict.setdefault(u, []).append(i)
+        self.testUser = np.zeros(0, np.int64)
+        self.testItem = np.zeros(0, np.int64)
+        if os.path.exists(test_file):
+            tu, toff, titems, tmu, tmi = parse_interactions(test_file, stop)
+            tcounts = np.diff(toff)
+            self.testUser = np.repeat(tu, tcounts)
+            self.testItem = titems
+            n_user, m_item = max(n_user, tmu), max(m_item, tmi)
+            d = self._testDict
+            nz = np.nonzero(tcounts)[0]
+            tl = titems.tolist()
+            for u, a, b in zip(tu[nz].tolist(), toff[nz].tolist(), toff[nz + 1].tolist()):
+                d.setdefault(u, []).extend(tl[a:b])
+        # the reference starts both maxima at 0 (dataloader.py:80-81, 121-122)
+        self.n_user = int(max(n_user, 0)) + 1
+        self.m_item = int(max(m_item, 0)) + 1
 
 
 class SyntheticBipartite(_Base):

@@ -86,6 +86,21 @@ int mirec_csr_long_rows(const int64_t *rowptr, int64_t n_rows, int32_t split,
                         int64_t *long_segptr, int32_t *seg_row,
                         int64_t *seg_beg);
 
+/* Ingest (dataloader.py:93-150): parse an interaction file held in memory,
+ * one line per user "uid i1 i2 ..." (spaces / tabs; empty lines skipped;
+ * a line with only a uid counts as a line without items).  If stop_uid >= 0
+ * parsing ends after the first line whose uid == stop_uid (the reference's
+ * test-mode cut).  Call once with line_uid == NULL to get the counts and
+ * maxima (-1 if none), then with line_uid[n_lines], line_off[n_lines + 1],
+ * items[n_items]: line k has uid line_uid[k] and items
+ * items[line_off[k] .. line_off[k+1]), in file order.  n_threads host
+ * threads (buffers under 1 MiB use one).  MIREC_ERR_ARG on a malformed
+ * token. */
+int mirec_parse_interactions(const char *buf, int64_t len, int64_t stop_uid,
+                             int32_t n_threads, int64_t *n_lines, int64_t *n_items,
+                             int64_t *max_uid, int64_t *max_item, int64_t *line_uid,
+                             int64_t *line_off, int64_t *items);
+
 /* Device-resident CSR descriptor (all pointers are device pointers). */
 typedef struct mirec_csr {
   const int64_t *rowptr;      /* [n_rows+1] */

@@ -28,6 +28,47 @@ def test_loader_parses_reference_format(tmp_path):
     assert ds.trainDataSize == 6
 
 
+def _write_random_file(path, rng, n_lines, max_items, messy):
+    rows = []
+    for k in range(n_lines):
+        uid = k if not messy else int(rng.integers(0, n_lines * 2))
+        items = rng.integers(0, 5000, int(rng.integers(1, max_items))).tolist()
+        sep = "  " if (messy and k % 7 == 3) else " "
+        tail = " " if (messy and k % 5 == 1) else ""
+        rows.append(str(uid) + sep + sep.join(map(str, items)) + tail)
+        if messy and k % 11 == 4:
+            rows.append("")
+    path.write_text("\n".join(rows) + ("\n" if messy else ""))
+
+
+@pytest.mark.parametrize("n_lines,messy,test_mode", [(50, True, False), (300, True, True),
+                                                     (60_000, False, False),
+                                                     (60_000, True, True)])
+def test_native_ingest_matches_reference_loop(tmp_path, n_lines, messy, test_mode):
+    """mirec_parse_interactions (multi-threaded above 1 MiB) == the
+    reference's line loop (oracle.parse_interaction_file), incl. repeated
+    and trailing spaces, blank lines, no final newline, the test-mode cut."""
+    from furusato_recommend_amd.dataloader import parse_interactions
+    rng = np.random.default_rng(n_lines)
+    f = tmp_path / "train.txt"
+    _write_random_file(f, rng, n_lines, 40, messy)
+    ref = O.parse_interaction_file(str(f), test_mode)
+    uid, off, items, mu, mi = parse_interactions(str(f), 100 if test_mode else -1, n_threads=8)
+    assert uid.tolist() == [u for u, _ in ref]
+    got = [items[a:b].tolist() for a, b in zip(off[:-1], off[1:])]
+    assert got == [it for _, it in ref]
+    assert mu == max(u for u, _ in ref) and mi == max(max(it) for _, it in ref)
+
+
+def test_native_ingest_rejects_malformed(tmp_path):
+    from furusato_recommend_amd._lib import MirecError
+    from furusato_recommend_amd.dataloader import parse_interactions
+    f = tmp_path / "bad.txt"
+    f.write_text("0 1 2\n1 3x 4\n")
+    with pytest.raises(MirecError):
+        parse_interactions(str(f))
+
+
 def test_synthetic_invariants():
     from furusato_recommend_amd import FiveCore, SyntheticBipartite
     ds = SyntheticBipartite(1000, 200, 20000, seed=0)
