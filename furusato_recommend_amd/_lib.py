@@ -99,6 +99,8 @@ SIGNATURES = {
                                c_float, c_float, c_int32, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_bpr_seed_reset": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "mirec_seed_dense": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                 c_int32, c_void_p, c_int32, c_void_p]),
     "mirec_seed_pack": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "mirec_seed_merge_workspace": (c_int, [c_int64, c_int64, POINTER(c_size_t)]),
     "mirec_seed_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,

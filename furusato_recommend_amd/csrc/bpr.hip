@@ -432,3 +432,42 @@ extern "C" int mirec_seed_merge(const int32_t *keys_packed, const float *rows_p,
   }
   return MIREC_ERR_DIM;
 }
+
+namespace mirec {
+// dense[v] = dinv[v] * seed[slot[v]] (or 0 when clearing) for the listed
+// nodes v = list[i], i < *count: one LPR-lane group per node, float4.
+__global__ __launch_bounds__(256) void seed_dense_kernel(const int32_t *__restrict__ list,
+                                                         const int32_t *__restrict__ count,
+                                                         const int32_t *__restrict__ slot,
+                                                         const float *__restrict__ dinv,
+                                                         const float *__restrict__ seed,
+                                                         int32_t d4, float *__restrict__ dense,
+                                                         int clear) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t e = i / d4, c = i - e * d4;
+  if (e >= *count) return;
+  const int32_t v = list[e];
+  float4 x = f4_zero();
+  if (!clear) {
+    const int32_t r = slot[v];
+    if (r >= 0) x = f4_scale(dinv[v], ld4(seed + ((int64_t)r * d4 + c) * 4));
+  }
+  st4(dense + ((int64_t)v * d4 + c) * 4, x);
+}
+}  // namespace mirec
+
+extern "C" int mirec_seed_dense(const int32_t *list, const int32_t *count, int64_t cap,
+                                const int32_t *slot, const float *dinv, const float *seed,
+                                int32_t dim, float *dense, int32_t clear,
+                                mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(list && count && dense && cap >= 0 && dim > 0 && dim % 4 == 0);
+  MIREC_CHECK_ARG(clear || (slot && dinv && seed));
+  if (cap == 0) return MIREC_OK;
+  const int64_t tot = cap * (dim / 4);
+  hipLaunchKernelGGL(seed_dense_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), list, count, slot, dinv, seed,
+                     dim / 4, dense, clear);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

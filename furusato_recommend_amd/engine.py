@@ -180,7 +180,8 @@ class PropagationEngine:
         self.reuse_prescaled = True   # fused update writes the next x~_0
         # first backward layer's neighbour filter: "slot" (one dependent load;
         # best for one batch), "bytemap" (S byte map, then the slot of the
-        # hits; best for the union of many ranks' seeds) or "auto"
+        # hits), "dense" (seed rows scattered into a zero [N, D] table and
+        # gathered as a byte-map-filtered PRESCALED input) or "auto"
         self.sparse_filter = "auto"
         self._masks_ready = False
         # rows of degree <= narrow_max are gathered one per lane group
@@ -314,6 +315,18 @@ class PropagationEngine:
         c = self.list_counts
         return dict(row_mask=bm, row_list=lists[0], row_count=c[2 * k], row_list_cap=cap,
                     wide_list=lists[1], wide_count=c[2 * k + 1])
+
+    def _dense_seeds(self, seed_p, clear: int):
+        """Write (clear=0) or zero (clear=1) the pre-scaled seed rows of S in an
+        all-zero [N, D] table (sparse_filter == "dense")."""
+        if getattr(self, "seed_dense", None) is None:
+            self.seed_dense = torch.zeros(self.g.n_nodes, self.dim, dtype=torch.float32,
+                                          device=self.g.device)
+        check(lib.mirec_seed_dense(self.self_list.data_ptr(), self.self_count.data_ptr(),
+                                   self._self_cap, self.slot.data_ptr(), self.g.dinv.data_ptr(),
+                                   seed_p.data_ptr(), self.dim, self.seed_dense.data_ptr(),
+                                   int(clear), _lib.stream_handle()), "seed_dense")
+        return self.seed_dense
 
     def _sparse_filter(self):
         f = self.sparse_filter
@@ -488,8 +501,13 @@ class PropagationEngine:
                 if first:
                     # input g_L = d lives on S only; with pruning its output
                     # g_{L-1} is written only on F1 = S ∪ N(S) (zero elsewhere)
-                    kw = dict(in_mode=IN_SPARSE, seed_in=seed_p, in_mask=self._sparse_filter(),
-                              **(self._hop_rows() if (self.prune and l > 0) else {}))
+                    rows = self._hop_rows() if (self.prune and l > 0) else {}
+                    if self.sparse_filter == "dense":
+                        kw = dict(in_mode=IN_PRESCALED, x_in=self._dense_seeds(seed_p, 0),
+                                  in_mask=self.bm_self, **rows)
+                    else:
+                        kw = dict(in_mode=IN_SPARSE, seed_in=seed_p,
+                                  in_mask=self._sparse_filter(), **rows)
                 else:
                     kw = dict(in_mode=IN_PRESCALED, x_in=self.xs[(L - 2 - l) % 2],
                               in_mask=self.bm_hop if (self.prune and l == L - 2) else None)
@@ -499,6 +517,8 @@ class PropagationEngine:
                 else:
                     kw.update(xs_out=self.xs[(L - 1 - l) % 2])
                 self._prop(**kw)
+        if self.sparse_filter == "dense" and L > 0:
+            self._dense_seeds(seed_p, 1)
         check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), keys_sorted.data_ptr(), n_keys,
                                        _lib.stream_handle()), "bpr_seed_reset")
         self._seeds = None

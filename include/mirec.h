@@ -276,6 +276,14 @@ int mirec_bpr_seed(const float *out, const float *emb, int64_t n_nodes,
 int mirec_bpr_seed_reset(int32_t *slot, const int32_t *keys_sorted, int64_t n,
                          mirec_stream_t stream);
 
+/* Dense pre-scaled seed rows: dense[v] = dinv[v] * seed[slot[v]] for the
+ * listed nodes v = list[i], i < *count (device count, host bound cap), or
+ * zeros when clear != 0 (restoring an all-zero table).  Feeds the first
+ * backward layer as a PRESCALED input filtered by the S byte map. */
+int mirec_seed_dense(const int32_t *list, const int32_t *count, int64_t cap,
+                     const int32_t *slot, const float *dinv, const float *seed,
+                     int32_t dim, float *dense, int32_t clear, mirec_stream_t stream);
+
 /* Data-parallel sparse gradient exchange (dist.py).  The backward pass is
  * linear in the seeds, so the union batch's gradient is the backward of the
  * SUM of every rank's seeds: ranks all-gather their (node, seed_p, seed_e)

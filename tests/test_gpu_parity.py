@@ -851,3 +851,19 @@ def test_fused_leaf_gather_mean_equals_unfused():
                                            ctypes.c_uint64(seed), g.data_ptr(), st), "fmg_bwd")
     assert torch.equal(out, ref.detach())
     assert rel(g, gref) < TOL
+
+
+@pytest.mark.parametrize("filt", ["slot", "bytemap", "dense"])
+def test_first_backward_layer_filters_agree(golden, filt):
+    """The three ways of feeding the first backward layer (slot-filtered
+    seeds, byte-map then slot, dense pre-scaled seed table) give the
+    reference's two training steps."""
+    f = golden("lgcn_d64_L3.npz")
+    m = lgcn_from(f)
+    m.engine.sparse_filter = filt
+    t = torch.from_numpy(f["triples"])
+    m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    m.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    assert rel(m.all_embedding.weight, f["emb_step2"]) < TOL
+    if filt == "dense":
+        assert float(m.engine.seed_dense.abs().max()) == 0.0  # table restored
