@@ -39,6 +39,53 @@ class _DS:
         self.n_users, self.m_items = n_users, m_items
 
 
+def cpu_baseline(m, seq, B, heads, rng):
+    """The oracle's restatement of sasrec.py:385-435 (torch CPU fp32, padded
+    batch as the reference's pad_sequence, dropout off) on one batch of the
+    same workload: blocks + pool, item tower, BPR + embedding-norm loss,
+    backward, torch Adam over every parameter."""
+    import torch.nn.functional as F
+
+    from oracle import lightgcn_oracle as O
+    L = m.num_layers
+    cpu = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.named_parameters()}
+    p = {}
+    for i in range(L):
+        a = f"attn_layers.{i}."
+        p.update({f"ln1_w{i}": cpu[f"attn_norm_layers.{i}.weight"],
+                  f"ln1_b{i}": cpu[f"attn_norm_layers.{i}.bias"],
+                  f"in_w{i}": cpu[a + "in_proj_weight"], f"in_b{i}": cpu[a + "in_proj_bias"],
+                  f"out_w{i}": cpu[a + "out_proj.weight"], f"out_b{i}": cpu[a + "out_proj.bias"],
+                  f"ln2_w{i}": cpu[f"ffn_norm_layers.{i}.weight"],
+                  f"ln2_b{i}": cpu[f"ffn_norm_layers.{i}.bias"],
+                  f"ffn_w{i}": cpu[f"ffn_layers.{i}.weight"], f"ffn_b{i}": cpu[f"ffn_layers.{i}.bias"]})
+    u = torch.from_numpy(rng.integers(0, seq.items.shape[0], B))
+    items = seq.items.cpu()[u].long()
+    length = seq.length.cpu()[u]
+    pos = items[torch.arange(B), (torch.rand(B) * length).long()]
+    neg = torch.randint(0, m.m_item, (B,))
+    opt = torch.optim.Adam(list(cpu.values()), lr=1e-3)
+    W = cpu["item_id_embedding.weight"]
+
+    def tower(x):
+        for j in range(L - 1):
+            x = F.linear(x, cpu[f"item_linears.{j}.weight"], cpu[f"item_linears.{j}.bias"]).relu()
+        return F.linear(x, cpu["item_last_proj.weight"], cpu["item_last_proj.bias"])
+
+    t0 = time.perf_counter()
+    T = seq.max_len
+    mask = (torch.arange(T)[None, :] < length[:, None]).float().unsqueeze(2)
+    ue = O.sasrec_forward_user(W[items] * mask, length, p, heads, L)
+    pe, ne = tower(W[pos]), tower(W[neg])
+    loss = F.softplus((ue * ne).sum(1) - (ue * pe).sum(1)).mean() + 1e-4 * W.norm(2) / B
+    loss.backward()
+    opt.step()
+    t = time.perf_counter() - t0
+    return {"value": round(B / t, 2), "unit": "positive-edges/s", "cores": torch.get_num_threads(),
+            "kind": "port", "step_s": round(t, 3),
+            "sample": f"1 training step (B={B}, padded T={T}) of the C4 workload"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -50,6 +97,7 @@ def main():
     ap.add_argument("--maxlen", type=int, default=50)
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--cpu-baseline", type=int, default=1)
     args = ap.parse_args()
     from furusato_recommend_amd import SASRec, sasrec as S
     from furusato_recommend_amd.sasrec import SequenceData
@@ -121,6 +169,7 @@ def main():
                           "unit": "TFLOP/s", "frac": round(t_mfma / t, 4)}
         roof[kind].update(avg_launch_ms=round(ms / cnt, 4), launches_per_step=cnt / args.steps,
                           flop_per_launch=fl, bytes_per_launch=by)
+    cpu = cpu_baseline(m, seq, B, args.heads, rng) if args.cpu_baseline else None
     print(json.dumps({
         "metric": "SASRec BPR positive-edges/sec (C4)",
         "value": round(args.steps * B / dt, 1), "unit": "positive-edges/s", "n_gpus": 1,
@@ -129,7 +178,7 @@ def main():
         "config": {"workload": "C4: SASRec L=%d heads=%d d=%d maxlen=%d, %d users x %d items"
                    % (args.layers, args.heads, args.dim, args.maxlen, args.users, args.items),
                    "bpr_batch": B},
-        "attention_roofline": roof}), flush=True)
+        "attention_roofline": roof, "cpu_baseline": cpu}), flush=True)
 
 
 if __name__ == "__main__":
