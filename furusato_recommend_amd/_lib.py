@@ -106,6 +106,8 @@ SIGNATURES = {
     "mirec_seed_merge": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int64,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                  c_void_p]),
+    "mirec_adam_multi": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                 POINTER(AdamH), c_void_p]),
     "mirec_adam_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                  POINTER(AdamH), c_void_p]),
     "mirec_sample_fanout": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int32, c_uint64,

@@ -41,7 +41,68 @@ __global__ void adam_tail_kernel(float *param, const float *grad, float *m, floa
   if (i < n) adam1(param[i], m[i], v[i], grad[i], h);
 }
 
+// Multi-tensor Adam: up to kAdamMulti (param, grad, m, v) tensors with the
+// same hyper-parameters in one launch (the pointer table travels in the
+// kernel arguments).  Work item i is float i of the concatenation; the
+// tensor is found by a scan of the prefix offsets (<= 32 entries).
+constexpr int kAdamMulti = 32;
+struct AdamMultiArgs {
+  float *p[kAdamMulti];
+  const float *g[kAdamMulti];
+  float *m[kAdamMulti];
+  float *v[kAdamMulti];
+  int64_t off[kAdamMulti + 1];
+  int32_t count;
+  mirec_adam_hparams_t h;
+};
+
+__global__ __launch_bounds__(256) void adam_multi_kernel(AdamMultiArgs a) {
+  const int64_t total = a.off[a.count];
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    int t = 0;
+    while (a.off[t + 1] <= i) ++t;
+    const int64_t j = i - a.off[t];
+    float pv = a.p[t][j], mv = a.m[t][j], vv = a.v[t][j];
+    adam1(pv, mv, vv, a.g[t][j], a.h);
+    a.p[t][j] = pv;
+    a.m[t][j] = mv;
+    a.v[t][j] = vv;
+  }
+}
+
 }  // namespace mirec
+
+extern "C" int mirec_adam_multi(int32_t count, float *const *params, const float *const *grads,
+                                float *const *exp_avg, float *const *exp_avg_sq,
+                                const int64_t *numel, const mirec_adam_hparams_t *h,
+                                mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(count >= 0 && h && (count == 0 || (params && grads && exp_avg && exp_avg_sq &&
+                                                    numel)));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  for (int32_t b = 0; b < count; b += kAdamMulti) {
+    AdamMultiArgs a;
+    a.count = std::min(kAdamMulti, count - b);
+    a.h = *h;
+    a.off[0] = 0;
+    for (int t = 0; t < a.count; ++t) {
+      MIREC_CHECK_ARG(params[b + t] && grads[b + t] && exp_avg[b + t] && exp_avg_sq[b + t] &&
+                      numel[b + t] >= 0);
+      a.p[t] = params[b + t];
+      a.g[t] = grads[b + t];
+      a.m[t] = exp_avg[b + t];
+      a.v[t] = exp_avg_sq[b + t];
+      a.off[t + 1] = a.off[t] + numel[b + t];
+    }
+    const int64_t total = a.off[a.count];
+    if (total == 0) continue;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(adam_multi_kernel, dim3(blocks), dim3(256), 0, st, a);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
 
 extern "C" int mirec_adam_dense(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
                                 int64_t n, const mirec_adam_hparams_t *h,

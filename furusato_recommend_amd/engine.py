@@ -111,6 +111,13 @@ class AdamState:
                                    self.param.numel(), ctypes.byref(hp), _lib.stream_handle()),
               "adam_dense")
 
+    def _launch(self, hp):
+        g = self.param.grad.contiguous()
+        check(lib.mirec_adam_dense(self.param.data_ptr(), g.data_ptr(),
+                                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                   self.param.numel(), ctypes.byref(hp), _lib.stream_handle()),
+              "adam_dense")
+
     def state_dict(self, param_id: int = 0) -> dict:
         """Same structure as torch.optim.Adam.state_dict() for one param."""
         return {
@@ -130,6 +137,53 @@ class AdamState:
             self.exp_avg_sq.copy_(st["exp_avg_sq"])
         g = sd["param_groups"][0]
         self.lr, self.betas, self.eps = float(g["lr"]), tuple(g["betas"]), float(g["eps"])
+
+
+class AdamGroup:
+    """Steps a model's AdamStates together: tensors of at least LARGE
+    elements with the float4 dense kernel, all the others in one
+    mirec_adam_multi launch per distinct (step, lr, betas, eps) — instead of
+    one launch (and one host round of Python) per parameter."""
+
+    LARGE = 1 << 20
+
+    def __init__(self, states):
+        self.states = list(states)
+
+    def __iter__(self):
+        return iter(self.states)
+
+    def __len__(self):
+        return len(self.states)
+
+    def zero_grad(self, set_to_none: bool = True):
+        for s in self.states:
+            s.zero_grad(set_to_none)
+
+    @torch.no_grad()
+    def step(self):
+        groups = {}
+        for s in self.states:
+            if s.param.grad is None:
+                continue
+            hp = s.next_hparams()
+            if s.param.numel() >= self.LARGE:
+                s._launch(hp)
+                continue
+            key = (s.n_steps, s.lr, s.betas, s.eps)
+            groups.setdefault(key, (hp, []))[1].append(s)
+        if not groups and not any(s.param.grad is not None for s in self.states):
+            return
+        _note_raw_write()
+        for hp, members in groups.values():
+            n = len(members)
+            grads = [m.param.grad.contiguous() for m in members]
+            arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+            numel = (ctypes.c_int64 * n)(*[m.param.numel() for m in members])
+            check(lib.mirec_adam_multi(n, arr([m.param for m in members]), arr(grads),
+                                       arr([m.exp_avg for m in members]),
+                                       arr([m.exp_avg_sq for m in members]), numel,
+                                       ctypes.byref(hp), _lib.stream_handle()), "adam_multi")
 
 
 class PropagationEngine:

@@ -30,8 +30,9 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
-from .engine import AdamState, sample_triples
+from .engine import AdamGroup, AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
+from .linear import Linear
 
 
 # ----------------------------------------------------------------- autograd
@@ -201,14 +202,14 @@ class GraphSAGE(nn.Module):
         # one [N, d] table; the reference's two id tables are views into it
         self._table = nn.Parameter(torch.empty(n, d, device=self.device))
         self.w_linears = nn.ModuleList(
-            [nn.Linear(2 * d, d, device=self.device) for _ in range(L)])
+            [Linear(2 * d, d, device=self.device) for _ in range(L)])
         self.init_parameters()
         self.graph = Graph.from_interactions(dataset.trainUser, dataset.trainItem,
                                              self.n_user, self.m_item, self.device,
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
         deg = torch.from_numpy(self.graph.degree()).to(self.device).float()
         self._mean_dinv = torch.where(deg > 0, 1.0 / deg.clamp(min=1), torch.zeros_like(deg))
-        self.optims = [AdamState(p, lr=config["lr"]) for p in self.parameters()]
+        self.optims = AdamGroup(AdamState(p, lr=config["lr"]) for p in self.parameters())
         self._step_seed = int(config.get("seed", 2020))
         self._calls = 0
 
@@ -349,9 +350,7 @@ class GraphSAGE(nn.Module):
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         if grad_hook is not None:
             grad_hook()
-        with torch.no_grad():
-            for opt in self.optims:
-                opt.step()
+        self.optims.step()
         return loss.detach()
 
     def OneEpoch(self, user, pos, neg):

@@ -22,7 +22,8 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib
-from .engine import AdamState
+from .engine import AdamGroup, AdamState
+from .linear import Linear, linear
 from .rows import gather_rows
 
 
@@ -116,14 +117,14 @@ class CausalSelfAttention(nn.Module):
         self.heads = heads
         self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d, device=device))
         self.in_proj_bias = nn.Parameter(torch.zeros(3 * d, device=device))
-        self.out_proj = nn.Linear(d, d, device=device)
+        self.out_proj = Linear(d, d, device=device)
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
 
     def forward(self, x, offsets=None):
         """x [B, T, d] (padded), or packed [n_tok, d] with int32 ``offsets``
         [B+1] (sequence b = rows offsets[b] .. offsets[b+1]-1)."""
-        qkv = F.linear(x, self.in_proj_weight, self.in_proj_bias)
+        qkv = linear(x, self.in_proj_weight, self.in_proj_bias)
         if offsets is None:
             att = _CausalAttention.apply(qkv, self.heads)
         else:
@@ -185,13 +186,13 @@ class SASRec(nn.Module):
         self.attn_layers = nn.ModuleList([CausalSelfAttention(d, heads, dev) for _ in range(L)])
         self.attn_norm_layers = nn.ModuleList([nn.LayerNorm(d, device=dev) for _ in range(L)])
         self.ffn_norm_layers = nn.ModuleList([nn.LayerNorm(d, device=dev) for _ in range(L)])
-        self.ffn_layers = nn.ModuleList([nn.Linear(d, d, device=dev) for _ in range(L)])
-        self.item_linears = nn.ModuleList([nn.Linear(d, d, device=dev) for _ in range(L - 1)])
-        self.item_last_proj = nn.Linear(d, d, device=dev)
+        self.ffn_layers = nn.ModuleList([Linear(d, d, device=dev) for _ in range(L)])
+        self.item_linears = nn.ModuleList([Linear(d, d, device=dev) for _ in range(L - 1)])
+        self.item_last_proj = Linear(d, d, device=dev)
         if sequences is None:
             sequences = SequenceData(dataset.allPos, dev)
         self.seq = sequences
-        self.optims = [AdamState(p, lr=config["lr"]) for p in self.parameters()]
+        self.optims = AdamGroup(AdamState(p, lr=config["lr"]) for p in self.parameters())
 
     # ------------------------------------------------------------- blocks
     def oneblock(self, x, layer, offsets=None):
@@ -318,9 +319,7 @@ class SASRec(nn.Module):
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         if grad_hook is not None:
             grad_hook()
-        with torch.no_grad():
-            for opt in self.optims:
-                opt.step()
+        self.optims.step()
         return loss.detach()
 
     def OneEpoch(self, user, pos, neg):

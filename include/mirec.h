@@ -313,6 +313,15 @@ int mirec_adam_dense(float *param, const float *grad, float *exp_avg,
                      float *exp_avg_sq, int64_t n,
                      const mirec_adam_hparams_t *h, mirec_stream_t stream);
 
+/* Multi-tensor form for the small parameters of a model sharing one step
+ * count: count (param, grad, exp_avg, exp_avg_sq, numel) tensors given as
+ * host arrays of device pointers, one launch per 32 tensors.  Same update
+ * as mirec_adam_dense. */
+int mirec_adam_multi(int32_t count, float *const *params, const float *const *grads,
+                     float *const *exp_avg, float *const *exp_avg_sq,
+                     const int64_t *numel, const mirec_adam_hparams_t *hp,
+                     mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* On-device BPR sampler (negative_sample.py:98-134 semantics)               */
 /* ------------------------------------------------------------------------ */

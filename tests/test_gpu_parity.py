@@ -867,3 +867,33 @@ def test_first_backward_layer_filters_agree(golden, filt):
     assert rel(m.all_embedding.weight, f["emb_step2"]) < TOL
     if filt == "dense":
         assert float(m.engine.seed_dense.abs().max()) == 0.0  # table restored
+
+
+def test_adam_group_equals_per_tensor_adam():
+    """AdamGroup (one multi-tensor launch per 32 small tensors, the dense
+    kernel for large ones) == per-tensor mirec_adam_dense == torch Adam
+    (same update; the compiler may contract FMAs differently per kernel)."""
+    from furusato_recommend_amd.engine import AdamGroup, AdamState
+    torch.manual_seed(2)
+    shapes = [(7,), (128,), (3, 5), (1 << 20, 2)] + [(33,)] * 35
+    a = [torch.randn(s, device="cuda") for s in shapes]
+    b = [t.clone() for t in a]
+    c = [t.clone().requires_grad_(True) for t in a]
+    ga = AdamGroup(AdamState(t, lr=1e-2) for t in a)
+    gb = [AdamState(t, lr=1e-2) for t in b]
+    tor = torch.optim.Adam(c, lr=1e-2)
+    for _ in range(3):
+        gr = [torch.randn_like(t) for t in a]
+        for t, g in zip(a, gr):
+            t.grad = g
+        for t, g in zip(b, gr):
+            t.grad = g.clone()
+        for t, g in zip(c, gr):
+            t.grad = g.clone()
+        ga.step()
+        for s in gb:
+            s.step()
+        tor.step()
+    for x, y, z in zip(a, b, c):
+        assert rel(x, y) < 1e-6  # fma contraction may differ between the kernels
+        assert rel(x, z.detach()) < TOL

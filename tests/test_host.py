@@ -270,3 +270,26 @@ def test_dense_grad_data_parallel_gloo():
         assert np.array_equal(a, b)
     for k, (a, b) in enumerate(zip(res[0][1], res[1][1])):
         assert np.array_equal(a, b) and np.all(a == 3.0 * (k + 1))
+
+
+def test_split_k_linear_matches_nn_linear():
+    """linear.Linear (split-K weight gradient, used on packed activations) ==
+    nn.Linear in value and in every gradient, above and below the split
+    threshold and with a ragged tail."""
+    from furusato_recommend_amd.linear import Linear, weight_grad
+    torch.manual_seed(0)
+    for n in (100, 8192, 20_011):
+        x = torch.randn(n, 128, dtype=torch.float64, requires_grad=True)
+        a = Linear(128, 96).double()
+        b = torch.nn.Linear(128, 96).double()
+        b.load_state_dict(a.state_dict())
+        x2 = x.detach().clone().requires_grad_(True)
+        gy = torch.randn(n, 96, dtype=torch.float64)
+        ya, yb = a(x), b(x2)
+        assert torch.allclose(ya, yb)
+        ya.backward(gy)
+        yb.backward(gy)
+        assert torch.allclose(x.grad, x2.grad)
+        assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-10, atol=1e-9)
+        assert torch.allclose(a.bias.grad, b.bias.grad)
+        assert torch.allclose(weight_grad(gy, x.detach()), gy.t() @ x.detach())
