@@ -114,7 +114,9 @@ extern "C" int mirec_adam_dense(float *param, const float *grad, float *exp_avg,
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t n4 = n / 4;
   if (n4 > 0) {
-    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 256 * 16);
+    // enough workgroups to keep ~8 float4 streams per CU in flight at
+    // table sizes (a 4096-block grid-stride loop measured 3.9 TB/s)
+    const int64_t blocks = std::min<int64_t>((n4 + 255) / 256, 65536);
     hipLaunchKernelGGL(adam_dense_kernel, dim3(blocks), dim3(256), 0, st, param, grad, exp_avg,
                        exp_avg_sq, n4, *h);
     MIREC_LAUNCH_CHECK();

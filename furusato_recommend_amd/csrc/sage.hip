@@ -138,24 +138,37 @@ __global__ __launch_bounds__(256) void fanout_mean_bwd_kernel(
 }
 
 // Backward of the fused gather + mean: table_grad[ids[child]] += mask *
-// grad_out[t] / cnt.  One thread per (child, float): a wave-instruction adds
-// 64 consecutive floats of one row (the full-rate atomic shape).
+// grad_out[t] / cnt.  One wave per target: the k child ids are read once
+// (cnt by ballot), grad_out[t] stays in registers, and every valid child's
+// row is added with one wave-instruction per 64 consecutive floats (the
+// full-rate atomic shape).  Dropout element index = child * d + col, as in
+// the unfused path.
 __global__ __launch_bounds__(256) void fanout_mean_gather_bwd_kernel(
     const float *__restrict__ grad_out, const int32_t *__restrict__ ids, int64_t n_targets,
     int32_t k, int32_t d, uint64_t key, uint32_t thresh, float scale,
     float *__restrict__ table_grad) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (child, column)
-  if (i >= n_targets * k * d) return;
-  const int64_t child = i / d;
-  const int64_t col = i - child * d;
-  const int32_t id = ids[child];
-  if (id < 0) return;
-  const int64_t t = child / k;
-  int cnt = 0;
-  for (int c = 0; c < k; ++c) cnt += ids[t * k + c] >= 0 ? 1 : 0;
-  float g = grad_out[t * d + col] / (float)cnt;
-  if (thresh != 0u) g = keep(key, (uint64_t)i, thresh) ? g * scale : 0.f;
-  atomicAdd(table_grad + (int64_t)id * d + col, g);
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (t >= n_targets) return;
+  const int32_t myid = lane < k ? ids[t * k + lane] : -1;  // k <= 64 (checked on host)
+  const unsigned long long valid = __ballot(myid >= 0);
+  const int cnt = __popcll(valid);
+  if (cnt == 0) return;
+  const float inv = 1.f / (float)cnt;
+  for (int c0 = 0; c0 < d; c0 += 64) {
+    const int col = c0 + lane;
+    const float g = col < d ? grad_out[t * d + col] * inv : 0.f;
+    for (int c = 0; c < k; ++c) {
+      if (!((valid >> c) & 1ull)) continue;  // wave-uniform
+      const int32_t id = __shfl(myid, c);
+      if (col < d) {
+        float x = g;
+        if (thresh != 0u)
+          x = keep(key, (uint64_t)((t * k + c) * (int64_t)d + col), thresh) ? x * scale : 0.f;
+        atomicAdd(table_grad + (int64_t)id * d + col, x);
+      }
+    }
+  }
 }
 
 static bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
@@ -273,8 +286,9 @@ extern "C" int mirec_fanout_mean_gather_bwd(const float *grad_out, const int32_t
   float scale;
   MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
   if (n_targets == 0) return MIREC_OK;
-  const int64_t tot = n_targets * k * dim;
-  hipLaunchKernelGGL(fanout_mean_gather_bwd_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+  MIREC_CHECK_ARG(k <= 64);
+  const int64_t tot = n_targets;  // one wave per target, 4 per block
+  hipLaunchKernelGGL(fanout_mean_gather_bwd_kernel, dim3((tot + 3) / 4), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), grad_out, ids, n_targets, k, dim,
                      key, thresh, scale, table_grad);
   MIREC_LAUNCH_CHECK();

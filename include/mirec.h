@@ -378,7 +378,7 @@ int mirec_fanout_mean_bwd(const float *grad_out, const int32_t *valid,
  * ids[t*k+c] >= 0 of dropout_p-dropout(table[ids[t*k+c]]) — the row gather
  * and mirec_fanout_mean in one pass (same dropout mask as gathering first
  * and calling mirec_fanout_mean).  The backward adds mask * grad_out[t] /
- * cnt into table_grad[ids[t*k+c]] (float atomics).  dim % 4 == 0. */
+ * cnt into table_grad[ids[t*k+c]] (float atomics; k <= 64).  dim % 4 == 0. */
 int mirec_fanout_mean_gather(const float *table, const int32_t *ids, int64_t n_targets,
                              int32_t k, int32_t dim, float dropout_p, uint64_t seed,
                              float *out, mirec_stream_t stream);
