@@ -294,7 +294,10 @@ __device__ __forceinline__ void prop_work(const PropK &a, int64_t w, int64_t nro
     if (have) {
       beg = a.rowptr[row];
       end = a.rowptr[row + 1];
-      if (a.split > 0 && end - beg > a.split) have = false;  // segments handle it
+      if (a.split > 0 && end - beg > a.split) {  // segments handle it
+        have = false;
+        beg = end = 0;  // the narrow gather must not walk the long row
+      }
     }
     const int64_t deg = have ? end - beg : 0;
     if (G > 1 && __ballot(deg > a.narrow_max) == 0ull) {
