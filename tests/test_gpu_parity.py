@@ -897,3 +897,31 @@ def test_adam_group_equals_per_tensor_adam():
     for x, y, z in zip(a, b, c):
         assert rel(x, y) < 1e-6  # fma contraction may differ between the kernels
         assert rel(x, z.detach()) < TOL
+
+
+def test_zipf_long_rows_not_walked_by_row_phase():
+    """Performance regression guard: rows longer than the split are covered
+    by their segments only (a wave's narrow gather once walked them serially:
+    200x slower at C2 scale).  Loose bound: the Zipf graph's launch stays
+    within 5x of a uniform graph with the same edge count."""
+    from furusato_recommend_amd import Graph, SyntheticBipartite
+    from furusato_recommend_amd.engine import propagate
+    times = []
+    for kind in ("zipf", "uniform"):
+        ds = SyntheticBipartite(200_000, 20_000, 4_000_000, seed=1, kind=kind)
+        g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items,
+                                    "cuda:0")
+        x = torch.randn(g.n_nodes, 64, device="cuda")
+        y = torch.empty_like(x)
+        for _ in range(2):
+            propagate(g, x, y)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        propagate(g, x, y)
+        e.record()
+        torch.cuda.synchronize()
+        times.append(s.elapsed_time(e))
+        if kind == "zipf":
+            assert g.n_long > 0
+    assert times[0] < 5 * times[1] + 0.5, times
