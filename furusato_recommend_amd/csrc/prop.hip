@@ -4,17 +4,20 @@
 // Replaces PyG LGConv (model/lgcn.py:66,82) / rAdjConv (model/radj.py:28-44):
 //   out[i] = sum_{(j -> i)} x[j] / sqrt(deg_i * deg_j)
 // which the reference evaluates as a [nnz, D] gather, a scale and an atomic
-// scatter-add.  Here one 64-lane wave owns one destination row: the row's
-// column indices are read once, coalesced (64 per load), and broadcast with
-// ds_bpermute; every LPR = D/4 lanes form a group that reads one whole
-// neighbour row as float4s (D=64: 16 lanes x 16 B = one 256-B row), so a wave
-// instruction pulls G = 64/LPR neighbour rows and UNROLL instructions are in
-// flight per lane.  Groups accumulate disjoint neighbour subsets in
-// registers and are combined with a xor-butterfly at the end: no atomics, no
-// LDS, a fixed summation order per row (deterministic).
+// scatter-add.  A wave owns G = 64/LPR consecutive rows (LPR = D/4 lanes read
+// one neighbour row as float4s: D=64 -> 16 lanes x 16 B = one 256-B row).
+// Short rows (degree <= narrow_max) are gathered one per lane group; a wave
+// with a longer row walks its rows one at a time with the whole wave: the
+// row's column indices are read once, coalesced (64 per load), broadcast
+// with ds_bpermute, and G x UNROLL neighbour rows are in flight per
+// instruction; groups hold disjoint neighbour subsets in registers and are
+// combined with a xor-butterfly.  No atomics, a fixed summation order per
+// row (deterministic).
 //
 // Masks (byte maps over nodes, optional; 1.1 MB at C2, L2-resident):
 //   row_mask  rows whose byte is 0 are skipped entirely (nothing written);
+//             with frontier row lists the rows come from the lists instead
+//             (narrow rows G per wave, wide rows one workgroup each);
 //   in_mask   neighbours whose byte is 0 contribute exactly 0 and are not
 //             read: the 64 candidates of a chunk are tested at once and the
 //             valid ones compacted to the front with ds_permute.
@@ -24,7 +27,8 @@
 //
 // Rows longer than csr->split are cut into segments processed by extra waves
 // of the same launch (partial sums to scratch) and summed in segment order by
-// a finalize launch, so a Zipf-skewed item cannot serialise the grid.
+// a finalize launch, so a Zipf-skewed item cannot serialise the grid (the
+// row phase leaves them to their segments entirely).
 //
 // Epilogue (per row, LPR lanes): z = dinv_i * sum + seed[slot_i];
 // xs_out = dinv_i * z (next layer's pre-scaled input);
