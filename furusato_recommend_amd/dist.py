@@ -66,6 +66,16 @@ class DataParallel:
         dist.all_gather_into_tensor(out, t.contiguous(), group=self.group)
         return out
 
+    def _exchange(self, keys, rows_p, rows_e):
+        """One all-gather of [key | seed_p | seed_e] records (the int32 key
+        travels bit-cast in the first float column), split back by rank-major
+        row order."""
+        D = rows_p.shape[1]
+        rec = torch.cat([keys.view(torch.float32).unsqueeze(1), rows_p, rows_e], dim=1)
+        allrec = self._all_gather(rec)
+        return (allrec[:, 0].contiguous().view(torch.int32), allrec[:, 1:1 + D].contiguous(),
+                allrec[:, 1 + D:].contiguous())
+
     def step(self, users, pos, neg, decay: float, loss_accum=None):
         eng = self.engine
         out = eng.forward_for_batch(self.emb, users, pos, neg)
@@ -74,8 +84,7 @@ class DataParallel:
         if self.mode == "sparse":
             keys, rows_p, rows_e = eng.export_seeds()
             if self.distributed:
-                keys, rows_p, rows_e = (self._all_gather(keys), self._all_gather(rows_p),
-                                        self._all_gather(rows_e))
+                keys, rows_p, rows_e = self._exchange(keys, rows_p, rows_e)
             eng.import_seeds(keys, rows_p, rows_e)
             eng.backward(self.emb, adam=self.adam)
         else:

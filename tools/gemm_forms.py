@@ -1,6 +1,7 @@
-"""Times equivalent formulations of the SASRec Linear GEMMs (f32) to pick the
-hipBLASLt problem orientation that runs fastest (C4 shapes: n packed tokens,
-d = 128, in_proj N = 384)."""
+"""SASRec Linear GEMMs (f32): device time of equivalent formulations and the
+host-side cost per call of each BLAS backend torch can use on ROCm."""
+import time
+
 import torch
 
 
@@ -17,29 +18,42 @@ def t(fn, reps=20):
     return s.elapsed_time(e) / reps * 1e3
 
 
+def host_us(fn, reps=200):
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    return (t1 - t0) / reps * 1e6
+
+
 def main():
-    n, K = 56_320, 128
-    for N in (384, 128):
-        x = torch.randn(n, K, device="cuda")
-        w = torch.randn(N, K, device="cuda")
-        b = torch.randn(N, device="cuda")
-        dy = torch.randn(n, N, device="cuda")
-        fl = 2.0 * n * K * N
+    n, K, N = 56_320, 128, 384
+    x = torch.randn(n, K, device="cuda")
+    w = torch.randn(N, K, device="cuda")
+    b = torch.randn(N, device="cuda")
+    dy = torch.randn(n, N, device="cuda")
+    xs, ws = torch.randn(64, K, device="cuda"), torch.randn(N, K, device="cuda")
+    for lib in ("default", "cublaslt", "cublas"):
+        try:
+            if lib != "default":
+                torch.backends.cuda.preferred_blas_library(lib)
+        except Exception as e:  # noqa: BLE001
+            print(lib, "unavailable", e)
+            continue
         res = {
-            "fwd F.linear": t(lambda: torch.nn.functional.linear(x, w, b)),
-            "fwd x@w.t()": t(lambda: x @ w.t()),
-            "fwd (w@x.t()).t()": t(lambda: (w @ x.t()).t()),
-            "fwd addmm": t(lambda: torch.addmm(b, x, w.t())),
-            "dX dy@w": t(lambda: dy @ w),
-            "dX (w.t()@dy.t()).t()": t(lambda: (w.t() @ dy.t()).t()),
-            "dW dy.t()@x": t(lambda: dy.t() @ x),
-            "dW (x.t()@dy).t()": t(lambda: (x.t() @ dy).t()),
-            "dW chunked4": t(lambda: sum(dy[i::4].t() @ x[i::4] for i in range(4))),
+            "addmm dev us": t(lambda: torch.addmm(b, x, w.t())),
+            "dX mm dev us": t(lambda: dy @ w),
+            "dW split32 dev us": t(lambda: torch.bmm(dy.view(32, n // 32, N).transpose(1, 2),
+                                                     x.view(32, n // 32, K)).sum(0)),
+            "small mm host us": host_us(lambda: xs @ ws.t()),
+            "small addmm host us": host_us(lambda: torch.addmm(b, xs, ws.t())),
+            "small bmm host us": host_us(lambda: torch.bmm(xs.view(4, 16, K), ws.t().expand(4, K, N))),
         }
-        for S in (4, 8, 16, 32, 64, 128):
-            res[f"dW bmm split{S}"] = t(lambda S=S: torch.bmm(
-                dy.view(S, n // S, N).transpose(1, 2), x.view(S, n // S, K)).sum(0))
-        print(f"N={N}", {k: f"{v:.1f}us {fl / v / 1e6:.1f}TF" for k, v in res.items()})
+        print(lib, torch.backends.cuda.preferred_blas_library(),
+              {k: round(v, 1) for k, v in res.items()}, flush=True)
 
 
 if __name__ == "__main__":
