@@ -10,6 +10,8 @@ parameters and state_dict keys as nn.Linear; the forward is unchanged.
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -58,3 +60,20 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> t
 class Linear(nn.Linear):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         return _LinearSplitK.apply(x, self.weight, self.bias)
+
+
+@contextlib.contextmanager
+def blas_backend(name: str | None):
+    """Temporarily select torch's BLAS backend ("cublas" = rocBLAS,
+    "cublaslt" = hipBLASLt on ROCm).  rocBLAS launches small GEMMs with
+    about half the host cost (8.5 vs 19 us per call, tools/gemm_forms.py),
+    which decides the step time of launch-bound models (SASRec)."""
+    if not name:
+        yield
+        return
+    prev = torch.backends.cuda.preferred_blas_library()
+    torch.backends.cuda.preferred_blas_library(name)
+    try:
+        yield
+    finally:
+        torch.backends.cuda.preferred_blas_library(prev)

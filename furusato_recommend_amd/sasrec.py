@@ -23,7 +23,7 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import check, lib
 from .engine import AdamGroup, AdamState
-from .linear import Linear, linear
+from .linear import Linear, blas_backend, linear
 from .rows import gather_rows
 
 
@@ -306,7 +306,13 @@ class SASRec(nn.Module):
     def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0):
         """One BPR step on packed sequences.  ``loss_scale`` scales the
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
-        between backward and Adam (DenseGradDataParallel's all-reduce)."""
+        between backward and Adam (DenseGradDataParallel's all-reduce).
+        The projections run on the BLAS backend of config "blas" (default
+        rocBLAS: the step is host-bound and rocBLAS launches cheaper)."""
+        with blas_backend(self.config.get("blas", "cublas")):
+            return self._stage_one(users, pos, neg, grad_hook, loss_scale)
+
+    def _stage_one(self, users, pos, neg, grad_hook, loss_scale):
         for p in self.parameters():
             p.grad = None
         pos, neg = (torch.as_tensor(t).to(self.device).long() for t in (pos, neg))

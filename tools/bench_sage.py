@@ -70,7 +70,10 @@ def main():
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--blas", default="", help="torch BLAS backend override (cublas / cublaslt)")
     args = ap.parse_args()
+    if args.blas:
+        torch.backends.cuda.preferred_blas_library(args.blas)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
