@@ -925,3 +925,26 @@ def test_zipf_long_rows_not_walked_by_row_phase():
         if kind == "zipf":
             assert g.n_long > 0
     assert times[0] < 5 * times[1] + 0.5, times
+
+
+@pytest.mark.parametrize("dim", [4, 8])
+def test_small_dims_train_like_oracle(dim):
+    """The smallest supported widths (one 16-B row per 1-2 lanes): two
+    training steps vs the CPU oracle."""
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from oracle.lightgcn_oracle import OracleLightGCN
+    ds = SyntheticBipartite(500, 120, 6000, seed=dim, test_frac=0.0)
+    torch.manual_seed(dim)
+    m = LightGCN({"recdim": dim, "layer": 3, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+                  "bpr_batch_size": 256}, ds)
+    o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, dim, 3, 1e-3, 1e-4,
+                       emb=m.all_embedding.weight.detach().cpu().clone())
+    rng = np.random.default_rng(dim)
+    for _ in range(2):
+        u = rng.integers(0, ds.n_users, 256)
+        p = rng.integers(0, ds.m_items, 256)
+        n = rng.integers(0, ds.m_items, 256)
+        lg = float(m.stageOne(torch.from_numpy(u), torch.from_numpy(p), torch.from_numpy(n)))
+        lo = o.stageOne(u, p, n)
+        assert abs(lg - lo) < TOL * abs(lo)
+    assert rel(m.all_embedding.weight, o.emb.detach()) < TOL
