@@ -178,8 +178,13 @@ extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t
   MIREC_CHECK_ARG(self_list == nullptr || self_count != nullptr);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const size_t bytes = (size_t)((c->n_rows + 3) / 4) * 4;  // whole words (test_and_set)
-  MIREC_HIP(hipMemsetAsync(bm_self, 0, bytes, st));
-  MIREC_HIP(hipMemsetAsync(bm_hop, 0, bytes, st));
+  const size_t bytes16 = (bytes + 15) / 16 * 16;
+  if (bm_hop == bm_self + bytes16) {  // adjacent maps (16-B row stride): one clear
+    MIREC_HIP(hipMemsetAsync(bm_self, 0, 2 * bytes16, st));
+  } else {
+    MIREC_HIP(hipMemsetAsync(bm_self, 0, bytes, st));
+    MIREC_HIP(hipMemsetAsync(bm_hop, 0, bytes, st));
+  }
   const int64_t n = keys != nullptr ? n_keys : 3 * batch;
   const int32_t split = c->n_seg > 0 ? c->split : 0;
   if (self_list != nullptr) {
@@ -216,8 +221,12 @@ extern "C" int mirec_mask_compact(const mirec_csr_t *c, const uint8_t *bm, int32
   MIREC_CHECK_ARG(wide_list == nullptr || wide_count != nullptr);
   MIREC_CHECK_ARG(((uintptr_t)bm & 15u) == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  MIREC_HIP(hipMemsetAsync(count, 0, 4, st));
-  if (wide_count != nullptr) MIREC_HIP(hipMemsetAsync(wide_count, 0, 4, st));
+  if (wide_count == count + 1) {  // adjacent counters: one clear
+    MIREC_HIP(hipMemsetAsync(count, 0, 8, st));
+  } else {
+    MIREC_HIP(hipMemsetAsync(count, 0, 4, st));
+    if (wide_count != nullptr) MIREC_HIP(hipMemsetAsync(wide_count, 0, 4, st));
+  }
   const int64_t threads = (c->n_rows + 15) / 16;
   if (threads > 0) {
     hipLaunchKernelGGL(mask_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, bm,

@@ -217,9 +217,10 @@ class PropagationEngine:
         self.xs = [torch.empty(N, D, **f32), torch.empty(N, D, **f32)] if self.L > 1 else \
             [torch.empty(N, D, **f32)] if self.L == 1 else []
         self.slot = torch.full((N,), -1, **i32)
-        words = (N + 3) // 4
-        self.bm_self = torch.zeros(words, **i32)  # S          (byte map, int32-backed)
-        self.bm_hop = torch.zeros(words, **i32)   # S ∪ N(S)   (byte map)
+        words = (N + 15) // 16 * 4  # 16-byte rows (mask_compact reads 16 B per thread)
+        # S and S ∪ N(S) byte maps (int32-backed), adjacent: cleared together
+        self._bm = torch.zeros(2, words, **i32)
+        self.bm_self, self.bm_hop = self._bm[0], self._bm[1]
         self.self_list = torch.zeros(3 * self.max_batch, **i32)  # S, deduplicated
         self.self_count = torch.zeros(1, **i32)
         self._self_cap = 0

@@ -206,7 +206,9 @@ int mirec_prescale(const float *x, const float *dinv, int64_t n_rows,
 /* Frontier bitmaps of a key set S (keys[n_keys], entries outside [0, n_rows)
  * ignored; or, if keys == NULL, the 3*batch nodes of the triples users[b],
  * n_users+pos[b], n_users+neg[b]):  bm_self = S, bm_hop = S ∪ N(S).  Both
- * are byte maps of ceil(n_rows/4)*4 bytes (4-byte aligned), cleared first.  If self_list
+ * are byte maps of ceil(n_rows/4)*4 bytes (4-byte aligned), cleared first
+ * (with one memset when bm_hop starts right after bm_self's 16-byte-rounded
+ * size).  If self_list
  * is given it receives the distinct nodes of S (in no particular order) and
  * *self_count their number (capacity: n_keys or 3*batch). */
 int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
