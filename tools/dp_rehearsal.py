@@ -8,7 +8,8 @@ bit-identical and that the 2-rank step equals one process stepping on the
 union of the ranks' batches.
 
     python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29531 tools/dp_rehearsal.py [--mode sparse|dense]
+        --master-port 29531 tools/dp_rehearsal.py [--model lgn|sage|sasrec]
+        [--mode sparse|dense]
 """
 import argparse
 import json
@@ -22,8 +23,48 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def autograd_models(args, rank, world, dev):
+    """GraphSAGE / SASRec under DenseGradDataParallel: different inits are
+    fixed by the broadcast, every rank steps on its own user shard, and the
+    gradient all-reduce keeps the replicas bit-identical."""
+    import numpy as np
+
+    from furusato_recommend_amd import GraphSAGE, SASRec, SyntheticBipartite
+    from furusato_recommend_amd.dist import DenseGradDataParallel
+    ds = SyntheticBipartite(50_000, 5_000, 500_000, seed=0)
+    torch.manual_seed(100 + rank)
+    cfg = {"recdim": 64, "layer": 2, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+           "bpr_batch_size": 512, "heads": 2, "fanouts": [10, 5]}
+    m = GraphSAGE(cfg, ds) if args.model == "sage" else SASRec(cfg, ds)
+    dp = DenseGradDataParallel(m)
+    rng = np.random.default_rng(rank)
+    losses = []
+    for i in range(args.steps):
+        if args.model == "sage":
+            u, p, n = m.sample(512, seed=5, offset=i * 512, shard=rank, n_shards=world)
+        else:
+            u = rng.integers(0, ds.n_users, 512) // world * world + rank
+            u = np.minimum(u, ds.n_users - 1)
+            p = torch.randint(0, ds.m_items, (512,), device=dev)
+            n = torch.randint(0, ds.m_items, (512,), device=dev)
+        losses.append(float(dp.step(u, p, n)))
+    torch.cuda.synchronize()
+    flat = torch.cat([q.detach().reshape(-1).cpu() for q in m.parameters()])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    if rank == 0:
+        same = all(torch.equal(gathered[0], g) for g in gathered[1:])
+        ok = same and all(np.isfinite(losses))
+        print(json.dumps({"world": world, "model": args.model, "replicas_identical": same,
+                          "losses": [round(x, 5) for x in losses], "ok": bool(ok)}), flush=True)
+        if not ok:
+            sys.exit(1)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="lgn", choices=["lgn", "sage", "sasrec"])
     ap.add_argument("--mode", default="sparse")
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--users", type=int, default=200_000)
@@ -35,6 +76,8 @@ def main():
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
+    if args.model != "lgn":
+        return autograd_models(args, rank, world, dev)
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     from furusato_recommend_amd.dist import DataParallel
     from furusato_recommend_amd.engine import sample_triples
