@@ -80,4 +80,27 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// Counter-hash dropout shared by the fused kernels: element idx is kept iff
+// the top 32 bits of mix64(key ^ idx) >= thresh = p * 2^32; kept values are
+// scaled by 1 / (1 - p).  The backward recomputes the mask from (seed, idx).
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ bool keep(uint64_t key, uint64_t idx, uint32_t thresh) {
+  return (uint32_t)(mix64(key ^ idx) >> 32) >= thresh;
+}
+
+static inline bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
+  if (!(p >= 0.f && p < 1.f)) return false;
+  *key = mix64(seed ^ 0xA24BAED4963EE407ull);
+  *thresh = (uint32_t)((double)p * 4294967296.0);
+  *scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  if (p > 0.f && *thresh == 0u) *thresh = 1u;
+  return true;
+}
+
 }  // namespace mirec

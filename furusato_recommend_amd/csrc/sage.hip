@@ -22,13 +22,6 @@
 
 namespace mirec {
 
-__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
 __global__ __launch_bounds__(256) void sample_fanout_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n_rows,
     const int32_t *__restrict__ nodes, int64_t n, int32_t k, uint64_t seed, uint64_t offset,
@@ -71,10 +64,6 @@ __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float *__re
   const int32_t id = ids[r];
   if (id < 0) return;
   atomicAdd(table_grad + (int64_t)id * d + (i - r * d), grad[i]);
-}
-
-__device__ __forceinline__ bool keep(uint64_t key, uint64_t idx, uint32_t thresh) {
-  return (uint32_t)(mix64(key ^ idx) >> 32) >= thresh;
 }
 
 // one thread per (target, float4 column).  GATHER: child rows are
@@ -169,15 +158,6 @@ __global__ __launch_bounds__(256) void fanout_mean_gather_bwd_kernel(
       }
     }
   }
-}
-
-static bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
-  if (!(p >= 0.f && p < 1.f)) return false;
-  *key = mix64(seed ^ 0xA24BAED4963EE407ull);
-  *thresh = (uint32_t)((double)p * 4294967296.0);
-  *scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  if (p > 0.f && *thresh == 0u) *thresh = 1u;
-  return true;
 }
 
 }  // namespace mirec

@@ -7,7 +7,8 @@ LN → Linear → dropout → residual), the masked mean pool over the first
 with the reference's embedding-norm term (:423-435) and OneEpoch (:437-474).
 The attention core softmax(QKᵀ/√d_h + causal)·V and its backward are one
 HIP launch each (csrc/attention.hip, f32 MFMA); the projections, LayerNorm
-and FFN are library GEMMs / torch elementwise.
+and FFN are library GEMMs, and the dropout / residual / ReLU /
+LayerNorm tail of each stage is one fused row kernel (csrc/resnorm.hip).
 Out of scope: the proprietary text / feature towers of the initial item
 embedding (:82-209): items start from an id embedding (N(0, 1), :205).
 The reference hard-codes 8 heads (:211); `heads` is a parameter here
@@ -104,6 +105,95 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         return dqkv, None, None
 
 
+def _ptr(t):
+    return 0 if t is None else t.data_ptr()
+
+
+def _dropout_seed(p: float) -> int:
+    # host draw from torch's default CPU generator (no device sync)
+    return int(torch.randint(0, 2 ** 62, (1,)).item()) if p > 0 else 0
+
+
+class _ResNorm(torch.autograd.Function):
+    """mirec_resnorm_fwd / _bwd on token rows [n, d]: out = act(res +
+    dropout(z + bias)) and y = LayerNorm(out) (sasrec.py:385-397, the
+    elementwise tail of a block stage).  Returns (out, y); y is None when
+    ``norm`` is None; out is None in the pure-LayerNorm form (``res``,
+    ``bias`` None, no ReLU, p = 0: out would equal z).  ``norm`` = (gamma,
+    beta, eps) of an nn.LayerNorm."""
+
+    @staticmethod
+    def forward(ctx, res, z, bias, gamma, beta, relu: bool, p: float, eps: float, norm: bool):
+        n, d = z.shape
+        pure = res is None and bias is None and not relu and p == 0
+        seed = _dropout_seed(p)
+        out = None if pure else torch.empty_like(z)
+        y = mean = rstd = None
+        if norm:
+            y = torch.empty_like(z)
+            mean = torch.empty(n, dtype=z.dtype, device=z.device)
+            rstd = torch.empty_like(mean)
+        check(lib.mirec_resnorm_fwd(_ptr(res), z.data_ptr(), _ptr(bias), _ptr(gamma),
+                                    _ptr(beta), n, d, int(relu), float(p), seed, float(eps),
+                                    _ptr(out), _ptr(y), _ptr(mean), _ptr(rstd),
+                                    _lib.stream_handle()), "resnorm_fwd")
+        ctx.save_for_backward(z if pure else out, mean, rstd, gamma)
+        ctx.cfg = (relu, float(p), seed, res is not None, bias is not None, norm)
+        ctx.set_materialize_grads(False)
+        return out, y
+
+    @staticmethod
+    def backward(ctx, g_out, g_y):
+        out, mean, rstd, gamma = ctx.saved_tensors
+        relu, p, seed, has_res, has_bias, norm = ctx.cfg
+        n, d = out.shape
+        need = ctx.needs_input_grad
+        if not norm:
+            g_y = None
+        g_out = None if g_out is None else g_out.contiguous()
+        g_y = None if g_y is None else g_y.contiguous()
+        d_res = torch.empty_like(out) if (has_res and need[0]) else None
+        d_z = torch.empty_like(out) if need[1] else None
+        d_bias = torch.empty(d, dtype=out.dtype, device=out.device) if (has_bias and need[2]) else None
+        d_gamma = d_beta = None
+        if g_y is not None and gamma is not None and need[3]:
+            d_gamma = torch.empty_like(gamma)
+        if g_y is not None and need[4]:
+            d_beta = torch.empty(d, dtype=out.dtype, device=out.device)
+        work = None
+        if d_gamma is not None or d_beta is not None or d_bias is not None:
+            work = torch.empty(int(lib.mirec_resnorm_work_floats(n, d)), dtype=out.dtype,
+                               device=out.device)
+        check(lib.mirec_resnorm_bwd(_ptr(g_y), _ptr(g_out), out.data_ptr(), _ptr(mean),
+                                    _ptr(rstd), _ptr(gamma), n, d, int(relu), p, seed,
+                                    _ptr(d_res), _ptr(d_z), _ptr(work), _ptr(d_gamma),
+                                    _ptr(d_beta), _ptr(d_bias), _lib.stream_handle()),
+              "resnorm_bwd")
+        if norm and g_y is None:  # y unused downstream: no LayerNorm gradients
+            d_gamma = torch.zeros_like(gamma) if need[3] and gamma is not None else None
+            d_beta = torch.zeros(d, dtype=out.dtype, device=out.device) if need[4] else None
+        return d_res, d_z, d_bias, d_gamma, d_beta, None, None, None, None
+
+
+def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
+            p: float = 0.0):
+    """(out, y) of _ResNorm for rows of width d = z.shape[-1] (any leading
+    shape); ``norm`` an nn.LayerNorm over d or None."""
+    shape = z.shape
+    d = shape[-1]
+    if d % 4 or not 4 <= d <= 1024:
+        raise ValueError("fused block rows need d % 4 == 0 and 4 <= d <= 1024")
+    z2 = z.reshape(-1, d).contiguous()
+    r2 = None if res is None else res.reshape(-1, d).contiguous()
+    if norm is not None:
+        gamma, beta, eps = norm.weight, norm.bias, norm.eps
+    else:
+        gamma = beta = None
+        eps = 0.0
+    out, y = _ResNorm.apply(r2, z2, bias, gamma, beta, relu, p, eps, norm is not None)
+    return (None if out is None else out.view(shape)), (None if y is None else y.view(shape))
+
+
 class CausalSelfAttention(nn.Module):
     """nn.MultiheadAttention(d, heads, batch_first=True) called as
     attn(x, x, x, attn_mask=causal)[0] — same parameter names
@@ -124,12 +214,14 @@ class CausalSelfAttention(nn.Module):
     def forward(self, x, offsets=None):
         """x [B, T, d] (padded), or packed [n_tok, d] with int32 ``offsets``
         [B+1] (sequence b = rows offsets[b] .. offsets[b+1]-1)."""
+        return self.out_proj(self.core(x, offsets))
+
+    def core(self, x, offsets=None):
+        """The heads' outputs before the out-projection."""
         qkv = linear(x, self.in_proj_weight, self.in_proj_bias)
         if offsets is None:
-            att = _CausalAttention.apply(qkv, self.heads)
-        else:
-            att = _CausalAttentionVarlen.apply(qkv, offsets, self.heads)
-        return self.out_proj(att)
+            return _CausalAttention.apply(qkv, self.heads)
+        return _CausalAttentionVarlen.apply(qkv, offsets, self.heads)
 
 
 class SequenceData:
@@ -208,11 +300,33 @@ class SASRec(nn.Module):
         x = self.ffn_layers[layer](x)
         return init_x + self.dropout(x)
 
+    def blocks(self, x, offsets=None):
+        """Every layer's oneblock, with the elementwise tail of each stage in
+        one fused row pass (mirec_resnorm_*: dropout + residual (+ ReLU) +
+        the next LayerNorm, the linear biases folded in).  Same values as
+        the oneblock chain (dropout draws differ: counter hash)."""
+        if not self.config.get("fused_rows", True):  # A/B: the torch composition
+            for i in range(self.num_layers):
+                x = self.oneblock(x, i, offsets)
+            return x
+        p = self.dropout.p if self.training else 0.0
+        _, y = resnorm(None, x, norm=self.attn_norm_layers[0])
+        res = x
+        L = self.num_layers
+        for i in range(L):
+            attn = self.attn_layers[i]
+            z = linear(attn.core(y, offsets), attn.out_proj.weight)
+            h, y = resnorm(res, z, attn.out_proj.bias, self.ffn_norm_layers[i], relu=True, p=p)
+            ffn = self.ffn_layers[i]
+            f = linear(y, ffn.weight)
+            nxt = self.attn_norm_layers[i + 1] if i + 1 < L else None
+            res, y = resnorm(h, f, ffn.bias, nxt, p=p)
+        return res
+
     def forward_user(self, x, length):
         """sasrec.py:399-413: blocks, then the mean over the first `length`
         positions of each sequence."""
-        for i in range(self.num_layers):
-            x = self.oneblock(x, i)
+        x = self.blocks(x)
         T = x.shape[1]
         mask = (torch.arange(T, device=x.device)[None, :] < length[:, None]).to(x.dtype)
         return (x * mask.unsqueeze(2)).sum(1) / length.to(x.dtype).unsqueeze(1)
@@ -222,8 +336,7 @@ class SASRec(nn.Module):
         the sequence of every row.  Padding positions never reach a real
         position under the causal mask and are excluded from the pool, so
         this equals forward_user on the padded batch while skipping them."""
-        for i in range(self.num_layers):
-            x = self.oneblock(x, i, offsets)
+        x = self.blocks(x, offsets)
         pooled = torch.zeros(length.numel(), x.shape[1], dtype=x.dtype, device=x.device)
         pooled = pooled.index_add(0, seg, x)
         return pooled / length.to(x.dtype).unsqueeze(1)

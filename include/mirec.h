@@ -419,6 +419,36 @@ int mirec_attention_varlen_bwd(const float *qkv, const float *dout, const int32_
                                int64_t batch, int32_t heads, int32_t head_dim,
                                float *dqkv, mirec_stream_t stream);
 
+/* Row tail of the SASRec block (model/sasrec.py:385-397 — the dropout,
+ * residual add, ReLU and LayerNorm around the attention and the FFN), one
+ * pass over the n x d token rows (d % 4 == 0, 4 <= d <= 1024):
+ *   pre = (res ? res : 0) + dropout_p-dropout(z + (bias ? bias : 0))
+ *   out = relu ? max(pre, 0) : pre                         (written if out)
+ *   y   = (out - mean) * rstd * (gamma ? gamma : 1) + (beta ? beta : 0),
+ *         rstd = 1 / sqrt(biased var + eps)                (written if y;
+ *         mean / rstd [n] then required)
+ * out may be NULL only when it equals z (no res / bias / relu / dropout).
+ * The dropout mask is the counter hash of (seed, row * d + col) — the same
+ * seed recomputes it in the backward. */
+int mirec_resnorm_fwd(const float *res, const float *z, const float *bias, const float *gamma,
+                      const float *beta, int64_t n, int32_t d, int32_t relu, float dropout_p,
+                      uint64_t seed, float eps, float *out, float *y, float *mean, float *rstd,
+                      mirec_stream_t stream);
+
+/* Floats of scratch mirec_resnorm_bwd needs for parameter gradients. */
+int64_t mirec_resnorm_work_floats(int64_t n, int32_t d);
+
+/* Backward of mirec_resnorm_fwd.  out: the forward's out (or z when out
+ * was omitted); g_y / g_out: gradients of y / out (either may be NULL =
+ * zero).  Writes d_res = d(pre) and d_z = d(z) = d(bias) per row (each
+ * optional), and the column sums d_gamma = Σ g_y·x̂, d_beta = Σ g_y,
+ * d_bias = Σ d_z (each optional; work then needs
+ * mirec_resnorm_work_floats floats).  Sums are added in a fixed order. */
+int mirec_resnorm_bwd(const float *g_y, const float *g_out, const float *out, const float *mean,
+                      const float *rstd, const float *gamma, int64_t n, int32_t d, int32_t relu,
+                      float dropout_p, uint64_t seed, float *d_res, float *d_z, float *work,
+                      float *d_gamma, float *d_beta, float *d_bias, mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* Evaluation (trainer.py:130-138)                                           */
 /* ------------------------------------------------------------------------ */

@@ -778,6 +778,100 @@ def test_sasrec_packed_path_equals_padded():
             assert rel(a, b) < TOL
 
 
+@pytest.mark.parametrize("d", [4, 12, 36, 64, 128, 256, 1024])
+def test_resnorm_rows_match_torch(d):
+    """mirec_resnorm_* (the fused dropout / residual / ReLU / LayerNorm row
+    pass) == the torch composition, fwd and every gradient incl. the column
+    sums, for the padded shapes of the dispatch (d/4 not a power of two,
+    several float4 per lane) and row counts 0, 1 and many."""
+    import torch.nn.functional as F
+
+    from furusato_recommend_amd.sasrec import resnorm
+    torch.manual_seed(d)
+    for n in (0, 1, 3001):
+        for relu, with_res in ((True, True), (False, True), (False, False)):
+            res = torch.randn(n, d, device="cuda", requires_grad=True) if with_res else None
+            z = torch.randn(n, d, device="cuda", requires_grad=True)
+            bias = (torch.randn(d, device="cuda") * 0.1).requires_grad_(True) if with_res else None
+            ln = torch.nn.LayerNorm(d, device="cuda")
+            with torch.no_grad():
+                ln.weight.uniform_(0.5, 1.5)
+                ln.bias.uniform_(-0.2, 0.2)
+            out, y = resnorm(res, z, bias, ln, relu=relu)
+            pre = z if not with_res else res + (z + bias)
+            o_ref = pre.relu() if relu else pre
+            y_ref = F.layer_norm(o_ref, (d,), ln.weight, ln.bias, ln.eps)
+            if n:
+                assert out is None or rel(out, o_ref) < TOL
+                assert rel(y, y_ref) < TOL
+            go = torch.randn(n, d, device="cuda")
+            gy = torch.randn(n, d, device="cuda")
+            leaves = [t for t in (res, z, bias, ln.weight, ln.bias) if t is not None]
+            outs = [y] + ([out] if out is not None else [])
+            grads_in = [gy] + ([go] if out is not None else [])
+            g1 = torch.autograd.grad(outs, leaves, grads_in)
+            outs_r = [y_ref] + ([o_ref] if out is not None else [])
+            g2 = torch.autograd.grad(outs_r, leaves, grads_in)
+            for a, b in zip(g1, g2):
+                if n:
+                    assert rel(a, b) < TOL
+                else:
+                    assert float(a.abs().sum()) == 0.0
+
+
+def test_resnorm_dropout_mask_is_recomputed():
+    """With p > 0: kept entries are scaled by 1/(1-p), the kept fraction is
+    1-p, and the backward applies the same mask (d_z = keep * g / (1-p))."""
+    from furusato_recommend_amd.sasrec import resnorm
+    torch.manual_seed(3)
+    n, d, p = 20000, 128, 0.3
+    z = (torch.rand(n, d, device="cuda") + 0.5).requires_grad_(True)
+    res = torch.zeros(n, d, device="cuda", requires_grad=True)
+    out, _ = resnorm(res, z, p=p)
+    kept = out != 0
+    frac = float(kept.float().mean())
+    assert abs(frac - (1 - p)) < 0.005
+    assert rel(out[kept], z.detach()[kept] / (1 - p)) < 1e-6
+    g = torch.randn(n, d, device="cuda")
+    gr, gz = torch.autograd.grad(out, [res, z], g)
+    assert torch.equal(gr, g)
+    assert rel(gz, g * kept / (1 - p)) < 1e-6
+    out2, _ = resnorm(res, z, p=p)   # a fresh draw
+    assert not torch.equal(out2 != 0, kept)
+
+
+@pytest.mark.parametrize("d,heads", [(64, 2), (128, 2), (48, 3)])
+def test_sasrec_fused_blocks_equal_oneblock_chain(d, heads):
+    """SASRec.blocks (fused row passes) == the reference-shaped oneblock
+    chain (nn.LayerNorm, nn.Dropout, separate residual / ReLU), dropout
+    off, packed and padded: outputs and every parameter / input gradient."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    ds = SyntheticBipartite(400, 200, 8_000, seed=2)
+    torch.manual_seed(1)
+    m = SASRec({"recdim": d, "layer": 3, "heads": heads, "lr": 1e-3, "decay": 1e-4,
+                "device": "cuda:0", "bpr_batch_size": 64, "dropout_p": 0.0}, ds)
+    with torch.no_grad():
+        for ln in list(m.attn_norm_layers) + list(m.ffn_norm_layers):
+            ln.weight.uniform_(0.5, 1.5)
+            ln.bias.uniform_(-0.2, 0.2)
+    params = [p for mod in (m.attn_layers, m.attn_norm_layers, m.ffn_norm_layers, m.ffn_layers)
+              for p in mod.parameters()]
+    x, offs, _, _ = m.packed_input(np.random.default_rng(0).integers(0, 400, 64))
+    xp = torch.randn(7, 50, d, device="cuda")
+    for inp, o in ((x.detach(), offs), (xp, None)):
+        inp = inp.clone().requires_grad_(True)
+        fused = m.blocks(inp, o)
+        ref = inp
+        for i in range(m.num_layers):
+            ref = m.oneblock(ref, i, o)
+        assert rel(fused, ref) < TOL
+        w = torch.randn_like(ref)
+        g1 = torch.autograd.grad((fused * w).sum(), [inp] + params)
+        g2 = torch.autograd.grad((ref * w).sum(), [inp] + params)
+        for a, b in zip(g1, g2):
+            assert rel(a, b) < TOL
+
+
 def test_sasrec_trains():
     from furusato_recommend_amd import SASRec, SyntheticBipartite
     ds = SyntheticBipartite(3000, 500, 40_000, seed=11, test_frac=0.1)

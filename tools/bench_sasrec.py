@@ -100,6 +100,8 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--blas", default="cublas", choices=["cublas", "cublaslt"],
                     help="BLAS backend of the projections (cublas = rocBLAS on ROCm)")
+    ap.add_argument("--fused-rows", type=int, default=1,
+                    help="0: the torch composition of dropout / residual / LayerNorm (A/B)")
     args = ap.parse_args()
     from furusato_recommend_amd import SASRec, sasrec as S
     from furusato_recommend_amd.sasrec import SequenceData
@@ -109,7 +111,8 @@ def main():
                                  seed=0)
     m = SASRec({"recdim": args.dim, "layer": args.layers, "heads": args.heads, "lr": 1e-3,
                 "decay": 1e-4, "device": "cuda:0", "bpr_batch_size": args.batch,
-                "dropout_p": 0.2, "blas": args.blas}, _DS(args.users, args.items),
+                "dropout_p": 0.2, "blas": args.blas,
+                "fused_rows": bool(args.fused_rows)}, _DS(args.users, args.items),
                sequences=seq)
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(7)
