@@ -345,6 +345,11 @@ class SASRec(nn.Module):
         """(x [n_tok, d], offsets [B+1] int32, seg [n_tok], length [B]) of the
         users' sequences.  The token count is taken from the host copy of
         the lengths (host ``users``: no device synchronisation)."""
+        ids, offsets, seg, length = self.packed_ids(users)
+        return gather_rows(self.item_id_embedding.weight, ids), offsets, seg, length
+
+    def packed_ids(self, users):
+        """packed_input's item ids [n_tok] (int32) instead of their rows."""
         if torch.is_tensor(users) and users.is_cuda:
             u_host = users.cpu().numpy()
         else:
@@ -359,8 +364,7 @@ class SASRec(nn.Module):
         seg = torch.repeat_interleave(torch.arange(len(u_host), device=dev), length,
                                       output_size=n_tok)
         pos = torch.arange(n_tok, device=dev) - offsets[seg].long()
-        ids = self.seq.items[u[seg], pos]
-        return gather_rows(self.item_id_embedding.weight, ids), offsets, seg, length
+        return self.seq.items[u[seg], pos], offsets, seg, length
 
     def _upload(self, host_ids) -> torch.Tensor:
         """int64 host ids -> device without a stream sync: a pageable H2D copy
@@ -428,12 +432,16 @@ class SASRec(nn.Module):
     def _stage_one(self, users, pos, neg, grad_hook, loss_scale):
         for p in self.parameters():
             p.grad = None
-        pos, neg = (torch.as_tensor(t).to(self.device).long() for t in (pos, neg))
-        x, offsets, seg, length = self.packed_input(users)
+        pos, neg = (torch.as_tensor(t).to(self.device) for t in (pos, neg))
+        ids, offsets, seg, length = self.packed_ids(users)
+        n_tok, B = ids.numel(), pos.numel()
+        # one lookup for the sequences, positives and negatives (one dense
+        # table gradient, no accumulation), one pass of the item tower over
+        # positives and negatives together (row-wise: same values)
+        rows = gather_rows(self.item_id_embedding.weight, torch.cat([ids, pos.int(), neg.int()]))
+        x, pn = rows.split([n_tok, 2 * B])
         u = self.forward_user_packed(x, offsets, seg, length)
-        item_w = self.item_id_embedding.weight
-        pe = self.forward_item(gather_rows(item_w, pos))
-        ne = self.forward_item(gather_rows(item_w, neg))
+        pe, ne = self.forward_item(pn).split(B)
         loss = self.loss(u, pe, ne)
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         if grad_hook is not None:

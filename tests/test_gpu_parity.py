@@ -872,6 +872,52 @@ def test_sasrec_fused_blocks_equal_oneblock_chain(d, heads):
             assert rel(a, b) < TOL
 
 
+def test_sasrec_stage_one_equals_unfused_composition():
+    """stageOne (one lookup for sequences / positives / negatives, one item
+    tower pass, fused block rows) == the reference-shaped step (separate
+    lookups, the tower once per side, oneblock chain): loss, every gradient
+    and every parameter after the Adam step, dropout off."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    from furusato_recommend_amd.rows import gather_rows
+    ds = SyntheticBipartite(500, 300, 10_000, seed=4)
+    cfg = {"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+           "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0}
+    torch.manual_seed(9)
+    a = SASRec(cfg, ds)
+    torch.manual_seed(9)
+    b = SASRec(dict(cfg, fused_rows=False), ds)
+    rng = np.random.default_rng(1)
+    users = rng.integers(0, 500, 128)
+    pos = torch.as_tensor(rng.integers(0, 300, 128), device="cuda")
+    neg = torch.as_tensor(rng.integers(0, 300, 128), device="cuda")
+    grads = {}
+
+    def grab():  # between backward and Adam
+        grads.update((n, q.grad.clone()) for n, q in a.named_parameters())
+    la = float(a.stageOne(users, pos, neg, grad_hook=grab))
+    x, offs, seg, length = b.packed_input(users)
+    u = b.forward_user_packed(x, offs, seg, length)
+    w = b.item_id_embedding.weight
+    loss = b.loss(u, b.forward_item(gather_rows(w, pos)), b.forward_item(gather_rows(w, neg)))
+    loss.backward()
+    lb = float(loss.detach())
+    assert abs(la - lb) <= TOL * abs(lb)
+    live = {}
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        scale = float(pb.grad.abs().max())
+        # item_last_proj.bias and the key part of in_proj_bias have exactly
+        # zero gradient (the bias cancels in pos - neg / in the softmax)
+        assert float((grads[name] - pb.grad).abs().max()) <= TOL * max(scale, 1e-4), name
+        live[name] = pb.grad.abs() > 1e-5 * scale
+    b.optims.step()
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        # Adam divides by sqrt(v): compare the update in units of lr; a zero
+        # gradient's rounding noise becomes a full lr step, so only elements
+        # above the noise floor are compared
+        diff = (pa - pb).abs()[live[name]]
+        assert diff.numel() == 0 or float(diff.max()) < 1e-2 * cfg["lr"], name
+
+
 def test_sasrec_trains():
     from furusato_recommend_amd import SASRec, SyntheticBipartite
     ds = SyntheticBipartite(3000, 500, 40_000, seed=11, test_frac=0.1)
