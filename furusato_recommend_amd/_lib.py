@@ -110,6 +110,10 @@ SIGNATURES = {
                                  POINTER(AdamH), c_void_p]),
     "mirec_adam_dense": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                  POINTER(AdamH), c_void_p]),
+    "mirec_adam_multi_dev": (c_int, [c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
+    "mirec_adam_dense_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                     c_void_p]),
     "mirec_sample_fanout": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int32, c_uint64,
                                     c_uint64, c_void_p, c_void_p]),
     "mirec_gather_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
@@ -131,13 +135,18 @@ SIGNATURES = {
                                            c_void_p, c_void_p]),
     "mirec_attention_varlen_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                            c_int32, c_void_p, c_void_p]),
+    "mirec_attention_bucketed_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_int32,
+                                             c_void_p, c_void_p]),
+    "mirec_attention_bucketed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                             c_int32, c_void_p, c_void_p]),
     "mirec_resnorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                  c_int32, c_int32, c_float, c_uint64, c_float, c_void_p,
-                                  c_void_p, c_void_p, c_void_p, c_void_p]),
+                                  c_int32, c_int32, c_float, c_uint64, c_void_p, c_float,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mirec_resnorm_work_floats": (c_int64, [c_int64, c_int32]),
     "mirec_resnorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_int64, c_int32, c_int32, c_float, c_uint64, c_void_p,
-                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                  c_void_p]),
     "mirec_topk_masked": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,

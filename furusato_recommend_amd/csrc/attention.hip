@@ -39,14 +39,22 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kT = 64;  // longest sequence
 constexpr int kB = 16;  // block edge = MFMA tile edge
-constexpr int kLdP = kT + 4;  // Pᵀ / dSᵀ row stride (≡ 4 mod 64 floats)
 
-template <int DPAD>
+// NB = number of 16-row blocks a workgroup holds (the bucket: sequences of
+// at most 16*NB positions); one wave per block, so a workgroup is 64*NB
+// threads and its LDS is sized for 16*NB rows.
+template <int DPAD, int NB>
 struct AttnShape {
-  static constexpr int Q4 = DPAD / 4;     // dims per lane group in the S products
+  static constexpr int TR = NB * kB;      // rows held
+  static constexpr int NT = 64 * NB;      // threads
+  static constexpr int Q4 = DPAD / 4;     // head dims per lane in the S / dP products
   static constexpr int NCB = DPAD / kB;   // 16-dim output blocks
-  static constexpr int LDK = DPAD + 4;    // K / V row stride (4 rows ≡ 16 mod 64)
-  static constexpr int LDQ = DPAD == 64 ? 80 : 48;  // Q / dO (phase B) row stride
+  static constexpr int LDK = DPAD + 4;    // K / V row stride (≡ 4 mod 32)
+  static constexpr int LDQ = DPAD == 64 ? 80 : 48;  // Q / dO (phase B) row stride (≡ 16 mod 32)
+  static constexpr int LDP = TR + 4;      // Pᵀ / dSᵀ row stride (≡ 4 mod 16)
+  static constexpr int fwd_lds = (int)sizeof(float) * 2 * TR * LDK;
+  static constexpr int bwd_region = 2 * TR * (LDK > LDQ ? LDK : LDQ);
+  static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 2 * TR * LDP);
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -55,13 +63,15 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 
 __device__ __forceinline__ f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
-// Rows of sequence b: [row0, row0 + T) — uniform (b*T, T) or from offsets.
-__device__ __forceinline__ void seq_rows(const int32_t *offsets, int b, int &T, int64_t &row0) {
+// Rows of sequence b: [row0, row0 + T) — uniform (b*T, T) or from offsets,
+// at most `cap` rows.
+__device__ __forceinline__ void seq_rows(const int32_t *offsets, int64_t b, int cap, int &T,
+                                         int64_t &row0) {
   if (offsets == nullptr) {
-    row0 = (int64_t)b * T;
+    row0 = b * T;
   } else {
     row0 = offsets[b];
-    T = min(offsets[b + 1] - offsets[b], kT);
+    T = min(offsets[b + 1] - offsets[b], cap);
   }
 }
 
@@ -69,41 +79,41 @@ __device__ __forceinline__ void seq_rows(const int32_t *offsets, int b, int &T, 
 // stride LD: rows >= T and columns >= dh are zero (padding must be finite:
 // a masked score still multiplies a V row).  All loads are issued before
 // the first LDS store.  float4 when dh % 4 == 0 (rows 16-byte aligned).
-template <int DPAD, int LD>
+template <int DPAD, int LD, int TR, int NT>
 __device__ __forceinline__ void load_pair(float *d0, float *d1, const float *s0, const float *s1,
                                           int64_t rs, int T, int R, int dh) {
   constexpr int C4 = DPAD / 4;
-  constexpr int PER = kT * C4 / 256;
   if ((dh & 3) == 0) {
+    constexpr int PER = TR * C4 / NT;
     float4 v0[PER], v1[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = threadIdx.x + q * 256, i = e / C4, c = e % C4;
+      const int e = threadIdx.x + q * NT, i = e / C4, c = e % C4;
       const bool ok = i < T && 4 * c < dh;
       v0[q] = ok ? ld4(s0 + (int64_t)i * rs + 4 * c) : f4_zero();
       v1[q] = ok ? ld4(s1 + (int64_t)i * rs + 4 * c) : f4_zero();
     }
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
-      const int e = threadIdx.x + q * 256, i = e / C4, c = e % C4;
+      const int e = threadIdx.x + q * NT, i = e / C4, c = e % C4;
       if (i < R) {
         st4(d0 + i * LD + 4 * c, v0[q]);
         st4(d1 + i * LD + 4 * c, v1[q]);
       }
     }
   } else {
-    constexpr int PS = kT * DPAD / 256;
+    constexpr int PS = TR * DPAD / NT;
     float v0[PS], v1[PS];
 #pragma unroll
     for (int q = 0; q < PS; ++q) {
-      const int e = threadIdx.x + q * 256, i = e / DPAD, c = e % DPAD;
+      const int e = threadIdx.x + q * NT, i = e / DPAD, c = e % DPAD;
       const bool ok = i < T && c < dh;
       v0[q] = ok ? s0[(int64_t)i * rs + c] : 0.f;
       v1[q] = ok ? s1[(int64_t)i * rs + c] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < PS; ++q) {
-      const int e = threadIdx.x + q * 256, i = e / DPAD, c = e % DPAD;
+      const int e = threadIdx.x + q * NT, i = e / DPAD, c = e % DPAD;
       if (i < R) {
         d0[i * LD + c] = v0[q];
         d1[i * LD + c] = v1[q];
@@ -112,23 +122,15 @@ __device__ __forceinline__ void load_pair(float *d0, float *d1, const float *s0,
   }
 }
 
-// A lane's Q4 dims [c0, c0 + Q4) of one row (zero if !valid or past dh).
+// A lane's Q4 head dims of one row in the S / dP contraction order: lane
+// group g holds dims 4t + g (t < Q4), zero if !valid or past dh.  With the
+// K / V row stride ≡ 4 (mod 32) the matching LDS reads (row j, dim 4t + g)
+// hit 64 distinct banks.
 template <int Q4>
-__device__ __forceinline__ void load_seg(const float *row, int c0, int dh, bool valid,
+__device__ __forceinline__ void load_seg(const float *row, int g, int dh, bool valid,
                                          float (&v)[Q4]) {
-  if (valid && (dh & 3) == 0) {
 #pragma unroll
-    for (int t = 0; t < Q4; t += 4) {
-      const float4 x = (c0 + t < dh) ? ld4(row + c0 + t) : f4_zero();
-      v[t] = x.x;
-      v[t + 1] = x.y;
-      v[t + 2] = x.z;
-      v[t + 3] = x.w;
-    }
-  } else {
-#pragma unroll
-    for (int t = 0; t < Q4; ++t) v[t] = (valid && c0 + t < dh) ? row[c0 + t] : 0.f;
-  }
+  for (int t = 0; t < Q4; ++t) v[t] = (valid && 4 * t + g < dh) ? row[4 * t + g] : 0.f;
 }
 
 // Store the 4 dims [c, c+4) held in a tile register group to row `row`.
@@ -144,23 +146,23 @@ __device__ __forceinline__ void store4(float *row, int c, int dh, f32x4 x) {
 
 // Pᵀ for query block w (key blocks 0..w) in registers: s[kb][r] =
 // P[query 16w + j][key 16kb + 4g + r] (j = lane & 15, g = lane >> 4).
-template <int DPAD>
+template <int DPAD, int NB>
 __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)[DPAD / 4], int w,
-                                               int T, float scale, f32x4 (&s)[4]) {
-  using S = AttnShape<DPAD>;
+                                               int T, float scale, f32x4 (&s)[NB]) {
+  using S = AttnShape<DPAD, NB>;
   const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) s[kb] = zero4();
+  for (int kb = 0; kb < NB; ++kb) s[kb] = zero4();
 #pragma unroll
   for (int t = 0; t < S::Q4; ++t) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-      if (kb <= w) s[kb] = mfma16(sK[(kB * kb + j) * S::LDK + g * S::Q4 + t], q[t], s[kb]);
+    for (int kb = 0; kb < NB; ++kb)
+      if (kb <= w) s[kb] = mfma16(sK[(kB * kb + j) * S::LDK + 4 * t + g], q[t], s[kb]);
   }
   const int qi = kB * w + j;
   float m = -INFINITY;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int kb = 0; kb < NB; ++kb) {
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -174,7 +176,7 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
   m = fmaxf(m, __shfl_xor(m, 32));
   float sum = 0.f;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int kb = 0; kb < NB; ++kb) {
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -187,43 +189,46 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
   sum += __shfl_xor(sum, 32);
   const float inv = 1.f / sum;
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int kb = 0; kb < NB; ++kb) {
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[kb][r] *= inv;
   }
 }
 
-template <int DPAD>
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__ qkv,
-                                                       float *__restrict__ out, int T, int H,
-                                                       int dh, float scale,
-                                                       const int32_t *__restrict__ offsets) {
-  using S = AttnShape<DPAD>;
-  __shared__ __attribute__((aligned(16))) float sK[kT * S::LDK];
-  __shared__ __attribute__((aligned(16))) float sV[kT * S::LDK];
+// Sequence seq0 + blockIdx.x / H, head blockIdx.x % H.
+template <int DPAD, int NB>
+__global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restrict__ qkv,
+                                                           float *__restrict__ out, int T, int H,
+                                                           int dh, float scale,
+                                                           const int32_t *__restrict__ offsets,
+                                                           int64_t seq0) {
+  using S = AttnShape<DPAD, NB>;
+  __shared__ __attribute__((aligned(16))) float sK[S::TR * S::LDK];
+  __shared__ __attribute__((aligned(16))) float sV[S::TR * S::LDK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int64_t b = seq0 + blockIdx.x / H;
+  const int h = blockIdx.x % H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   int64_t row0;
-  seq_rows(offsets, b, T, row0);
+  seq_rows(offsets, b, S::TR, T, row0);
   const int nb = (T + kB - 1) / kB;
   const float *base = qkv + row0 * rs + h * dh;
-  load_pair<DPAD, S::LDK>(sK, sV, base + d, base + 2 * d, rs, T, kB * nb, dh);
+  load_pair<DPAD, S::LDK, S::TR, S::NT>(sK, sV, base + d, base + 2 * d, rs, T, kB * nb, dh);
   const int qi = kB * w + j;
   float q[S::Q4];
-  load_seg<S::Q4>(base + (int64_t)qi * rs, g * S::Q4, dh, w < nb && qi < T, q);
+  load_seg<S::Q4>(base + (int64_t)qi * rs, g, dh, w < nb && qi < T, q);
   __syncthreads();
   if (w >= nb) return;  // no barrier below
-  f32x4 p[4];
-  scores_softmax<DPAD>(sK, q, w, T, scale, p);
+  f32x4 p[NB];
+  scores_softmax<DPAD, NB>(sK, q, w, T, scale, p);
   f32x4 o[S::NCB];
 #pragma unroll
   for (int cb = 0; cb < S::NCB; ++cb) o[cb] = zero4();
 #pragma unroll
-  for (int kb = 0; kb < 4; ++kb) {
+  for (int kb = 0; kb < NB; ++kb) {
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -239,51 +244,51 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const float *__restrict__
   }
 }
 
-template <int DPAD>
-__global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__ qkv,
-                                                       const float *__restrict__ dout,
-                                                       float *__restrict__ dqkv, int T, int H,
-                                                       int dh, float scale,
-                                                       const int32_t *__restrict__ offsets) {
-  using S = AttnShape<DPAD>;
+template <int DPAD, int NB>
+__global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restrict__ qkv,
+                                                           const float *__restrict__ dout,
+                                                           float *__restrict__ dqkv, int T, int H,
+                                                           int dh, float scale,
+                                                           const int32_t *__restrict__ offsets,
+                                                           int64_t seq0) {
+  using S = AttnShape<DPAD, NB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int kv = 2 * kT * S::LDK, qd = 2 * kT * S::LDQ;
-  constexpr int region = kv > qd ? kv : qd;
-  float *sK = smem, *sV = smem + kT * S::LDK;           // phase A
-  float *sQ = smem, *sDO = smem + kT * S::LDQ;          // phase B (same region)
-  float *sP = smem + region, *sDS = sP + kT * kLdP;
+  float *sK = smem, *sV = smem + S::TR * S::LDK;         // phase A
+  float *sQ = smem, *sDO = smem + S::TR * S::LDQ;        // phase B (same region)
+  float *sP = smem + S::bwd_region, *sDS = sP + S::TR * S::LDP;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int b = blockIdx.x / H, h = blockIdx.x - (blockIdx.x / H) * H;
+  const int64_t b = seq0 + blockIdx.x / H;
+  const int h = blockIdx.x % H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   int64_t row0;
-  seq_rows(offsets, b, T, row0);
+  seq_rows(offsets, b, S::TR, T, row0);
   const int nb = (T + kB - 1) / kB;
   const float *base = qkv + row0 * rs + h * dh;
   float *gbase = dqkv + row0 * rs + h * dh;
-  load_pair<DPAD, S::LDK>(sK, sV, base + d, base + 2 * d, rs, T, kB * nb, dh);
+  load_pair<DPAD, S::LDK, S::TR, S::NT>(sK, sV, base + d, base + 2 * d, rs, T, kB * nb, dh);
   const int qi = kB * w + j;
   const bool qvalid = w < nb && qi < T;
   float q[S::Q4], dov[S::Q4];
-  load_seg<S::Q4>(base + (int64_t)qi * rs, g * S::Q4, dh, qvalid, q);
-  load_seg<S::Q4>(dout + (row0 + qi) * d + h * dh, g * S::Q4, dh, qvalid, dov);
+  load_seg<S::Q4>(base + (int64_t)qi * rs, g, dh, qvalid, q);
+  load_seg<S::Q4>(dout + (row0 + qi) * d + h * dh, g, dh, qvalid, dov);
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
   if (w < nb) {
-    f32x4 p[4], dp[4];
-    scores_softmax<DPAD>(sK, q, w, T, scale, p);
+    f32x4 p[NB], dp[NB];
+    scores_softmax<DPAD, NB>(sK, q, w, T, scale, p);
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) dp[kb] = zero4();
+    for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
 #pragma unroll
     for (int t = 0; t < S::Q4; ++t) {
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-        if (kb <= w) dp[kb] = mfma16(sV[(kB * kb + j) * S::LDK + g * S::Q4 + t], dov[t], dp[kb]);
+      for (int kb = 0; kb < NB; ++kb)
+        if (kb <= w) dp[kb] = mfma16(sV[(kB * kb + j) * S::LDK + 4 * t + g], dov[t], dp[kb]);
     }
     float delta = 0.f;
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < NB; ++kb) {
       if (kb > w) break;
 #pragma unroll
       for (int r = 0; r < 4; ++r) delta += p[kb][r] * dp[kb][r];
@@ -295,14 +300,14 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__
 #pragma unroll
     for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = zero4();
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < NB; ++kb) {
       if (kb > w) break;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dp[kb][r] = p[kb][r] * (dp[kb][r] - delta) * scale;
         const int key = kB * kb + 4 * g + r;
-        sP[key * kLdP + qi] = p[kb][r];
-        sDS[key * kLdP + qi] = dp[kb][r];
+        sP[key * S::LDP + qi] = p[kb][r];
+        sDS[key * S::LDP + qi] = dp[kb][r];
         const float *krow = sK + key * S::LDK + j;
 #pragma unroll
         for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = mfma16(krow[kB * cb], dp[kb][r], dq[cb]);
@@ -318,8 +323,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__
   if (w < nb) {
 #pragma unroll
     for (int t = 0; t < S::Q4; ++t) {
-      sQ[qi * S::LDQ + g * S::Q4 + t] = q[t];
-      sDO[qi * S::LDQ + g * S::Q4 + t] = dov[t];
+      sQ[qi * S::LDQ + 4 * t + g] = q[t];
+      sDO[qi * S::LDQ + 4 * t + g] = dov[t];
     }
   }
   __syncthreads();
@@ -335,8 +340,8 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__
     const int key = kB * kb + j;
     for (int q0 = kB * kb; q0 < kB * nb; q0 += 4) {
       const int qq = q0 + g;
-      const float pb = sP[key * kLdP + qq];
-      const float db = sDS[key * kLdP + qq];
+      const float pb = sP[key * S::LDP + qq];
+      const float db = sDS[key * S::LDP + qq];
       const float *dorow = sDO + qq * S::LDQ + j;
       const float *qrow = sQ + qq * S::LDQ + j;
 #pragma unroll
@@ -356,57 +361,79 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const float *__restrict__
   }
 }
 
-template <int DPAD>
-constexpr int bwd_smem() {
-  using S = AttnShape<DPAD>;
-  constexpr int kv = 2 * kT * S::LDK, qd = 2 * kT * S::LDQ;
-  return (int)sizeof(float) * ((kv > qd ? kv : qd) + 2 * kT * kLdP);
-}
-
 // Dynamic LDS above 64 KiB needs an explicit opt-in per kernel (once).
-static int allow_big_lds() {
+template <int DPAD, int NB>
+static int allow_lds() {
   static int rc = -1;
-  if (rc < 0) {
-    rc = 0;
-    const void *fns[2] = {(const void *)attn_bwd_kernel<32>, (const void *)attn_bwd_kernel<64>};
-    for (const void *f : fns)
-      if (hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
-          hipSuccess)
-        rc = 1;
-  }
+  if (rc < 0)
+    rc = hipFuncSetAttribute((const void *)attn_bwd_kernel<DPAD, NB>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                             AttnShape<DPAD, NB>::bwd_lds) == hipSuccess ? 0 : 1;
   return rc;
 }
 
-static int launch_fwd(const float *qkv, const int32_t *offsets, int64_t batch, int T,
-                      int heads, int head_dim, float *out, hipStream_t st) {
-  if (batch == 0) return MIREC_OK;
-  const float scale = 1.f / sqrtf((float)head_dim);
-  const dim3 grid((unsigned)(batch * heads));
-  if (head_dim <= 32)
-    hipLaunchKernelGGL(attn_fwd_kernel<32>, grid, dim3(256), 0, st, qkv, out, T, heads,
-                       head_dim, scale, offsets);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(256), 0, st, qkv, out, T, heads,
-                       head_dim, scale, offsets);
+// One launch over sequences [seq0, seq0 + n) of the bucket NB.
+template <int DPAD, int NB>
+static int launch_bucket(bool bwd, const float *qkv, const float *dout, const int32_t *offsets,
+                         int64_t seq0, int64_t n, int T, int heads, int dh, float *outp,
+                         hipStream_t st) {
+  if (n <= 0) return MIREC_OK;
+  const float scale = 1.f / sqrtf((float)dh);
+  const dim3 grid((unsigned)(n * heads)), block(64 * NB);
+  if (!bwd) {
+    hipLaunchKernelGGL((attn_fwd_kernel<DPAD, NB>), grid, block, 0, st, qkv, outp, T, heads, dh,
+                       scale, offsets, seq0);
+  } else {
+    if (allow_lds<DPAD, NB>() != 0) return MIREC_ERR_HIP;
+    constexpr int lds = AttnShape<DPAD, NB>::bwd_lds;
+    hipLaunchKernelGGL((attn_bwd_kernel<DPAD, NB>), grid, block, lds, st, qkv, dout, outp, T,
+                       heads, dh, scale, offsets, seq0);
+  }
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
 
-static int launch_bwd(const float *qkv, const float *dout, const int32_t *offsets,
-                      int64_t batch, int T, int heads, int head_dim, float *dqkv,
-                      hipStream_t st) {
-  if (batch == 0) return MIREC_OK;
-  if (allow_big_lds() != 0) return MIREC_ERR_HIP;
-  const float scale = 1.f / sqrtf((float)head_dim);
-  const dim3 grid((unsigned)(batch * heads));
-  if (head_dim <= 32)
-    hipLaunchKernelGGL(attn_bwd_kernel<32>, grid, dim3(256), bwd_smem<32>(), st, qkv, dout,
-                       dqkv, T, heads, head_dim, scale, offsets);
-  else
-    hipLaunchKernelGGL(attn_bwd_kernel<64>, grid, dim3(256), bwd_smem<64>(), st, qkv, dout,
-                       dqkv, T, heads, head_dim, scale, offsets);
-  MIREC_LAUNCH_CHECK();
+template <int DPAD>
+static int launch_nb(int nb, bool bwd, const float *qkv, const float *dout,
+                     const int32_t *offsets, int64_t seq0, int64_t n, int T, int heads, int dh,
+                     float *outp, hipStream_t st) {
+  switch (nb) {
+    case 1: return launch_bucket<DPAD, 1>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
+    case 2: return launch_bucket<DPAD, 2>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
+    case 3: return launch_bucket<DPAD, 3>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
+    default: return launch_bucket<DPAD, 4>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
+  }
+}
+
+// bucket_end[k] (k < 4): sequences [bucket_end[k-1], bucket_end[k]) run on
+// the NB = k+1 kernel.  Uniform batches pass T and one bucket.
+static int launch(bool bwd, const float *qkv, const float *dout, const int32_t *offsets,
+                  const int64_t *bucket_end, int T, int heads, int dh, float *outp,
+                  hipStream_t st) {
+  int64_t prev = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int64_t end = bucket_end[k];
+    const int rc = dh <= 32 ? launch_nb<32>(k + 1, bwd, qkv, dout, offsets, prev, end - prev, T,
+                                            heads, dh, outp, st)
+                            : launch_nb<64>(k + 1, bwd, qkv, dout, offsets, prev, end - prev, T,
+                                            heads, dh, outp, st);
+    if (rc != MIREC_OK) return rc;
+    prev = end;
+  }
   return MIREC_OK;
+}
+
+// Uniform batch: every sequence has T rows -> the NB = ceil(T/16) bucket.
+static void uniform_buckets(int64_t batch, int T, int64_t (&be)[4]) {
+  const int nb = (T + kB - 1) / kB;
+  for (int k = 0; k < 4; ++k) be[k] = (k + 1 >= nb) ? batch : 0;
+}
+
+static bool valid_buckets(const int64_t *be) {
+  if (be[0] < 0) return false;
+  for (int k = 1; k < 4; ++k)
+    if (be[k] < be[k - 1]) return false;
+  return true;
 }
 
 }  // namespace mirec
@@ -416,8 +443,10 @@ extern "C" int mirec_attention_fwd(const float *qkv, int64_t batch, int32_t T, i
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && out && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  return launch_fwd(qkv, nullptr, batch, T, heads, head_dim, out,
-                    reinterpret_cast<hipStream_t>(stream));
+  int64_t be[4];
+  uniform_buckets(batch, T, be);
+  return launch(false, qkv, nullptr, nullptr, be, T, heads, head_dim, out,
+                reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t batch, int32_t T,
@@ -426,8 +455,10 @@ extern "C" int mirec_attention_bwd(const float *qkv, const float *dout, int64_t 
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && dout && dqkv && batch >= 0 && T >= 1 && T <= kT && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  return launch_bwd(qkv, dout, nullptr, batch, T, heads, head_dim, dqkv,
-                    reinterpret_cast<hipStream_t>(stream));
+  int64_t be[4];
+  uniform_buckets(batch, T, be);
+  return launch(true, qkv, dout, nullptr, be, T, heads, head_dim, dqkv,
+                reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mirec_attention_varlen_fwd(const float *qkv, const int32_t *offsets,
@@ -436,8 +467,9 @@ extern "C" int mirec_attention_varlen_fwd(const float *qkv, const int32_t *offse
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && offsets && out && batch >= 0 && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  return launch_fwd(qkv, offsets, batch, kT, heads, head_dim, out,
-                    reinterpret_cast<hipStream_t>(stream));
+  const int64_t be[4] = {0, 0, 0, batch};
+  return launch(false, qkv, nullptr, offsets, be, kT, heads, head_dim, out,
+                reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" int mirec_attention_varlen_bwd(const float *qkv, const float *dout,
@@ -446,6 +478,28 @@ extern "C" int mirec_attention_varlen_bwd(const float *qkv, const float *dout,
   using namespace mirec;
   MIREC_CHECK_ARG(qkv && dout && offsets && dqkv && batch >= 0 && heads >= 1);
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
-  return launch_bwd(qkv, dout, offsets, batch, kT, heads, head_dim, dqkv,
-                    reinterpret_cast<hipStream_t>(stream));
+  const int64_t be[4] = {0, 0, 0, batch};
+  return launch(true, qkv, dout, offsets, be, kT, heads, head_dim, dqkv,
+                reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mirec_attention_bucketed_fwd(const float *qkv, const int32_t *offsets,
+                                            const int64_t *bucket_end, int32_t heads,
+                                            int32_t head_dim, float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && offsets && bucket_end && out && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64 && valid_buckets(bucket_end));
+  return launch(false, qkv, nullptr, offsets, bucket_end, kT, heads, head_dim, out,
+                reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mirec_attention_bucketed_bwd(const float *qkv, const float *dout,
+                                            const int32_t *offsets, const int64_t *bucket_end,
+                                            int32_t heads, int32_t head_dim, float *dqkv,
+                                            mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && dout && offsets && bucket_end && dqkv && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64 && valid_buckets(bucket_end));
+  return launch(true, qkv, dout, offsets, bucket_end, kT, heads, head_dim, dqkv,
+                reinterpret_cast<hipStream_t>(stream));
 }

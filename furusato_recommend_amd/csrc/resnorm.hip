@@ -37,6 +37,7 @@ struct FwdArgs {
   uint64_t key;
   uint32_t thresh;
   float scale, eps;
+  const uint64_t *key_base;  // device; mixed into key at run time (graph replays)
 };
 
 struct BwdArgs {
@@ -47,7 +48,13 @@ struct BwdArgs {
   uint64_t key;
   uint32_t thresh;
   float scale;
+  const uint64_t *key_base;
 };
+
+// The mask key of a launch: the host key, mixed with *key_base when given.
+__device__ __forceinline__ uint64_t run_key(uint64_t key, const uint64_t *key_base) {
+  return key_base ? mix64(key ^ *key_base) : key;
+}
 
 __device__ __forceinline__ float4 drop4(float4 v, uint64_t key, uint64_t e, uint32_t thresh,
                                         float scale) {
@@ -70,6 +77,7 @@ __device__ __forceinline__ float4 f4_mul(float4 a, float4 b) {
 template <int LPR, int NC>
 __global__ __launch_bounds__(kBlock) void resnorm_fwd_kernel(FwdArgs a) {
   constexpr int RPB = kBlock / LPR;
+  const uint64_t key = a.thresh != 0u ? run_key(a.key, a.key_base) : 0ull;
   const int lane = threadIdx.x % LPR;
   const int64_t d = a.d;
   const float inv_d = 1.f / (float)a.d;
@@ -93,7 +101,7 @@ __global__ __launch_bounds__(kBlock) void resnorm_fwd_kernel(FwdArgs a) {
       if (c < a.d) {
         const int64_t e = r * d + c;
         float4 x = f4_add(ld4(a.z + e), bia[k]);
-        if (a.thresh != 0u) x = drop4(x, a.key, (uint64_t)e, a.thresh, a.scale);
+        if (a.thresh != 0u) x = drop4(x, key, (uint64_t)e, a.thresh, a.scale);
         if (a.res) x = f4_add(x, ld4(a.res + e));
         if (a.relu)
           x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(kBlock) void resnorm_fwd_kernel(FwdArgs a) {
 template <int LPR, int NC>
 __global__ __launch_bounds__(kBlock) void resnorm_bwd_kernel(BwdArgs a) {
   constexpr int RPB = kBlock / LPR;
+  const uint64_t key = a.thresh != 0u ? run_key(a.key, a.key_base) : 0ull;
   constexpr int DW = 4 * LPR * NC;  // padded row width
   __shared__ float red[RPB][3][DW];
   const int lane = threadIdx.x % LPR, grp = threadIdx.x / LPR;
@@ -191,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void resnorm_bwd_kernel(BwdArgs a) {
         const int64_t e = r * d + c;
         float4 x = a.relu ? relu_mask(g[k], v[k]) : g[k];
         if (a.d_res) st4(a.d_res + e, x);
-        if (a.thresh != 0u) x = drop4(x, a.key, (uint64_t)e, a.thresh, a.scale);
+        if (a.thresh != 0u) x = drop4(x, key, (uint64_t)e, a.thresh, a.scale);
         if (a.d_z) st4(a.d_z + e, x);
         pz[k] = f4_add(pz[k], x);
       }
@@ -287,12 +296,13 @@ using namespace mirec;
 
 extern "C" int mirec_resnorm_fwd(const float *res, const float *z, const float *bias,
                                  const float *gamma, const float *beta, int64_t n, int32_t d,
-                                 int32_t relu, float dropout_p, uint64_t seed, float eps,
-                                 float *out, float *y, float *mean, float *rstd,
-                                 mirec_stream_t stream) {
+                                 int32_t relu, float dropout_p, uint64_t seed,
+                                 const uint64_t *seed_base, float eps, float *out, float *y,
+                                 float *mean, float *rstd, mirec_stream_t stream) {
   Shape sh;
   MIREC_CHECK_ARG(n >= 0 && pick_shape(d, &sh));
-  FwdArgs a{res, z, bias, gamma, beta, out, y, mean, rstd, n, d, relu ? 1 : 0, 0, 0u, 1.f, eps};
+  FwdArgs a{res, z, bias, gamma, beta, out, y, mean, rstd, n, d, relu ? 1 : 0, 0, 0u, 1.f, eps,
+            seed_base};
   MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &a.key, &a.thresh, &a.scale));
   if (n == 0) return MIREC_OK;  // (empty tensors may carry null pointers)
   MIREC_CHECK_ARG(z != nullptr);
@@ -316,12 +326,14 @@ extern "C" int64_t mirec_resnorm_work_floats(int64_t n, int32_t d) {
 extern "C" int mirec_resnorm_bwd(const float *g_y, const float *g_out, const float *out,
                                  const float *mean, const float *rstd, const float *gamma,
                                  int64_t n, int32_t d, int32_t relu, float dropout_p,
-                                 uint64_t seed, float *d_res, float *d_z, float *work,
+                                 uint64_t seed, const uint64_t *seed_base, float *d_res,
+                                 float *d_z, float *work,
                                  float *d_gamma, float *d_beta, float *d_bias,
                                  mirec_stream_t stream) {
   Shape sh;
   MIREC_CHECK_ARG(n >= 0 && pick_shape(d, &sh));
-  BwdArgs a{g_y, g_out, out, mean, rstd, gamma, d_res, d_z, work, n, d, relu ? 1 : 0, 0, 0u, 1.f};
+  BwdArgs a{g_y, g_out, out, mean, rstd, gamma, d_res, d_z, work, n, d, relu ? 1 : 0, 0, 0u, 1.f,
+            seed_base};
   MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &a.key, &a.thresh, &a.scale));
   hipStream_t s = (hipStream_t)stream;
   if (n == 0) {  // empty sums; empty tensors may carry null pointers

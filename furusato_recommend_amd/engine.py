@@ -185,6 +185,43 @@ class AdamGroup:
                                        arr([m.exp_avg_sq for m in members]), numel,
                                        ctypes.byref(hp), _lib.stream_handle()), "adam_multi")
 
+    # -- graph-captured steps: the scalars live in device memory ------------
+    def next_shared_hparams(self):
+        """Advance every state (all must have a gradient and share lr /
+        betas / eps / step count) and return the one hparams struct of this
+        step — what a captured step reads through step_device."""
+        keys = {(s.n_steps, s.lr, s.betas, s.eps) for s in self.states}
+        if len(keys) != 1 or any(s.param.grad is None for s in self.states):
+            raise RuntimeError("device-scalar Adam needs one shared step for every parameter")
+        hps = [s.next_hparams() for s in self.states]
+        return hps[0]
+
+    @torch.no_grad()
+    def step_device(self, h_dev: torch.Tensor):
+        """The update of step() with the hyper-parameters read from ``h_dev``
+        (a device buffer of one mirec_adam_hparams_t) when the kernels run:
+        capturable in a HIP graph.  Does not advance the host step counts
+        (next_shared_hparams does, once per replay)."""
+        _note_raw_write()
+        large = [s for s in self.states if s.param.numel() >= self.LARGE]
+        small = [s for s in self.states if s.param.numel() < self.LARGE]
+        for s in large:
+            g = s.param.grad.contiguous()
+            check(lib.mirec_adam_dense_dev(s.param.data_ptr(), g.data_ptr(), s.exp_avg.data_ptr(),
+                                           s.exp_avg_sq.data_ptr(), s.param.numel(),
+                                           h_dev.data_ptr(), _lib.stream_handle()),
+                  "adam_dense_dev")
+        if small:
+            n = len(small)
+            grads = [m.param.grad.contiguous() for m in small]
+            arr = lambda xs: (ctypes.c_void_p * n)(*[x.data_ptr() for x in xs])  # noqa: E731
+            numel = (ctypes.c_int64 * n)(*[m.param.numel() for m in small])
+            check(lib.mirec_adam_multi_dev(n, arr([m.param for m in small]), arr(grads),
+                                           arr([m.exp_avg for m in small]),
+                                           arr([m.exp_avg_sq for m in small]), numel,
+                                           h_dev.data_ptr(), _lib.stream_handle()),
+                  "adam_multi_dev")
+
 
 class PropagationEngine:
     """Owns the per-model scratch buffers and issues the HIP launches.

@@ -16,6 +16,9 @@ The reference hard-codes 8 heads (:211); `heads` is a parameter here
 """
 from __future__ import annotations
 
+import ctypes
+from typing import NamedTuple
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -23,7 +26,7 @@ import torch.nn.functional as F
 
 from . import _lib
 from ._lib import check, lib
-from .engine import AdamGroup, AdamState
+from .engine import AdamGroup, AdamState, _note_raw_write
 from .linear import Linear, blas_backend, linear
 from .rows import gather_rows
 
@@ -73,22 +76,45 @@ class _CausalAttention(torch.autograd.Function):
         return dqkv, None
 
 
+class Packing(NamedTuple):
+    """Packed sequences: int32 ``offsets`` [B+1] on the device (sequence b =
+    rows offsets[b] .. offsets[b+1]-1) and, when the sequences are ordered by
+    length bucket, the host counts ``bucket_end`` (sequences [bucket_end[k-1],
+    bucket_end[k]) have at most 16(k+1) positions; mirec_attention_bucketed_*)."""
+    offsets: torch.Tensor
+    bucket_end: tuple | None = None
+    padded: bool = False  # rows past offsets[B] belong to no sequence (capacity padding)
+
+
 class _CausalAttentionVarlen(torch.autograd.Function):
     """Packed sequences: qkv [n_tok, 3d], sequence b = rows offsets[b] ..
-    offsets[b+1]-1 (mirec_attention_varlen_*)."""
+    offsets[b+1]-1 (mirec_attention_varlen_*, or mirec_attention_bucketed_*
+    given the length buckets)."""
 
     @staticmethod
-    def forward(ctx, qkv, offsets, heads: int):
+    def forward(ctx, qkv, offsets, heads: int, bucket_end=None, padded: bool = False):
         n, d3 = qkv.shape
         d = d3 // 3
         B = offsets.numel() - 1
         qkv = qkv.contiguous()
-        out = torch.empty(n, d, dtype=qkv.dtype, device=qkv.device)
-        _timed("fwd", (B, -1, heads, d // heads), lambda: check(lib.mirec_attention_varlen_fwd(
-            qkv.data_ptr(), offsets.data_ptr(), B, heads, d // heads, out.data_ptr(),
-            _lib.stream_handle()), "attention_varlen_fwd"), offsets)
+        # rows outside every sequence (capacity padding) are not written by
+        # the kernels: zero them so they stay finite downstream
+        alloc = torch.zeros if padded else torch.empty
+        out = alloc(n, d, dtype=qkv.dtype, device=qkv.device)
+        if bucket_end is None:
+            launch = lambda: check(lib.mirec_attention_varlen_fwd(  # noqa: E731
+                qkv.data_ptr(), offsets.data_ptr(), B, heads, d // heads, out.data_ptr(),
+                _lib.stream_handle()), "attention_varlen_fwd")
+        else:
+            be = _bucket_array(bucket_end, B)
+            launch = lambda: check(lib.mirec_attention_bucketed_fwd(  # noqa: E731
+                qkv.data_ptr(), offsets.data_ptr(), be, heads, d // heads, out.data_ptr(),
+                _lib.stream_handle()), "attention_bucketed_fwd")
+        _timed("fwd", (B, -1, heads, d // heads), launch, offsets)
         ctx.save_for_backward(qkv, offsets)
         ctx.heads = heads
+        ctx.bucket_end = bucket_end
+        ctx.padded = padded
         return out
 
     @staticmethod
@@ -97,16 +123,44 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         n, d3 = qkv.shape
         B = offsets.numel() - 1
         dh = d3 // 3 // ctx.heads
-        dqkv = torch.empty_like(qkv)
+        dqkv = torch.zeros_like(qkv) if ctx.padded else torch.empty_like(qkv)
         dout = dout.contiguous()
-        _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(lib.mirec_attention_varlen_bwd(
-            qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), B, ctx.heads, dh,
-            dqkv.data_ptr(), _lib.stream_handle()), "attention_varlen_bwd"), offsets)
-        return dqkv, None, None
+        if ctx.bucket_end is None:
+            launch = lambda: check(lib.mirec_attention_varlen_bwd(  # noqa: E731
+                qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), B, ctx.heads, dh,
+                dqkv.data_ptr(), _lib.stream_handle()), "attention_varlen_bwd")
+        else:
+            be = _bucket_array(ctx.bucket_end, B)
+            launch = lambda: check(lib.mirec_attention_bucketed_bwd(  # noqa: E731
+                qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), be, ctx.heads, dh,
+                dqkv.data_ptr(), _lib.stream_handle()), "attention_bucketed_bwd")
+        _timed("bwd", (B, -1, ctx.heads, dh), launch, offsets)
+        return dqkv, None, None, None, None
+
+
+def _bucket_array(bucket_end, batch: int):
+    be = tuple(int(x) for x in bucket_end)
+    if len(be) != 4 or be[3] != batch or any(b < a for a, b in zip((0,) + be, be)):
+        raise ValueError(f"bucket_end {be} does not partition {batch} sequences")
+    return (ctypes.c_int64 * 4)(*be)
+
+
+def length_buckets(lengths) -> tuple[np.ndarray, tuple]:
+    """Host lengths -> (stable order by bucket ceil(len/16) in 1..4, the
+    bucket_end counts of that order)."""
+    nb = np.clip((np.asarray(lengths, dtype=np.int64) + 15) // 16, 1, 4)
+    order = np.argsort(nb, kind="stable")
+    return order, tuple(int(x) for x in np.cumsum(np.bincount(nb - 1, minlength=4)))
 
 
 def _ptr(t):
     return 0 if t is None else t.data_ptr()
+
+
+# Device uint64 [1] mixed into every dropout mask key while a step is being
+# captured (None in eager mode): the host writes a fresh value before each
+# graph replay (mirec_resnorm_*'s seed_base).
+_SEED_BASE = None
 
 
 def _dropout_seed(p: float) -> int:
@@ -127,6 +181,7 @@ class _ResNorm(torch.autograd.Function):
         n, d = z.shape
         pure = res is None and bias is None and not relu and p == 0
         seed = _dropout_seed(p)
+        base = _SEED_BASE if p > 0 else None
         out = None if pure else torch.empty_like(z)
         y = mean = rstd = None
         if norm:
@@ -134,11 +189,13 @@ class _ResNorm(torch.autograd.Function):
             mean = torch.empty(n, dtype=z.dtype, device=z.device)
             rstd = torch.empty_like(mean)
         check(lib.mirec_resnorm_fwd(_ptr(res), z.data_ptr(), _ptr(bias), _ptr(gamma),
-                                    _ptr(beta), n, d, int(relu), float(p), seed, float(eps),
+                                    _ptr(beta), n, d, int(relu), float(p), seed, _ptr(base),
+                                    float(eps),
                                     _ptr(out), _ptr(y), _ptr(mean), _ptr(rstd),
                                     _lib.stream_handle()), "resnorm_fwd")
         ctx.save_for_backward(z if pure else out, mean, rstd, gamma)
         ctx.cfg = (relu, float(p), seed, res is not None, bias is not None, norm)
+        ctx.seed_base = base
         ctx.set_materialize_grads(False)
         return out, y
 
@@ -166,6 +223,7 @@ class _ResNorm(torch.autograd.Function):
                                device=out.device)
         check(lib.mirec_resnorm_bwd(_ptr(g_y), _ptr(g_out), out.data_ptr(), _ptr(mean),
                                     _ptr(rstd), _ptr(gamma), n, d, int(relu), p, seed,
+                                    _ptr(ctx.seed_base),
                                     _ptr(d_res), _ptr(d_z), _ptr(work), _ptr(d_gamma),
                                     _ptr(d_beta), _ptr(d_bias), _lib.stream_handle()),
               "resnorm_bwd")
@@ -213,7 +271,7 @@ class CausalSelfAttention(nn.Module):
 
     def forward(self, x, offsets=None):
         """x [B, T, d] (padded), or packed [n_tok, d] with int32 ``offsets``
-        [B+1] (sequence b = rows offsets[b] .. offsets[b+1]-1)."""
+        [B+1] (sequence b = rows offsets[b] .. offsets[b+1]-1) or a Packing."""
         return self.out_proj(self.core(x, offsets))
 
     def core(self, x, offsets=None):
@@ -221,6 +279,9 @@ class CausalSelfAttention(nn.Module):
         qkv = linear(x, self.in_proj_weight, self.in_proj_bias)
         if offsets is None:
             return _CausalAttention.apply(qkv, self.heads)
+        if isinstance(offsets, Packing):
+            return _CausalAttentionVarlen.apply(qkv, offsets.offsets, self.heads,
+                                                offsets.bucket_end, offsets.padded)
         return _CausalAttentionVarlen.apply(qkv, offsets, self.heads)
 
 
@@ -333,38 +394,53 @@ class SASRec(nn.Module):
 
     def forward_user_packed(self, x, offsets, seg, length):
         """forward_user on packed sequences: x [n_tok, d], ``seg`` [n_tok]
-        the sequence of every row.  Padding positions never reach a real
-        position under the causal mask and are excluded from the pool, so
-        this equals forward_user on the padded batch while skipping them."""
+        the sequence of every row (B for capacity padding rows, which the
+        pool drops).  Padding positions never reach a real position under
+        the causal mask and are excluded from the pool, so this equals
+        forward_user on the padded batch while skipping them."""
         x = self.blocks(x, offsets)
-        pooled = torch.zeros(length.numel(), x.shape[1], dtype=x.dtype, device=x.device)
-        pooled = pooled.index_add(0, seg, x)
+        B = length.numel()
+        pooled = torch.zeros(B + 1, x.shape[1], dtype=x.dtype, device=x.device)
+        pooled = pooled.index_add(0, seg, x)[:B]
         return pooled / length.to(x.dtype).unsqueeze(1)
 
     def packed_input(self, users):
-        """(x [n_tok, d], offsets [B+1] int32, seg [n_tok], length [B]) of the
-        users' sequences.  The token count is taken from the host copy of
-        the lengths (host ``users``: no device synchronisation)."""
-        ids, offsets, seg, length = self.packed_ids(users)
-        return gather_rows(self.item_id_embedding.weight, ids), offsets, seg, length
+        """(x [n_tok, d], packing, seg [n_tok], length [B]) of the users'
+        sequences.  The token count is taken from the host copy of the
+        lengths (host ``users``: no device synchronisation)."""
+        ids, packing, seg, length = self.packed_ids(users)
+        return gather_rows(self.item_id_embedding.weight, ids), packing, seg, length
 
     def packed_ids(self, users):
-        """packed_input's item ids [n_tok] (int32) instead of their rows."""
+        """packed_input's item ids [n_tok] (int32) instead of their rows.
+
+        The sequences are packed in length-bucket order (ceil(len/16) = 1..4,
+        stable), so each bucket's attention runs on a workgroup sized for it
+        (Packing.bucket_end); ``seg`` maps every packed row to its sequence's
+        position in ``users`` and ``length`` follows ``users``, so the pooled
+        user embeddings come out in the caller's order."""
         if torch.is_tensor(users) and users.is_cuda:
             u_host = users.cpu().numpy()
         else:
             u_host = np.asarray(users)
+        B = len(u_host)
         lens_h = self.seq.length_host[u_host]
         n_tok = int(lens_h.sum())
+        order, bucket_end = length_buckets(lens_h)
         dev = self.device
-        u = self._upload(u_host)
-        length = self.seq.length[u]
-        offsets = torch.zeros(len(u_host) + 1, dtype=torch.int32, device=dev)
-        offsets[1:] = torch.cumsum(length, 0).to(torch.int32)
-        seg = torch.repeat_interleave(torch.arange(len(u_host), device=dev), length,
-                                      output_size=n_tok)
-        pos = torch.arange(n_tok, device=dev) - offsets[seg].long()
-        return self.seq.items[u[seg], pos], offsets, seg, length
+        up = self._upload(np.concatenate([u_host, order]))
+        u, perm = up[:B], up[B:]
+        u_p = u[perm]
+        length_p = self.seq.length[u_p]
+        offsets = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        offsets[1:] = torch.cumsum(length_p, 0).to(torch.int32)
+        seg_p = torch.repeat_interleave(torch.arange(B, device=dev), length_p,
+                                        output_size=n_tok)
+        pos = torch.arange(n_tok, device=dev) - offsets[seg_p].long()
+        ids = self.seq.items[u_p[seg_p], pos]
+        if not self.config.get("attn_buckets", False):  # default: one 64-row bucket
+            bucket_end = None
+        return ids, Packing(offsets, bucket_end), perm[seg_p], self.seq.length[u]
 
     def _upload(self, host_ids) -> torch.Tensor:
         """int64 host ids -> device without a stream sync: a pageable H2D copy
@@ -425,7 +501,12 @@ class SASRec(nn.Module):
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
         between backward and Adam (DenseGradDataParallel's all-reduce).
         The projections run on the BLAS backend of config "blas" (default
-        rocBLAS: the step is host-bound and rocBLAS launches cheaper)."""
+        rocBLAS).  With config "graph" (default on) a single-process step
+        (no hook, no scale) replays a captured HIP graph of the whole step
+        (_CapturedStep); otherwise the step runs eagerly."""
+        if (self.config.get("graph", True) and grad_hook is None and loss_scale == 1.0
+                and len(users) > 0):
+            return self._graph_step(users, pos, neg)
         with blas_backend(self.config.get("blas", "cublas")):
             return self._stage_one(users, pos, neg, grad_hook, loss_scale)
 
@@ -433,21 +514,67 @@ class SASRec(nn.Module):
         for p in self.parameters():
             p.grad = None
         pos, neg = (torch.as_tensor(t).to(self.device) for t in (pos, neg))
-        ids, offsets, seg, length = self.packed_ids(users)
+        ids, packing, seg, length = self.packed_ids(users)
+        loss = self._step_body(ids, packing, seg, length, pos, neg, loss_scale)
+        if grad_hook is not None:
+            grad_hook()
+        self.optims.step()
+        return loss.detach()
+
+    def _step_body(self, ids, packing, seg, length, pos, neg, loss_scale=1.0):
+        """Forward, loss and backward of one packed batch; returns the loss."""
         n_tok, B = ids.numel(), pos.numel()
         # one lookup for the sequences, positives and negatives (one dense
         # table gradient, no accumulation), one pass of the item tower over
         # positives and negatives together (row-wise: same values)
         rows = gather_rows(self.item_id_embedding.weight, torch.cat([ids, pos.int(), neg.int()]))
         x, pn = rows.split([n_tok, 2 * B])
-        u = self.forward_user_packed(x, offsets, seg, length)
+        u = self.forward_user_packed(x, packing, seg, length)
         pe, ne = self.forward_item(pn).split(B)
         loss = self.loss(u, pe, ne)
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
-        if grad_hook is not None:
-            grad_hook()
-        self.optims.step()
-        return loss.detach()
+        return loss
+
+    # ------------------------------------------------------- graph capture
+    def packed_ids_static(self, u, capacity: int):
+        """packed_ids on the device for device user ids ``u`` [B] into a fixed
+        token capacity (>= the batch's token count): rows past the last
+        sequence get item id -1 (a zero row) and ``seg`` = B, so every shape
+        is static and the step can be captured.  Returns (ids [capacity],
+        Packing(offsets, padded=True), seg [capacity], length [B])."""
+        B = u.numel()
+        dev = self.device
+        length = self.seq.length[u]
+        offsets = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        # clamped to the capacity: a batch that did not fit could never make
+        # the kernels read past the token buffers (the host sizes capacity
+        # from the batch, so this never cuts a real batch)
+        offsets[1:] = torch.cumsum(length, 0).clamp(max=capacity).to(torch.int32)
+        t = torch.arange(capacity, dtype=torch.int32, device=dev)
+        seg = torch.searchsorted(offsets[1:], t, right=True)
+        segc = seg.clamp(max=B - 1)
+        pos = (t.long() - offsets[segc].long()).clamp(0, self.seq.max_len - 1)
+        ids = torch.where(seg < B, self.seq.items[u[segc], pos],
+                          torch.full_like(pos, -1, dtype=self.seq.items.dtype))
+        return ids, Packing(offsets, None, True), seg, length
+
+    def _graph_step(self, users, pos, neg):
+        u_host = users.cpu().numpy() if torch.is_tensor(users) else np.asarray(users)
+        B = len(u_host)
+        n_tok = int(self.seq.length_host[u_host].sum())
+        graphs = self.__dict__.setdefault("_graphs", {})
+        fits = [k for k in graphs if k[0] == B and k[2] == self.training and k[1] >= n_tok]
+        if fits:
+            g = graphs[min(fits, key=lambda k: k[1])]
+        else:
+            # capacity for this batch and, with margin (mean + 4 sd of a
+            # random batch's token count), for the batches after it: one
+            # capture serves the run
+            lens = self.seq.length_host
+            expect = B * float(lens.mean()) + 4.0 * float(lens.std()) * B ** 0.5
+            cap = -(-max(n_tok, int(expect)) // 1024) * 1024
+            g = graphs[(B, cap, self.training)] = _CapturedStep(self, B, cap, u_host)
+        return g.run(u_host, pos, neg)
 
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])
@@ -471,3 +598,97 @@ class SASRec(nn.Module):
     @torch.no_grad()
     def getUsersRating(self, users):
         return self.eval_ratings()(torch.as_tensor(users, device=self.device))
+
+
+class _CapturedStep:
+    """One SASRec training step (packing, forward, loss, backward, Adam)
+    captured in a HIP graph for batch size B and token capacity C, replayed
+    every step: the step's ~170 kernel launches cost one graph launch on
+    the host.  Everything that changes per step is read from device memory
+    when the kernels run: the users / positives / negatives (one staging
+    copy), the Adam scalars (mirec_adam_*_dev) and the dropout key base
+    (mirec_resnorm_*'s seed_base).  Shapes that depend on the batch are fixed
+    by packing into the capacity (packed_ids_static).  Capture runs one eager
+    warm-up step on a side stream first (library handles, lazy autograd
+    state) and restores the parameters and Adam moments it touched."""
+
+    def __init__(self, model: "SASRec", B: int, capacity: int, u_host):
+        global _SEED_BASE
+        self.m, self.B, self.C = model, B, capacity
+        dev = model.device
+        # [users | pos | neg | Adam hparams (6 f32 = 3 int64) | seed base];
+        # the warm-up runs on the first batch's users (fits the capacity)
+        # and first-step Adam scalars
+        init = np.zeros(3 * B + 4, dtype=np.int64)
+        init[:B] = u_host
+        s0 = model.optims.states[0]
+        hp0 = _lib.adam_hparams(s0.lr, s0.betas[0], s0.betas[1], s0.eps, 1)
+        init[3 * B:3 * B + 3] = np.frombuffer(bytes(hp0), dtype=np.int64)
+        self.inbuf = torch.from_numpy(init).to(dev)
+        self.stage = [torch.zeros(3 * B + 4, dtype=torch.int64).pin_memory() for _ in range(2)]
+        self.events = [None, None]
+        self.turn = 0
+        pool = model.__dict__.setdefault("_graph_pool", torch.cuda.graph_pool_handle())
+        params = list(model.parameters())
+        snap = [p.detach().clone() for p in params]
+        adam = [(s.exp_avg.clone(), s.exp_avg_sq.clone(), s.n_steps) for s in model.optims]
+        for p in params:
+            p.grad = None
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        self.graph = torch.cuda.CUDAGraph()
+        try:
+            _SEED_BASE = self.inbuf[3 * B + 3:]
+            with blas_backend(model.config.get("blas", "cublas")):
+                with torch.cuda.stream(side):
+                    self._body()  # warm-up (eager, on the side stream)
+                torch.cuda.current_stream().wait_stream(side)
+                for p in params:
+                    p.grad = None
+                with torch.cuda.graph(self.graph, pool=pool):
+                    self.loss = self._body()
+        finally:
+            _SEED_BASE = None
+        with torch.no_grad():
+            for p, v in zip(params, snap):
+                p.copy_(v)
+            for s, (a, b, n) in zip(model.optims, adam):
+                s.exp_avg.copy_(a)
+                s.exp_avg_sq.copy_(b)
+                s.n_steps = n
+
+    def _body(self):
+        m, B = self.m, self.B
+        buf = self.inbuf
+        u, pos, neg = buf[:B], buf[B:2 * B], buf[2 * B:3 * B]
+        hdev = buf[3 * B:3 * B + 3].view(torch.float32)
+        ids, packing, seg, length = m.packed_ids_static(u, self.C)
+        loss = m._step_body(ids, packing, seg, length, pos, neg)
+        m.optims.step_device(hdev)
+        return loss.detach()
+
+    def run(self, u_host, pos, neg):
+        B = self.B
+        k = self.turn
+        self.turn ^= 1
+        if self.events[k] is not None:
+            self.events[k].synchronize()  # staging buffer k's last copy is done
+        st = self.stage[k].numpy()
+        st[:B] = u_host
+        on_dev = [torch.is_tensor(t) and t.is_cuda for t in (pos, neg)]
+        for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
+            if not dv:
+                st[(j + 1) * B:(j + 2) * B] = np.asarray(t.cpu() if torch.is_tensor(t) else t)
+        hp = self.m.optims.next_shared_hparams()
+        st[3 * B:3 * B + 3] = np.frombuffer(bytes(hp), dtype=np.int64)
+        st[3 * B + 3] = int(torch.randint(0, 2 ** 62, (1,)).item())  # torch's CPU generator
+        self.inbuf.copy_(self.stage[k], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.events[k] = ev
+        for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
+            if dv:  # device ids: copied after the staging copy (stream order)
+                self.inbuf[(j + 1) * B:(j + 2) * B].copy_(t)
+        _note_raw_write()
+        self.graph.replay()
+        return self.loss.clone()

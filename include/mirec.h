@@ -324,6 +324,18 @@ int mirec_adam_multi(int32_t count, float *const *params, const float *const *gr
                      const int64_t *numel, const mirec_adam_hparams_t *hp,
                      mirec_stream_t stream);
 
+/* The same two updates with the hyper-parameters read from DEVICE memory
+ * when the kernel runs (h_device: one mirec_adam_hparams_t), so a captured
+ * HIP graph replays each step with the scalars the host wrote there for
+ * that step (bias corrections change every step). */
+int mirec_adam_dense_dev(float *param, const float *grad, float *exp_avg,
+                         float *exp_avg_sq, int64_t n,
+                         const mirec_adam_hparams_t *h_device, mirec_stream_t stream);
+int mirec_adam_multi_dev(int32_t count, float *const *params, const float *const *grads,
+                         float *const *exp_avg, float *const *exp_avg_sq,
+                         const int64_t *numel, const mirec_adam_hparams_t *h_device,
+                         mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* On-device BPR sampler (negative_sample.py:98-134 semantics)               */
 /* ------------------------------------------------------------------------ */
@@ -419,6 +431,20 @@ int mirec_attention_varlen_bwd(const float *qkv, const float *dout, const int32_
                                int64_t batch, int32_t heads, int32_t head_dim,
                                float *dqkv, mirec_stream_t stream);
 
+/* Packed form with the sequences ordered by length bucket: bucket_end (HOST
+ * array of 4 non-decreasing counts; batch = bucket_end[3]) says sequences
+ * [bucket_end[k-1], bucket_end[k]) have at most 16*(k+1) positions.  Each
+ * bucket runs on a kernel whose workgroup holds only 16*(k+1) rows (one
+ * wave per 16-row block, LDS sized to match), so short sequences neither
+ * idle three waves nor reserve a 64-row LDS image.  A longer sequence placed
+ * in a bucket is cut to the bucket's rows (an input error). */
+int mirec_attention_bucketed_fwd(const float *qkv, const int32_t *offsets,
+                                 const int64_t *bucket_end, int32_t heads, int32_t head_dim,
+                                 float *out, mirec_stream_t stream);
+int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                                 const int64_t *bucket_end, int32_t heads, int32_t head_dim,
+                                 float *dqkv, mirec_stream_t stream);
+
 /* Row tail of the SASRec block (model/sasrec.py:385-397 — the dropout,
  * residual add, ReLU and LayerNorm around the attention and the FFN), one
  * pass over the n x d token rows (d % 4 == 0, 4 <= d <= 1024):
@@ -429,11 +455,14 @@ int mirec_attention_varlen_bwd(const float *qkv, const float *dout, const int32_
  *         mean / rstd [n] then required)
  * out may be NULL only when it equals z (no res / bias / relu / dropout).
  * The dropout mask is the counter hash of (seed, row * d + col) — the same
- * seed recomputes it in the backward. */
+ * seed recomputes it in the backward.  seed_base (device, may be NULL): when
+ * given, *seed_base is mixed into the mask key when the kernel runs, so a
+ * captured HIP graph draws a fresh mask on every replay (the host writes a
+ * new base before each replay; the backward reads the same base). */
 int mirec_resnorm_fwd(const float *res, const float *z, const float *bias, const float *gamma,
                       const float *beta, int64_t n, int32_t d, int32_t relu, float dropout_p,
-                      uint64_t seed, float eps, float *out, float *y, float *mean, float *rstd,
-                      mirec_stream_t stream);
+                      uint64_t seed, const uint64_t *seed_base, float eps, float *out, float *y,
+                      float *mean, float *rstd, mirec_stream_t stream);
 
 /* Floats of scratch mirec_resnorm_bwd needs for parameter gradients. */
 int64_t mirec_resnorm_work_floats(int64_t n, int32_t d);
@@ -446,8 +475,9 @@ int64_t mirec_resnorm_work_floats(int64_t n, int32_t d);
  * mirec_resnorm_work_floats floats).  Sums are added in a fixed order. */
 int mirec_resnorm_bwd(const float *g_y, const float *g_out, const float *out, const float *mean,
                       const float *rstd, const float *gamma, int64_t n, int32_t d, int32_t relu,
-                      float dropout_p, uint64_t seed, float *d_res, float *d_z, float *work,
-                      float *d_gamma, float *d_beta, float *d_bias, mirec_stream_t stream);
+                      float dropout_p, uint64_t seed, const uint64_t *seed_base, float *d_res,
+                      float *d_z, float *work, float *d_gamma, float *d_beta, float *d_bias,
+                      mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* Evaluation (trainer.py:130-138)                                           */

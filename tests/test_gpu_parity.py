@@ -753,6 +753,36 @@ def test_sasrec_varlen_attention_matches_padded():
         assert rel(gv, gp[mask]) < TOL
 
 
+def test_sasrec_bucketed_attention_matches_varlen():
+    """Length-bucketed launches (workgroups of 16*NB rows) == the one-bucket
+    packed kernels, fwd and bwd, at every bucket edge (0, 1, 16, 17, 32, 33,
+    48, 49, 64), with empty buckets, odd head dims and dh = 64; malformed
+    bucket counts are rejected."""
+    from furusato_recommend_amd.sasrec import _CausalAttentionVarlen, length_buckets
+    torch.manual_seed(2)
+    edge = [0, 1, 16, 17, 32, 33, 48, 49, 64, 5, 50, 40, 23, 9]
+    for heads, dh, lens in (((2, 64, edge)), ((8, 16, edge)), ((3, 20, edge)),
+                            ((2, 64, [3, 7, 12, 16])), ((1, 32, [60, 64, 49])),
+                            ((2, 8, [20, 33, 1]))):
+        order, be = length_buckets(lens)
+        lens_o = torch.tensor(lens)[torch.from_numpy(order)]
+        d, B = heads * dh, len(lens)
+        offsets = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+        offsets[1:] = torch.cumsum(lens_o.cuda(), 0).int()
+        n = int(lens_o.sum())
+        qkv = torch.randn(n, 3 * d, device="cuda")
+        go = torch.randn(n, d, device="cuda")
+        q1 = qkv.clone().requires_grad_(True)
+        o1 = _CausalAttentionVarlen.apply(q1, offsets, heads)
+        g1, = torch.autograd.grad(o1, q1, go)
+        q2 = qkv.clone().requires_grad_(True)
+        o2 = _CausalAttentionVarlen.apply(q2, offsets, heads, be)
+        g2, = torch.autograd.grad(o2, q2, go)
+        assert rel(o2, o1) < TOL and rel(g2, g1) < TOL
+    with pytest.raises(ValueError):
+        _CausalAttentionVarlen.apply(qkv, offsets, heads, (0, 2, 1, B))
+
+
 def test_sasrec_packed_path_equals_padded():
     """The training path (packed sequences) gives the padded path's user
     embeddings and parameter gradients (dropout off)."""
@@ -1112,3 +1142,97 @@ def test_soak_many_steps_stay_finite_and_learn():
     assert np.isfinite(first) and np.isfinite(last) and last < 0.8 * first
     assert bool(torch.isfinite(m.all_embedding.weight).all())
     assert int((m.engine.slot != -1).sum()) == 0
+
+
+def test_adam_device_hparams_equal_host_hparams():
+    """mirec_adam_dense_dev / mirec_adam_multi_dev (scalars read from device
+    memory, the graph-captured path) == the host-scalar kernels, bitwise."""
+    import ctypes
+
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd.engine import AdamGroup, AdamState
+    torch.manual_seed(4)
+    shapes = [(3000, 128), (7,), (129, 3), (1 << 20,)]
+    ps = [torch.randn(*s, device="cuda") for s in shapes]
+    qs = [p.clone() for p in ps]
+    ga, gb = AdamGroup(AdamState(p, lr=1e-3) for p in ps), AdamGroup(AdamState(q, lr=1e-3) for q in qs)
+    for it in range(3):
+        for p, q in zip(ps, qs):
+            p.grad = torch.randn_like(p)
+            q.grad = p.grad.clone()
+        ga.step()
+        hp = gb.next_shared_hparams()
+        h_dev = torch.frombuffer(bytearray(bytes(hp)), dtype=torch.float32).cuda()
+        gb.step_device(h_dev)
+        for p, q in zip(ps, qs):
+            assert torch.equal(p, q)
+    assert ctypes.sizeof(_lib.AdamH) == 24
+
+
+def test_resnorm_seed_base_draws_fresh_masks():
+    """With a device seed base (graph replays), the dropout mask changes with
+    the base value and the backward recomputes the forward's mask."""
+    from furusato_recommend_amd import sasrec as S
+    torch.manual_seed(5)
+    n, d, p = 4096, 128, 0.25
+    z = (torch.rand(n, d, device="cuda") + 0.5).requires_grad_(True)
+    res = torch.zeros(n, d, device="cuda", requires_grad=True)
+    base = torch.zeros(1, dtype=torch.int64, device="cuda")
+    masks = []
+    try:
+        S._SEED_BASE = base
+        torch.manual_seed(11)
+        out, _ = S.resnorm(res, z, p=p)
+        g = torch.randn(n, d, device="cuda")
+        base.fill_(12345)  # the backward must read the base its forward used
+        base.fill_(0)
+        gz, = torch.autograd.grad(out, [z], g)
+        kept = out != 0
+        assert rel(gz, g * kept / (1 - p)) < 1e-6
+        masks.append(kept)
+        for b in (1, 2):
+            base.fill_(b)
+            torch.manual_seed(11)  # same host seed: only the device base differs
+            o2, _ = S.resnorm(res, z, p=p)
+            masks.append(o2 != 0)
+    finally:
+        S._SEED_BASE = None
+    assert not torch.equal(masks[0], masks[1]) and not torch.equal(masks[1], masks[2])
+    for mk in masks:
+        assert abs(float(mk.float().mean()) - (1 - p)) < 0.01
+
+
+def test_sasrec_graph_step_equals_eager():
+    """stageOne replaying a captured HIP graph (capacity-padded packing,
+    device Adam scalars) == the eager step: losses of consecutive steps and
+    every gradient of the first step (dropout off); the captured model keeps
+    learning with dropout on and draws a fresh mask each replay."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    ds = SyntheticBipartite(700, 300, 14_000, seed=6)
+    cfg = {"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+           "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0}
+    torch.manual_seed(3)
+    a = SASRec(dict(cfg, graph=True), ds)
+    torch.manual_seed(3)
+    b = SASRec(dict(cfg, graph=False), ds)
+    rng = np.random.default_rng(2)
+    for it in range(3):
+        users = rng.integers(0, 700, 128)
+        pos = torch.as_tensor(rng.integers(0, 300, 128), device="cuda")
+        neg = rng.integers(0, 300, 128)  # host array: goes through the staging copy
+        la, lb = float(a.stageOne(users, pos, neg)), float(b.stageOne(users, pos, neg))
+        assert abs(la - lb) <= 1e-5 * abs(lb), (it, la, lb)
+        if it == 0:
+            for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+                scale = float(pb.grad.abs().max())
+                assert float((pa.grad - pb.grad).abs().max()) <= TOL * max(scale, 1e-4), name
+    assert len(a._graphs) >= 1 and not getattr(b, "_graphs", None)
+    # dropout on: same batch twice -> different losses (fresh masks), and
+    # repeated steps on one batch lower its loss
+    torch.manual_seed(3)
+    c = SASRec(dict(cfg, dropout_p=0.3, lr=1e-2), ds)
+    users = rng.integers(0, 700, 128)
+    pos, neg = rng.integers(0, 300, 128), rng.integers(0, 300, 128)
+    losses = [float(c.stageOne(users, pos, neg)) for _ in range(30)]
+    assert len(set(losses[:5])) == 5
+    assert np.mean(losses[-5:]) < np.mean(losses[:5])

@@ -293,3 +293,22 @@ def test_split_k_linear_matches_nn_linear():
         assert torch.allclose(a.weight.grad, b.weight.grad, rtol=1e-10, atol=1e-9)
         assert torch.allclose(a.bias.grad, b.bias.grad)
         assert torch.allclose(weight_grad(gy, x.detach()), gy.t() @ x.detach())
+
+
+def test_length_buckets_order_and_counts():
+    """Host bucketing of the packed SASRec batch: stable order by
+    ceil(len/16) clipped to 1..4 (length 0 joins bucket 1), counts that
+    partition the batch, and every sequence inside its bucket's row limit."""
+    from furusato_recommend_amd.sasrec import length_buckets
+    rng = np.random.default_rng(0)
+    for lens in ([0, 1, 16, 17, 32, 33, 48, 49, 64], rng.integers(0, 65, 1000), [50] * 5, [3]):
+        lens = np.asarray(lens)
+        order, be = length_buckets(lens)
+        assert sorted(order.tolist()) == list(range(len(lens)))
+        assert len(be) == 4 and be[3] == len(lens) and list(be) == sorted(be)
+        lo = 0
+        for k, hi in enumerate(be):
+            seg = order[lo:hi]
+            assert (lens[seg] <= 16 * (k + 1)).all()
+            assert (np.diff(seg) > 0).all()  # stable inside a bucket
+            lo = hi

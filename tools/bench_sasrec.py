@@ -100,6 +100,10 @@ def main():
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--blas", default="cublas", choices=["cublas", "cublaslt"],
                     help="BLAS backend of the projections (cublas = rocBLAS on ROCm)")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: replay the captured HIP graph of the step; 0: eager step")
+    ap.add_argument("--attn-buckets", type=int, default=0,
+                    help="0: every packed sequence on the 64-row attention kernel (A/B)")
     ap.add_argument("--fused-rows", type=int, default=1,
                     help="0: the torch composition of dropout / residual / LayerNorm (A/B)")
     args = ap.parse_args()
@@ -112,7 +116,8 @@ def main():
     m = SASRec({"recdim": args.dim, "layer": args.layers, "heads": args.heads, "lr": 1e-3,
                 "decay": 1e-4, "device": "cuda:0", "bpr_batch_size": args.batch,
                 "dropout_p": 0.2, "blas": args.blas,
-                "fused_rows": bool(args.fused_rows)}, _DS(args.users, args.items),
+                "fused_rows": bool(args.fused_rows), "attn_buckets": bool(args.attn_buckets),
+                "graph": bool(args.graph)}, _DS(args.users, args.items),
                sequences=seq)
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(7)
@@ -135,13 +140,21 @@ def main():
     for _ in range(args.warmup):
         m.stageOne(*batch())
     torch.cuda.synchronize()
-    S.ATTN_EVENTS = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         m.stageOne(*batch())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # per-launch attention timing: a few eager steps of the same kernels
+    # (events on the launch stream; a replayed graph records none)
+    graph_mode = m.config["graph"]
+    m.config["graph"] = False
+    S.ATTN_EVENTS = []
+    for _ in range(5):
+        m.stageOne(*batch())
+    torch.cuda.synchronize()
     ev, S.ATTN_EVENTS = S.ATTN_EVENTS, None
+    m.config["graph"] = graph_mode
 
     kinds = {}
     for kind, s, e, (b, T, h, dh), offs in ev:
@@ -173,7 +186,7 @@ def main():
         else:
             roof[kind] = {"bound": "mfma", "achieved": round(fl / t / 1e12, 2), "peak": 157.3,
                           "unit": "TFLOP/s", "frac": round(t_mfma / t, 4)}
-        roof[kind].update(avg_launch_ms=round(ms / cnt, 4), launches_per_step=cnt / args.steps,
+        roof[kind].update(avg_launch_ms=round(ms / cnt, 4), launches_per_step=cnt / 5,
                           flop_per_launch=fl, bytes_per_launch=by)
     cpu = cpu_baseline(m, seq, B, args.heads, rng) if args.cpu_baseline else None
     print(json.dumps({
@@ -183,7 +196,7 @@ def main():
         "dtype": "f32", "data": "synthetic sequences U[5,%d], random-init weights" % args.maxlen,
         "config": {"workload": "C4: SASRec L=%d heads=%d d=%d maxlen=%d, %d users x %d items"
                    % (args.layers, args.heads, args.dim, args.maxlen, args.users, args.items),
-                   "bpr_batch": B},
+                   "bpr_batch": B, "step": "HIP graph replay" if graph_mode else "eager"},
         "attention_roofline": roof, "cpu_baseline": cpu}), flush=True)
 
 
