@@ -500,15 +500,20 @@ class SASRec(nn.Module):
         """One BPR step on packed sequences.  ``loss_scale`` scales the
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
         between backward and Adam (DenseGradDataParallel's all-reduce).
-        The projections run on the BLAS backend of config "blas" (default
-        rocBLAS).  With config "graph" (default on) a single-process step
-        (no hook, no scale) replays a captured HIP graph of the whole step
-        (_CapturedStep); otherwise the step runs eagerly."""
+        With config "graph" (default on) a single-process step (no hook, no
+        scale) replays a captured HIP graph of the whole step
+        (_CapturedStep); otherwise the step runs eagerly.  The projections
+        run on the BLAS backend of config "blas" (default: hipBLASLt in the
+        captured step, where its faster kernels win; rocBLAS in the eager
+        step, which is host-bound and rocBLAS launches cost less host time)."""
         if (self.config.get("graph", True) and grad_hook is None and loss_scale == 1.0
                 and len(users) > 0):
             return self._graph_step(users, pos, neg)
         with blas_backend(self.config.get("blas", "cublas")):
             return self._stage_one(users, pos, neg, grad_hook, loss_scale)
+
+    def graph_blas(self) -> str:
+        return self.config.get("blas", "cublaslt")
 
     def _stage_one(self, users, pos, neg, grad_hook, loss_scale):
         for p in self.parameters():
@@ -639,7 +644,7 @@ class _CapturedStep:
         self.graph = torch.cuda.CUDAGraph()
         try:
             _SEED_BASE = self.inbuf[3 * B + 3:]
-            with blas_backend(model.config.get("blas", "cublas")):
+            with blas_backend(model.graph_blas()):
                 with torch.cuda.stream(side):
                     self._body()  # warm-up (eager, on the side stream)
                 torch.cuda.current_stream().wait_stream(side)

@@ -98,8 +98,9 @@ def main():
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--blas", default="cublas", choices=["cublas", "cublaslt"],
-                    help="BLAS backend of the projections (cublas = rocBLAS on ROCm)")
+    ap.add_argument("--blas", default="", choices=["", "cublas", "cublaslt"],
+                    help="BLAS backend of the projections (cublas = rocBLAS, cublaslt = "
+                         "hipBLASLt on ROCm; default: the model's choice per step mode)")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: replay the captured HIP graph of the step; 0: eager step")
     ap.add_argument("--attn-buckets", type=int, default=0,
@@ -115,7 +116,7 @@ def main():
                                  seed=0)
     m = SASRec({"recdim": args.dim, "layer": args.layers, "heads": args.heads, "lr": 1e-3,
                 "decay": 1e-4, "device": "cuda:0", "bpr_batch_size": args.batch,
-                "dropout_p": 0.2, "blas": args.blas,
+                "dropout_p": 0.2, **({"blas": args.blas} if args.blas else {}),
                 "fused_rows": bool(args.fused_rows), "attn_buckets": bool(args.attn_buckets),
                 "graph": bool(args.graph)}, _DS(args.users, args.items),
                sequences=seq)
