@@ -12,20 +12,26 @@
 // queries on the lanes): the softmax over keys is then a per-lane reduction
 // plus two lane shuffles, and Pᵀ sits in registers in exactly the layout the
 // next MFMA takes as its B operand (Oᵀ = Vᵀ Pᵀ sums over Pᵀ's row index), so
-// P never goes through LDS in the forward.  The contraction over head dims in
-// Sᵀ uses a permuted dim order (lane group g owns dims g*DPAD/4 ..), which
-// lets each lane hold its query row segment as a few float4 registers.
+// P never goes through LDS in the forward.  The contraction over head dims
+// uses the dim order 4t + g (lane group g, step t), which with row strides
+// ≡ 4 (mod 32) floats makes every strided operand read hit 64 distinct banks.
 //
 // Forward, wave w = query block w:   Sᵀ_kb = K_kb Q_wᵀ (kb <= w), scale,
 //   causal mask, column softmax -> Pᵀ; Oᵀ = Σ_kb Vᵀ_kb Pᵀ_kb; store O rows.
 // Backward, phase A (wave w = query block w): recompute Pᵀ; dPᵀ = V dOᵀ;
 //   δ_q = Σ_k P dP; dSᵀ = Pᵀ ⊙ (dPᵀ − δ) / sqrt(dh); dQᵀ = Kᵀ dSᵀ -> store;
-//   Pᵀ, dSᵀ tiles -> LDS.  Phase B (wave w = key block w): dVᵀ = Σ_q dOᵀ P,
-//   dKᵀ = Σ_q Qᵀ dS over the query blocks >= w -> store.
-// LDS (head dim padded to DPAD = 32 / 64): forward K, V (35 KB at DPAD 64);
-// backward K, V (later reused for Q, dO) + Pᵀ, dSᵀ (76 KB): 4 / 2
-// workgroups per CU.  Row strides are chosen so the strided operand reads
-// and the tile writes hit 64 distinct banks.
+//   the softmax statistics (max, 1/sum) and δ of each query -> LDS, the
+//   wave's own K / V block -> registers.  Phase B (wave w = key block w), per
+//   query block qb >= w: S = Q_qb K_wᵀ and dP = dO_qb V_wᵀ (queries on the
+//   accumulator rows, keys on the lanes — the layout in which P and dS are
+//   the B operands of the next products), P and dS from the statistics;
+//   dVᵀ += Σ_q dOᵀ P, dKᵀ += Σ_q Qᵀ dS -> store.  Recomputing P / dS in
+//   phase B (twice its MFMAs) instead of keeping Pᵀ / dSᵀ tiles in LDS halves
+//   the backward's LDS: more workgroups per CU hide the per-workgroup
+//   memory latency that bounds these small problems.
+// LDS (head dim padded to DPAD = 32 / 64): forward K, V (35 KB at DPAD 64,
+// 16 rows per block); backward K, V, later reused for Q, dO, plus 3 floats
+// per row of statistics (36 KB): 4 workgroups per CU either way.
 // q/k/v are read straight from the packed in-projection output (head h =
 // columns h*dh .. of each third); O / dQKV are written in the same layout.
 // Sequences come either as a uniform [B, T, 3d] batch or packed by offsets.
@@ -49,12 +55,10 @@ struct AttnShape {
   static constexpr int NT = 64 * NB;      // threads
   static constexpr int Q4 = DPAD / 4;     // head dims per lane in the S / dP products
   static constexpr int NCB = DPAD / kB;   // 16-dim output blocks
-  static constexpr int LDK = DPAD + 4;    // K / V row stride (≡ 4 mod 32)
-  static constexpr int LDQ = DPAD == 64 ? 80 : 48;  // Q / dO (phase B) row stride (≡ 16 mod 32)
-  static constexpr int LDP = TR + 4;      // Pᵀ / dSᵀ row stride (≡ 4 mod 16)
+  static constexpr int LDK = DPAD + 4;    // K / V, then Q / dO row stride (≡ 4 mod 32)
   static constexpr int fwd_lds = (int)sizeof(float) * 2 * TR * LDK;
-  static constexpr int bwd_region = 2 * TR * (LDK > LDQ ? LDK : LDQ);
-  static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 2 * TR * LDP);
+  static constexpr int bwd_region = 2 * TR * LDK;
+  static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 3 * TR);
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -148,7 +152,8 @@ __device__ __forceinline__ void store4(float *row, int c, int dh, f32x4 x) {
 // P[query 16w + j][key 16kb + 4g + r] (j = lane & 15, g = lane >> 4).
 template <int DPAD, int NB>
 __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)[DPAD / 4], int w,
-                                               int T, float scale, f32x4 (&s)[NB]) {
+                                               int T, float scale, f32x4 (&s)[NB], float &m_out,
+                                               float &inv_out) {
   using S = AttnShape<DPAD, NB>;
   const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -194,6 +199,8 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[kb][r] *= inv;
   }
+  m_out = m;
+  inv_out = inv;
 }
 
 // Sequence seq0 + blockIdx.x / H, head blockIdx.x % H.
@@ -223,7 +230,8 @@ __global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restri
   __syncthreads();
   if (w >= nb) return;  // no barrier below
   f32x4 p[NB];
-  scores_softmax<DPAD, NB>(sK, q, w, T, scale, p);
+  float m_, inv_;
+  scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, m_, inv_);
   f32x4 o[S::NCB];
 #pragma unroll
   for (int cb = 0; cb < S::NCB; ++cb) o[cb] = zero4();
@@ -244,8 +252,10 @@ __global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restri
   }
 }
 
+// waves_per_eu(4): at most 128 registers, so four workgroups (the LDS
+// limit) fit per CU
 template <int DPAD, int NB>
-__global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restrict__ qkv,
+__global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_kernel(const float *__restrict__ qkv,
                                                            const float *__restrict__ dout,
                                                            float *__restrict__ dqkv, int T, int H,
                                                            int dh, float scale,
@@ -253,9 +263,9 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restri
                                                            int64_t seq0) {
   using S = AttnShape<DPAD, NB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  float *sK = smem, *sV = smem + S::TR * S::LDK;         // phase A
-  float *sQ = smem, *sDO = smem + S::TR * S::LDQ;        // phase B (same region)
-  float *sP = smem + S::bwd_region, *sDS = sP + S::TR * S::LDP;
+  float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
+  float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
+  float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
   const int64_t b = seq0 + blockIdx.x / H;
@@ -275,9 +285,11 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restri
   load_seg<S::Q4>(dout + (row0 + qi) * d + h * dh, g, dh, qvalid, dov);
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
+  float kr[S::Q4], vr[S::Q4];  // K / V rows 16w + j, dims 4t + g (phase B operands)
   if (w < nb) {
     f32x4 p[NB], dp[NB];
-    scores_softmax<DPAD, NB>(sK, q, w, T, scale, p);
+    float m, inv;
+    scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, m, inv);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
 #pragma unroll
@@ -295,6 +307,11 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restri
     }
     delta += __shfl_xor(delta, 16);
     delta += __shfl_xor(delta, 32);
+    if (g == 0) {
+      sM[qi] = m;
+      sL[qi] = inv;
+      sD[qi] = delta;
+    }
     // dSᵀ (in dp), then dQᵀ = Kᵀ dSᵀ
     f32x4 dq[S::NCB];
 #pragma unroll
@@ -305,10 +322,7 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restri
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dp[kb][r] = p[kb][r] * (dp[kb][r] - delta) * scale;
-        const int key = kB * kb + 4 * g + r;
-        sP[key * S::LDP + qi] = p[kb][r];
-        sDS[key * S::LDP + qi] = dp[kb][r];
-        const float *krow = sK + key * S::LDK + j;
+        const float *krow = sK + (kB * kb + 4 * g + r) * S::LDK + j;
 #pragma unroll
         for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = mfma16(krow[kB * cb], dp[kb][r], dq[cb]);
       }
@@ -318,36 +332,59 @@ __global__ __launch_bounds__(64 * NB) void attn_bwd_kernel(const float *__restri
 #pragma unroll
       for (int cb = 0; cb < S::NCB; ++cb) store4(row, kB * cb + 4 * g, dh, dq[cb]);
     }
+#pragma unroll
+    for (int t = 0; t < S::Q4; ++t) {
+      kr[t] = sK[qi * S::LDK + 4 * t + g];
+      vr[t] = sV[qi * S::LDK + 4 * t + g];
+    }
   }
-  __syncthreads();  // K / V no longer read; Pᵀ, dSᵀ complete
+  __syncthreads();  // K / V no longer read from LDS; statistics complete
   if (w < nb) {
 #pragma unroll
     for (int t = 0; t < S::Q4; ++t) {
-      sQ[qi * S::LDQ + 4 * t + g] = q[t];
-      sDO[qi * S::LDQ + 4 * t + g] = dov[t];
+      sQ[qi * S::LDK + 4 * t + g] = q[t];
+      sDO[qi * S::LDK + 4 * t + g] = dov[t];
     }
   }
   __syncthreads();
   // ------------------------------------------------------ phase B: key block w
   if (w < nb) {
-    const int kb = w;
+    const int key = kB * w + j;
     f32x4 dv[S::NCB], dk[S::NCB];
 #pragma unroll
     for (int cb = 0; cb < S::NCB; ++cb) {
       dv[cb] = zero4();
       dk[cb] = zero4();
     }
-    const int key = kB * kb + j;
-    for (int q0 = kB * kb; q0 < kB * nb; q0 += 4) {
-      const int qq = q0 + g;
-      const float pb = sP[key * S::LDP + qq];
-      const float db = sDS[key * S::LDP + qq];
-      const float *dorow = sDO + qq * S::LDQ + j;
-      const float *qrow = sQ + qq * S::LDQ + j;
+    for (int qb = w; qb < nb; ++qb) {
+      // S[query 16qb + 4g + r][key 16w + j] and dP likewise
+      f32x4 sc = zero4(), dpc = zero4();
+      const float *qrow = sQ + (kB * qb + j) * S::LDK + g;
+      const float *orow = sDO + (kB * qb + j) * S::LDK + g;
 #pragma unroll
-      for (int cb = 0; cb < S::NCB; ++cb) {
-        dv[cb] = mfma16(dorow[kB * cb], pb, dv[cb]);
-        dk[cb] = mfma16(qrow[kB * cb], db, dk[cb]);
+      for (int t = 0; t < S::Q4; ++t) {
+        sc = mfma16(qrow[4 * t], kr[t], sc);
+        dpc = mfma16(orow[4 * t], vr[t], dpc);
+      }
+      float pr[4], dsr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = kB * qb + 4 * g + r;
+        const bool ok = key <= qq && qq < T;
+        const float pv = ok ? expf(sc[r] * scale - sM[qq]) * sL[qq] : 0.f;
+        pr[r] = pv;
+        dsr[r] = pv * (dpc[r] - sD[qq]) * scale;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = kB * qb + 4 * g + r;
+        const float *dorow = sDO + qq * S::LDK + j;
+        const float *qr = sQ + qq * S::LDK + j;
+#pragma unroll
+        for (int cb = 0; cb < S::NCB; ++cb) {
+          dv[cb] = mfma16(dorow[kB * cb], pr[r], dv[cb]);
+          dk[cb] = mfma16(qr[kB * cb], dsr[r], dk[cb]);
+        }
       }
     }
     if (key < T) {
