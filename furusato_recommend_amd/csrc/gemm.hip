@@ -1,0 +1,319 @@
+// f32 GEMMs of the Linear layers of the SASRec block and the GraphSAGE hop
+// (model/sasrec.py:385-421, model/graphsage.py:311-324: nn.Linear forward,
+// input gradient and weight / bias gradient) on gfx950 MFMA.
+//
+// The token-row activations are tall and thin (tens of thousands of rows x
+// d = 128..384), so two shapes cover every product:
+//   gemm_nt:  C[n, No] = A[n, Kr] · B[No, Kr]ᵀ (+ bias[No])
+//             forward y = x Wᵀ + b, and dX = dY W with B = Wᵀ (a copy of the
+//             small weight), so both operands are k-contiguous rows.
+//   gemm_tn:  C[M, No] = Σ_r A[r, M] B[r, No] over the n rows (+ the column
+//             sums of A): dW = dYᵀ X and db = Σ_r dY.  The long reduction is
+//             cut into row slices (one workgroup per slice and 128 x 128
+//             output tile, partial tiles in a workspace) and the slices are
+//             summed in a fixed order by a second kernel: deterministic.
+// Every product is built from v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains,
+// 64 FLOP/clk/SIMD: the f32 matrix peak).  A 256-thread workgroup owns a
+// 128 x 128 output tile, each of its 4 waves a 64 x 64 quarter (2 x 2 MFMA
+// tiles, 64 accumulator registers); the k loop runs in chunks of 32 staged
+// through LDS with the next chunk's global loads in flight (in registers)
+// while the current chunk is multiplied.
+//
+// MFMA operand order: step s (0..3) of an 8-wide k sub-chunk takes, in lane
+// half h = lane >> 5, the k index 4h + s — both operands use the same
+// bijection, so the sum is unchanged — which lets a lane fetch its four
+// steps' operands with one 16-byte LDS read in gemm_nt.
+#include <algorithm>
+
+#include "common.h"
+
+namespace mirec {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int kTile = 128;   // output tile edge
+constexpr int kChunk = 32;   // k per LDS stage
+constexpr int kLdNT = kChunk + 4;   // gemm_nt LDS row stride [row][k]: 16-B reads, 4-bank groups
+constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two lane halves
+                                    // (k and k + 4) land 32 banks apart
+
+// ------------------------------------------------------------------ gemm_nt
+// Workgroup (tile_m, tile_n): rows [128 tile_m, +128) of C, columns
+// [128 tile_n, +128).  LDS: sA[128][36], sB[128][36] (k-contiguous rows).
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict__ A,
+                                                        const float *__restrict__ B,
+                                                        const float *__restrict__ bias,
+                                                        float *__restrict__ C, int64_t n,
+                                                        int Kr, int No) {
+  __shared__ __attribute__((aligned(16))) float sA[kTile * kLdNT];
+  __shared__ __attribute__((aligned(16))) float sB[kTile * kLdNT];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  // column tile fastest: the column tiles of one row tile run together and
+  // share its A rows through L2
+  const int ncol = No / kTile;
+  const int64_t m0 = (int64_t)(blockIdx.x / ncol) * kTile;
+  const int n0 = (int)(blockIdx.x % ncol) * kTile;
+  // global -> register staging: 4 float4 of A and of B per thread per chunk
+  // (element e = t + 256 q: row e >> 3, float4 column e & 7)
+  float4 ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int64_t row = m0 + r;
+      ra[q] = row < n ? ld4(A + row * Kr + k0 + 4 * c4) : f4_zero();
+      rb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      st4(sA + r * kLdNT + 4 * c4, ra[q]);
+      st4(sB + r * kLdNT + 4 * c4, rb[q]);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  load(0);
+  for (int k0 = 0; k0 < Kr; k0 += kChunk) {
+    __syncthreads();  // the previous chunk's LDS reads are done
+    stage();
+    __syncthreads();
+    if (k0 + kChunk < Kr) load(k0 + kChunk);  // in flight during the products
+#pragma unroll
+    for (int sub = 0; sub < kChunk / 8; ++sub) {
+      float4 fa[2], fb[2];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+        fa[tm] = ld4(sA + (wm * 64 + tm * 32 + i) * kLdNT + sub * 8 + 4 * h);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+        fb[tn] = ld4(sB + (wn * 64 + tn * 32 + i) * kLdNT + sub * 8 + 4 * h);
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          acc[tm][tn] = mfma32(fa[tm].x, fb[tn].x, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].y, fb[tn].y, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].z, fb[tn].z, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].w, fb[tn].w, acc[tm][tn]);
+        }
+    }
+  }
+  // C layout of 32x32: lane holds column i, rows (r & 3) + 8 (r >> 2) + 4 h
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) {
+    const int col = n0 + wn * 64 + tn * 32 + i;
+    const float bv = bias ? bias[col] : 0.f;
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * 64 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (row < n) C[row * No + col] = acc[tm][tn][r] + bv;
+      }
+  }
+}
+
+// ------------------------------------------------------------------ gemm_tn
+// Workgroup (slice s, tile_m, tile_n): partial C tile over rows
+// [s * rows_per_slice, +rows_per_slice) -> work[s][M][No]; with colsum, the
+// tile_n == 0 workgroups also write the slice's column sums of A ->
+// work_cs[s][M].  LDS: sA[32][136], sB[32][136] (k-major, as in memory).
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict__ A,
+                                                        const float *__restrict__ B,
+                                                        float *__restrict__ work,
+                                                        float *__restrict__ work_cs,
+                                                        int64_t n, int M, int No,
+                                                        int64_t rows_per_slice) {
+  __shared__ __attribute__((aligned(16))) float sA[kChunk * kLdTN];
+  __shared__ __attribute__((aligned(16))) float sB[kChunk * kLdTN];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int s = blockIdx.x;
+  const int m0 = blockIdx.y * kTile, n0 = blockIdx.z * kTile;
+  const int64_t r_beg = (int64_t)s * rows_per_slice;
+  const int64_t r_end = min(n, r_beg + rows_per_slice);
+  const bool do_cs = work_cs != nullptr && blockIdx.z == 0;
+  // element e = t + 256 q: chunk row e >> 5, float4 column e & 31
+  float4 ra[4], rb[4];
+  auto load = [&](int64_t r0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+      const int64_t r = r0 + kk;
+      const bool ok = r < r_end;
+      ra[q] = ok ? ld4(A + r * M + m0 + 4 * c4) : f4_zero();
+      rb[q] = ok ? ld4(B + r * No + n0 + 4 * c4) : f4_zero();
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+      st4(sA + kk * kLdTN + 4 * c4, ra[q]);
+      st4(sB + kk * kLdTN + 4 * c4, rb[q]);
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  float cs = 0.f;  // column sum of A (column m0 + t, threads t < 128)
+  if (r_beg < r_end) load(r_beg);
+  for (int64_t r0 = r_beg; r0 < r_end; r0 += kChunk) {
+    __syncthreads();
+    stage();
+    __syncthreads();
+    if (r0 + kChunk < r_end) load(r0 + kChunk);
+    if (do_cs && t < kTile) {
+#pragma unroll 8
+      for (int kk = 0; kk < kChunk; ++kk) cs += sA[kk * kLdTN + t];
+    }
+#pragma unroll
+    for (int sub = 0; sub < kChunk / 8; ++sub) {
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int kk = sub * 8 + 4 * h + st;
+        float fa[2], fb[2];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) fa[tm] = sA[kk * kLdTN + wm * 64 + tm * 32 + i];
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) fb[tn] = sB[kk * kLdTN + wn * 64 + tn * 32 + i];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma32(fa[tm], fb[tn], acc[tm][tn]);
+      }
+    }
+  }
+  float *out = work + (int64_t)s * M * No;
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) {
+    const int col = n0 + wn * 64 + tn * 32 + i;
+#pragma unroll
+    for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm * 64 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(int64_t)row * No + col] = acc[tm][tn][r];
+      }
+  }
+  if (do_cs && t < kTile) work_cs[(int64_t)s * M + m0 + t] = cs;
+}
+
+// C[e] = Σ_s work[s][e] (float4 e), colsum[m] = Σ_s work_cs[s][m].  A
+// 1024-thread block owns 64 float4 elements: wave g sums the slices s ≡ g
+// (mod 16) of its lane's element, then the 16 partials are added in wave
+// order through LDS (a fixed order: deterministic).  Block 0..M/64 also
+// reduce colsum the same way.
+constexpr int kRedGroups = 16;
+__global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__restrict__ work,
+                                                              const float *__restrict__ work_cs,
+                                                              float *__restrict__ C,
+                                                              float *__restrict__ colsum,
+                                                              int slices, int64_t n4, int M) {
+  __shared__ float4 part[kRedGroups][64];
+  __shared__ float pcs[kRedGroups][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  float4 a = f4_zero();
+  float c = 0.f;
+  if (e < n4) {
+#pragma unroll 4
+    for (int s = g; s < slices; s += kRedGroups) a = f4_add(a, ld4(work + ((int64_t)s * n4 + e) * 4));
+  }
+  const bool do_cs = colsum != nullptr && e < M;
+  if (do_cs) {
+    for (int s = g; s < slices; s += kRedGroups) c += work_cs[(int64_t)s * M + e];
+  }
+  part[g][lane] = a;
+  pcs[g][lane] = c;
+  __syncthreads();
+  if (g == 0) {
+    for (int q = 1; q < kRedGroups; ++q) {
+      a = f4_add(a, part[q][lane]);
+      c += pcs[q][lane];
+    }
+    if (e < n4) st4(C + e * 4, a);
+    if (do_cs) colsum[e] = c;
+  }
+}
+
+// Row slices of gemm_tn: enough workgroups to fill the chip twice over,
+// at least 256 rows (8 chunks) per slice.
+static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
+  const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
+  const int64_t want = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+  int64_t r = std::max<int64_t>(256, (n + want - 1) / want);
+  r = (r + kChunk - 1) / kChunk * kChunk;
+  *rows = r;
+  *slices = (int)std::max<int64_t>(1, (n + r - 1) / r);
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C,
+                             int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(n >= 0 && Kr > 0 && No > 0 && Kr % kChunk == 0 && No % kTile == 0);
+  if (n == 0) return MIREC_OK;  // (empty tensors may carry null pointers)
+  MIREC_CHECK_ARG(A && B && C && ((uintptr_t)A | (uintptr_t)B) % 16 == 0);
+  const dim3 grid((unsigned)(((n + kTile - 1) / kTile) * (No / kTile)));
+  hipLaunchKernelGGL(gemm_nt_kernel, grid, dim3(256), 0, (hipStream_t)stream, A, B, bias, C, n,
+                     (int)Kr, (int)No);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No) {
+  if (n < 0 || M <= 0 || No <= 0 || M % kTile || No % kTile) return -1;
+  int slices;
+  int64_t rows;
+  tn_slices(std::max<int64_t>(n, 1), M, No, &slices, &rows);
+  return (int64_t)slices * M * No + (int64_t)slices * M;
+}
+
+extern "C" int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n,
+                             int32_t M, int32_t No, float *work, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(C && work && n >= 0 && M > 0 && No > 0 && M % kTile == 0 && No % kTile == 0);
+  MIREC_CHECK_ARG(n == 0 || (A && B));  // (empty tensors may carry null pointers)
+  MIREC_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)work) % 16 == 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    MIREC_HIP(hipMemsetAsync(C, 0, sizeof(float) * M * No, st));
+    if (colsum) MIREC_HIP(hipMemsetAsync(colsum, 0, sizeof(float) * M, st));
+    return MIREC_OK;
+  }
+  int slices;
+  int64_t rows;
+  tn_slices(n, M, No, &slices, &rows);
+  float *work_cs = work + (int64_t)slices * M * No;
+  const dim3 grid((unsigned)slices, (unsigned)(M / kTile), (unsigned)(No / kTile));
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, st, A, B, work,
+                     colsum ? work_cs : nullptr, n, (int)M, (int)No, rows);
+  MIREC_LAUNCH_CHECK();
+  const int64_t n4 = (int64_t)M * No / 4;
+  const int64_t blocks = (std::max<int64_t>(n4, M) + 63) / 64;
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3((unsigned)blocks), dim3(1024), 0, st, work,
+                     work_cs, C, colsum, slices, n4, (int)M);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

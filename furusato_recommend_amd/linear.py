@@ -1,27 +1,80 @@
-"""nn.Linear with a split-K weight gradient.
+"""nn.Linear on token rows: f32 MFMA GEMMs (csrc/gemm.hip) for the forward,
+the input gradient and the weight + bias gradient.
 
-On the packed SASRec / GraphSAGE activations (tens of thousands of rows,
-d = 128) the library GEMM for dW = dYᵀ X (a reduction over every row) runs
-at ~20 TFLOP/s f32, 4x below the forward GEMMs of the same size: the
-reduction dimension is the long one.  Cutting the rows into 32 slices, one
-batched GEMM over the slices and a sum of the 32 partial [N, K] products
-runs at 60-85 TFLOP/s (measured on MI355X, tools/gemm_forms.py).  Same
-parameters and state_dict keys as nn.Linear; the forward is unchanged.
+The packed SASRec / GraphSAGE activations are tall and thin (tens of
+thousands of rows x d = 128..384).  mirec_gemm_nt computes y = x Wᵀ + b and
+dX = dY W (B = Wᵀ, a copy of the small weight); mirec_gemm_tn computes
+dW = dYᵀ X and db = Σ dY in one pass over dY, cutting the long row reduction
+into slices summed in a fixed order.  Shapes the kernels do not take (a
+width not a multiple of 32 / 128) go to torch's GEMMs, where the weight
+gradient is split over 32 row slices (one batched GEMM + a sum): the
+library GEMM for dYᵀ X runs ~4x below its forward rate when the reduction
+dimension is the long one (tools/gemm_forms.py).  Same parameters and
+state_dict keys as nn.Linear.
 """
 from __future__ import annotations
 
 import contextlib
+import os
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from . import _lib
+from ._lib import check, lib
+
 SPLIT = 32
 MIN_ROWS_PER_SLICE = 256
+# MIREC_GEMM=0 routes every Linear through torch's GEMMs (A/B timing)
+USE_MIREC_GEMM = os.environ.get("MIREC_GEMM", "1") != "0"
+FORCE_MIREC_GEMM = False  # tests: every eligible shape on the mirec kernels
+
+
+def _aligned(*ts) -> bool:
+    return all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+               and t.data_ptr() % 16 == 0 for t in ts)
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None):
+    """a [n, Kr] · b[No, Kr]ᵀ (+ bias) on mirec_gemm_nt, or None if the
+    shapes are not the kernel's (Kr % 32, No % 128)."""
+    n, kr = a.shape
+    no = b.shape[0]
+    if not (USE_MIREC_GEMM and kr % 32 == 0 and no % 128 == 0 and b.shape[1] == kr
+            and _aligned(a, b) and (bias is None or _aligned(bias))):
+        return None
+    if kr <= 128 and no > 128 and not FORCE_MIREC_GEMM:
+        # short reduction, wide output (the QKV projection): hipBLASLt's
+        # kernel is faster there (62 vs 76 us at 56K x 128 x 384,
+        # tools/gemm_forms.py); every other Linear shape runs faster here
+        return None
+    c = torch.empty(n, no, dtype=a.dtype, device=a.device)
+    check(lib.mirec_gemm_nt(a.data_ptr(), b.data_ptr(), 0 if bias is None else bias.data_ptr(),
+                            c.data_ptr(), n, kr, no, _lib.stream_handle()), "gemm_nt")
+    return c
+
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, colsum: bool):
+    """(a[n, M]ᵀ b[n, No], Σ_rows a or None) on mirec_gemm_tn, or None if
+    the shapes are not the kernel's (M % 128, No % 128)."""
+    n, m = a.shape
+    no = b.shape[1]
+    if not (USE_MIREC_GEMM and m % 128 == 0 and no % 128 == 0 and b.shape[0] == n
+            and _aligned(a, b)):
+        return None
+    c = torch.empty(m, no, dtype=a.dtype, device=a.device)
+    cs = torch.empty(m, dtype=a.dtype, device=a.device) if colsum else None
+    work = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, m, no)), dtype=a.dtype,
+                       device=a.device)
+    check(lib.mirec_gemm_tn(a.data_ptr(), b.data_ptr(), c.data_ptr(),
+                            0 if cs is None else cs.data_ptr(), n, m, no, work.data_ptr(),
+                            _lib.stream_handle()), "gemm_tn")
+    return c, cs
 
 
 def weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dyᵀ x for dy [n, N], x [n, K] (contiguous rows)."""
+    """dyᵀ x for dy [n, N], x [n, K] (contiguous rows), torch GEMMs."""
     n = dy.shape[0]
     if n < SPLIT * MIN_ROWS_PER_SLICE:
         return dy.t() @ x
@@ -39,17 +92,32 @@ class _LinearSplitK(torch.autograd.Function):
     def forward(ctx, x, w, b):
         ctx.save_for_backward(x, w)
         ctx.has_bias = b is not None
-        return F.linear(x, w, b)
+        x2 = x.reshape(-1, x.shape[-1])
+        y = gemm_nt(x2, w, b) if x2.is_contiguous() else None
+        if y is None:
+            return F.linear(x, w, b)
+        return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
         x, w = ctx.saved_tensors
         shape = x.shape
-        x2 = x.reshape(-1, shape[-1])
+        x2 = x.reshape(-1, shape[-1]).contiguous()
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        dx = (dy2 @ w).view(shape) if ctx.needs_input_grad[0] else None
-        dw = weight_grad(dy2, x2.contiguous()) if ctx.needs_input_grad[1] else None
-        db = dy2.sum(0) if (ctx.has_bias and ctx.needs_input_grad[2]) else None
+        need = ctx.needs_input_grad
+        dx = dw = db = None
+        if need[0]:
+            dx = gemm_nt(dy2, w.t().contiguous())
+            dx = (dy2 @ w if dx is None else dx).view(shape)
+        want_db = ctx.has_bias and need[2]
+        if need[1]:
+            r = gemm_tn(dy2, x2, want_db)
+            if r is None:
+                dw = weight_grad(dy2, x2)
+            else:
+                dw, db = r
+        if want_db and db is None:
+            db = dy2.sum(0)
         return dx, dw, db
 
 

@@ -445,6 +445,24 @@ int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int3
                                  const int64_t *bucket_end, int32_t heads, int32_t head_dim,
                                  float *dqkv, mirec_stream_t stream);
 
+/* f32 MFMA GEMMs of the Linear layers on token rows (model/sasrec.py:385-421,
+ * model/graphsage.py:311-324).  Row-major, device pointers, 16-byte aligned.
+ *
+ * C[n, No] = A[n, Kr] · B[No, Kr]ᵀ (+ bias[No] if bias != NULL): the forward
+ * y = x Wᵀ + b, and the input gradient dX = dY W with B = Wᵀ (a [K, N] copy
+ * of the weight).  Kr % 32 == 0, No % 128 == 0. */
+int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C, int64_t n,
+                  int32_t Kr, int32_t No, mirec_stream_t stream);
+
+/* C[M, No] = A[n, M]ᵀ · B[n, No] summed over the n rows, and (if colsum !=
+ * NULL) colsum[M] = Σ_rows A: the weight gradient dW = dYᵀ X and the bias
+ * gradient db = Σ dY in one pass over dY.  M % 128 == 0, No % 128 == 0;
+ * work: mirec_gemm_tn_work_floats(n, M, No) floats (per-slice partial
+ * sums, added in a fixed order: deterministic). */
+int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No);
+int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n, int32_t M,
+                  int32_t No, float *work, mirec_stream_t stream);
+
 /* Row tail of the SASRec block (model/sasrec.py:385-397 — the dropout,
  * residual add, ReLU and LayerNorm around the attention and the FFN), one
  * pass over the n x d token rows (d % 4 == 0, 4 <= d <= 1024):

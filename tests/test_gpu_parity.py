@@ -1236,3 +1236,63 @@ def test_sasrec_graph_step_equals_eager():
     losses = [float(c.stageOne(users, pos, neg)) for _ in range(30)]
     assert len(set(losses[:5])) == 5
     assert np.mean(losses[-5:]) < np.mean(losses[:5])
+
+
+@pytest.mark.parametrize("n,kr,no", [(1, 32, 128), (100, 128, 128), (4096, 128, 384),
+                                     (56_321, 128, 384), (3000, 384, 128), (777, 256, 256)])
+def test_gemm_nt_matches_fp64(n, kr, no):
+    """mirec_gemm_nt (the Linear forward / input-gradient GEMM) vs a float64
+    reference, ragged row counts, with and without bias."""
+    from furusato_recommend_amd import linear as LN
+    from furusato_recommend_amd.linear import gemm_nt
+    LN.FORCE_MIREC_GEMM = True
+    torch.manual_seed(n)
+    a = torch.randn(n, kr, device="cuda")
+    b = torch.randn(no, kr, device="cuda")
+    bias = torch.randn(no, device="cuda")
+    for bb in (None, bias):
+        c = gemm_nt(a, b, bb)
+        ref = a.double() @ b.double().t() + (0 if bb is None else bb.double())
+        assert c is not None and rel(c, ref) < 1e-6
+    LN.FORCE_MIREC_GEMM = False
+
+
+@pytest.mark.parametrize("n,m,no", [(0, 128, 128), (1, 128, 128), (100, 384, 128),
+                                    (56_321, 384, 128), (9000, 128, 256), (33, 256, 384)])
+def test_gemm_tn_matches_fp64(n, m, no):
+    """mirec_gemm_tn (dW = dYᵀ X and db = Σ dY, sliced rows summed in a fixed
+    order) vs float64, ragged and empty row counts; bitwise deterministic."""
+    from furusato_recommend_amd.linear import gemm_tn
+    torch.manual_seed(n + m)
+    a = torch.randn(n, m, device="cuda")
+    b = torch.randn(n, no, device="cuda")
+    c, cs = gemm_tn(a, b, True)
+    if n == 0:
+        assert float(c.abs().max()) == 0.0 and float(cs.abs().max()) == 0.0
+        return
+    ref = a.double().t() @ b.double()
+    assert rel(c, ref) < 1e-6
+    assert rel(cs, a.double().sum(0)) < 1e-6
+    c2, cs2 = gemm_tn(a, b, True)
+    assert torch.equal(c, c2) and torch.equal(cs, cs2)
+
+
+def test_linear_on_mirec_gemms_matches_torch():
+    """Linear (mirec GEMMs) == F.linear: output, input / weight / bias
+    gradients, token-row shapes of the SASRec block and odd widths that fall
+    back to torch."""
+    import torch.nn.functional as F
+
+    from furusato_recommend_amd.linear import Linear
+    torch.manual_seed(8)
+    for n, k, nout in ((56_320, 128, 384), (4096, 128, 128), (5000, 256, 128), (300, 48, 20)):
+        lin = Linear(k, nout, device="cuda")
+        x = torch.randn(n, k, device="cuda", requires_grad=True)
+        y = lin(x)
+        yr = F.linear(x, lin.weight, lin.bias)
+        assert rel(y, yr) < 1e-5
+        g = torch.randn_like(y)
+        g1 = torch.autograd.grad(y, [x, lin.weight, lin.bias], g)
+        g2 = torch.autograd.grad(yr, [x, lin.weight, lin.bias], g)
+        for a, b in zip(g1, g2):
+            assert rel(a, b) < 1e-5

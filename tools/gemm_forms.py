@@ -1,8 +1,12 @@
 """SASRec Linear GEMMs (f32): device time of equivalent formulations and the
 host-side cost per call of each BLAS backend torch can use on ROCm."""
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def t(fn, reps=20):
@@ -36,6 +40,23 @@ def main():
     b = torch.randn(N, device="cuda")
     dy = torch.randn(n, N, device="cuda")
     xs, ws = torch.randn(64, K, device="cuda"), torch.randn(N, K, device="cuda")
+    from furusato_recommend_amd.linear import gemm_nt, gemm_tn
+    wt = w.t().contiguous()
+    for (nn_, kk, NN) in ((n, K, N), (n, K, K)):
+        xa, wa, ba = torch.randn(nn_, kk, device="cuda"), torch.randn(NN, kk, device="cuda"), \
+            torch.randn(NN, device="cuda")
+        dya = torch.randn(nn_, NN, device="cuda")
+        wta = wa.t().contiguous()
+        fl = 2.0 * nn_ * kk * NN
+        r = {"fwd": t(lambda: gemm_nt(xa, wa, ba)), "dX": t(lambda: gemm_nt(dya, wta)),
+             "dW+db": t(lambda: gemm_tn(dya, xa, True)),
+             "torch fwd": t(lambda: torch.addmm(ba, xa, wa.t())),
+             "torch dX": t(lambda: dya @ wa),
+             "torch dW split32 + db": t(lambda: (torch.bmm(
+                 dya.view(32, nn_ // 32, NN).transpose(1, 2), xa.view(32, nn_ // 32, kk)).sum(0),
+                 dya.sum(0)))}
+        print(f"mirec gemm n={nn_} K={kk} N={NN}:",
+              {k_: f"{v:.1f} us {fl / v / 1e6:.0f} TF/s" for k_, v in r.items()}, flush=True)
     for lib in ("default", "cublaslt", "cublas"):
         try:
             if lib != "default":
