@@ -143,6 +143,10 @@ SIGNATURES = {
                                   c_int32, c_int32, c_float, c_uint64, c_void_p, c_float,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mirec_resnorm_work_floats": (c_int64, [c_int64, c_int32]),
+    "mirec_segment_mean": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
+                                   c_void_p]),
+    "mirec_segment_mean_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
+                                       c_void_p, c_void_p]),
     "mirec_gemm_nt": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p]),
     "mirec_gemm_tn_work_floats": (c_int64, [c_int64, c_int32, c_int32]),

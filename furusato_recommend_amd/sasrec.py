@@ -84,6 +84,7 @@ class Packing(NamedTuple):
     offsets: torch.Tensor
     bucket_end: tuple | None = None
     padded: bool = False  # rows past offsets[B] belong to no sequence (capacity padding)
+    order: torch.Tensor | None = None  # caller position of each packed sequence (None: same)
 
 
 class _CausalAttentionVarlen(torch.autograd.Function):
@@ -155,6 +156,34 @@ def length_buckets(lengths) -> tuple[np.ndarray, tuple]:
 
 def _ptr(t):
     return 0 if t is None else t.data_ptr()
+
+
+class _SegmentMean(torch.autograd.Function):
+    """Mean of the packed rows of each sequence (mirec_segment_mean): x
+    [n, d], int32 offsets [B+1], int64 seg [n] (the sequence of every row, B
+    for padding), int64 length [B] (the divisor, sasrec.py:412)."""
+
+    @staticmethod
+    def forward(ctx, x, offsets, seg, length):
+        x = x.contiguous()
+        B, d = length.numel(), x.shape[1]
+        out = torch.empty(B, d, dtype=x.dtype, device=x.device)
+        check(lib.mirec_segment_mean(x.data_ptr(), offsets.data_ptr(), length.data_ptr(), B, d,
+                                     out.data_ptr(), _lib.stream_handle()), "segment_mean")
+        ctx.save_for_backward(seg, length)
+        ctx.n = x.shape[0]
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        seg, length = ctx.saved_tensors
+        g = g.contiguous()
+        B, d = g.shape
+        gx = torch.empty(ctx.n, d, dtype=g.dtype, device=g.device)
+        check(lib.mirec_segment_mean_bwd(g.data_ptr(), seg.data_ptr(), length.data_ptr(), ctx.n,
+                                         B, d, gx.data_ptr(), _lib.stream_handle()),
+              "segment_mean_bwd")
+        return gx, None, None, None
 
 
 # Device uint64 [1] mixed into every dropout mask key while a step is being
@@ -394,15 +423,16 @@ class SASRec(nn.Module):
 
     def forward_user_packed(self, x, offsets, seg, length):
         """forward_user on packed sequences: x [n_tok, d], ``seg`` [n_tok]
-        the sequence of every row (B for capacity padding rows, which the
-        pool drops).  Padding positions never reach a real position under
+        the packed sequence of every row (B for capacity padding rows, which
+        the pool drops), ``length`` [B] in packed order.  Padding positions never reach a real position under
         the causal mask and are excluded from the pool, so this equals
         forward_user on the padded batch while skipping them."""
         x = self.blocks(x, offsets)
-        B = length.numel()
-        pooled = torch.zeros(B + 1, x.shape[1], dtype=x.dtype, device=x.device)
-        pooled = pooled.index_add(0, seg, x)[:B]
-        return pooled / length.to(x.dtype).unsqueeze(1)
+        packed = isinstance(offsets, Packing)
+        pooled = _SegmentMean.apply(x, offsets.offsets if packed else offsets, seg, length)
+        if packed and offsets.order is not None:  # back to the caller's order
+            pooled = torch.empty_like(pooled).index_copy(0, offsets.order, pooled)
+        return pooled
 
     def packed_input(self, users):
         """(x [n_tok, d], packing, seg [n_tok], length [B]) of the users'
@@ -414,11 +444,12 @@ class SASRec(nn.Module):
     def packed_ids(self, users):
         """packed_input's item ids [n_tok] (int32) instead of their rows.
 
-        The sequences are packed in length-bucket order (ceil(len/16) = 1..4,
-        stable), so each bucket's attention runs on a workgroup sized for it
-        (Packing.bucket_end); ``seg`` maps every packed row to its sequence's
-        position in ``users`` and ``length`` follows ``users``, so the pooled
-        user embeddings come out in the caller's order."""
+        With config "attn_buckets" the sequences are packed in length-bucket
+        order (ceil(len/16) = 1..4, stable), so each bucket's attention runs
+        on a workgroup sized for it (Packing.bucket_end, Packing.order = the
+        user position of every packed sequence); ``seg`` (the packed sequence
+        of every row) and ``length`` follow the packed order, and
+        forward_user_packed returns the users in the caller's order."""
         if torch.is_tensor(users) and users.is_cuda:
             u_host = users.cpu().numpy()
         else:
@@ -426,21 +457,22 @@ class SASRec(nn.Module):
         B = len(u_host)
         lens_h = self.seq.length_host[u_host]
         n_tok = int(lens_h.sum())
-        order, bucket_end = length_buckets(lens_h)
         dev = self.device
-        up = self._upload(np.concatenate([u_host, order]))
-        u, perm = up[:B], up[B:]
-        u_p = u[perm]
+        if self.config.get("attn_buckets", False):
+            order, bucket_end = length_buckets(lens_h)
+            up = self._upload(np.concatenate([u_host, order]))
+            perm = up[B:]
+            u_p = up[:B][perm]
+        else:  # default: one 64-row bucket, users in the caller's order
+            bucket_end = perm = None
+            u_p = self._upload(u_host)
         length_p = self.seq.length[u_p]
         offsets = torch.zeros(B + 1, dtype=torch.int32, device=dev)
         offsets[1:] = torch.cumsum(length_p, 0).to(torch.int32)
-        seg_p = torch.repeat_interleave(torch.arange(B, device=dev), length_p,
-                                        output_size=n_tok)
-        pos = torch.arange(n_tok, device=dev) - offsets[seg_p].long()
-        ids = self.seq.items[u_p[seg_p], pos]
-        if not self.config.get("attn_buckets", False):  # default: one 64-row bucket
-            bucket_end = None
-        return ids, Packing(offsets, bucket_end), perm[seg_p], self.seq.length[u]
+        seg = torch.repeat_interleave(torch.arange(B, device=dev), length_p, output_size=n_tok)
+        pos = torch.arange(n_tok, device=dev) - offsets[seg].long()
+        ids = self.seq.items[u_p[seg], pos]
+        return ids, Packing(offsets, bucket_end, False, perm), seg, length_p
 
     def _upload(self, host_ids) -> torch.Tensor:
         """int64 host ids -> device without a stream sync: a pageable H2D copy

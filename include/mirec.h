@@ -445,6 +445,17 @@ int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int3
                                  const int64_t *bucket_end, int32_t heads, int32_t head_dim,
                                  float *dqkv, mirec_stream_t stream);
 
+/* Masked mean pool of the SASRec user tower (model/sasrec.py:399-413) on
+ * packed sequences: out[b] = Σ_{r in [offsets[b], offsets[b+1])} x[r] /
+ * length[b] (rows summed in order), x [n, d], out [B, d], d % 4 == 0,
+ * d <= 1024.  Backward: grad_x[t] = grad_out[seg[t]] / length[seg[t]] for
+ * the n_rows rows (0 where seg[t] is outside [0, B): capacity padding). */
+int mirec_segment_mean(const float *x, const int32_t *offsets, const int64_t *length, int64_t B,
+                       int32_t d, float *out, mirec_stream_t stream);
+int mirec_segment_mean_bwd(const float *grad_out, const int64_t *seg, const int64_t *length,
+                           int64_t n_rows, int64_t B, int32_t d, float *grad_x,
+                           mirec_stream_t stream);
+
 /* f32 MFMA GEMMs of the Linear layers on token rows (model/sasrec.py:385-421,
  * model/graphsage.py:311-324).  Row-major, device pointers, 16-byte aligned.
  *

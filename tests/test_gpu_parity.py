@@ -792,20 +792,23 @@ def test_sasrec_packed_path_equals_padded():
     m = SASRec({"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
                 "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0}, ds)
     u_h = np.random.default_rng(0).integers(0, 600, 128)
-    x, offs, seg, length = m.packed_input(u_h)
-    up = m.forward_user_packed(x, offs, seg, length)
-    xp, lp = m.sequence_input(torch.as_tensor(u_h, device="cuda"))
-    ud = m.forward_user(xp, lp)
-    assert rel(up, ud) < TOL
-    w = torch.randn_like(up)
-    params = [p for p in m.parameters() if p.requires_grad]
-    g1 = torch.autograd.grad((up * w).sum(), params, allow_unused=True)
-    g2 = torch.autograd.grad((ud * w).sum(), params, allow_unused=True)
-    for a, b in zip(g1, g2):
-        if b is None:
-            assert a is None or float(a.abs().max()) == 0.0
-        else:
-            assert rel(a, b) < TOL
+    for buckets in (False, True):  # caller order / length-bucket order
+        m.config["attn_buckets"] = buckets
+        x, offs, seg, length = m.packed_input(u_h)
+        assert (offs.order is not None) == buckets
+        up = m.forward_user_packed(x, offs, seg, length)
+        xp, lp = m.sequence_input(torch.as_tensor(u_h, device="cuda"))
+        ud = m.forward_user(xp, lp)
+        assert rel(up, ud) < TOL
+        w = torch.randn_like(up)
+        params = [p for p in m.parameters() if p.requires_grad]
+        g1 = torch.autograd.grad((up * w).sum(), params, allow_unused=True)
+        g2 = torch.autograd.grad((ud * w).sum(), params, allow_unused=True)
+        for a, b in zip(g1, g2):
+            if b is None:
+                assert a is None or float(a.abs().max()) == 0.0
+            else:
+                assert rel(a, b) < TOL
 
 
 @pytest.mark.parametrize("d", [4, 12, 36, 64, 128, 256, 1024])
@@ -1224,8 +1227,10 @@ def test_sasrec_graph_step_equals_eager():
         assert abs(la - lb) <= 1e-5 * abs(lb), (it, la, lb)
         if it == 0:
             for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+                # (item_last_proj.bias has an exactly-zero gradient: the bias
+                # cancels in pos - neg; both sides hold ~1e-9 rounding noise)
                 scale = float(pb.grad.abs().max())
-                assert float((pa.grad - pb.grad).abs().max()) <= TOL * max(scale, 1e-4), name
+                assert float((pa.grad - pb.grad).abs().max()) <= TOL * max(scale, 1e-3), name
     assert len(a._graphs) >= 1 and not getattr(b, "_graphs", None)
     # dropout on: same batch twice -> different losses (fresh masks), and
     # repeated steps on one batch lower its loss
@@ -1296,3 +1301,37 @@ def test_linear_on_mirec_gemms_matches_torch():
         g2 = torch.autograd.grad(yr, [x, lin.weight, lin.bias], g)
         for a, b in zip(g1, g2):
             assert rel(a, b) < 1e-5
+
+
+def test_segment_mean_pool_and_backward():
+    """mirec_segment_mean (the packed masked-mean pool) == per-sequence means
+    in float64, empty sequences give 0/0 like the reference's division, and
+    the backward spreads grad / length over each sequence's rows with zero on
+    padding rows (seg == B)."""
+    from furusato_recommend_amd.sasrec import _SegmentMean
+    torch.manual_seed(12)
+    lens = torch.tensor([3, 1, 64, 0, 17, 50], device="cuda")
+    B, d = lens.numel(), 128
+    offsets = torch.zeros(B + 1, dtype=torch.int32, device="cuda")
+    offsets[1:] = torch.cumsum(lens, 0).int()
+    n_tok = int(lens.sum())
+    pad = 7
+    x = torch.randn(n_tok + pad, d, device="cuda", requires_grad=True)
+    seg = torch.cat([torch.repeat_interleave(torch.arange(B, device="cuda"), lens),
+                     torch.full((pad,), B, device="cuda")])
+    out = _SegmentMean.apply(x, offsets, seg, lens)
+    xd = x.detach().double()
+    for b in range(B):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        if e > s:
+            assert rel(out[b], xd[s:e].mean(0)) < 1e-6
+        else:
+            assert torch.isnan(out[b]).all()
+    g = torch.randn(B, d, device="cuda")
+    g[3] = 0  # the empty sequence has no rows to receive its gradient
+    gx, = torch.autograd.grad(out, x, g)
+    ref = torch.zeros_like(gx)
+    for b in range(B):
+        s, e = int(offsets[b]), int(offsets[b + 1])
+        ref[s:e] = g[b] / max(e - s, 1)
+    assert rel(gx, ref) < 1e-6 and float(gx[n_tok:].abs().max()) == 0.0
