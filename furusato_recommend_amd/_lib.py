@@ -147,6 +147,7 @@ SIGNATURES = {
                                    c_void_p]),
     "mirec_segment_mean_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                        c_void_p, c_void_p]),
+    "mirec_zero_tail_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
     "mirec_gemm_nt": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p]),
     "mirec_gemm_tn_work_floats": (c_int64, [c_int64, c_int32, c_int32]),

@@ -45,9 +45,33 @@ __global__ __launch_bounds__(256) void segment_mean_bwd_kernel(const float *__re
   st4(gx + t * d + c, v);
 }
 
+// Zero rows [offsets[B], n_rows) of a [n_rows, row_floats] buffer: the
+// capacity-padding rows the packed kernels leave unwritten.
+__global__ __launch_bounds__(256) void zero_tail_rows_kernel(float *__restrict__ buf,
+                                                             const int32_t *__restrict__ offsets,
+                                                             int64_t B, int64_t n_rows,
+                                                             int32_t row_floats) {
+  const int64_t r0 = offsets[B];
+  const int64_t total = (n_rows - r0) * row_floats;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x)
+    buf[r0 * row_floats + e] = 0.f;
+}
+
 }  // namespace mirec
 
 using namespace mirec;
+
+extern "C" int mirec_zero_tail_rows(float *buf, const int32_t *offsets, int64_t B, int64_t n_rows,
+                                    int32_t row_floats, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(B >= 0 && n_rows >= 0 && row_floats > 0);
+  if (n_rows == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(buf && offsets);
+  hipLaunchKernelGGL(zero_tail_rows_kernel, dim3(256), dim3(256), 0, (hipStream_t)stream, buf,
+                     offsets, B, n_rows, row_floats);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
 
 extern "C" int mirec_segment_mean(const float *x, const int32_t *offsets, const int64_t *length,
                                   int64_t B, int32_t d, float *out, mirec_stream_t stream) {

@@ -98,10 +98,9 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         d = d3 // 3
         B = offsets.numel() - 1
         qkv = qkv.contiguous()
-        # rows outside every sequence (capacity padding) are not written by
-        # the kernels: zero them so they stay finite downstream
-        alloc = torch.zeros if padded else torch.empty
-        out = alloc(n, d, dtype=qkv.dtype, device=qkv.device)
+        out = torch.empty(n, d, dtype=qkv.dtype, device=qkv.device)
+        if padded:  # rows outside every sequence: not written by the kernels
+            _zero_tail(out, offsets)
         if bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_fwd(  # noqa: E731
                 qkv.data_ptr(), offsets.data_ptr(), B, heads, d // heads, out.data_ptr(),
@@ -124,7 +123,9 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         n, d3 = qkv.shape
         B = offsets.numel() - 1
         dh = d3 // 3 // ctx.heads
-        dqkv = torch.zeros_like(qkv) if ctx.padded else torch.empty_like(qkv)
+        dqkv = torch.empty_like(qkv)
+        if ctx.padded:
+            _zero_tail(dqkv, offsets)
         dout = dout.contiguous()
         if ctx.bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_bwd(  # noqa: E731
@@ -137,6 +138,14 @@ class _CausalAttentionVarlen(torch.autograd.Function):
                 dqkv.data_ptr(), _lib.stream_handle()), "attention_bucketed_bwd")
         _timed("bwd", (B, -1, ctx.heads, dh), launch, offsets)
         return dqkv, None, None, None, None
+
+
+def _zero_tail(buf, offsets):
+    """Zero the rows of buf past the last sequence (capacity padding) so
+    they stay finite downstream (mirec_zero_tail_rows)."""
+    check(lib.mirec_zero_tail_rows(buf.data_ptr(), offsets.data_ptr(), offsets.numel() - 1,
+                                   buf.shape[0], buf.shape[1], _lib.stream_handle()),
+          "zero_tail_rows")
 
 
 def _bucket_array(bucket_end, batch: int):

@@ -456,6 +456,12 @@ int mirec_segment_mean_bwd(const float *grad_out, const int64_t *seg, const int6
                            int64_t n_rows, int64_t B, int32_t d, float *grad_x,
                            mirec_stream_t stream);
 
+/* Zero rows [offsets[B], n_rows) of buf [n_rows, row_floats] (offsets on the
+ * device): the capacity-padding rows of a packed batch, which the packed
+ * attention kernels do not write. */
+int mirec_zero_tail_rows(float *buf, const int32_t *offsets, int64_t B, int64_t n_rows,
+                         int32_t row_floats, mirec_stream_t stream);
+
 /* f32 MFMA GEMMs of the Linear layers on token rows (model/sasrec.py:385-421,
  * model/graphsage.py:311-324).  Row-major, device pointers, 16-byte aligned.
  *
