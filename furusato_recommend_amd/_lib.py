@@ -147,6 +147,11 @@ SIGNATURES = {
                                    c_void_p]),
     "mirec_segment_mean_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int32,
                                        c_void_p, c_void_p]),
+    "mirec_bpr_rows_loss": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
+                                    c_float, c_void_p, c_void_p, c_void_p]),
+    "mirec_bpr_rows_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                        c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
     "mirec_zero_tail_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
     "mirec_gemm_nt": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p]),

@@ -58,9 +58,104 @@ __global__ __launch_bounds__(256) void zero_tail_rows_kernel(float *__restrict__
     buf[r0 * row_floats + e] = 0.f;
 }
 
+// BPR loss on embedding rows (model/sasrec.py:423-435): x_r = <u_r, n_r> -
+// <u_r, p_r>, loss = mean_r softplus(x_r) + coef * extra[0] (extra: the
+// embedding-norm term, or NULL).  Pass 1: one wave per row writes x_r and
+// softplus(x_r) (torch's: beta 1, threshold 20); pass 2: one workgroup adds
+// the B terms in a fixed order (deterministic).
+__device__ __forceinline__ float softplus20(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+__global__ __launch_bounds__(256) void bpr_rows_kernel(const float *__restrict__ u,
+                                                       const float *__restrict__ p,
+                                                       const float *__restrict__ n, int64_t B,
+                                                       int32_t d, float *__restrict__ x_out,
+                                                       float *__restrict__ sp_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= B) return;
+  float sp = 0.f, sn = 0.f;
+  for (int c = lane; c < d; c += 64) {
+    const float uv = u[r * d + c];
+    sp += uv * p[r * d + c];
+    sn += uv * n[r * d + c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sp += __shfl_xor(sp, o);
+    sn += __shfl_xor(sn, o);
+  }
+  if (lane == 0) {
+    const float x = sn - sp;
+    x_out[r] = x;
+    sp_out[r] = softplus20(x);
+  }
+}
+
+__global__ __launch_bounds__(1024) void bpr_rows_sum_kernel(const float *__restrict__ sp,
+                                                            int64_t B,
+                                                            const float *__restrict__ extra,
+                                                            float coef, float *__restrict__ loss) {
+  __shared__ float part[1024];
+  float a = 0.f;
+  for (int64_t r = threadIdx.x; r < B; r += 1024) a += sp[r];
+  part[threadIdx.x] = a;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) part[threadIdx.x] += part[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) loss[0] = part[0] / (float)B + (extra ? coef * extra[0] : 0.f);
+}
+
+// s_r = g * sigmoid(x_r) / B;  du = s (n - p), dp = -s u, dn = s u;
+// g_extra = g * coef.
+__global__ __launch_bounds__(256) void bpr_rows_loss_bwd_kernel(
+    const float *__restrict__ u, const float *__restrict__ p, const float *__restrict__ n,
+    const float *__restrict__ x, int64_t B, int32_t d, const float *__restrict__ g_loss,
+    float coef, float *__restrict__ du, float *__restrict__ dp, float *__restrict__ dn,
+    float *__restrict__ g_extra) {
+  const float g = g_loss[0];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0 && g_extra) g_extra[0] = g * coef;
+  if (e >= B * d) return;
+  const int64_t r = e / d;
+  const float s = g / (1.f + expf(-x[r])) / (float)B;
+  const float uv = u[e], pv = p[e], nv = n[e];
+  du[e] = s * (nv - pv);
+  dp[e] = -s * uv;
+  dn[e] = s * uv;
+}
+
 }  // namespace mirec
 
 using namespace mirec;
+
+extern "C" int mirec_bpr_rows_loss(const float *u, const float *p, const float *n, int64_t B,
+                                   int32_t d, const float *extra, float coef, float *x_out,
+                                   float *loss, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(B > 0 && d > 0 && u && p && n && x_out && loss);
+  hipStream_t st = (hipStream_t)stream;
+  // x_out holds 2B floats: x, then the per-row softplus terms
+  hipLaunchKernelGGL(bpr_rows_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, u, p, n, B,
+                     d, x_out, x_out + B);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bpr_rows_sum_kernel, dim3(1), dim3(1024), 0, st, x_out + B, B, extra, coef,
+                     loss);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_bpr_rows_loss_bwd(const float *u, const float *p, const float *n,
+                                       const float *x, int64_t B, int32_t d, const float *g_loss,
+                                       float coef, float *du, float *dp, float *dn,
+                                       float *g_extra, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(B > 0 && d > 0 && u && p && n && x && g_loss && du && dp && dn);
+  const int64_t total = B * d;
+  hipLaunchKernelGGL(bpr_rows_loss_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, u, p, n, x, B, d, g_loss, coef, du, dp, dn, g_extra);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
 
 extern "C" int mirec_zero_tail_rows(float *buf, const int32_t *offsets, int64_t B, int64_t n_rows,
                                     int32_t row_floats, mirec_stream_t stream) {

@@ -43,3 +43,45 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     flat = ids.reshape(-1).to(torch.int32).contiguous()
     out = _GatherRows.apply(table.contiguous(), flat)
     return out.view(*ids.shape, table.shape[1])
+
+
+class _GatherRowsNorm(torch.autograd.Function):
+    """(table[ids], ‖table‖₂) as one autograd node: the embedding lookup and
+    the embedding-norm term of the SASRec loss (model/sasrec.py:423-435) both
+    differentiate into the same table gradient, which the backward writes
+    once — (g_norm / ‖table‖) · table (0 when the norm is 0, as torch's
+    norm backward) — and then scatter-adds the row gradients into, instead of
+    two table-sized gradients added by autograd."""
+
+    @staticmethod
+    def forward(ctx, table, ids):
+        n, d = ids.numel(), table.shape[1]
+        out = torch.empty(n, d, dtype=table.dtype, device=table.device)
+        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
+                                    _lib.stream_handle()), "gather_rows")
+        norm = torch.linalg.vector_norm(table)
+        ctx.save_for_backward(table, ids, norm)
+        return out, norm
+
+    @staticmethod
+    def backward(ctx, grad, g_norm):
+        table, ids, norm = ctx.saved_tensors
+        if g_norm is None:
+            g = torch.zeros_like(table)
+        else:
+            scale = torch.where(norm > 0, g_norm / norm, torch.zeros_like(norm))
+            g = table * scale
+        if grad is not None:
+            check(lib.mirec_scatter_add_rows(grad.contiguous().data_ptr(), ids.data_ptr(),
+                                             ids.numel(), table.shape[1], g.data_ptr(),
+                                             _lib.stream_handle()), "scatter_add_rows")
+        return g, None
+
+
+def gather_rows_norm(table: torch.Tensor, ids: torch.Tensor):
+    """(gather_rows(table, ids), table.norm(2)) with one fused backward."""
+    if table.dtype != torch.float32 or table.dim() != 2 or table.shape[1] % 4:
+        raise ValueError("gather_rows_norm: float32 [n, d] table with d % 4 == 0")
+    flat = ids.reshape(-1).to(torch.int32).contiguous()
+    out, norm = _GatherRowsNorm.apply(table.contiguous(), flat)
+    return out.view(*ids.shape, table.shape[1]), norm

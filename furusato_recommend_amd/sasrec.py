@@ -28,7 +28,7 @@ from . import _lib
 from ._lib import check, lib
 from .engine import AdamGroup, AdamState, _note_raw_write
 from .linear import Linear, blas_backend, linear
-from .rows import gather_rows
+from .rows import gather_rows, gather_rows_norm
 
 
 # Optional per-launch timing (tools/bench_sasrec.py): a list receiving
@@ -165,6 +165,40 @@ def length_buckets(lengths) -> tuple[np.ndarray, tuple]:
 
 def _ptr(t):
     return 0 if t is None else t.data_ptr()
+
+
+class _BPRRowsLoss(torch.autograd.Function):
+    """SASRec.loss as two kernels (mirec_bpr_rows_loss / _bwd): mean
+    softplus(<u, ne> - <u, pe>) + coef * extra, with extra the embedding-norm
+    term (a 0-d tensor) and coef = decay / B (sasrec.py:423-435 with its one
+    'emb' parameter: the doubling accumulation leaves the norm itself)."""
+
+    @staticmethod
+    def forward(ctx, u, pe, ne, extra, coef: float):
+        u, pe, ne = u.contiguous(), pe.contiguous(), ne.contiguous()
+        B, d = u.shape
+        x = torch.empty(2 * B, dtype=u.dtype, device=u.device)  # x, then scratch
+        loss = torch.empty((), dtype=u.dtype, device=u.device)
+        check(lib.mirec_bpr_rows_loss(u.data_ptr(), pe.data_ptr(), ne.data_ptr(), B, d,
+                                      extra.data_ptr(), float(coef), x.data_ptr(),
+                                      loss.data_ptr(), _lib.stream_handle()), "bpr_rows_loss")
+        ctx.save_for_backward(u, pe, ne, x)
+        ctx.coef = float(coef)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        u, pe, ne, x = ctx.saved_tensors
+        B, d = u.shape
+        du, dpe, dne = torch.empty_like(u), torch.empty_like(pe), torch.empty_like(ne)
+        g_extra = torch.empty((), dtype=u.dtype, device=u.device)
+        g = g.contiguous()
+        check(lib.mirec_bpr_rows_loss_bwd(u.data_ptr(), pe.data_ptr(), ne.data_ptr(),
+                                          x.data_ptr(), B, d, g.data_ptr(), ctx.coef,
+                                          du.data_ptr(), dpe.data_ptr(), dne.data_ptr(),
+                                          g_extra.data_ptr(), _lib.stream_handle()),
+              "bpr_rows_loss_bwd")
+        return du, dpe, dne, g_extra, None
 
 
 class _SegmentMean(torch.autograd.Function):
@@ -573,11 +607,15 @@ class SASRec(nn.Module):
         # one lookup for the sequences, positives and negatives (one dense
         # table gradient, no accumulation), one pass of the item tower over
         # positives and negatives together (row-wise: same values)
-        rows = gather_rows(self.item_id_embedding.weight, torch.cat([ids, pos.int(), neg.int()]))
+        # The table's norm (the loss's only 'emb' parameter term) comes from
+        # the same node (one table gradient, written once), and the BPR
+        # score / softplus / mean / norm term are one kernel each way.
+        rows, wnorm = gather_rows_norm(self.item_id_embedding.weight,
+                                       torch.cat([ids, pos.int(), neg.int()]))
         x, pn = rows.split([n_tok, 2 * B])
         u = self.forward_user_packed(x, packing, seg, length)
         pe, ne = self.forward_item(pn).split(B)
-        loss = self.loss(u, pe, ne)
+        loss = _BPRRowsLoss.apply(u, pe, ne, wnorm, self.config["decay"] / B)
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         return loss
 

@@ -456,6 +456,20 @@ int mirec_segment_mean_bwd(const float *grad_out, const int64_t *seg, const int6
                            int64_t n_rows, int64_t B, int32_t d, float *grad_x,
                            mirec_stream_t stream);
 
+/* BPR loss on embedding rows (model/sasrec.py:423-435): x_r = <u_r, n_r> -
+ * <u_r, p_r> (written to x_out[0..B); x_out holds 2B floats, the second half
+ * scratch), loss[0] = mean_r softplus(x_r) + coef * extra[0] (extra: a
+ * device scalar such as the embedding-norm term, or NULL); u, p, n [B, d].
+ * Fixed summation order (deterministic).  Backward:
+ * with g = g_loss[0] (device) and s_r = g sigmoid(x_r) / B: du = s (n - p),
+ * dp = -s u, dn = s u, and g_extra[0] = g coef (if g_extra != NULL). */
+int mirec_bpr_rows_loss(const float *u, const float *p, const float *n, int64_t B, int32_t d,
+                        const float *extra, float coef, float *x_out, float *loss,
+                        mirec_stream_t stream);
+int mirec_bpr_rows_loss_bwd(const float *u, const float *p, const float *n, const float *x,
+                            int64_t B, int32_t d, const float *g_loss, float coef, float *du,
+                            float *dp, float *dn, float *g_extra, mirec_stream_t stream);
+
 /* Zero rows [offsets[B], n_rows) of buf [n_rows, row_floats] (offsets on the
  * device): the capacity-padding rows of a packed batch, which the packed
  * attention kernels do not write. */
