@@ -126,9 +126,92 @@ __global__ __launch_bounds__(256) void bpr_rows_loss_bwd_kernel(
   dn[e] = s * uv;
 }
 
+// Packing of a SASRec batch into a token capacity (graph-captured step):
+// pass 1 (one workgroup) gathers the users' lengths and scans them into
+// offsets (clamped to the capacity) and converts the positive / negative
+// ids; pass 2 (one lane per token row) finds the row's sequence by binary
+// search over the offsets and writes its item id (-1 and seg = B for rows
+// past the last sequence).
+__global__ __launch_bounds__(1024) void seq_pack_scan_kernel(
+    const int64_t *__restrict__ users, int64_t B, const int64_t *__restrict__ length_tab,
+    const int64_t *__restrict__ pos, const int64_t *__restrict__ neg, int64_t capacity,
+    int32_t *__restrict__ offsets, int64_t *__restrict__ length, int32_t *__restrict__ ids_all) {
+  __shared__ int64_t part[1024];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) {
+    carry = 0;
+    offsets[0] = 0;
+  }
+  __syncthreads();
+  for (int64_t base = 0; base < B; base += 1024) {
+    const int64_t b = base + threadIdx.x;
+    int64_t len = 0;
+    if (b < B) {
+      len = length_tab[users[b]];
+      length[b] = len;
+      ids_all[capacity + b] = (int32_t)pos[b];
+      ids_all[capacity + B + b] = (int32_t)neg[b];
+    }
+    part[threadIdx.x] = len;
+    __syncthreads();
+    for (int s = 1; s < 1024; s <<= 1) {  // inclusive Hillis-Steele scan
+      const int64_t v = (int)threadIdx.x >= s ? part[threadIdx.x - s] : 0;
+      __syncthreads();
+      part[threadIdx.x] += v;
+      __syncthreads();
+    }
+    if (b < B) offsets[b + 1] = (int32_t)min(carry + part[threadIdx.x], capacity);
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void seq_pack_rows_kernel(
+    const int64_t *__restrict__ users, int64_t B, const int32_t *__restrict__ items,
+    int32_t max_len, int64_t capacity, const int32_t *__restrict__ offsets,
+    int32_t *__restrict__ ids_all, int64_t *__restrict__ seg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= capacity) return;
+  int64_t lo = 0, hi = B;  // first b with offsets[b + 1] > t, or B
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (offsets[mid + 1] > t) hi = mid;
+    else lo = mid + 1;
+  }
+  if (lo < B) {
+    const int64_t k = t - offsets[lo];
+    ids_all[t] = items[users[lo] * max_len + k];
+    seg[t] = lo;
+  } else {
+    ids_all[t] = -1;
+    seg[t] = B;
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
+
+extern "C" int mirec_seq_pack(const int64_t *users, int64_t B, const int32_t *items,
+                              int32_t max_len, const int64_t *length_tab, const int64_t *pos,
+                              const int64_t *neg, int64_t capacity, int32_t *offsets,
+                              int64_t *length, int32_t *ids_all, int64_t *seg,
+                              mirec_stream_t stream) {
+  MIREC_CHECK_ARG(B > 0 && max_len > 0 && capacity >= 0 && capacity < (int64_t)1 << 31);
+  MIREC_CHECK_ARG(users && items && length_tab && pos && neg && offsets && length && ids_all &&
+                  (capacity == 0 || seg));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(seq_pack_scan_kernel, dim3(1), dim3(1024), 0, st, users, B, length_tab, pos,
+                     neg, capacity, offsets, length, ids_all);
+  MIREC_LAUNCH_CHECK();
+  if (capacity > 0) {
+    hipLaunchKernelGGL(seq_pack_rows_kernel, dim3((unsigned)((capacity + 255) / 256)), dim3(256),
+                       0, st, users, B, items, max_len, capacity, offsets, ids_all, seg);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
 
 extern "C" int mirec_bpr_rows_loss(const float *u, const float *p, const float *n, int64_t B,
                                    int32_t d, const float *extra, float coef, float *x_out,

@@ -601,17 +601,21 @@ class SASRec(nn.Module):
         self.optims.step()
         return loss.detach()
 
-    def _step_body(self, ids, packing, seg, length, pos, neg, loss_scale=1.0):
-        """Forward, loss and backward of one packed batch; returns the loss."""
-        n_tok, B = ids.numel(), pos.numel()
+    def _step_body(self, ids, packing, seg, length, pos, neg, loss_scale=1.0, n_tok=None):
+        """Forward, loss and backward of one packed batch; returns the loss.
+        ``ids`` = the packed item ids, or (with ``n_tok``) the ids already
+        followed by pos and neg (mirec_seq_pack's ids_all)."""
+        B = pos.numel()
+        if n_tok is None:
+            n_tok = ids.numel()
+            ids = torch.cat([ids, pos.int(), neg.int()])
         # one lookup for the sequences, positives and negatives (one dense
         # table gradient, no accumulation), one pass of the item tower over
-        # positives and negatives together (row-wise: same values)
-        # The table's norm (the loss's only 'emb' parameter term) comes from
-        # the same node (one table gradient, written once), and the BPR
-        # score / softplus / mean / norm term are one kernel each way.
-        rows, wnorm = gather_rows_norm(self.item_id_embedding.weight,
-                                       torch.cat([ids, pos.int(), neg.int()]))
+        # positives and negatives together (row-wise: same values).  The
+        # table's norm (the loss's only 'emb' parameter term) comes from the
+        # same node (one table gradient, written once), and the BPR score /
+        # softplus / mean / norm term are one kernel each way.
+        rows, wnorm = gather_rows_norm(self.item_id_embedding.weight, ids)
         x, pn = rows.split([n_tok, 2 * B])
         u = self.forward_user_packed(x, packing, seg, length)
         pe, ne = self.forward_item(pn).split(B)
@@ -620,27 +624,30 @@ class SASRec(nn.Module):
         return loss
 
     # ------------------------------------------------------- graph capture
-    def packed_ids_static(self, u, capacity: int):
-        """packed_ids on the device for device user ids ``u`` [B] into a fixed
-        token capacity (>= the batch's token count): rows past the last
-        sequence get item id -1 (a zero row) and ``seg`` = B, so every shape
-        is static and the step can be captured.  Returns (ids [capacity],
-        Packing(offsets, padded=True), seg [capacity], length [B])."""
+    def packed_ids_static(self, u, capacity: int, pos, neg):
+        """packed_ids on the device (mirec_seq_pack, two kernels) for device
+        user ids ``u`` [B] into a fixed token capacity (>= the batch's token
+        count): rows past the last sequence get item id -1 (a zero row) and
+        ``seg`` = B, so every shape is static and the step can be captured.
+        The offsets are clamped to the capacity, so a batch that did not fit
+        could never make a kernel read past the token buffers (the host sizes
+        the capacity from the batch).  Returns (ids_all [capacity + 2B]: the
+        token ids then pos and neg as int32, Packing(offsets, padded=True),
+        seg [capacity], length [B])."""
         B = u.numel()
         dev = self.device
-        length = self.seq.length[u]
-        offsets = torch.zeros(B + 1, dtype=torch.int32, device=dev)
-        # clamped to the capacity: a batch that did not fit could never make
-        # the kernels read past the token buffers (the host sizes capacity
-        # from the batch, so this never cuts a real batch)
-        offsets[1:] = torch.cumsum(length, 0).clamp(max=capacity).to(torch.int32)
-        t = torch.arange(capacity, dtype=torch.int32, device=dev)
-        seg = torch.searchsorted(offsets[1:], t, right=True)
-        segc = seg.clamp(max=B - 1)
-        pos = (t.long() - offsets[segc].long()).clamp(0, self.seq.max_len - 1)
-        ids = torch.where(seg < B, self.seq.items[u[segc], pos],
-                          torch.full_like(pos, -1, dtype=self.seq.items.dtype))
-        return ids, Packing(offsets, None, True), seg, length
+        items, length_tab = self.seq.items.contiguous(), self.seq.length.contiguous()
+        if items.dtype != torch.int32 or length_tab.dtype != torch.int64:
+            raise ValueError("SequenceData: int32 items and int64 lengths expected")
+        offsets = torch.empty(B + 1, dtype=torch.int32, device=dev)
+        length = torch.empty(B, dtype=torch.int64, device=dev)
+        ids_all = torch.empty(capacity + 2 * B, dtype=torch.int32, device=dev)
+        seg = torch.empty(capacity, dtype=torch.int64, device=dev)
+        check(lib.mirec_seq_pack(u.data_ptr(), B, items.data_ptr(), items.shape[1],
+                                 length_tab.data_ptr(), pos.data_ptr(), neg.data_ptr(), capacity,
+                                 offsets.data_ptr(), length.data_ptr(), ids_all.data_ptr(),
+                                 seg.data_ptr(), _lib.stream_handle()), "seq_pack")
+        return ids_all, Packing(offsets, None, True), seg, length
 
     def _graph_step(self, users, pos, neg):
         u_host = users.cpu().numpy() if torch.is_tensor(users) else np.asarray(users)
@@ -746,8 +753,8 @@ class _CapturedStep:
         buf = self.inbuf
         u, pos, neg = buf[:B], buf[B:2 * B], buf[2 * B:3 * B]
         hdev = buf[3 * B:3 * B + 3].view(torch.float32)
-        ids, packing, seg, length = m.packed_ids_static(u, self.C)
-        loss = m._step_body(ids, packing, seg, length, pos, neg)
+        ids_all, packing, seg, length = m.packed_ids_static(u, self.C, pos, neg)
+        loss = m._step_body(ids_all, packing, seg, length, pos, neg, n_tok=self.C)
         m.optims.step_device(hdev)
         return loss.detach()
 

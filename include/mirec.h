@@ -470,6 +470,19 @@ int mirec_bpr_rows_loss_bwd(const float *u, const float *p, const float *n, cons
                             int64_t B, int32_t d, const float *g_loss, float coef, float *du,
                             float *dp, float *dn, float *g_extra, mirec_stream_t stream);
 
+/* Pack a SASRec batch into a fixed token capacity (the graph-captured step,
+ * model/sasrec.py:449-455's pad_sequence without the padding): users [B]
+ * (device int64), items [n_users, max_len] (int32, each user's last items),
+ * length_tab [n_users] (int64), pos / neg [B] (int64).  Writes length[b] =
+ * length_tab[users[b]], offsets[B+1] = the prefix sums clamped to capacity
+ * (int32), ids_all[capacity + 2B] (int32) = the item id of every token row
+ * (-1 past the last sequence) followed by pos and neg, and seg[capacity]
+ * (int64) = the sequence of every row (B past the last sequence). */
+int mirec_seq_pack(const int64_t *users, int64_t B, const int32_t *items, int32_t max_len,
+                   const int64_t *length_tab, const int64_t *pos, const int64_t *neg,
+                   int64_t capacity, int32_t *offsets, int64_t *length, int32_t *ids_all,
+                   int64_t *seg, mirec_stream_t stream);
+
 /* Zero rows [offsets[B], n_rows) of buf [n_rows, row_floats] (offsets on the
  * device): the capacity-padding rows of a packed batch, which the packed
  * attention kernels do not write. */

@@ -1335,3 +1335,39 @@ def test_segment_mean_pool_and_backward():
         s, e = int(offsets[b]), int(offsets[b + 1])
         ref[s:e] = g[b] / max(e - s, 1)
     assert rel(gx, ref) < 1e-6 and float(gx[n_tok:].abs().max()) == 0.0
+
+
+def test_seq_pack_matches_host_packing():
+    """mirec_seq_pack (the captured step's packing) == the packing computed
+    on the host: offsets, lengths, token ids, seg, padding rows (-1 / B), the
+    int32 positives / negatives after the tokens, and clamping when the batch
+    exceeds the capacity (no row past it is ever addressed)."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    ds = SyntheticBipartite(900, 200, 20_000, seed=8)
+    m = SASRec({"recdim": 64, "layer": 1, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+                "device": "cuda:0", "bpr_batch_size": 1500, "dropout_p": 0.0}, ds)
+    rng = np.random.default_rng(4)
+    items = m.seq.items.cpu().numpy()
+    lens_tab = m.seq.length_host
+    for B in (1, 7, 1500):
+        users = rng.integers(0, 900, B)
+        pos, neg = rng.integers(0, 200, B), rng.integers(0, 200, B)
+        lens = lens_tab[users]
+        n_tok = int(lens.sum())
+        for cap in (n_tok + 300, max(n_tok // 2, 1)):
+            ud = torch.as_tensor(users, device="cuda")
+            ids_all, pk, seg, length = m.packed_ids_static(
+                ud, cap, torch.as_tensor(pos, device="cuda"), torch.as_tensor(neg, device="cuda"))
+            off = np.minimum(np.concatenate([[0], np.cumsum(lens)]), cap)
+            assert np.array_equal(pk.offsets.cpu().numpy(), off)
+            assert np.array_equal(length.cpu().numpy(), lens)
+            ids_ref = np.full(cap, -1)
+            seg_ref = np.full(cap, B)
+            for b in range(B):
+                for t in range(off[b], off[b + 1]):
+                    ids_ref[t] = items[users[b], t - off[b]]
+                    seg_ref[t] = b
+            got = ids_all.cpu().numpy()
+            assert np.array_equal(got[:cap], ids_ref)
+            assert np.array_equal(seg.cpu().numpy(), seg_ref)
+            assert np.array_equal(got[cap:cap + B], pos) and np.array_equal(got[cap + B:], neg)
