@@ -152,6 +152,8 @@ SIGNATURES = {
     "mirec_bpr_rows_loss_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                         c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),
+    "mirec_slice_norms_work_floats": (c_int64, []),
+    "mirec_slice_norms": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "mirec_seq_pack": (c_int, [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
                                c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p]),

@@ -189,9 +189,82 @@ __global__ __launch_bounds__(256) void seq_pack_rows_kernel(
   }
 }
 
+// L2 norms of x[0, split) and x[split, n) (the user / item slices of an id
+// table: the parameter-norm term of model/graphsage.py:326-337 and
+// model/sasrec.py:423-435).  Pass 1: each workgroup sums the squares of a
+// fixed stride of float4 per slice into its partial pair; pass 2: one
+// workgroup adds the partials in block order and takes the roots
+// (deterministic).  split % 4 == 0, n % 4 == 0.
+constexpr int kNormBlocks = 1024;
+__global__ __launch_bounds__(256) void slice_sumsq_kernel(const float *__restrict__ x, int64_t n4,
+                                                          int64_t split4,
+                                                          float *__restrict__ partial) {
+  __shared__ float red[2][256];
+  float a = 0.f, b = 0.f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < n4; e += (int64_t)kNormBlocks * 256) {
+    const float4 v = ld4(x + 4 * e);
+    const float s = v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    if (e < split4) a += s;
+    else b += s;
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = red[0][0];
+    partial[2 * blockIdx.x + 1] = red[1][0];
+  }
+}
+
+__global__ __launch_bounds__(256) void slice_norm_final_kernel(const float *__restrict__ partial,
+                                                               float *__restrict__ norms) {
+  __shared__ float red[2][256];
+  float a = 0.f, b = 0.f;
+  for (int k = threadIdx.x; k < kNormBlocks; k += 256) {
+    a += partial[2 * k];
+    b += partial[2 * k + 1];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    norms[0] = sqrtf(red[0][0]);
+    norms[1] = sqrtf(red[1][0]);
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
+
+extern "C" int64_t mirec_slice_norms_work_floats(void) { return 2 * kNormBlocks; }
+
+extern "C" int mirec_slice_norms(const float *x, int64_t n, int64_t split, float *work,
+                                 float *norms, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(x && work && norms && n >= 0 && split >= 0 && split <= n);
+  MIREC_CHECK_ARG(n % 4 == 0 && split % 4 == 0 && (uintptr_t)x % 16 == 0);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(slice_sumsq_kernel, dim3(kNormBlocks), dim3(256), 0, st, x, n / 4, split / 4,
+                     work);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(slice_norm_final_kernel, dim3(1), dim3(256), 0, st, work, norms);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
 
 extern "C" int mirec_seq_pack(const int64_t *users, int64_t B, const int32_t *items,
                               int32_t max_len, const int64_t *length_tab, const int64_t *pos,

@@ -33,6 +33,7 @@ from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamGroup, AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
 from .linear import Linear
+from .rows import slice_norms
 
 
 # ----------------------------------------------------------------- autograd
@@ -66,8 +67,7 @@ class _TableTerms(torch.autograd.Function):
                                                float(p), ctypes.c_uint64(seed), out.data_ptr(),
                                                st), "fanout_mean_gather")
             aggrs.append(out)
-        nu = table[:n_user].norm(2)
-        ni = table[n_user:].norm(2)
+        nu, ni = slice_norms(table, n_user)  # both slices in one pass
         ctx.save_for_backward(table, ids, nu, ni, *[l[0] for l in leaves])
         ctx.leaf_cfg = [(k, p, seed) for _, k, p, seed in leaves]
         ctx.n_user = n_user

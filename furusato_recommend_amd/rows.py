@@ -45,6 +45,21 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return out.view(*ids.shape, table.shape[1])
 
 
+def slice_norms(table: torch.Tensor, split_rows: int):
+    """(‖table[:split_rows]‖₂, ‖table[split_rows:]‖₂) as 0-d tensors, one
+    pass over the table (mirec_slice_norms; fixed summation order)."""
+    if not (table.is_cuda and table.dtype == torch.float32 and table.is_contiguous()
+            and table.shape[-1] % 4 == 0):
+        raise ValueError("slice_norms: contiguous float32 table with rows of 4k floats")
+    norms = torch.empty(2, dtype=table.dtype, device=table.device)
+    work = torch.empty(int(lib.mirec_slice_norms_work_floats()), dtype=table.dtype,
+                       device=table.device)
+    check(lib.mirec_slice_norms(table.data_ptr(), table.numel(), split_rows * table.shape[-1],
+                                work.data_ptr(), norms.data_ptr(), _lib.stream_handle()),
+          "slice_norms")
+    return norms[0], norms[1]
+
+
 class _GatherRowsNorm(torch.autograd.Function):
     """(table[ids], ‖table‖₂) as one autograd node: the embedding lookup and
     the embedding-norm term of the SASRec loss (model/sasrec.py:423-435) both
@@ -59,7 +74,7 @@ class _GatherRowsNorm(torch.autograd.Function):
         out = torch.empty(n, d, dtype=table.dtype, device=table.device)
         check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
                                     _lib.stream_handle()), "gather_rows")
-        norm = torch.linalg.vector_norm(table)
+        norm = slice_norms(table, table.shape[0])[0]
         ctx.save_for_backward(table, ids, norm)
         return out, norm
 

@@ -470,6 +470,15 @@ int mirec_bpr_rows_loss_bwd(const float *u, const float *p, const float *n, cons
                             int64_t B, int32_t d, const float *g_loss, float coef, float *du,
                             float *dp, float *dn, float *g_extra, mirec_stream_t stream);
 
+/* L2 norms of x[0, split) and x[split, n) -> norms[0], norms[1] (the
+ * parameter-norm terms of model/graphsage.py:326-337 / model/sasrec.py:
+ * 423-435 over an id table's user / item slices; split = n for one norm).
+ * n % 4 == 0, split % 4 == 0, x 16-byte aligned; work:
+ * mirec_slice_norms_work_floats() floats.  Fixed summation order. */
+int64_t mirec_slice_norms_work_floats(void);
+int mirec_slice_norms(const float *x, int64_t n, int64_t split, float *work, float *norms,
+                      mirec_stream_t stream);
+
 /* Pack a SASRec batch into a fixed token capacity (the graph-captured step,
  * model/sasrec.py:449-455's pad_sequence without the padding): users [B]
  * (device int64), items [n_users, max_len] (int32, each user's last items),

@@ -1371,3 +1371,18 @@ def test_seq_pack_matches_host_packing():
             assert np.array_equal(got[:cap], ids_ref)
             assert np.array_equal(seg.cpu().numpy(), seg_ref)
             assert np.array_equal(got[cap:cap + B], pos) and np.array_equal(got[cap + B:], neg)
+
+
+def test_slice_norms_match_fp64():
+    """mirec_slice_norms (the id-table norm terms of the SAGE / SASRec loss)
+    == float64 norms of both slices, empty slices give 0, bitwise repeatable."""
+    from furusato_recommend_amd.rows import slice_norms
+    torch.manual_seed(13)
+    for rows, split in ((1000, 600), (1, 0), (1, 1), (70_001, 35_000), (4, 4)):
+        t = torch.randn(rows, 128, device="cuda")
+        a, b = slice_norms(t, split)
+        td = t.double()
+        assert abs(float(a) - float(td[:split].norm())) <= 1e-6 * max(1.0, float(td[:split].norm()))
+        assert abs(float(b) - float(td[split:].norm())) <= 1e-6 * max(1.0, float(td[split:].norm()))
+        a2, b2 = slice_norms(t, split)
+        assert torch.equal(a, a2) and torch.equal(b, b2)
