@@ -18,7 +18,7 @@ i (hop L-i) updates every group of depth <= L-1-i from its hop-(L-i)
 children.  All groups' rows are gathered from the embedding table in ONE
 launch (mirec_gather_rows; backward = one atomic scatter-add), every hop mean
 is one mirec_fanout_mean (dropout fused, mask recomputed in the backward),
-the Linear layers are library GEMMs (hipBLASLt via torch).
+the Linear layers run on f32 MFMA GEMMs (csrc/gemm.hip via linear.py).
 """
 from __future__ import annotations
 

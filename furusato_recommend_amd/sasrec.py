@@ -6,9 +6,12 @@ LN → Linear → dropout → residual), the masked mean pool over the first
 `length` positions (:399-413), the item MLP tower (:415-421), the BPR loss
 with the reference's embedding-norm term (:423-435) and OneEpoch (:437-474).
 The attention core softmax(QKᵀ/√d_h + causal)·V and its backward are one
-HIP launch each (csrc/attention.hip, f32 MFMA); the projections, LayerNorm
-and FFN are library GEMMs, and the dropout / residual / ReLU /
-LayerNorm tail of each stage is one fused row kernel (csrc/resnorm.hip).
+HIP launch each (csrc/attention.hip, f32 MFMA); the Linear layers run on
+f32 MFMA GEMMs (csrc/gemm.hip; the QKV forward on hipBLASLt), the dropout /
+residual / ReLU / LayerNorm tail of each stage is one fused row kernel
+(csrc/resnorm.hip), and pooling, packing and the loss have kernels of their
+own (csrc/pool.hip).  On one GPU the whole training step is replayed from a
+captured HIP graph (_CapturedStep).
 Out of scope: the proprietary text / feature towers of the initial item
 embedding (:82-209): items start from an id embedding (N(0, 1), :205).
 The reference hard-codes 8 heads (:211); `heads` is a parameter here
