@@ -127,6 +127,11 @@ SIGNATURES = {
                                          c_float, c_uint64, c_void_p, c_void_p]),
     "mirec_fanout_mean_gather_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                              c_float, c_uint64, c_void_p, c_void_p]),
+    "mirec_fanout_mean_gather_bwd_sorted_workspace": (c_int, [c_int64, c_int32, c_int32,
+                                                              POINTER(c_size_t)]),
+    "mirec_fanout_mean_gather_bwd_sorted": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                                    c_float, c_uint64, c_int32, c_void_p,
+                                                    c_void_p, c_size_t, c_void_p]),
     "mirec_attention_fwd": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
                                     c_void_p]),
     "mirec_attention_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,

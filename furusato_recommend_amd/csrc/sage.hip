@@ -18,6 +18,8 @@
 //                         backward scatter-adds into the table gradient)
 // Dropout masks are a counter hash of (seed, element index), recomputed in
 // the backward (nothing stored).
+#include <hipcub/hipcub.hpp>
+
 #include "common.h"
 
 namespace mirec {
@@ -160,7 +162,183 @@ __global__ __launch_bounds__(256) void fanout_mean_gather_bwd_kernel(
   }
 }
 
+// Sorted form of the same backward (deterministic, no atomics): the leaf
+// entries e = t*k + c are radix-sorted by child id (stable, so each id's
+// entries stay in e order), then every run of equal ids is summed — mask *
+// grad_out[t] / cnt_t, in that order — by exactly one wave and added to the
+// id's row once.  Invalid entries (id < 0) sort to the key n_rows, last.
+__global__ __launch_bounds__(256) void fanout_sort_prep_kernel(const int32_t *__restrict__ ids,
+                                                               int64_t n_targets, int32_t k,
+                                                               int32_t n_rows,
+                                                               int32_t *__restrict__ keys,
+                                                               int32_t *__restrict__ vals,
+                                                               float *__restrict__ inv_cnt) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < n_targets * k) {
+    const int32_t id = ids[e];
+    keys[e] = id >= 0 ? id : n_rows;
+    vals[e] = (int32_t)e;
+  }
+  if (e < n_targets) {
+    int cnt = 0;
+    for (int c = 0; c < k; ++c) cnt += ids[e * k + c] >= 0 ? 1 : 0;
+    inv_cnt[e] = cnt > 0 ? 1.f / (float)cnt : 0.f;
+  }
+}
+
+// One wave per chunk of 64 sorted entries; a run belongs to the chunk that
+// holds its head, and its owner keeps reading past the chunk end while the
+// run continues.  Keys / entry ids / 1/cnt are loaded 64 at a time
+// (coalesced) and broadcast with readlane; each lane sums 4 columns (d % 4
+// == 0), with kSortBatch grad_out rows in flight before they are added in
+// order.
+constexpr int kSortBatch = 8;
+
+__global__ __launch_bounds__(256) void fanout_sorted_sum_kernel(
+    const float *__restrict__ grad_out, const int32_t *__restrict__ keys,
+    const int32_t *__restrict__ vals, const float *__restrict__ inv_cnt, int64_t n, int32_t k,
+    int32_t d, int32_t n_rows, uint64_t key, uint32_t thresh, float scale,
+    float *__restrict__ table_grad) {
+  constexpr int32_t kEnd = 0x7fffffff;  // key past the last entry
+  const int lane = threadIdx.x & 63;
+  const int64_t base = ((int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64;
+  if (base >= n) return;
+  const int64_t end = base + 64 < n ? base + 64 : n;
+  int64_t pos = base;
+  if (base > 0) {  // skip the tail of a run whose head is in an earlier chunk
+    const int32_t prev = keys[base - 1];
+    const int32_t kl = base + lane < n ? keys[base + lane] : kEnd;
+    const unsigned long long diff = __ballot(kl != prev);
+    if (diff == 0ull) return;
+    pos = base + (int64_t)__builtin_ctzll(diff);
+  }
+  if (pos >= end) return;
+  const int32_t first = keys[pos];
+  if (first >= n_rows) return;  // only invalid entries from here on
+  for (int c0 = 0; c0 < d; c0 += 256) {
+    const int col = c0 + 4 * lane;
+    const bool act = col < d;
+    int32_t cur = first;
+    float4 acc = f4_zero();
+    bool done = false;
+    for (int64_t p = pos; !done; p += 64) {
+      const int64_t j = p + lane;
+      const int32_t kb = j < n ? keys[j] : kEnd;
+      const int32_t vb = j < n ? vals[j] : 0;
+      const float ib = inv_cnt[vb / k];
+      for (int m0 = 0; m0 < 64 && !done; m0 += kSortBatch) {
+        float4 x[kSortBatch];
+        int32_t kk[kSortBatch], ee[kSortBatch];
+#pragma unroll
+        for (int u = 0; u < kSortBatch; ++u) {
+          kk[u] = __builtin_amdgcn_readlane(kb, m0 + u);
+          ee[u] = __builtin_amdgcn_readlane(vb, m0 + u);
+          const float iv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ib), m0 + u));
+          const int64_t t = ee[u] / k;
+          x[u] = act ? f4_scale(iv, ld4(grad_out + t * d + col)) : f4_zero();
+        }
+#pragma unroll
+        for (int u = 0; u < kSortBatch; ++u) {
+          if (kk[u] != cur) {  // wave-uniform: the run `cur` ends here
+            if (act) {
+              float *row = table_grad + (int64_t)cur * d + col;
+              st4(row, f4_add(ld4(row), acc));
+            }
+            if (p + m0 + u >= end || kk[u] >= n_rows) {
+              done = true;
+              break;
+            }
+            cur = kk[u];
+            acc = f4_zero();
+          }
+          float4 v = x[u];
+          if (thresh != 0u) {
+            const uint64_t e = (uint64_t)((int64_t)ee[u] * d + col);
+            v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
+            v.y = keep(key, e + 1, thresh) ? v.y * scale : 0.f;
+            v.z = keep(key, e + 2, thresh) ? v.z * scale : 0.f;
+            v.w = keep(key, e + 3, thresh) ? v.w * scale : 0.f;
+          }
+          acc = f4_add(acc, v);
+        }
+      }
+    }
+  }
+}
+
+// Workspace layout of the sorted backward: keys / vals in and out (int32),
+// inv_cnt (float), then the radix sort's temporary storage.
+static size_t fanout_sorted_layout(int64_t n_targets, int32_t k, int32_t n_rows,
+                                   size_t *sort_off, size_t *sort_bytes, int *end_bit) {
+  const int64_t n = n_targets * k;
+  const auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  size_t off = 4 * up(sizeof(int32_t) * n) + up(sizeof(float) * n_targets);
+  int bits = 1;
+  while (bits < 31 && ((int64_t)1 << bits) <= n_rows) ++bits;
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (int32_t *)nullptr, (int32_t *)nullptr,
+                                           (int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0,
+                                           bits);
+  *sort_off = off;
+  *sort_bytes = tb;
+  *end_bit = bits;
+  return off + up(tb);
+}
+
 }  // namespace mirec
+
+extern "C" int mirec_fanout_mean_gather_bwd_sorted_workspace(int64_t n_targets, int32_t k,
+                                                             int32_t n_rows, size_t *bytes) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(bytes && n_targets >= 0 && k > 0 && n_rows > 0 &&
+                  n_targets * (int64_t)k < ((int64_t)1 << 31));
+  size_t so, sb;
+  int eb;
+  *bytes = fanout_sorted_layout(n_targets, k, n_rows, &so, &sb, &eb);
+  return MIREC_OK;
+}
+
+extern "C" int mirec_fanout_mean_gather_bwd_sorted(const float *grad_out, const int32_t *ids,
+                                                   int64_t n_targets, int32_t k, int32_t dim,
+                                                   float dropout_p, uint64_t seed,
+                                                   int32_t n_rows, float *table_grad,
+                                                   void *workspace, size_t workspace_bytes,
+                                                   mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(table_grad && n_targets >= 0 && k > 0 && dim > 0 && dim % 4 == 0 &&
+                  n_rows > 0 && n_targets * (int64_t)k < ((int64_t)1 << 31));
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &key, &thresh, &scale));
+  if (n_targets == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(grad_out && ids && workspace);
+  size_t sort_off, sort_bytes;
+  int end_bit;
+  const size_t need = fanout_sorted_layout(n_targets, k, n_rows, &sort_off, &sort_bytes, &end_bit);
+  if (workspace_bytes < need) return MIREC_ERR_WORKSPACE;
+  const int64_t n = n_targets * k;
+  const size_t seg = (sizeof(int32_t) * n + 255) / 256 * 256;
+  char *ws = static_cast<char *>(workspace);
+  int32_t *keys_in = reinterpret_cast<int32_t *>(ws);
+  int32_t *keys_out = reinterpret_cast<int32_t *>(ws + seg);
+  int32_t *vals_in = reinterpret_cast<int32_t *>(ws + 2 * seg);
+  int32_t *vals_out = reinterpret_cast<int32_t *>(ws + 3 * seg);
+  float *inv_cnt = reinterpret_cast<float *>(ws + 4 * seg);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(fanout_sort_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     st, ids, n_targets, k, n_rows, keys_in, vals_in, inv_cnt);
+  MIREC_LAUNCH_CHECK();
+  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws + sort_off, sort_bytes, keys_in, keys_out,
+                                               vals_in, vals_out, (int)n, 0, end_bit, st));
+  const int64_t chunks = (n + 63) / 64;  // one wave per 64 sorted entries
+  hipLaunchKernelGGL(fanout_sorted_sum_kernel, dim3((unsigned)((chunks + 3) / 4)), dim3(256), 0, st,
+                     grad_out, keys_out, vals_out, inv_cnt, n, k, dim, n_rows, key, thresh, scale,
+                     table_grad);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
 
 extern "C" int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
                                    int32_t k, uint64_t seed, uint64_t offset, int32_t *children,

@@ -36,6 +36,11 @@ from .linear import Linear
 from .rows import slice_norms
 
 
+# The leaf hop's backward: sorted by child id (True: deterministic, no
+# atomics) or float-atomic scatter (False; A/B timing).
+SORTED_LEAF_BACKWARD = True
+
+
 # ----------------------------------------------------------------- autograd
 class _TableTerms(torch.autograd.Function):
     """Everything the loss takes from the [N, d] id table in one node:
@@ -93,10 +98,23 @@ class _TableTerms(torch.autograd.Function):
         for g, lid, (kk, p, seed) in zip(g_aggrs, leaf_ids, ctx.leaf_cfg):
             if g is None:
                 continue
-            check(lib.mirec_fanout_mean_gather_bwd(g.contiguous().data_ptr(), lid.data_ptr(),
-                                                   lid.numel() // kk, kk, d, float(p),
-                                                   ctypes.c_uint64(seed), grad.data_ptr(), st),
-                  "fanout_mean_gather_bwd")
+            n_t = lid.numel() // kk
+            if SORTED_LEAF_BACKWARD:
+                # entries sorted by child id, one ordered sum per row: no
+                # float atomics, deterministic
+                nb = ctypes.c_size_t()
+                check(lib.mirec_fanout_mean_gather_bwd_sorted_workspace(
+                    n_t, kk, table.shape[0], ctypes.byref(nb)), "fanout_sorted_workspace")
+                ws = torch.empty(nb.value, dtype=torch.uint8, device=table.device)
+                check(lib.mirec_fanout_mean_gather_bwd_sorted(
+                    g.contiguous().data_ptr(), lid.data_ptr(), n_t, kk, d, float(p),
+                    ctypes.c_uint64(seed), table.shape[0], grad.data_ptr(), ws.data_ptr(),
+                    nb.value, st), "fanout_mean_gather_bwd_sorted")
+            else:
+                check(lib.mirec_fanout_mean_gather_bwd(g.contiguous().data_ptr(), lid.data_ptr(),
+                                                       n_t, kk, d, float(p),
+                                                       ctypes.c_uint64(seed), grad.data_ptr(),
+                                                       st), "fanout_mean_gather_bwd")
         return grad, None, None, None
 
 

@@ -401,6 +401,18 @@ int mirec_fanout_mean_gather_bwd(const float *grad_out, const int32_t *ids,
                                  float dropout_p, uint64_t seed, float *table_grad,
                                  mirec_stream_t stream);
 
+/* Deterministic form of mirec_fanout_mean_gather_bwd: the entries are
+ * radix-sorted by child id and each id's contributions are summed in entry
+ * order and added to its row once (no float atomics).  n_rows = rows of the
+ * table (child ids < n_rows); workspace: ..._sorted_workspace bytes. */
+int mirec_fanout_mean_gather_bwd_sorted_workspace(int64_t n_targets, int32_t k, int32_t n_rows,
+                                                  size_t *bytes);
+int mirec_fanout_mean_gather_bwd_sorted(const float *grad_out, const int32_t *ids,
+                                        int64_t n_targets, int32_t k, int32_t dim,
+                                        float dropout_p, uint64_t seed, int32_t n_rows,
+                                        float *table_grad, void *workspace,
+                                        size_t workspace_bytes, mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* SASRec causal self-attention (model/sasrec.py:385-397), f32 MFMA          */
 /* ------------------------------------------------------------------------ */

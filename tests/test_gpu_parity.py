@@ -1386,3 +1386,39 @@ def test_slice_norms_match_fp64():
         assert abs(float(b) - float(td[split:].norm())) <= 1e-6 * max(1.0, float(td[split:].norm()))
         a2, b2 = slice_norms(t, split)
         assert torch.equal(a, a2) and torch.equal(b, b2)
+
+
+def test_sorted_leaf_backward_matches_atomic_and_is_deterministic():
+    """mirec_fanout_mean_gather_bwd_sorted (radix sort by child id + ordered
+    per-row sums) == the float-atomic scatter within fp32 rounding, with
+    dropout, invalid (-1) children and hub ids repeated many times; two runs
+    are bitwise equal."""
+    import ctypes
+
+    from furusato_recommend_amd import _lib
+    lib = _lib.lib
+    torch.manual_seed(14)
+    n_rows, d, k, n_t = 5000, 128, 10, 30_000
+    ids = torch.randint(0, n_rows, (n_t * k,), dtype=torch.int32, device="cuda")
+    ids[torch.rand(n_t * k, device="cuda") < 0.1] = -1
+    ids[::7] = 3  # a hub
+    g = torch.randn(n_t, d, device="cuda")
+    base = torch.randn(n_rows, d, device="cuda")
+    st = _lib.stream_handle()
+    for p in (0.0, 0.3):
+        a = base.clone()
+        _lib.check(lib.mirec_fanout_mean_gather_bwd(g.data_ptr(), ids.data_ptr(), n_t, k, d, p,
+                                                    ctypes.c_uint64(5), a.data_ptr(), st), "atomic")
+        outs = []
+        for _ in range(2):
+            b = base.clone()
+            nb = ctypes.c_size_t()
+            _lib.check(lib.mirec_fanout_mean_gather_bwd_sorted_workspace(n_t, k, n_rows,
+                                                                         ctypes.byref(nb)), "ws")
+            ws = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+            _lib.check(lib.mirec_fanout_mean_gather_bwd_sorted(
+                g.data_ptr(), ids.data_ptr(), n_t, k, d, p, ctypes.c_uint64(5), n_rows,
+                b.data_ptr(), ws.data_ptr(), nb.value, st), "sorted")
+            outs.append(b)
+        assert rel(outs[0], a) < 1e-5
+        assert torch.equal(outs[0], outs[1])

@@ -71,7 +71,11 @@ def main():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--blas", default="", help="torch BLAS backend override (cublas / cublaslt)")
+    ap.add_argument("--leaf-bwd", choices=("sorted", "atomic"), default="sorted",
+                    help="leaf-hop backward: radix-sorted ordered sums or float atomics")
     args = ap.parse_args()
+    from furusato_recommend_amd import graphsage as _gs
+    _gs.SORTED_LEAF_BACKWARD = args.leaf_bwd == "sorted"
     if args.blas:
         torch.backends.cuda.preferred_blas_library(args.blas)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -120,7 +124,8 @@ def main():
             "unit": "positive-edges/s", "n_gpus": world, "steps": args.steps,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "dtype": "f32",
             "config": {"workload": "C3: GraphSAGE 2-hop fanout %s d=%d on the C2 graph" % (fan, args.dim),
-                       "bpr_batch_per_rank": B, "parallelism": f"dp{world} (dense grad all-reduce)"},
+                       "bpr_batch_per_rank": B, "parallelism": f"dp{world} (dense grad all-reduce)",
+                       "leaf_bwd": args.leaf_bwd},
             "cpu_baseline": cpu}),
             flush=True)
     if world > 1:
