@@ -11,16 +11,33 @@ computed there only (engine.py); --prune 0 runs every layer on every row.  `valu
 consumed by all ranks / wall time of the K timed steps (max over ranks),
 inputs resident in HBM.
 
+Launch:
     python bench.py [--gpus N --steps K --warmup W]
+With N > 1 and no WORLD_SIZE in the environment the script starts the N
+ranks itself (torch.distributed.run as a child process; this parent never
+touches the GPU) and exits with the ranks' status — the reference's
+mp.spawn(demo, nprocs=world_size) entry (ddp_lgcn.py:760-768).  The
+explicit form works too:
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
+--rehearse runs every rank on cuda:0 with gloo collectives (the N-rank code
+path on a one-GPU box; not a throughput measurement).
+
+Quality leg (--quality-steps S, default 3000 at N=1): a second C2-sized
+graph with community structure (kind='cluster'), S training steps of the
+same engine from random init, then Recall@20 / NDCG@20 with trainer.py /
+metric.py semantics — reported beside the throughput, which is measured on
+the structureless uniform graph where any recall is chance.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,9 +52,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # mirec::prop_kernel<D=64, UNROLL=4, IN_PRESCALED, in_mask=false, row_mask=false>
 DOMINANT = "prop_kernel<D, UNROLL, 0, false, false>"
 KIND_NAMES = {0: "prescaled", 1: "raw", 2: "sparse", 3: "none"}
+PMC_FILE = os.path.join("profiles", "pmc_prop_kernel.json")
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -50,16 +68,82 @@ def parse():
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--kind", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--cpu-baseline", default="step", choices=["step", "forward", "off"])
-    ap.add_argument("--recall", type=int, default=1)
+    ap.add_argument("--cpu-k", type=int, default=3, help="timed CPU steps after 1 warm-up")
+    ap.add_argument("--quality-steps", type=int, default=-1,
+                    help="training steps of the Recall@20 leg (-1: 3000 at N=1, 0 at N>1)")
+    ap.add_argument("--quality-clusters", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=2020)
     ap.add_argument("--prune", type=int, default=1,
                     help="frontier pruning (1) or every layer on every row (0)")
-    ap.add_argument("--dp-mode", default="sparse", choices=["sparse", "dense"])
-    return ap.parse_args()
+    ap.add_argument("--dp-mode", default="sparse", choices=["sparse", "dense", "sharded"])
+    ap.add_argument("--rehearse", action="store_true",
+                    help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
+    ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
 
-def c2_workload(args) -> bool:
-    return (args.users, args.items, args.edges) == (1_000_000, 100_000, 20_000_000)
+# ---------------------------------------------------------------- launcher
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_command(n: int, argv: list[str], port: int) -> list[str]:
+    """The child command that starts n ranks of this script (one process
+    per GPU) with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def needs_launch(args, env=os.environ) -> bool:
+    return args.gpus > 1 and "WORLD_SIZE" not in env
+
+
+def launch(args, argv: list[str], runner=subprocess.run) -> int:
+    """Start the ranks as a child process tree and return their exit status.
+    Nothing here initialises HIP: the parent only waits."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", str(max(1, host_threads() // args.gpus)))
+    r = runner(launch_command(args.gpus, argv, free_port()), env=env)
+    return int(r.returncode)
+
+
+def launch_selftest(args) -> None:
+    """CPU-only rank body used by the launcher test: gloo rendezvous, one
+    all-reduce, rank 0 prints one JSON line."""
+    from furusato_recommend_amd.dist import init_distributed
+    init_distributed("gloo", timeout_s=60)
+    t = torch.tensor([float(dist.get_rank() + 1)])
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"n_gpus": dist.get_world_size(), "sum": float(t)}), flush=True)
+    dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------- host info
+
+def host_threads() -> int:
+    """CPU threads this process may actually use: the affinity mask, capped
+    by a cgroup CPU quota (on the GPU box os.cpu_count() reports the whole
+    host while the job's share is smaller)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, int(n))
 
 
 def cpu_model():
@@ -73,46 +157,139 @@ def cpu_model():
     return platform.processor()
 
 
+def layer_bytes(n_nodes: int, nnz: int, d: int) -> int:
+    """BASELINE.md §3 per-layer algorithmic bytes of the CPU propagation."""
+    return nnz * d * 4 + nnz * 4 + (n_nodes + 1) * 4 + n_nodes * 4 + n_nodes * d * 4
+
+
 def cpu_baseline(ds, args, users, pos, neg):
-    """The CPU oracle (torch, fp32, all host threads given to torch) on a
-    bounded sample of the same workload: one full training step (B triples)
-    on the full C2 graph, or the 3-layer forward only."""
+    """The CPU oracle (torch fp32) on a bounded sample of the same workload,
+    timed per BASELINE.md §3: one warm-up training step, then the mean of K
+    full training steps (B triples each, full C2 graph); the 3-layer forward
+    the same way (warmed by the warm-up step)."""
     from oracle.lightgcn_oracle import OracleLightGCN, forward
-    threads = torch.get_num_threads()
+    threads = host_threads()
+    torch.set_num_threads(threads)
     o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, args.dim,
                        args.layers, 1e-3, 1e-4, seed=args.seed)
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        forward(o.emb, o.ei, ds.n_users, args.layers, o.div)
-    t_fwd = time.perf_counter() - t0
-    res = {"cores": threads, "kind": "port", "cpu": cpu_model(),
-           "forward_s": round(t_fwd, 3)}
+    K = max(1, args.cpu_k)
+    res = {"cores": threads, "threads": threads, "os_cpu_count": os.cpu_count(),
+           "kind": "port", "cpu": cpu_model(), "warmup": 1, "k": K}
     if args.cpu_baseline == "step":
-        t0 = time.perf_counter()
-        o.stageOne(users, pos, neg)
-        t_step = time.perf_counter() - t0
+        o.stageOne(users, pos, neg)  # warm-up
+        ts = []
+        for _ in range(K):
+            t0 = time.perf_counter()
+            o.stageOne(users, pos, neg)
+            ts.append(time.perf_counter() - t0)
+        t_step = sum(ts) / K
         res.update(value=round(len(users) / t_step, 3), unit="positive-edges/s",
-                   step_s=round(t_step, 3),
-                   sample=f"1 full training step (B={len(users)}) of the C2 workload "
-                          f"(3-layer fwd+bwd+Adam over {ds.n_users + ds.m_items} nodes, "
-                          f"{2 * ds.trainDataSize} adjacency entries)")
+                   step_s=round(t_step, 3), step_s_each=[round(t, 3) for t in ts],
+                   sample=f"1 warm-up + mean of {K} full training steps (B={len(users)}) of "
+                          f"the C2 workload (3-layer fwd+bwd+Adam over "
+                          f"{ds.n_users + ds.m_items} nodes, {2 * ds.trainDataSize} "
+                          f"adjacency entries)")
     else:
+        with torch.no_grad():
+            forward(o.emb, o.ei, ds.n_users, args.layers, o.div)  # warm-up
+    tf = []
+    with torch.no_grad():
+        for _ in range(K):
+            t0 = time.perf_counter()
+            forward(o.emb, o.ei, ds.n_users, args.layers, o.div)
+            tf.append(time.perf_counter() - t0)
+    t_fwd = sum(tf) / K
+    nbytes = args.layers * layer_bytes(ds.n_users + ds.m_items, 2 * ds.trainDataSize, args.dim)
+    res.update(forward_s=round(t_fwd, 3),
+               forward_gbs=round(nbytes / t_fwd / 1e9, 3))
+    if args.cpu_baseline == "forward":
         res.update(value=round(1.0 / t_fwd, 4), unit="forward passes/s",
-                   sample="one 3-layer full-graph forward of the C2 graph")
+                   sample=f"1 warm-up + mean of {K} 3-layer full-graph forwards of the C2 graph")
     return res
 
 
-def main():
-    args = parse()
+def pmc_traffic(args):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    passes (rocprofv3 FETCH_SIZE / WRITE_SIZE, gfx950 correction; the
+    counters cannot be read from inside this process)."""
+    path = os.path.join(ROOT, PMC_FILE)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        j = json.load(f)
+    kname = f"prop_kernel<{args.dim}, {({32: 2, 64: 4, 128: 4, 256: 8}).get(args.dim, 1)}, 0, false, false>"
+    if (c2_workload(args) and j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
+            and kname in j.get("kernel", "")):
+        return j.get("hbm_bytes_per_launch"), f"{PMC_FILE} ({j.get('round', 'r05')})"
+    return None, None
+
+
+def c2_workload(args) -> bool:
+    return (args.users, args.items, args.edges) == (1_000_000, 100_000, 20_000_000)
+
+
+# ---------------------------------------------------------------- quality leg
+
+def quality_leg(args, dev, steps: int):
+    """Recall@20 that measures something: train the same engine on a
+    C2-sized graph with community structure (items i % K == user u % K with
+    probability 0.9), `steps` steps of B triples from the on-device sampler,
+    then the evaluation path (trainer.py:115-187 semantics)."""
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from furusato_recommend_amd.engine import sample_triples
+    from furusato_recommend_amd.evaluate import evaluate
+    t0 = time.perf_counter()
+    ds = SyntheticBipartite(args.users, args.items, args.edges, seed=7, kind="cluster",
+                            n_clusters=args.quality_clusters, p_in=0.9, test_frac=0.1)
+    torch.manual_seed(args.seed)
+    cfg = {"recdim": args.dim, "layer": args.layers, "lr": 1e-3, "decay": 1e-4,
+           "device": str(dev), "bpr_batch_size": args.batch, "prune": bool(args.prune)}
+    model = LightGCN(cfg, ds)
+    eng, emb = model.engine, model.all_embedding.weight.data
+    B = args.batch
+    u = torch.empty(B, dtype=torch.int32, device=dev)
+    p, n = torch.empty_like(u), torch.empty_like(u)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    r0 = evaluate(model, ds.testDict, topks=(20,))
+    torch.cuda.synchronize()
+    t_train = time.perf_counter()
+    for i in range(steps):
+        sample_triples(model.graph, B, args.seed + 1, i * B, u, p, n, err, 0, 1)
+        eng.train_step(emb, model.optim, u, p, n, cfg["decay"])
+    torch.cuda.synchronize()
+    t_train = time.perf_counter() - t_train
+    r = evaluate(model, ds.testDict, topks=(10, 20))
+    mean_deg = ds.trainDataSize / ds.n_users
+    return {"recall@20": float(r["recall"][1]), "ndcg@20": float(r["ndcg"][1]),
+            "recall@10": float(r["recall"][0]), "recall@20_at_init": float(r0["recall"][0]),
+            "chance_recall@20": round(20.0 / (ds.m_items - mean_deg), 7),
+            "test_users": len(ds.testDict), "train_steps": steps, "batch": B, "lr": 1e-3,
+            "train_s": round(t_train, 2), "leg_s": round(time.perf_counter() - t0, 2),
+            "graph": f"cluster: {args.users} x {args.items} / {args.edges} edges, "
+                     f"{args.quality_clusters} communities, p_in 0.9, seed 7"}
+
+
+# ---------------------------------------------------------------- main
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if needs_launch(args):
+        sys.exit(launch(args, argv))
+    if args.launch_selftest:
+        return launch_selftest(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if args.rehearse else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        from furusato_recommend_amd.dist import init_distributed
+        init_distributed("gloo" if args.rehearse else "nccl", dev)
+        world = dist.get_world_size()
 
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     from furusato_recommend_amd.dist import DataParallel
@@ -157,7 +334,8 @@ def main():
     dt = time.perf_counter() - t0
     events, eng.prop_events = eng.prop_events, None
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt], dtype=torch.float64,
+                         device="cpu" if args.rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     if int(err.item()) != 0:
@@ -187,22 +365,14 @@ def main():
     avg_ms = dom[1] / dom[0]
     avg_bytes = dom[2] / dom[0]
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_prop_kernel.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            j = json.load(f)
-        kname = f"prop_kernel<{args.dim}, {({32: 2, 64: 4, 128: 4, 256: 8}).get(args.dim, 1)}, 0, false, false>"
-        if (c2_workload(args) and j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
-                and kname in j.get("kernel", "")):
-            traffic = j.get("hbm_bytes_per_launch")
+    traffic, traffic_src = pmc_traffic(args)
 
+    qsteps = args.quality_steps if args.quality_steps >= 0 else (3000 if world == 1 else 0)
     recall = None
-    if args.recall and rank == 0:
-        from furusato_recommend_amd.evaluate import evaluate
-        r = evaluate(model, ds.testDict, topks=(10, 20))
-        recall = {"recall@20": float(r["recall"][1]), "ndcg@20": float(r["ndcg"][1]),
-                  "recall@10": float(r["recall"][0]), "test_users": len(ds.testDict)}
+    if qsteps > 0 and rank == 0:
+        del model, eng, emb, dp
+        torch.cuda.empty_cache()
+        recall = quality_leg(args, dev, qsteps)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
@@ -215,12 +385,15 @@ def main():
         wl = ("C2" if c2 else "custom") + (
             f": LightGCN {args.layers}-layer d={args.dim}, synthetic {args.users} users x "
             f"{args.items} items / {args.edges} edges ({args.kind})")
+        par = (f"dp{world} rehearsal: {world} ranks on one GPU, gloo collectives"
+               if args.rehearse else
+               f"dp{world} (user-sharded, RCCL {args.dp_mode} gradient exchange)")
         line = {
             "metric": f"BPR positive-edges/sec (LightGCN-{args.layers} d={args.dim}, "
                       f"{args.users} x {args.items} / {args.edges} edges)",
             "value": round(value, 1),
             "unit": "positive-edges/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.rehearse else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 3),
@@ -233,13 +406,13 @@ def main():
                        "users": args.users, "items": args.items, "edges": args.edges,
                        "graph": args.kind, "dim": args.dim, "layers": args.layers,
                        "bpr_batch_per_rank": B, "global_batch": B * world,
-                       "parallelism": f"dp{world} (user-sharded, RCCL {args.dp_mode} "
-                                      f"gradient exchange)"},
+                       "ranks": world, "parallelism": par},
             "roofline": {"bound": "hbm",
                          "kernel": DOMINANT.replace("D, UNROLL", f"{args.dim}, "
                                                     f"{ {32: 2, 64: 4, 128: 4, 256: 8}.get(args.dim, 1)}"),
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": int(avg_bytes),
                          "launches_per_step": round(dom[0] / args.steps, 2)},
@@ -254,6 +427,8 @@ def main():
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 2),
         }
+        if args.rehearse:
+            line["rehearsal"] = True
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -36,8 +36,27 @@ batch; after the sparse exchange the backward is pruned to the union seeds.
 """
 from __future__ import annotations
 
+import datetime
+import os
+
 import torch
 import torch.distributed as dist
+
+# Watchdog on rendezvous and collectives (the reference's ranks hang
+# forever on a barrier when one dies, ddp_lgcn.py:671).
+DEFAULT_TIMEOUT_S = float(os.environ.get("MIREC_DIST_TIMEOUT_S", "300"))
+
+
+def init_distributed(backend: str = "nccl", device: torch.device | None = None,
+                     timeout_s: float = DEFAULT_TIMEOUT_S, **kw) -> None:
+    """`dist.init_process_group` with a finite timeout (replaces the
+    unbounded NCCL setup of ddp_lgcn.py:748-755).  A rank that dies or stalls
+    makes the others raise after `timeout_s` seconds instead of hanging the
+    job; for RCCL the same bound applies to every collective (the process
+    group's watchdog)."""
+    if backend == "nccl" and device is not None:
+        kw.setdefault("device_id", device)
+    dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
 class DataParallel:

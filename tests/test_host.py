@@ -312,3 +312,52 @@ def test_length_buckets_order_and_counts():
             assert (lens[seg] <= 16 * (k + 1)).all()
             assert (np.diff(seg) > 0).all()  # stable inside a bucket
             lo = hi
+
+
+def test_bench_launcher_command():
+    """`python bench.py --gpus N` with no WORLD_SIZE starts N ranks itself
+    (torch.distributed.run as a child; ddp_lgcn.py:760-768 mp.spawn) and
+    returns their exit status; under a launcher it runs as a rank."""
+    import bench
+    a = bench.parse(["--gpus", "4", "--steps", "3"])
+    assert bench.needs_launch(a, env={})
+    assert not bench.needs_launch(a, env={"WORLD_SIZE": "4"})
+    assert not bench.needs_launch(bench.parse([]), env={})
+    seen = {}
+
+    class R:
+        returncode = 7
+
+    def runner(cmd, env):
+        seen["cmd"], seen["env"] = cmd, env
+        return R()
+    assert bench.launch(a, ["--gpus", "4", "--steps", "3"], runner=runner) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-3:] == ["--gpus", "4", "--steps", "3"][-3:] and cmd[-4] == "--gpus"
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_bench_self_launch_two_ranks_gloo():
+    """The real process tree on CPU: the parent spawns 2 ranks, they meet
+    over gloo (with the watchdog timeout), rank 0 prints one JSON line."""
+    import json
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                        "--launch-selftest"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    assert json.loads(lines[0]) == {"n_gpus": 2, "sum": 3.0}
+
+
+def test_host_threads_bounded():
+    import bench
+    n = bench.host_threads()
+    assert 1 <= n <= (os.cpu_count() or 1)
