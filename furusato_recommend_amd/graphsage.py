@@ -316,6 +316,10 @@ class GraphSAGE(nn.Module):
             h = new
         return h[0]
 
+    def table_grad_dense(self) -> torch.Tensor:
+        """The id table's gradient after a backward, as a dense [N, d] tensor."""
+        return self._table.grad
+
     def reg_parameters(self):
         """The in-scope parameters in the reference's registration order
         (graphsage.py:96-118): user ids, item ids, then w_linears."""

@@ -177,18 +177,18 @@ def tree_to_adjs(groups, children, L, sizes):
     return n_id, adjs
 
 
-def make_sage_golden(ds, u, i, n_users, m_items):
+def make_sage_golden(ds, u, i, n_users, m_items, d=16, sizes=(4, 3), B=16,
+                     name="sage_d16_L2.npz", decay=1e-2, lr=1e-2):
     from types import SimpleNamespace
 
     from model import graphsage as ref_sage  # noqa: E402
-    L, sizes, d, decay, lr = 2, [4, 3], 16, 1e-2, 1e-2
+    L, sizes = len(sizes), list(sizes)
     rows = [[] for _ in range(n_users + m_items)]
     for a, b in zip(u, i):
         rows[a].append(n_users + b)
         rows[n_users + b].append(a)
     rows = [np.array(r, np.int64) for r in rows]
     rng = np.random.default_rng(21)
-    B = 16
     users = rng.integers(0, n_users, B)
     pos = rng.integers(0, m_items, B)
     neg = rng.integers(0, m_items, B)
@@ -229,13 +229,13 @@ def make_sage_golden(ds, u, i, n_users, m_items):
     flat_groups = np.concatenate([gr[0] for gr in groups])
     group_len = np.array([len(gr[0]) for gr in groups])
     group_depth = np.array([gr[1] for gr in groups])
-    np.savez_compressed(os.path.join(OUT, "sage_d16_L2.npz"), train_user=u, train_item=i,
+    np.savez_compressed(os.path.join(OUT, name), train_user=u, train_item=i,
                         n_users=n_users, m_items=m_items, dim=d, n_layers=L,
                         sizes=np.array(sizes), lr=lr, decay=decay, batch=B, seeds=seeds,
                         groups=flat_groups, group_len=group_len, group_depth=group_depth,
                         emb_out=out.detach().numpy(), loss=float(loss), table0=t0,
                         **w0, **b0, **grads, **after)
-    print("sage", float(loss))
+    print("sage", name, float(loss))
 
 
 def skewed_graph(seed, n, m_per_node, directed):
@@ -343,6 +343,11 @@ def make_sasrec_golden():
 
 
 def main():
+    # optional filter: fixture name prefixes to (re)write, e.g. lgcn_d256_L3 sage_d128
+    only = sys.argv[1:]
+
+    def want(name):
+        return not only or any(name.startswith(o) for o in only)
     sys.dont_write_bytecode = True
     sys.argv = ["make_golden"]
     sys.path.insert(0, REF)
@@ -359,7 +364,9 @@ def main():
     n_users, m_items = 200, 50
     u, i = tiny_graph(1)
     ds = TinyDataset(u, i, n_users, m_items)
-    for dim, L in ((64, 3), (32, 2), (128, 3), (256, 1), (16, 3)):
+    for dim, L in ((64, 3), (32, 2), (128, 3), (256, 1), (16, 3), (256, 3)):
+        if not want(f"lgcn_d{dim}_L{L}"):
+            continue
         cfg = {"recdim": dim, "layer": L, "lr": 1e-3, "decay": 1e-4, "device": "cpu",
                "bpr_batch_size": 64, "r": 0.5}
         g = torch.Generator().manual_seed(dim * 10 + L)
@@ -404,11 +411,23 @@ def main():
         print("lgcn", dim, L, float(loss), float(reg))
 
     # ----------------------------------------------------------- GraphSAGE
-    make_sage_golden(ds, u, i, n_users, m_items)
-
-    make_sasrec_golden()
-
-    make_graph_op_golden()
+    if want("sage_d16_L2"):
+        make_sage_golden(ds, u, i, n_users, m_items)
+    if want("sage_d128_L2"):
+        # C3's model configuration (model/graphsage.py:311-324 with the
+        # ddp_sage.py sizes): d=128, fanout [25, 10], on a graph whose rows
+        # are longer than the fanout (item degree ~60) and shorter (users ~8)
+        n_u3, m_i3 = 1500, 250
+        u3, i3 = tiny_graph(3, n_u3, m_i3, 12_000)
+        make_sage_golden(TinyDataset(u3, i3, n_u3, m_i3), u3, i3, n_u3, m_i3, d=128,
+                         sizes=(25, 10), B=24, name="sage_d128_L2_f25x10.npz",
+                         decay=1e-4, lr=1e-3)
+    if want("sasrec"):
+        make_sasrec_golden()
+    if want("lgconv"):
+        make_graph_op_golden()
+    if only and not any(want(k) for k in ("mf", "sampler", "metrics")):
+        return
 
     # ---------------------------------------------------------------- MF
     cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",

@@ -16,6 +16,8 @@ from tests.conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 TOL = 1e-4
 LGCN = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "lgcn_*.npz")))
+# sage_d16_L2 (fanout [4,3]) and sage_d128_L2_f25x10 (C3: d=128, fanout [25,10])
+SAGE = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "sage_*.npz")))
 
 
 def rel(a, b):
@@ -542,12 +544,13 @@ def sage_from(f, dropout=0.0):
     return m
 
 
-def test_sage_step_matches_reference(golden):
+@pytest.mark.parametrize("name", SAGE)
+def test_sage_step_matches_reference(golden, name):
     """GraphSAGE forward on the reference's sampled tree, its loss, gradients
     (HIP gather/scatter + fanout mean) and one Adam step == the reference's
     own GraphSAGE.forward / loss + torch Adam (dropout off)."""
     from furusato_recommend_amd.graphsage import SampleTree
-    f = golden("sage_d16_L2.npz")
+    f = golden(name)
     m = sage_from(f)
     L, B = int(f["n_layers"]), int(f["batch"])
     groups = [torch.from_numpy(g.astype(np.int32)).cuda()
@@ -559,15 +562,32 @@ def test_sage_step_matches_reference(golden):
     loss = float(m.stageOne(seeds[:B], seeds[B:2 * B] - int(f["n_users"]),
                             seeds[2 * B:] - int(f["n_users"]), tree=tree))
     assert abs(loss - float(f["loss"])) < TOL * abs(float(f["loss"]))
-    assert rel(m._table, f["table_step1"]) < TOL
-    for k, li in enumerate(m.w_linears):
-        assert rel(li.weight, f[f"w{k}_step1"]) < TOL
-        assert rel(li.bias, f[f"b{k}_step1"]) < TOL
+    # Adam's first step is lr * g / (|g| + eps): for |g| near eps it maps
+    # fp32 summation-order noise in g onto the update with a gain of up to
+    # lr * eps / (|g| + eps)^2 (~5e4 at |g| = 4e-9), so the reference's own
+    # CPU arithmetic under another order moves such elements by ~1e-5.
+    # The stepped tensors are compared where the step is well conditioned
+    # (|g_ref| >= 1e-6, gain <= 10); the gradients themselves are compared
+    # everywhere in test_sage_gradients_match_reference, and the Adam kernel
+    # against torch.optim.Adam on this path's own gradient below.
+    pairs = [(m._table, "table_step1", "g_table", "table0")]
+    pairs += [(li.weight, f"w{k}_step1", f"g_w{k}", f"w{k}") for k, li in enumerate(m.w_linears)]
+    pairs += [(li.bias, f"b{k}_step1", f"g_b{k}", f"b{k}") for k, li in enumerate(m.w_linears)]
+    for prm, after, gname, before in pairs:
+        ok = np.abs(f[gname]) >= 1e-6
+        assert ok.mean() > 0.9
+        got = prm.detach().cpu().numpy()
+        assert rel(got[ok], f[after][ok]) < TOL, after
+        ref = torch.nn.Parameter(torch.from_numpy(f[before]).clone())
+        ref.grad = prm.grad.detach().cpu().clone()
+        torch.optim.Adam([ref], lr=float(f["lr"])).step()
+        assert rel(prm, ref) < 1e-6, after
 
 
-def test_sage_gradients_match_reference(golden):
+@pytest.mark.parametrize("name", SAGE)
+def test_sage_gradients_match_reference(golden, name):
     from furusato_recommend_amd.graphsage import SampleTree
-    f = golden("sage_d16_L2.npz")
+    f = golden(name)
     m = sage_from(f)
     L, B = int(f["n_layers"]), int(f["batch"])
     groups = [torch.from_numpy(g.astype(np.int32)).cuda()
@@ -1422,3 +1442,238 @@ def test_sorted_leaf_backward_matches_atomic_and_is_deterministic():
             outs.append(b)
         assert rel(outs[0], a) < 1e-5
         assert torch.equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------------------ C5 / C3 full size
+@pytest.mark.timeout(900)
+def test_c5_full_size_properties():
+    """BASELINE C5 model configuration on one GPU: LightGCN-3 d=256 on the
+    10M users x 1M items / 200M-edge graph (SURVEY §8d recipe).  Size-
+    independent checks: sqrt(deg) is a fixed point of Â, 256 sampled rows vs
+    float64 host sums, and two frontier-pruned training steps equal two
+    full-graph steps (fp32 summation order aside)."""
+    from furusato_recommend_amd import Graph, SyntheticBipartite
+    from furusato_recommend_amd.engine import AdamState, PropagationEngine, sample_triples
+    ds = SyntheticBipartite(10_000_000, 1_000_000, 200_000_000, seed=0, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    del ds
+    N, D = g.n_nodes, 256
+    assert N == 11_000_000 and g.nnz == 400_000_000
+    eng = PropagationEngine(g, D, 3, 2048)
+    x = torch.randn(N, D, device="cuda") * 0.1
+    deg = torch.from_numpy(g.degree().astype(np.float32)).cuda()
+    x[:, 0] = deg.sqrt()
+    y = torch.empty_like(x)
+    eng.propagate_once(x, y)
+    assert rel(y[:, 0], x[:, 0]) < 1e-5
+    rows = np.random.default_rng(1).choice(N, 256, replace=False)
+    rows = np.concatenate([rows, [N - 1, g.n_users - 1, g.n_users]])  # ends of both halves
+    xr = {}
+    rp, col = g.rowptr_host, g.col_host
+    need = np.unique(np.concatenate([col[rp[r]:rp[r + 1]] for r in rows]))
+    xh = dict(zip(need.tolist(), x[torch.from_numpy(need).cuda()].cpu().double().numpy()))
+    dinv = g.dinv.cpu().double().numpy()
+    for r in rows:
+        nb = col[rp[r]:rp[r + 1]]
+        xr[r] = dinv[r] * sum(dinv[j] * xh[int(j)] for j in nb) if len(nb) else np.zeros(D)
+    ref = np.stack([xr[r] for r in rows])
+    assert rel(y[torch.from_numpy(rows).cuda()], ref) < 1e-5
+    del x, y, eng
+    torch.cuda.empty_cache()
+    torch.manual_seed(0)
+    e0 = torch.randn(N, D, device="cuda") * 0.1
+    tables, losses = [], []
+    for prune in (True, False):
+        eng = PropagationEngine(g, D, 3, 2048, prune=prune)
+        e = e0.clone()
+        adam = AdamState(e, 1e-3)
+        u = torch.empty(2048, dtype=torch.int32, device="cuda")
+        p, n = torch.empty_like(u), torch.empty_like(u)
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        ls = []
+        for step in range(2):
+            sample_triples(g, 2048, 7, step * 2048, u, p, n, err)
+            ls.append(float(eng.train_step(e, adam, u, p, n, 1e-4)))
+        assert int(err.item()) == 0
+        # compare on a fixed random subset of rows + every batch row
+        pick = torch.cat([torch.randint(0, N, (200_000,), device="cuda",
+                                        generator=torch.Generator("cuda").manual_seed(3)),
+                          u.long(), p.long() + g.n_users, n.long() + g.n_users])
+        tables.append(e[pick].cpu())
+        losses.append(ls)
+        del eng, e, adam
+        torch.cuda.empty_cache()
+    assert rel(tables[0], tables[1]) < 1e-5
+    assert np.allclose(losses[0], losses[1], rtol=1e-5)
+    assert not torch.equal(tables[0], e0[pick].cpu())
+
+
+@pytest.mark.timeout(600)
+def test_c3_full_size_sorted_vs_atomic_and_learns():
+    """BASELINE C3 model configuration: GraphSAGE 2-hop fanout [25, 10],
+    d=128 on the C2 graph (1M x 100K / 20M).  The deterministic sorted
+    table-gradient path equals the float-atomic one (fp32 order aside) and
+    is bitwise repeatable; training from random init drives the BPR loss
+    down and stays finite."""
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    from furusato_recommend_amd import graphsage as gs
+    ds = SyntheticBipartite(1_000_000, 100_000, 20_000_000, seed=0, test_frac=0)
+    cfg = {"recdim": 128, "layer": 2, "fanouts": [25, 10], "lr": 1e-3, "decay": 1e-7,
+           "device": "cuda:0", "bpr_batch_size": 2048}
+    torch.manual_seed(2020)
+    m = GraphSAGE(cfg, ds)
+    u, p, n = m.sample(2048, seed=7)
+    seeds = torch.cat([u, p + m.n_user, n + m.n_user])
+    tree = m.sample_tree(seeds, 1234)
+    grads = []
+    saved = gs.SORTED_LEAF_BACKWARD
+    try:
+        for mode in (True, True, False):
+            gs.SORTED_LEAF_BACKWARD = mode
+            for q in m.parameters():
+                q.grad = None
+            out = m.forward(tree, dropout_seed=99)
+            B = 2048
+            m.loss(out[:B], out[B:2 * B], out[2 * B:]).backward()
+            grads.append(m.table_grad_dense().clone())
+    finally:
+        gs.SORTED_LEAF_BACKWARD = saved
+    assert torch.equal(grads[0], grads[1])          # deterministic
+    assert rel(grads[2], grads[0]) < 1e-5            # == float-atomic scatter
+    assert float(grads[0].abs().sum()) > 0
+    losses = []
+    for i in range(40):
+        u, p, n = m.sample(2048, seed=11, offset=i * 2048)
+        losses.append(float(m.stageOne(u, p, n)))
+    assert np.all(np.isfinite(losses))
+    assert np.mean(losses[-8:]) < np.mean(losses[:8])
+    assert torch.isfinite(m._table).all()
+
+
+# ------------------------------------------------------------ multi-rank on one GPU
+def _dp_rank_lgcn(rank, world, port, fpath, mode, q):
+    """One rank of the LightGCN data-parallel step on cuda:0 (gloo
+    collectives; RCCL needs a GPU per rank): the real PropagationEngine,
+    disjoint halves of the fixture's triples."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from furusato_recommend_amd.dist import DataParallel, init_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    init_distributed("gloo", rank=rank, world_size=world, timeout_s=120)
+    try:
+        f = dict(np.load(fpath))
+        m = lgcn_from(f)
+        if rank:  # a different init: the constructor broadcast must fix it
+            with torch.no_grad():
+                m.all_embedding.weight.add_(0.5)
+        dp = DataParallel(m.engine, m.all_embedding.weight.data, m.optim, mode=mode)
+        t = torch.from_numpy(f["triples"]).cuda().int()
+        half = t.shape[0] // world
+        mine = t[rank * half:(rank + 1) * half]
+        tabs = []
+        for _ in range(2):
+            dp.step(mine[:, 0].contiguous(), mine[:, 1].contiguous(), mine[:, 2].contiguous(),
+                    float(f["decay"]))
+            tabs.append(m.all_embedding.weight.detach().cpu().numpy().copy())
+        torch.cuda.synchronize()
+        q.put((rank, tabs))
+    finally:
+        dist.destroy_process_group()
+
+
+def _dp_rank_autograd(rank, world, port, kind, q):
+    """One rank of DenseGradDataParallel over the real GraphSAGE / SASRec on
+    cuda:0: every rank steps on its own user shard; the gradient all-reduce
+    must keep the replicas identical."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import torch.distributed as dist
+
+    from furusato_recommend_amd import GraphSAGE, SASRec, SyntheticBipartite
+    from furusato_recommend_amd.dist import DenseGradDataParallel, init_distributed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    init_distributed("gloo", rank=rank, world_size=world, timeout_s=120)
+    try:
+        ds = SyntheticBipartite(20_000, 2_000, 200_000, seed=0)
+        torch.manual_seed(100 + rank)
+        cfg = {"recdim": 64, "layer": 2, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+               "bpr_batch_size": 256, "heads": 2, "fanouts": [10, 5]}
+        m = GraphSAGE(cfg, ds) if kind == "sage" else SASRec(cfg, ds)
+        init = [x.detach().cpu().clone() for x in m.parameters()]
+        dp = DenseGradDataParallel(m)
+        if rank == 0:
+            init = [x.detach().cpu().clone() for x in m.parameters()]
+        batches = []
+        for i in range(3):
+            if kind == "sage":
+                u, p, n = m.sample(256, seed=5, offset=i * 256, shard=rank, n_shards=world)
+            else:
+                g = torch.Generator().manual_seed(1000 * i + rank)
+                u = torch.randint(0, ds.n_users // world, (256,), generator=g) * world + rank
+                p = torch.randint(0, ds.m_items, (256,), generator=g)
+                n = torch.randint(0, ds.m_items, (256,), generator=g)
+            batches.append([x.cpu() for x in (u, p, n)])
+            dp.step(u, p, n)
+        torch.cuda.synchronize()
+        q.put((rank, [x.detach().cpu().numpy().copy() for x in m.parameters()], batches,
+               [x.numpy() for x in init]))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_ranks(target, args, world=2, timeout=300):
+    import multiprocessing as mpp
+    import socket
+    ctx = mpp.get_context("spawn")
+    q = ctx.Queue()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = [ctx.Process(target=target, args=(r, world, port, *args, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = dict((r, rest) for r, *rest in (q.get(timeout=timeout) for _ in range(world)))
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+            if pr.is_alive():
+                pr.kill()
+    assert all(pr.exitcode == 0 for pr in procs)
+    return res
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_data_parallel_two_ranks_hip_engine(golden, mode):
+    """2 ranks (processes) of dist.DataParallel with the real HIP engine on
+    one GPU: replicas bit-identical after each step and equal to the
+    reference's stageOne on the union batch (emb_step1 / emb_step2)."""
+    from tests.conftest import GOLDEN
+    f = golden("lgcn_d64_L3.npz")
+    res = _run_ranks(_dp_rank_lgcn, (os.path.join(GOLDEN, "lgcn_d64_L3.npz"), mode))
+    for k in range(2):
+        assert np.array_equal(res[0][0][k], res[1][0][k])
+        assert rel(res[0][0][k], f[f"emb_step{k + 1}"]) < TOL
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("kind", ["sage", "sasrec"])
+def test_dense_grad_data_parallel_two_ranks(kind):
+    """DenseGradDataParallel over the real GraphSAGE / SASRec, 2 ranks on one
+    GPU: replicas stay bit-identical and move away from the broadcast init."""
+    res = _run_ranks(_dp_rank_autograd, (kind,))
+    p0, p1 = res[0][0], res[1][0]
+    assert len(p0) == len(p1)
+    for a, b in zip(p0, p1):
+        assert np.array_equal(a, b)
+        assert np.all(np.isfinite(a))
+    init0 = res[0][2]
+    assert any(not np.array_equal(a, b) for a, b in zip(p0, init0))

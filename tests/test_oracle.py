@@ -96,10 +96,14 @@ def sage_groups(f):
     return np.split(f["groups"], np.cumsum(f["group_len"])[:-1])
 
 
-def test_sage_matches_reference(golden):
+SAGE = sorted(os.path.basename(p) for p in glob.glob(os.path.join(GOLDEN, "sage_*.npz")))
+
+
+@pytest.mark.parametrize("name", SAGE)
+def test_sage_matches_reference(golden, name):
     """The tree restatement of GraphSAGE.forward / loss == the reference's
     own forward on the equivalent PyG adjacency (model/graphsage.py:311-337)."""
-    f = golden("sage_d16_L2.npz")
+    f = golden(name)
     L, sizes, d = int(f["n_layers"]), [int(x) for x in f["sizes"]], int(f["dim"])
     nu = int(f["n_users"])
     table = torch.nn.Parameter(torch.from_numpy(f["table0"]).clone())
