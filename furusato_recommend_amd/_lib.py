@@ -64,6 +64,16 @@ class Prop(Structure):
     ]
 
 
+class RowGradGroup(Structure):
+    """mirec_row_grad_group_t (one group of table-gradient row contributions)."""
+    _fields_ = [
+        ("ids", c_void_p), ("grad_out", c_void_p), ("n_targets", c_int64), ("k", c_int32),
+        ("mean", c_int32), ("dropout_p", c_float), ("_pad", c_int32), ("seed", c_uint64),
+    ]
+
+
+TABLE_GRAD_MAX_GROUPS = 8
+
 # name -> (restype, argtypes); the single source of truth for the exports
 # test (tests/test_abi.py checks these against include/mirec.h).
 SIGNATURES = {
@@ -132,6 +142,18 @@ SIGNATURES = {
     "mirec_fanout_mean_gather_bwd_sorted": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                                     c_float, c_uint64, c_int32, c_void_p,
                                                     c_void_p, c_size_t, c_void_p]),
+    "mirec_row_grad_group_size": (c_int64, []),
+    "mirec_table_grad_workspace": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
+                                           POINTER(c_size_t)]),
+    "mirec_table_grad_sorted": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
+                                        c_void_p, c_void_p, c_int32, c_void_p, c_size_t,
+                                        c_void_p]),
+    "mirec_table_grad_dense": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32,
+                                       c_int64, c_int32, c_void_p, c_void_p]),
+    "mirec_adam_table_sumsq_floats": (c_int64, [c_int64, c_int32]),
+    "mirec_adam_table": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                 c_void_p, c_int32, c_int64, c_int32, POINTER(AdamH), c_void_p,
+                                 c_void_p, c_void_p]),
     "mirec_attention_fwd": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
                                     c_void_p]),
     "mirec_attention_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,
@@ -198,6 +220,8 @@ def _load():
     want = (ctypes.sizeof(CSR), ctypes.sizeof(Prop), ctypes.sizeof(AdamH))
     if tuple(x.value for x in sizes) != want:
         raise ImportError(f"struct layout mismatch: lib {[x.value for x in sizes]} vs {want}")
+    if lib.mirec_row_grad_group_size() != ctypes.sizeof(RowGradGroup):
+        raise ImportError("struct layout mismatch: mirec_row_grad_group_t")
     return lib
 
 

@@ -8,14 +8,6 @@
 
 namespace mirec {
 
-__device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
-                                      const mirec_adam_hparams_t &h) {
-  m = m + h.one_minus_beta1 * (g - m);
-  v = v * h.beta2 + h.one_minus_beta2 * g * g;
-  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
-  p = p + h.neg_step_size * (m / denom);
-}
-
 // Hyper-parameters by value, or read from device memory when hp != NULL
 // (the *_dev entry points: a captured HIP graph replays with the step's
 // scalars written there by the host before each replay).

@@ -80,9 +80,12 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// Counter-hash dropout shared by the fused kernels: element idx is kept iff
-// the top 32 bits of mix64(key ^ idx) >= thresh = p * 2^32; kept values are
-// scaled by 1 / (1 - p).  The backward recomputes the mask from (seed, idx).
+// Counter-hash dropout shared by the fused kernels: the four elements of an
+// aligned quad (idx >> 2) share one mix64(key + quad); element idx & 3 takes
+// its 16-bit slice and is kept iff slice >= thresh = round(p * 2^16); kept
+// values are scaled by 1 / (1 - p).  The backward recomputes the mask from
+// (seed, idx).  One hash per float4 (the kernels' unit) instead of per
+// element: the hashing was the ALU floor of the dropout-mean gathers.
 __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -91,16 +94,45 @@ __host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 }
 
 __device__ __forceinline__ bool keep(uint64_t key, uint64_t idx, uint32_t thresh) {
-  return (uint32_t)(mix64(key ^ idx) >> 32) >= thresh;
+  const uint64_t h = mix64(key + (idx >> 2));
+  return (uint32_t)((h >> (16 * (idx & 3))) & 0xffffu) >= thresh;
+}
+
+// v * mask * scale for the quad with hash input hq = key + quad index.
+__device__ __forceinline__ float4 drop4_hq(float4 v, uint64_t hq, uint32_t thresh, float scale) {
+  const uint64_t h = mix64(hq);
+  v.x = (uint32_t)(h & 0xffffu) >= thresh ? v.x * scale : 0.f;
+  v.y = (uint32_t)((h >> 16) & 0xffffu) >= thresh ? v.y * scale : 0.f;
+  v.z = (uint32_t)((h >> 32) & 0xffffu) >= thresh ? v.z * scale : 0.f;
+  v.w = (uint32_t)(h >> 48) >= thresh ? v.w * scale : 0.f;
+  return v;
+}
+
+// v * mask * scale for elements idx .. idx + 3 (idx % 4 == 0): one hash.
+__device__ __forceinline__ float4 drop4(float4 v, uint64_t key, uint64_t idx, uint32_t thresh,
+                                        float scale) {
+  return drop4_hq(v, key + (idx >> 2), thresh, scale);
 }
 
 static inline bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
   if (!(p >= 0.f && p < 1.f)) return false;
   *key = mix64(seed ^ 0xA24BAED4963EE407ull);
-  *thresh = (uint32_t)((double)p * 4294967296.0);
+  *thresh = (uint32_t)((double)p * 65536.0 + 0.5);
   *scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   if (p > 0.f && *thresh == 0u) *thresh = 1u;
+  if (*thresh > 65535u) *thresh = 65535u;
   return true;
+}
+
+// One element of torch.optim.Adam (amsgrad=False, weight_decay=0): every
+// Adam kernel uses this one expression, so fused and unfused steps agree
+// bitwise.
+__device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
+                                      const mirec_adam_hparams_t &h) {
+  m = m + h.one_minus_beta1 * (g - m);
+  v = v * h.beta2 + h.one_minus_beta2 * g * g;
+  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
+  p = p + h.neg_step_size * (m / denom);
 }
 
 }  // namespace mirec

@@ -56,15 +56,6 @@ __device__ __forceinline__ uint64_t run_key(uint64_t key, const uint64_t *key_ba
   return key_base ? mix64(key ^ *key_base) : key;
 }
 
-__device__ __forceinline__ float4 drop4(float4 v, uint64_t key, uint64_t e, uint32_t thresh,
-                                        float scale) {
-  v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
-  v.y = keep(key, e + 1, thresh) ? v.y * scale : 0.f;
-  v.z = keep(key, e + 2, thresh) ? v.z * scale : 0.f;
-  v.w = keep(key, e + 3, thresh) ? v.w * scale : 0.f;
-  return v;
-}
-
 __device__ __forceinline__ float4 relu_mask(float4 g, float4 v) {
   return make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f,
                      v.w > 0.f ? g.w : 0.f);

@@ -88,11 +88,7 @@ __global__ __launch_bounds__(256) void fanout_mean_kernel(
     const int64_t row = GATHER ? (int64_t)valid[child] : child;
     float4 v = ld4(x + row * d + c4 * 4);
     if (thresh != 0u) {
-      const uint64_t e = (uint64_t)(child * d + c4 * 4);
-      v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
-      v.y = keep(key, e + 1, thresh) ? v.y * scale : 0.f;
-      v.z = keep(key, e + 2, thresh) ? v.z * scale : 0.f;
-      v.w = keep(key, e + 3, thresh) ? v.w * scale : 0.f;
+      v = drop4(v, key, (uint64_t)(child * d + c4 * 4), thresh, scale);
     }
     acc = f4_add(acc, v);
   }
@@ -118,11 +114,7 @@ __global__ __launch_bounds__(256) void fanout_mean_bwd_kernel(
     }
     g = f4_div(ld4(grad_out + t * d + c4 * 4), (float)cnt);
     if (thresh != 0u) {
-      const uint64_t e = (uint64_t)(child * d + c4 * 4);
-      g.x = keep(key, e, thresh) ? g.x * scale : 0.f;
-      g.y = keep(key, e + 1, thresh) ? g.y * scale : 0.f;
-      g.z = keep(key, e + 2, thresh) ? g.z * scale : 0.f;
-      g.w = keep(key, e + 3, thresh) ? g.w * scale : 0.f;
+      g = drop4(g, key, (uint64_t)(child * d + c4 * 4), thresh, scale);
     }
   }
   st4(grad_x + i * 4, g);
@@ -253,11 +245,7 @@ __global__ __launch_bounds__(256) void fanout_sorted_sum_kernel(
           }
           float4 v = x[u];
           if (thresh != 0u) {
-            const uint64_t e = (uint64_t)((int64_t)ee[u] * d + col);
-            v.x = keep(key, e, thresh) ? v.x * scale : 0.f;
-            v.y = keep(key, e + 1, thresh) ? v.y * scale : 0.f;
-            v.z = keep(key, e + 2, thresh) ? v.z * scale : 0.f;
-            v.w = keep(key, e + 3, thresh) ? v.w * scale : 0.f;
+            v = drop4(v, key, (uint64_t)((int64_t)ee[u] * d + col), thresh, scale);
           }
           acc = f4_add(acc, v);
         }

@@ -1,0 +1,586 @@
+// Deterministic id-table gradient of the GraphSAGE hop path and the Adam
+// step that consumes it without a dense gradient tensor
+// (model/graphsage.py:311-337: the table rows gathered for the sampled tree,
+// the leaf hop's dropout-mean, and the parameter-norm term of the loss; the
+// optimizer step of graphsage.py:388-397).
+//
+// The table gradient of one step is
+//     G[r] = c_slice(r) * W[r]  +  S[r]
+// where c_user / c_item = dL/d|slice| / |slice| come from the norm term
+// (dense: every row) and S is the sum of the row contributions of the tree:
+// the gradient rows of the gathered inner rows, and mask * g_out[t] / cnt_t
+// for every leaf entry (sparse: the rows the tree touched).
+//
+//   mirec_table_grad_sorted  S for every touched row: the entries of all
+//       groups are radix-sorted by row id (stable: each id keeps entry
+//       order) and every run of equal ids is summed in that order — no
+//       float atomics, bitwise repeatable.  The sums are STORED (not added)
+//       into acc[r] and stamp[r] = gen marks the row as touched this step,
+//       so neither buffer is ever cleared.  Pass 1: a group of LPR lanes
+//       owns a chunk of 64 sorted entries and sums every run segment in it,
+//       kBatch rows in flight; runs wholly inside the chunk are final, a
+//       segment continuing into / from a neighbouring chunk goes to that
+//       chunk's partial slot.  Pass 2: the chunk holding a crossing run's
+//       head adds the partials of the chunks the run covers, in chunk order
+//       (a hub id in 10^5 entries is 1.5 K partial rows, read LPR at a time,
+//       not a serial walk over its entries).
+//   mirec_adam_table   Adam over the whole table with G formed on the fly
+//       (W, m, v read once, written once; S read for stamped rows only) —
+//       the dense gradient is never written.  Optionally the sums of squares
+//       of the updated user / item slices (next step's norm term) per block.
+//   mirec_table_grad_dense   G materialised (the data-parallel path, which
+//       all-reduces it before the dense Adam).
+#include <algorithm>
+
+#include <hipcub/hipcub.hpp>
+
+#include "common.h"
+
+#ifndef MIREC_TG_CHUNK
+#define MIREC_TG_CHUNK 8
+#endif
+
+namespace mirec {
+
+constexpr int kMaxGroups = MIREC_TABLE_GRAD_MAX_GROUPS;
+constexpr int kCh = MIREC_TG_CHUNK;  // sorted entries per chunk (pass 1 loads them at once)
+constexpr int kBatch = 8;            // partial rows in flight per lane in pass 2
+constexpr int32_t kEnd = 0x7fffffff;
+
+struct GroupArgs {
+  int64_t ent_off[kMaxGroups + 1];  // entry offsets of the groups
+  int64_t tgt_off[kMaxGroups + 1];  // target offsets (weight table)
+  const int32_t *ids[kMaxGroups];
+  const float *grad[kMaxGroups];
+  uint64_t key[kMaxGroups];
+  uint32_t thresh[kMaxGroups];
+  float scale[kMaxGroups];
+  int32_t k[kMaxGroups];
+  int32_t mean[kMaxGroups];
+  int32_t n_groups;
+};
+
+// Group of a global entry / target index (unrolled selects: the argument
+// struct is never indexed dynamically, which would spill it to scratch).
+__device__ __forceinline__ int group_of(const int64_t (&off)[kMaxGroups + 1], int n_groups,
+                                        int64_t x) {
+  int g = 0;
+#pragma unroll
+  for (int q = 1; q < kMaxGroups; ++q) g += (q < n_groups && x >= off[q]) ? 1 : 0;
+  return g;
+}
+
+template <typename T, int N>
+__device__ __forceinline__ T pick(const T (&a)[N], int g) {
+  T r = a[0];
+#pragma unroll
+  for (int q = 1; q < N; ++q) r = (g == q) ? a[q] : r;
+  return r;
+}
+
+// The LPR low bits (all 64 for LPR = 64).
+template <int LPR>
+__device__ __forceinline__ unsigned long long low_bits() {
+  if constexpr (LPR == 64) return ~0ull;
+  else return (1ull << LPR) - 1ull;
+}
+
+// keys[c] = row id of entry c (n_rows for an invalid child: sorts last),
+// vals[c] = c; wt[t] = the weight of target t (1/cnt over its valid children
+// for a mean group, else 1).
+__global__ __launch_bounds__(256) void tg_prep_kernel(GroupArgs ga, int64_t n_ent, int64_t n_tgt,
+                                                      int32_t n_rows, int32_t *__restrict__ keys,
+                                                      int32_t *__restrict__ vals,
+                                                      float *__restrict__ wt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_ent) {
+    const int g = group_of(ga.ent_off, ga.n_groups, i);
+    const int32_t id = pick(ga.ids, g)[i - pick(ga.ent_off, g)];
+    keys[i] = (id >= 0 && id < n_rows) ? id : n_rows;
+    vals[i] = (int32_t)i;
+  }
+  if (i < n_tgt) {
+    const int g = group_of(ga.tgt_off, ga.n_groups, i);
+    const int64_t t = i - pick(ga.tgt_off, g);
+    const int k = pick(ga.k, g);
+    const int32_t *ids = pick(ga.ids, g) + t * k;
+    int cnt = 0;
+    for (int c = 0; c < k; ++c) cnt += ids[c] >= 0 ? 1 : 0;
+    wt[i] = pick(ga.mean, g) ? (cnt > 0 ? 1.f / (float)cnt : 0.f) : 1.f;
+  }
+}
+
+// Pass 1.  A group of LPR lanes (LPR >= kCh; d <= 4 LPR, or LPR = 64 with a
+// column loop) owns a chunk of kCh sorted entries.  Lane j < kCh loads and
+// decodes entry j (row id, grad row, weight, dropout element); the group then
+// fetches all kCh rows at once (ids broadcast by shuffle), weights and masks
+// them while they are in flight, and adds them in entry order.  Short chunks
+// keep many rows in flight chip-wide (the gathers are latency-bound: most
+// rows come from the L2 / Infinity Cache); runs that cross chunks go through
+// the partial slots and pass 2.
+template <int LPR>
+__global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
+                                                     const int32_t *__restrict__ vals,
+                                                     const float *__restrict__ wt, int64_t n,
+                                                     int32_t d, int32_t n_rows,
+                                                     float *__restrict__ acc_out,
+                                                     int32_t *__restrict__ stamp, int32_t gen,
+                                                     float *__restrict__ part) {
+  static_assert(LPR >= kCh, "chunk layout: one entry per lane");
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const int base = lane - sub;
+  const int64_t chunk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int64_t beg = chunk * kCh;
+  if (beg >= n) return;  // the whole group leaves together
+  const int64_t end = beg + kCh < n ? beg + kCh : n;
+  const int32_t kprev = beg > 0 ? keys[beg - 1] : -1;
+  const int32_t knext = end < n ? keys[end] : -1;
+  // decode entry beg + sub: row id, grad row address, hash base of its
+  // dropout quads (key + first quad), threshold, weight (x dropout scale)
+  const int64_t pe = beg + sub;
+  const int32_t km = (sub < kCh && pe < end) ? keys[pe] : kEnd;
+  uint64_t am = 0, hm = 0;
+  uint32_t thm = 0;
+  float wm = 0.f;
+  if (km < n_rows) {
+    const int32_t v = vals[pe];
+    const int g = group_of(ga.ent_off, ga.n_groups, v);
+    const int32_t e = v - (int32_t)pick(ga.ent_off, g);
+    const int32_t t = e / pick(ga.k, g);
+    thm = pick(ga.thresh, g);
+    const float w = wt[pick(ga.tgt_off, g) + t];
+    wm = thm ? w * pick(ga.scale, g) : w;
+    am = (uint64_t)(pick(ga.grad, g) + (int64_t)t * d);
+    hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
+  }
+  const int32_t first = __shfl(km, base);
+  if (first >= n_rows) return;  // only invalid entries from here on
+  const uint32_t am_lo = (uint32_t)am, am_hi = (uint32_t)(am >> 32);
+  const uint32_t hm_lo = (uint32_t)hm, hm_hi = (uint32_t)(hm >> 32);
+  for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
+    const int col = c0 + 4 * sub;
+    const bool act = col < d;
+    // all kCh rows in flight; weight and mask are applied after the loads
+    // (their inputs re-broadcast) so only the rows stay live meanwhile
+    float4 x[kCh];
+    int32_t kk[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int src = base + u;
+      kk[u] = __shfl(km, src);
+      const uint64_t a = (uint64_t)(uint32_t)__shfl((int)am_lo, src) |
+                         ((uint64_t)(uint32_t)__shfl((int)am_hi, src) << 32);
+      x[u] = (act && kk[u] < n_rows) ? ld4(reinterpret_cast<const float *>(a) + col)
+                                     : f4_zero();
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int src = base + u;
+      const uint32_t th = (uint32_t)__shfl((int)thm, src);
+      const float w = __shfl(wm, src);
+      if (th != 0u) {
+        const uint64_t hq = ((uint64_t)(uint32_t)__shfl((int)hm_lo, src) |
+                             ((uint64_t)(uint32_t)__shfl((int)hm_hi, src) << 32)) +
+                            (uint64_t)(col >> 2);
+        x[u] = drop4_hq(x[u], hq, th, w);
+      } else {
+        x[u] = f4_scale(w, x[u]);
+      }
+    }
+    int32_t cur = first;
+    int64_t seg_beg = beg;
+    float4 acc = f4_zero();
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u <= kCh; ++u) {
+      const int64_t pos = beg + u;
+      const int32_t ku = u < kCh ? kk[u] : kEnd;
+      if (!done && (pos >= end || ku != cur)) {
+        // segment [seg_beg, pos) of id cur ends
+        const bool cont_prev = seg_beg == beg && kprev == cur;
+        const bool cont_next = pos == end && knext == cur;
+        float *dst;
+        if (!cont_prev && !cont_next) {
+          dst = acc_out + (int64_t)cur * d;
+          if (sub == 0 && c0 == 0) stamp[cur] = gen;
+        } else {
+          dst = part + (2 * chunk + (cont_prev ? 0 : 1)) * (int64_t)d;
+        }
+        if (act) st4(dst + col, acc);
+        if (pos >= end || ku >= n_rows) {
+          done = true;
+        } else {
+          cur = ku;
+          seg_beg = pos;
+          acc = f4_zero();
+        }
+      }
+      if (!done && u < kCh) acc = f4_add(acc, x[u]);
+    }
+  }
+}
+
+// Pass 2: the group of the chunk holding a crossing run's head adds the
+// partials of the chunks the run covers, in chunk order, and stores the sum.
+template <int LPR>
+__global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict__ keys, int64_t n,
+                                                       int32_t d, int32_t n_rows,
+                                                       const float *__restrict__ part,
+                                                       float *__restrict__ acc_out,
+                                                       int32_t *__restrict__ stamp, int32_t gen) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const int base = lane - sub;
+  const int64_t chunk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int64_t n_chunks = (n + kCh - 1) / kCh;
+  const int64_t beg = chunk * kCh;
+  if (beg >= n) return;
+  const int64_t end = beg + kCh;
+  if (end >= n) return;  // no next chunk
+  const int32_t klast = keys[end - 1];
+  if (klast >= n_rows || keys[end] != klast) return;  // last segment stays inside
+  if (beg > 0 && keys[beg - 1] == klast) return;       // the run's head is earlier
+  const unsigned long long gmask = low_bits<LPR>() << base;
+  for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
+    const int col = c0 + 4 * sub;
+    const bool act = col < d;
+    float4 sum = act ? ld4(part + (2 * chunk + 1) * (int64_t)d + col) : f4_zero();
+    int64_t cc = chunk + 1;  // chunks cc.. hold the run's continuation
+    while (true) {
+      // lane j: does the run cover all of chunk cc + j and continue past it?
+      const int64_t cj = cc + sub;
+      const int64_t ej = (cj + 1) * kCh;
+      const bool full = cj < n_chunks && ej < n && keys[ej] == klast;
+      const unsigned long long bal = (__ballot(full) & gmask) >> base;
+      const unsigned long long low = low_bits<LPR>();
+      // consecutive full chunks from cc
+      const int nfull = bal == low ? LPR : (int)__builtin_ctzll(~bal);
+      const int take = nfull < LPR ? nfull + 1 : LPR;  // + the chunk holding the tail
+      for (int j0 = 0; j0 < take; j0 += kBatch) {
+        float4 x[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+          x[u] = (act && j0 + u < take) ? ld4(part + (2 * (cc + j0 + u)) * (int64_t)d + col)
+                                        : f4_zero();
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u)
+          if (j0 + u < take) sum = f4_add(sum, x[u]);
+      }
+      if (nfull < LPR) break;
+      cc += LPR;
+    }
+    if (act) st4(acc_out + (int64_t)klast * d + col, sum);
+  }
+  if (sub == 0) stamp[klast] = gen;
+}
+
+// ------------------------------------------------------------ consumers
+// G = c * W[r] + (S[r] if row r was touched this step, else 0), float4 at
+// offset off: one explicit fma per element, so the fused Adam and the
+// materialised gradient round identically.
+__device__ __forceinline__ float4 table_grad4(float4 w, const float *__restrict__ acc,
+                                              const int32_t *__restrict__ stamp, int32_t gen,
+                                              int64_t r, int64_t off, float c) {
+  const float4 s = stamp[r] == gen ? ld4(acc + off) : f4_zero();
+  return make_float4(fmaf(c, w.x, s.x), fmaf(c, w.y, s.y), fmaf(c, w.z, s.z), fmaf(c, w.w, s.w));
+}
+
+// Row of float4 element i: a shift when d/4 is a power of two (the table
+// widths in use), else a division.
+__device__ __forceinline__ int64_t row_of(int64_t i, int32_t d4, int32_t shift) {
+  return shift >= 0 ? (i >> shift) : i / d4;
+}
+
+__global__ __launch_bounds__(256) void tg_dense_kernel(const float *__restrict__ table,
+                                                       const float *__restrict__ coef,
+                                                       int64_t n_user, const float *__restrict__ acc,
+                                                       const int32_t *__restrict__ stamp,
+                                                       int32_t gen, int64_t n_rows, int32_t d4,
+                                                       int32_t shift, float *__restrict__ grad) {
+  const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
+  const int64_t n4 = n_rows * d4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row_of(i, d4, shift);
+    const float4 w = ld4(table + 4 * i);
+    st4(grad + 4 * i, table_grad4(w, acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci));
+  }
+}
+
+__global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
+                                                      float *__restrict__ m, float *__restrict__ v,
+                                                      const float *__restrict__ coef, int64_t n_user,
+                                                      const float *__restrict__ acc,
+                                                      const int32_t *__restrict__ stamp,
+                                                      int32_t gen, int64_t n_rows, int32_t d4,
+                                                      int32_t shift, mirec_adam_hparams_t h,
+                                                      float *__restrict__ sumsq) {
+  __shared__ float red[2][256];
+  const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
+  const int64_t n4 = n_rows * d4;
+  float su = 0.f, si = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = row_of(i, d4, shift);
+    float4 p = ld4(param + 4 * i), a = ld4(m + 4 * i), b = ld4(v + 4 * i);
+    const float4 g = table_grad4(p, acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci);
+    adam1(p.x, a.x, b.x, g.x, h);
+    adam1(p.y, a.y, b.y, g.y, h);
+    adam1(p.z, a.z, b.z, g.z, h);
+    adam1(p.w, a.w, b.w, g.w, h);
+    st4(param + 4 * i, p);
+    st4(m + 4 * i, a);
+    st4(v + 4 * i, b);
+    const float s = p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
+    if (r < n_user) su += s;
+    else si += s;
+  }
+  if (sumsq == nullptr) return;
+  red[0][threadIdx.x] = su;
+  red[1][threadIdx.x] = si;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sumsq[2 * blockIdx.x] = red[0][0];
+    sumsq[2 * blockIdx.x + 1] = red[1][0];
+  }
+}
+
+// norms[0..1] = sqrt of the block partials summed in a fixed order: 1024
+// threads, thread j adds partials j, j + 1024, ... (8 loads in flight), then
+// a tree over the threads.
+__global__ __launch_bounds__(1024) void tg_norm_final_kernel(const float *__restrict__ sumsq,
+                                                             int64_t blocks,
+                                                             float *__restrict__ norms) {
+  __shared__ float red[2][1024];
+  float a = 0.f, b = 0.f;
+  for (int64_t k0 = threadIdx.x; k0 < blocks; k0 += 8 * 1024) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t k = k0 + (int64_t)u * 1024;
+      v[u] = k < blocks ? *reinterpret_cast<const float2 *>(sumsq + 2 * k) : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      a += v[u].x;
+      b += v[u].y;
+    }
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = 512; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    norms[0] = sqrtf(red[0][0]);
+    norms[1] = sqrtf(red[1][0]);
+  }
+}
+
+// ------------------------------------------------------------ host side
+static int lanes_per_row(int32_t d) {
+  const int d4 = (d + 3) / 4;
+  int l = kCh;  // pass 1: one entry per lane of a group
+  while (l < d4 && l < 64) l <<= 1;
+  return l;
+}
+
+struct TgLayout {
+  int64_t n_ent, n_tgt, n_chunks;
+  size_t keys_in, keys_out, vals_in, vals_out, wt, part, sort, sort_bytes, total;
+  int end_bit;
+};
+
+static int tg_layout(const mirec_row_grad_group_t *groups, int32_t n_groups, int32_t n_rows,
+                     int32_t dim, TgLayout *L) {
+  MIREC_CHECK_ARG(n_groups >= 1 && n_groups <= kMaxGroups && n_rows > 0 && dim > 0 &&
+                  dim % 4 == 0 && groups);
+  int64_t n_ent = 0, n_tgt = 0;
+  for (int g = 0; g < n_groups; ++g) {
+    const mirec_row_grad_group_t &q = groups[g];
+    MIREC_CHECK_ARG(q.n_targets >= 0 && q.k >= 1 && q.dropout_p >= 0.f && q.dropout_p < 1.f);
+    n_ent += q.n_targets * q.k;
+    n_tgt += q.n_targets;
+  }
+  MIREC_CHECK_ARG(n_ent < ((int64_t)1 << 31) - kCh);
+  const auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  L->n_ent = n_ent;
+  L->n_tgt = n_tgt;
+  L->n_chunks = (n_ent + kCh - 1) / kCh;
+  const size_t seg = up(sizeof(int32_t) * std::max<int64_t>(n_ent, 1));
+  L->keys_in = 0;
+  L->keys_out = seg;
+  L->vals_in = 2 * seg;
+  L->vals_out = 3 * seg;
+  L->wt = 4 * seg;
+  L->part = L->wt + up(sizeof(float) * std::max<int64_t>(n_tgt, 1));
+  L->sort = L->part + up(sizeof(float) * 2 * std::max<int64_t>(L->n_chunks, 1) * dim);
+  int bits = 1;
+  while (bits < 31 && ((int64_t)1 << bits) <= n_rows) ++bits;
+  L->end_bit = bits;
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (int32_t *)nullptr, (int32_t *)nullptr,
+                                           (int32_t *)nullptr, (int32_t *)nullptr,
+                                           (int)std::max<int64_t>(n_ent, 1), 0, bits);
+  L->sort_bytes = tb;
+  L->total = L->sort + up(tb);
+  return MIREC_OK;
+}
+
+}  // namespace mirec
+
+using namespace mirec;
+
+extern "C" int64_t mirec_row_grad_group_size(void) {
+  return (int64_t)sizeof(mirec_row_grad_group_t);
+}
+
+extern "C" int mirec_table_grad_workspace(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                                          int32_t n_rows, int32_t dim, size_t *bytes) {
+  MIREC_CHECK_ARG(bytes);
+  TgLayout L;
+  const int rc = tg_layout(groups, n_groups, n_rows, dim, &L);
+  if (rc != MIREC_OK) return rc;
+  *bytes = L.total;
+  return MIREC_OK;
+}
+
+extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                                       int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
+                                       int32_t gen, void *workspace, size_t workspace_bytes,
+                                       mirec_stream_t stream) {
+  TgLayout L;
+  const int rc = tg_layout(groups, n_groups, n_rows, dim, &L);
+  if (rc != MIREC_OK) return rc;
+  MIREC_CHECK_ARG(acc && stamp);
+  if (L.n_ent == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(workspace);
+  if (workspace_bytes < L.total) return MIREC_ERR_WORKSPACE;
+  GroupArgs ga = {};
+  ga.n_groups = n_groups;
+  for (int g = 0; g < kMaxGroups; ++g) {
+    const bool real = g < n_groups;
+    const mirec_row_grad_group_t *q = real ? &groups[g] : nullptr;
+    ga.ent_off[g + 1] = ga.ent_off[g] + (real ? q->n_targets * q->k : 0);
+    ga.tgt_off[g + 1] = ga.tgt_off[g] + (real ? q->n_targets : 0);
+    ga.ids[g] = real ? q->ids : nullptr;
+    ga.grad[g] = real ? q->grad_out : nullptr;
+    ga.k[g] = real ? q->k : 1;
+    ga.mean[g] = real ? q->mean : 0;
+    uint64_t key = 0;
+    uint32_t th = 0;
+    float sc = 1.f;
+    if (real) {
+      MIREC_CHECK_ARG(q->n_targets == 0 || (q->ids && q->grad_out));
+      MIREC_CHECK_ARG(dropout_params(q->dropout_p, q->seed, &key, &th, &sc));
+    }
+    ga.key[g] = key;
+    ga.thresh[g] = th;
+    ga.scale[g] = sc;
+  }
+  char *ws = static_cast<char *>(workspace);
+  int32_t *keys_in = reinterpret_cast<int32_t *>(ws + L.keys_in);
+  int32_t *keys_out = reinterpret_cast<int32_t *>(ws + L.keys_out);
+  int32_t *vals_in = reinterpret_cast<int32_t *>(ws + L.vals_in);
+  int32_t *vals_out = reinterpret_cast<int32_t *>(ws + L.vals_out);
+  float *wt = reinterpret_cast<float *>(ws + L.wt);
+  float *part = reinterpret_cast<float *>(ws + L.part);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nprep = std::max(L.n_ent, L.n_tgt);
+  hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
+                     L.n_ent, L.n_tgt, n_rows, keys_in, vals_in, wt);
+  MIREC_LAUNCH_CHECK();
+  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.sort, L.sort_bytes, keys_in, keys_out,
+                                               vals_in, vals_out, (int)L.n_ent, 0, L.end_bit, st));
+  const int lpr = lanes_per_row(dim);
+  const int64_t threads = L.n_chunks * lpr;
+  const dim3 grid((unsigned)((threads + 255) / 256));
+#define MIREC_TG_LAUNCH(LP)                                                                   \
+  case LP:                                                                                   \
+    hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga, keys_out, vals_out, wt, \
+                       L.n_ent, dim, n_rows, acc, stamp, gen, part);                          \
+    MIREC_LAUNCH_CHECK();                                                                    \
+    hipLaunchKernelGGL(tg_fixup_kernel<LP>, grid, dim3(256), 0, st, keys_out, L.n_ent, dim,   \
+                       n_rows, part, acc, stamp, gen);                                       \
+    MIREC_LAUNCH_CHECK();                                                                    \
+    break;
+  switch (lpr) {
+    MIREC_TG_LAUNCH(16)
+    MIREC_TG_LAUNCH(32)
+    MIREC_TG_LAUNCH(64)
+    default:
+      return MIREC_ERR_ARG;
+  }
+#undef MIREC_TG_LAUNCH
+  return MIREC_OK;
+}
+
+static int32_t pow2_shift(int32_t d4) {
+  for (int s = 0; s < 31; ++s)
+    if ((1 << s) == d4) return s;
+  return -1;
+}
+
+static unsigned tg_blocks(int64_t n4) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 65536));
+}
+
+extern "C" int64_t mirec_adam_table_sumsq_floats(int64_t n_rows, int32_t dim) {
+  if (n_rows < 0 || dim <= 0 || dim % 4) return -1;
+  return 2 * (int64_t)tg_blocks(n_rows * (dim / 4));
+}
+
+extern "C" int mirec_table_grad_dense(const float *table, const float *coef, int64_t n_user,
+                                      const float *acc, const int32_t *stamp, int32_t gen,
+                                      int64_t n_rows, int32_t dim, float *grad,
+                                      mirec_stream_t stream) {
+  MIREC_CHECK_ARG(table && acc && stamp && grad && n_rows >= 0 && dim > 0 && dim % 4 == 0 &&
+                  n_user >= 0 && n_user <= n_rows);
+  MIREC_CHECK_ARG(((uintptr_t)table | (uintptr_t)acc | (uintptr_t)grad) % 16 == 0);
+  if (n_rows == 0) return MIREC_OK;
+  const int64_t n4 = n_rows * (dim / 4);
+  hipLaunchKernelGGL(tg_dense_kernel, dim3(tg_blocks(n4)), dim3(256), 0, (hipStream_t)stream,
+                     table, coef, n_user, acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4),
+                     grad);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
+                                int64_t n_user, const float *acc, const int32_t *stamp,
+                                int32_t gen, int64_t n_rows, int32_t dim,
+                                const mirec_adam_hparams_t *h, float *sumsq, float *norms,
+                                mirec_stream_t stream) {
+  MIREC_CHECK_ARG(param && exp_avg && exp_avg_sq && acc && stamp && h && n_rows >= 0 &&
+                  dim > 0 && dim % 4 == 0 && n_user >= 0 && n_user <= n_rows);
+  MIREC_CHECK_ARG(((uintptr_t)param | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq |
+                   (uintptr_t)acc) % 16 == 0);
+  MIREC_CHECK_ARG((sumsq == nullptr) == (norms == nullptr));
+  if (n_rows == 0) return MIREC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n4 = n_rows * (dim / 4);
+  const unsigned blocks = tg_blocks(n4);
+  hipLaunchKernelGGL(tg_adam_kernel, dim3(blocks), dim3(256), 0, st, param, exp_avg, exp_avg_sq,
+                     coef, n_user, acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4), *h,
+                     sumsq);
+  MIREC_LAUNCH_CHECK();
+  if (norms) {
+    hipLaunchKernelGGL(tg_norm_final_kernel, dim3(1), dim3(1024), 0, st, sumsq, (int64_t)blocks,
+                       norms);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}

@@ -129,6 +129,11 @@ class DenseGradDataParallel:
         self.distributed = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
+        tg = getattr(model, "_tg", None)
+        if tg is not None and self.world > 1:
+            # GraphSAGE's sorted table gradient: materialise it as .grad so it
+            # can be all-reduced (the fused table Adam needs the local S only)
+            tg.dense = True
         if self.world > 1:
             for p in model.parameters():
                 dist.broadcast(p.data, src=0, group=group)

@@ -29,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import engine as _engine
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamGroup, AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
@@ -36,9 +37,79 @@ from .linear import Linear
 from .rows import slice_norms
 
 
-# The leaf hop's backward: sorted by child id (True: deterministic, no
-# atomics) or float-atomic scatter (False; A/B timing).
+# The id table's backward: the deterministic sorted form (True: every row
+# contribution of the tree sorted by row id and summed in entry order, Adam
+# fused on top, no dense gradient written) or the float-atomic scatter into a
+# dense gradient (False; A/B timing, tools/bench_sage.py --leaf-bwd atomic).
 SORTED_LEAF_BACKWARD = True
+
+
+class TableGrad:
+    """The table gradient of one step in the sorted form (csrc/tablegrad.hip):
+    G = c[slice] * table + S, with S stored in ``acc`` for the rows whose
+    ``stamp`` equals ``gen`` (never cleared) and c = (c_user, c_item) the
+    norm-term coefficients on the device.  ``dense`` selects whether the
+    backward also materialises G as the table's .grad (data parallelism,
+    which all-reduces it) or leaves it to ``adam`` (single GPU)."""
+
+    def __init__(self, n_rows: int, n_user: int, dim: int, device):
+        self.n_rows, self.n_user, self.dim = int(n_rows), int(n_user), int(dim)
+        self.acc = torch.empty(n_rows, dim, device=device)
+        self.stamp = torch.zeros(n_rows, dtype=torch.int32, device=device)
+        self.coef = torch.zeros(2, device=device)
+        self.gen = 0
+        self.pending = False  # S / coef of the last backward not yet consumed
+        self.dense = False
+        self._ws = None
+
+    def accumulate(self, groups):
+        """groups: [(ids int32, grad_out [n_t, d], k, mean, dropout p, seed)]."""
+        n = len(groups)
+        if not 1 <= n <= _lib.TABLE_GRAD_MAX_GROUPS:
+            raise ValueError("table gradient: 1..8 row groups")
+        arr = (_lib.RowGradGroup * n)()
+        keep = []
+        for a, (ids, g, k, mean, p, seed) in zip(arr, groups):
+            g = g.contiguous()
+            keep.append(g)
+            a.ids, a.grad_out = ids.data_ptr(), g.data_ptr()
+            a.n_targets, a.k, a.mean = ids.numel() // k, int(k), int(mean)
+            a.dropout_p, a.seed = float(p), int(seed)
+        nb = ctypes.c_size_t()
+        check(lib.mirec_table_grad_workspace(arr, n, self.n_rows, self.dim, ctypes.byref(nb)),
+              "table_grad_workspace")
+        if self._ws is None or self._ws.numel() < nb.value:
+            self._ws = torch.empty(nb.value, dtype=torch.uint8, device=self.acc.device)
+        self.gen += 1
+        check(lib.mirec_table_grad_sorted(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
+                                          self.stamp.data_ptr(), self.gen, self._ws.data_ptr(),
+                                          self._ws.numel(), _lib.stream_handle()),
+              "table_grad_sorted")
+        self.pending = True
+
+    def materialize(self, table: torch.Tensor) -> torch.Tensor:
+        """G as a dense [N, d] tensor."""
+        grad = torch.empty_like(table)
+        check(lib.mirec_table_grad_dense(table.data_ptr(), self.coef.data_ptr(), self.n_user,
+                                         self.acc.data_ptr(), self.stamp.data_ptr(), self.gen,
+                                         self.n_rows, self.dim, grad.data_ptr(),
+                                         _lib.stream_handle()), "table_grad_dense")
+        return grad
+
+    def adam(self, state: AdamState, norms: torch.Tensor | None = None):
+        """One Adam step of the table with G formed in the kernel; writes the
+        updated slices' norms to ``norms`` (2 floats) if given."""
+        hp = state.next_hparams()
+        sumsq = None
+        if norms is not None:
+            sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(self.n_rows, self.dim)),
+                                device=self.acc.device)
+        check(lib.mirec_adam_table(state.param.data_ptr(), state.exp_avg.data_ptr(),
+                                   state.exp_avg_sq.data_ptr(), self.coef.data_ptr(), self.n_user,
+                                   self.acc.data_ptr(), self.stamp.data_ptr(), self.gen,
+                                   self.n_rows, self.dim, ctypes.byref(hp), _lib.ptr(sumsq),
+                                   _lib.ptr(norms), _lib.stream_handle()), "adam_table")
+        self.pending = False
 
 
 # ----------------------------------------------------------------- autograd
@@ -50,15 +121,19 @@ class _TableTerms(torch.autograd.Function):
         layer 0) the parent's dropout-mean over its children's table rows,
         gathered and averaged in one pass (mirec_fanout_mean_gather) — the
         leaf rows, ~90 % of a [25, 10] tree, are never materialised,
-      * the norms of the user and item slices (graphsage.py:326-337).
-    The backward writes the table gradient once — [g_u u/|u| ; g_i i/|i|] as
-    one dense pass — and scatter-adds the inner row gradients and the leaf
-    means' gradients into it (float atomics), instead of autograd
-    materialising and summing full-size tensors.
+      * the norms of the user and item slices (graphsage.py:326-337; reused
+        from the previous step's fused Adam when the table is unchanged).
+    Backward, sorted form (``sink`` given): the inner row gradients and every
+    leaf entry's mask * g_out[t] / cnt_t are sorted by row id and summed in
+    entry order (mirec_table_grad_sorted) and the norm coefficients are kept
+    on the device — the dense gradient is formed inside the Adam kernel, or
+    materialised for data parallelism.  Atomic form (``sink`` None): the
+    dense gradient [g_u u/|u| ; g_i i/|i|] is written, then the row
+    gradients are scatter-added with float atomics.
     ``leaves`` = ((ids, k, dropout p, seed), ...)."""
 
     @staticmethod
-    def forward(ctx, table, ids, n_user: int, leaves):
+    def forward(ctx, table, ids, n_user: int, leaves, sink, norms):
         n, d = ids.numel(), table.shape[1]
         st = _lib.stream_handle()
         rows = torch.empty(n, d, dtype=table.dtype, device=table.device)
@@ -72,11 +147,15 @@ class _TableTerms(torch.autograd.Function):
                                                float(p), ctypes.c_uint64(seed), out.data_ptr(),
                                                st), "fanout_mean_gather")
             aggrs.append(out)
-        nu, ni = slice_norms(table, n_user)  # both slices in one pass
+        if norms is None:
+            nu, ni = slice_norms(table, n_user)  # both slices in one pass
+        else:
+            nu, ni = norms[0], norms[1]
         ctx.save_for_backward(table, ids, nu, ni, *[l[0] for l in leaves])
         ctx.leaf_cfg = [(k, p, seed) for _, k, p, seed in leaves]
         ctx.n_user = n_user
-        return (rows, nu, ni, *aggrs)
+        ctx.sink = sink
+        return (rows, nu.clone(), ni.clone(), *aggrs)
 
     @staticmethod
     def backward(ctx, g_rows, g_nu, g_ni, *g_aggrs):
@@ -84,11 +163,26 @@ class _TableTerms(torch.autograd.Function):
         k = ctx.n_user
         d = table.shape[1]
         st = _lib.stream_handle()
-        grad = torch.empty_like(table)
         zero = torch.zeros_like(nu)
         # d|x|/dx = x/|x| (0 for a zero slice, as torch's norm backward)
         cu = zero if g_nu is None else torch.where(nu > 0, g_nu / nu, zero)
         ci = zero if g_ni is None else torch.where(ni > 0, g_ni / ni, zero)
+        sink = ctx.sink
+        if sink is not None:
+            torch.stack([cu, ci], out=sink.coef)
+            groups = []
+            if g_rows is not None:
+                groups.append((ids, g_rows, 1, 0, 0.0, 0))
+            for g, lid, (kk, p, seed) in zip(g_aggrs, leaf_ids, ctx.leaf_cfg):
+                if g is not None:
+                    groups.append((lid, g, kk, 1, p, seed))
+            if groups:
+                sink.accumulate(groups)
+            else:  # S = 0: a fresh generation stamps nothing
+                sink.gen += 1
+                sink.pending = True
+            return (sink.materialize(table) if sink.dense else None), None, None, None, None, None
+        grad = torch.empty_like(table)
         torch.mul(table[:k], cu, out=grad[:k])
         torch.mul(table[k:], ci, out=grad[k:])
         if g_rows is not None:
@@ -99,23 +193,11 @@ class _TableTerms(torch.autograd.Function):
             if g is None:
                 continue
             n_t = lid.numel() // kk
-            if SORTED_LEAF_BACKWARD:
-                # entries sorted by child id, one ordered sum per row: no
-                # float atomics, deterministic
-                nb = ctypes.c_size_t()
-                check(lib.mirec_fanout_mean_gather_bwd_sorted_workspace(
-                    n_t, kk, table.shape[0], ctypes.byref(nb)), "fanout_sorted_workspace")
-                ws = torch.empty(nb.value, dtype=torch.uint8, device=table.device)
-                check(lib.mirec_fanout_mean_gather_bwd_sorted(
-                    g.contiguous().data_ptr(), lid.data_ptr(), n_t, kk, d, float(p),
-                    ctypes.c_uint64(seed), table.shape[0], grad.data_ptr(), ws.data_ptr(),
-                    nb.value, st), "fanout_mean_gather_bwd_sorted")
-            else:
-                check(lib.mirec_fanout_mean_gather_bwd(g.contiguous().data_ptr(), lid.data_ptr(),
-                                                       n_t, kk, d, float(p),
-                                                       ctypes.c_uint64(seed), grad.data_ptr(),
-                                                       st), "fanout_mean_gather_bwd")
-        return grad, None, None, None
+            check(lib.mirec_fanout_mean_gather_bwd(g.contiguous().data_ptr(), lid.data_ptr(),
+                                                   n_t, kk, d, float(p), ctypes.c_uint64(seed),
+                                                   grad.data_ptr(), st),
+                  "fanout_mean_gather_bwd")
+        return grad, None, None, None, None, None
 
 
 class _FanoutMean(torch.autograd.Function):
@@ -227,7 +309,13 @@ class GraphSAGE(nn.Module):
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
         deg = torch.from_numpy(self.graph.degree()).to(self.device).float()
         self._mean_dinv = torch.where(deg > 0, 1.0 / deg.clamp(min=1), torch.zeros_like(deg))
-        self.optims = AdamGroup(AdamState(p, lr=config["lr"]) for p in self.parameters())
+        # the table's Adam state is stepped by the fused kernel (TableGrad.adam)
+        # or, when its gradient is materialised, with the others
+        self._table_state = AdamState(self._table, lr=config["lr"])
+        self.optims = AdamGroup([self._table_state] +
+                                [AdamState(p, lr=config["lr"]) for p in self.w_linears.parameters()])
+        self._tg = TableGrad(n, self.n_user, d, self.device)
+        self._norm_cache = None  # (norms [2], token) of the table after the fused Adam
         self._step_seed = int(config.get("seed", 2020))
         self._calls = 0
 
@@ -291,7 +379,9 @@ class GraphSAGE(nn.Module):
         leaves = tuple((groups[ci][0], self.sizes[L - 1], p, seed_of(parent[ci], 0))
                        for ci in leaf)
         ids = torch.cat([groups[gi][0] for gi in inner])
-        rows, nu, ni, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves)
+        sink = self._tg if SORTED_LEAF_BACKWARD else None
+        rows, nu, ni, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves, sink,
+                                                 self._cached_norms())
         self._slice_norms = (nu, ni)  # consumed by loss()
         # one split node: its backward concatenates the group gradients once
         # (per-slice views would each materialise a full-size zero tensor)
@@ -317,8 +407,41 @@ class GraphSAGE(nn.Module):
         return h[0]
 
     def table_grad_dense(self) -> torch.Tensor:
-        """The id table's gradient after a backward, as a dense [N, d] tensor."""
-        return self._table.grad
+        """The id table's gradient after a backward (before the step), as a
+        dense [N, d] tensor."""
+        if self._table.grad is not None:
+            return self._table.grad
+        if not self._tg.pending:
+            raise RuntimeError("no pending table gradient")
+        return self._tg.materialize(self._table.detach())
+
+    def _norm_token(self):
+        return (self._table._version, _engine._raw_writes)
+
+    def _cached_norms(self):
+        c = self._norm_cache
+        if c is not None and c[1] == self._norm_token():
+            return c[0]
+        self._norm_cache = None
+        return None
+
+    @torch.no_grad()
+    def optimizer_step(self):
+        """Adam over every parameter (graphsage.py:388-397): the Linear
+        layers with the multi-tensor kernel; the table through the fused
+        kernel from the pending sorted gradient (which also leaves the
+        updated slices' norms for the next forward), or with the others when
+        its gradient was materialised."""
+        if self._table.grad is not None or not self._tg.pending:
+            self.optims.step()
+            self._tg.pending = False
+            return
+        lin = AdamGroup(self.optims.states[1:])
+        lin.step()
+        norms = torch.empty(2, device=self.device)
+        self._tg.adam(self._table_state, norms)
+        _engine._note_raw_write()
+        self._norm_cache = (norms, self._norm_token())
 
     def reg_parameters(self):
         """The in-scope parameters in the reference's registration order
@@ -372,7 +495,7 @@ class GraphSAGE(nn.Module):
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         if grad_hook is not None:
             grad_hook()
-        self.optims.step()
+        self.optimizer_step()
         return loss.detach()
 
     def OneEpoch(self, user, pos, neg):

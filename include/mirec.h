@@ -413,6 +413,61 @@ int mirec_fanout_mean_gather_bwd_sorted(const float *grad_out, const int32_t *id
                                         float *table_grad, void *workspace,
                                         size_t workspace_bytes, mirec_stream_t stream);
 
+/* Deterministic id-table gradient (model/graphsage.py:311-337) and the Adam
+ * step that consumes it (graphsage.py:388-397).  The table gradient of one
+ * step is G[r] = c[slice(r)] * table[r] + S[r]: c = (c_user, c_item) the
+ * norm-term coefficients dL/d|slice| / |slice| (device, 2 floats; rows
+ * [0, n_user) are the user slice), S the sum of the tree's row
+ * contributions, given as up to MIREC_TABLE_GRAD_MAX_GROUPS groups: entry
+ * t*k + c of a group adds w_t * dropout(grad_out[t]) to row ids[t*k + c]
+ * (ids < 0 skipped), with w_t = 1/(valid children of t) for a mean group
+ * (the leaf hop's dropout-mean; mask element (t*k + c)*dim + col as in
+ * mirec_fanout_mean_gather) and 1 otherwise (a plain row gather: k = 1,
+ * dropout_p = 0). */
+#define MIREC_TABLE_GRAD_MAX_GROUPS 8
+typedef struct mirec_row_grad_group {
+  const int32_t *ids;       /* [n_targets * k] row ids, -1 = none */
+  const float *grad_out;    /* [n_targets, dim] */
+  int64_t n_targets;
+  int32_t k;
+  int32_t mean;             /* 1: w_t = 1/cnt_t, 0: w_t = 1 */
+  float dropout_p;
+  int32_t _pad;
+  uint64_t seed;
+} mirec_row_grad_group_t;
+
+/* sizeof(mirec_row_grad_group_t), for FFI struct-mirror checks. */
+int64_t mirec_row_grad_group_size(void);
+
+/* S for every touched row: the entries of all groups radix-sorted by row id
+ * (stable), each id's contributions summed in entry order (runs longer than
+ * a 64-entry chunk: per-chunk partials added in chunk order) — no float
+ * atomics, bitwise repeatable.  Writes acc[r] = S[r] and stamp[r] = gen for
+ * the touched rows only (nothing is cleared: a row belongs to this step iff
+ * stamp[r] == gen).  acc [n_rows, dim], stamp [n_rows]; workspace:
+ * mirec_table_grad_workspace bytes. */
+int mirec_table_grad_workspace(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                               int32_t n_rows, int32_t dim, size_t *bytes);
+int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                            int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
+                            void *workspace, size_t workspace_bytes, mirec_stream_t stream);
+
+/* grad = G materialised (coef may be NULL = 0), [n_rows, dim]. */
+int mirec_table_grad_dense(const float *table, const float *coef, int64_t n_user,
+                           const float *acc, const int32_t *stamp, int32_t gen, int64_t n_rows,
+                           int32_t dim, float *grad, mirec_stream_t stream);
+
+/* Adam (torch.optim.Adam, as mirec_adam_dense) of the whole table with G
+ * formed on the fly: param / exp_avg / exp_avg_sq read and written once,
+ * the dense gradient never stored.  If sumsq and norms are given (sumsq:
+ * mirec_adam_table_sumsq_floats floats), norms[0..1] = the L2 norms of the
+ * UPDATED user / item slices (the next step's norm term), fixed order. */
+int64_t mirec_adam_table_sumsq_floats(int64_t n_rows, int32_t dim);
+int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
+                     int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
+                     int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h, float *sumsq,
+                     float *norms, mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* SASRec causal self-attention (model/sasrec.py:385-397), f32 MFMA          */
 /* ------------------------------------------------------------------------ */
