@@ -181,12 +181,21 @@ SIGNATURES = {
                                         c_void_p]),
     "mirec_slice_norms_work_floats": (c_int64, []),
     "mirec_slice_norms": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mirec_norm_terms": (c_int, [c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
+                                 c_int32, c_void_p, c_void_p, c_void_p]),
+    "mirec_norm_terms_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                     c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "mirec_seq_pack": (c_int, [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
                                c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p]),
     "mirec_zero_tail_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
     "mirec_gemm_nt": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p]),
+    "mirec_gemm_nt_ex": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                 c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32,
+                                 c_void_p]),
+    "mirec_gemm_tn_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
+                                 c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "mirec_gemm_tn_work_floats": (c_int64, [c_int64, c_int32, c_int32]),
     "mirec_gemm_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p, c_void_p]),

@@ -125,14 +125,15 @@ static inline bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_
 }
 
 // One element of torch.optim.Adam (amsgrad=False, weight_decay=0): every
-// Adam kernel uses this one expression, so fused and unfused steps agree
-// bitwise.
+// Adam kernel uses this one expression, written with explicit fmas so the
+// compiler's contraction choices cannot differ between kernels (fused and
+// unfused steps agree bitwise).
 __device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
                                       const mirec_adam_hparams_t &h) {
-  m = m + h.one_minus_beta1 * (g - m);
-  v = v * h.beta2 + h.one_minus_beta2 * g * g;
+  m = fmaf(h.one_minus_beta1, g - m, m);
+  v = fmaf(v, h.beta2, h.one_minus_beta2 * (g * g));
   const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
-  p = p + h.neg_step_size * (m / denom);
+  p = fmaf(h.neg_step_size, m / denom, p);
 }
 
 }  // namespace mirec

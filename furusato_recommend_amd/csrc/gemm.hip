@@ -46,12 +46,26 @@ constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two 
 // [128 tile_n, +128); waves 2 x 2, each BM/2 x 64 (BM/64 x 2 MFMA tiles).
 // LDS: sA[BM][36], sB[128][36] (k-contiguous rows).  PF chunks of global
 // loads are in flight ahead of the one being multiplied (register staging).
+//
+// Fused forms (the GraphSAGE hop, model/graphsage.py:314-315, without the
+// concatenation): A may be two row-major blocks side by side — columns
+// [0, Ks) from A (row stride Ks) and [Ks, Kr) from A2 (row stride Kr - Ks);
+// Amask (same layout as a single A) zeroes A elements whose mask is <= 0 (the
+// ReLU backward, dY * (y > 0), applied as dY is loaded); C may be split the
+// same way at column Ns into C / C2; relu applies max(., 0) after the bias.
+struct NtArgs {
+  const float *A2;
+  const float *Amask;
+  float *C2;
+  int Ks, Ns, relu;
+};
+
 template <int BM, int PF>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         const float *__restrict__ bias,
                                                         float *__restrict__ C, int64_t n,
-                                                        int Kr, int No) {
+                                                        int Kr, int No, NtArgs fx) {
   constexpr int TM = BM / 64;        // 32-row MFMA tiles per wave
   constexpr int QA = BM * 8 / 256;   // float4 of A per thread per chunk
   constexpr int QB = 4;              // float4 of B per thread per chunk
@@ -72,7 +86,24 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
     for (int q = 0; q < QA; ++q) {
       const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
       const int64_t row = m0 + r;
-      xa[q] = row < n ? ld4(A + row * Kr + k0 + 4 * c4) : f4_zero();
+      float4 v = f4_zero();
+      if (row < n) {
+        if (fx.A2 == nullptr) {
+          v = ld4(A + row * Kr + k0 + 4 * c4);
+        } else if (k0 < fx.Ks) {
+          v = ld4(A + row * fx.Ks + k0 + 4 * c4);
+        } else {
+          v = ld4(fx.A2 + row * (Kr - fx.Ks) + (k0 - fx.Ks) + 4 * c4);
+        }
+        if (fx.Amask != nullptr) {
+          const float4 mk = ld4(fx.Amask + row * Kr + k0 + 4 * c4);
+          v.x = mk.x > 0.f ? v.x : 0.f;
+          v.y = mk.y > 0.f ? v.y : 0.f;
+          v.z = mk.z > 0.f ? v.z : 0.f;
+          v.w = mk.w > 0.f ? v.w : 0.f;
+        }
+      }
+      xa[q] = v;
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
@@ -142,12 +173,26 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
   for (int tn = 0; tn < 2; ++tn) {
     const int col = n0 + wn * 64 + tn * 32 + i;
     const float bv = bias ? bias[col] : 0.f;
+    // output block of this column (a split at Ns is tile-aligned)
+    float *cb = C;
+    int ldc = No, cc = col;
+    if (fx.C2 != nullptr) {
+      if (col < fx.Ns) {
+        ldc = fx.Ns;
+      } else {
+        cb = fx.C2;
+        ldc = No - fx.Ns;
+        cc = col - fx.Ns;
+      }
+    }
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (row < n) C[row * No + col] = acc[tm][tn][r] + bv;
+        float y = acc[tm][tn][r] + bv;
+        if (fx.relu) y = fmaxf(y, 0.f);
+        if (row < n) cb[row * ldc + cc] = y;
       }
   }
 }
@@ -157,12 +202,21 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
 // [s * rows_per_slice, +rows_per_slice) -> work[s][M][No]; with colsum, the
 // tile_n == 0 workgroups also write the slice's column sums of A ->
 // work_cs[s][M].  LDS: sA[32][136], sB[32][136] (k-major, as in memory).
+// Fused forms: Amask zeroes A elements whose mask (same layout) is <= 0 (the
+// ReLU backward); B may be two blocks side by side, columns [0, Ns) from B
+// (row stride Ns) and [Ns, No) from B2 (row stride No - Ns), Ns % 128 == 0.
+struct TnArgs {
+  const float *Amask;
+  const float *B2;
+  int Ns;
+};
+
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         float *__restrict__ work,
                                                         float *__restrict__ work_cs,
                                                         int64_t n, int M, int No,
-                                                        int64_t rows_per_slice) {
+                                                        int64_t rows_per_slice, TnArgs fx) {
   __shared__ __attribute__((aligned(16))) float sA[kChunk * kLdTN];
   __shared__ __attribute__((aligned(16))) float sB[kChunk * kLdTN];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -181,8 +235,24 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
       const int64_t r = r0 + kk;
       const bool ok = r < r_end;
-      ra[q] = ok ? ld4(A + r * M + m0 + 4 * c4) : f4_zero();
-      rb[q] = ok ? ld4(B + r * No + n0 + 4 * c4) : f4_zero();
+      float4 a = ok ? ld4(A + r * M + m0 + 4 * c4) : f4_zero();
+      if (ok && fx.Amask != nullptr) {
+        const float4 mk = ld4(fx.Amask + r * M + m0 + 4 * c4);
+        a.x = mk.x > 0.f ? a.x : 0.f;
+        a.y = mk.y > 0.f ? a.y : 0.f;
+        a.z = mk.z > 0.f ? a.z : 0.f;
+        a.w = mk.w > 0.f ? a.w : 0.f;
+      }
+      ra[q] = a;
+      if (!ok) {
+        rb[q] = f4_zero();
+      } else if (fx.B2 == nullptr) {
+        rb[q] = ld4(B + r * No + n0 + 4 * c4);
+      } else if (n0 < fx.Ns) {
+        rb[q] = ld4(B + r * fx.Ns + n0 + 4 * c4);
+      } else {
+        rb[q] = ld4(fx.B2 + r * (No - fx.Ns) + (n0 - fx.Ns) + 4 * c4);
+      }
     }
   };
   auto stage = [&]() {
@@ -296,19 +366,37 @@ static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
 
 using namespace mirec;
 
-extern "C" int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C,
-                             int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream) {
+static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Amask,
+                   const float *B, const float *bias, float *C, float *C2, int32_t Ns,
+                   int32_t relu, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream) {
   MIREC_CHECK_ARG(n >= 0 && Kr > 0 && No > 0 && Kr % kChunk == 0 && No % kTile == 0);
   if (n == 0) return MIREC_OK;  // (empty tensors may carry null pointers)
   MIREC_CHECK_ARG(A && B && C && ((uintptr_t)A | (uintptr_t)B) % 16 == 0);
+  MIREC_CHECK_ARG(A2 == nullptr || (Ks > 0 && Ks < Kr && Ks % kChunk == 0 &&
+                                    (uintptr_t)A2 % 16 == 0));
+  MIREC_CHECK_ARG(Amask == nullptr || (A2 == nullptr && (uintptr_t)Amask % 16 == 0));
+  MIREC_CHECK_ARG(C2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0));
+  NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0};
   // 128-row tiles, one chunk of loads ahead: 64-row tiles and two chunks
   // ahead measured the same (29.5-30.2 us at 56 K x 128 x 128): the shape is
   // bound by the MFMA time of the busiest CU plus fixed prologue / epilogue
   const unsigned ncol = (unsigned)(No / kTile);
   hipLaunchKernelGGL((gemm_nt_kernel<128, 1>), dim3((unsigned)((n + 127) / 128) * ncol),
-                     dim3(256), 0, (hipStream_t)stream, A, B, bias, C, n, (int)Kr, (int)No);
+                     dim3(256), 0, (hipStream_t)stream, A, B, bias, C, n, (int)Kr, (int)No, fx);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
+}
+
+extern "C" int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C,
+                             int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream) {
+  return gemm_nt(A, nullptr, 0, nullptr, B, bias, C, nullptr, 0, 0, n, Kr, No, stream);
+}
+
+extern "C" int mirec_gemm_nt_ex(const float *A, const float *A2, int32_t Ks, const float *Amask,
+                                const float *B, const float *bias, float *C, float *C2,
+                                int32_t Ns, int32_t relu, int64_t n, int32_t Kr, int32_t No,
+                                mirec_stream_t stream) {
+  return gemm_nt(A, A2, Ks, Amask, B, bias, C, C2, Ns, relu, n, Kr, No, stream);
 }
 
 extern "C" int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No) {
@@ -319,11 +407,15 @@ extern "C" int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No) {
   return (int64_t)slices * M * No + (int64_t)slices * M;
 }
 
-extern "C" int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n,
-                             int32_t M, int32_t No, float *work, mirec_stream_t stream) {
+static int gemm_tn(const float *A, const float *Amask, const float *B, const float *B2,
+                   int32_t Ns, float *C, float *colsum, int64_t n, int32_t M, int32_t No,
+                   float *work, mirec_stream_t stream) {
   MIREC_CHECK_ARG(C && work && n >= 0 && M > 0 && No > 0 && M % kTile == 0 && No % kTile == 0);
   MIREC_CHECK_ARG(n == 0 || (A && B));  // (empty tensors may carry null pointers)
   MIREC_CHECK_ARG(((uintptr_t)A | (uintptr_t)B | (uintptr_t)C | (uintptr_t)work) % 16 == 0);
+  MIREC_CHECK_ARG(Amask == nullptr || (uintptr_t)Amask % 16 == 0);
+  MIREC_CHECK_ARG(B2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0 &&
+                                    (uintptr_t)B2 % 16 == 0));
   hipStream_t st = (hipStream_t)stream;
   if (n == 0) {
     MIREC_HIP(hipMemsetAsync(C, 0, sizeof(float) * M * No, st));
@@ -335,8 +427,9 @@ extern "C" int mirec_gemm_tn(const float *A, const float *B, float *C, float *co
   tn_slices(n, M, No, &slices, &rows);
   float *work_cs = work + (int64_t)slices * M * No;
   const dim3 grid((unsigned)slices, (unsigned)(M / kTile), (unsigned)(No / kTile));
+  TnArgs fx{Amask, B2, Ns};
   hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, st, A, B, work,
-                     colsum ? work_cs : nullptr, n, (int)M, (int)No, rows);
+                     colsum ? work_cs : nullptr, n, (int)M, (int)No, rows, fx);
   MIREC_LAUNCH_CHECK();
   const int64_t n4 = (int64_t)M * No / 4;
   const int64_t blocks = (std::max<int64_t>(n4, M) + 63) / 64;
@@ -344,4 +437,15 @@ extern "C" int mirec_gemm_tn(const float *A, const float *B, float *C, float *co
                      work_cs, C, colsum, slices, n4, (int)M);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
+}
+
+extern "C" int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n,
+                             int32_t M, int32_t No, float *work, mirec_stream_t stream) {
+  return gemm_tn(A, nullptr, B, nullptr, 0, C, colsum, n, M, No, work, stream);
+}
+
+extern "C" int mirec_gemm_tn_ex(const float *A, const float *Amask, const float *B,
+                                const float *B2, int32_t Ns, float *C, float *colsum, int64_t n,
+                                int32_t M, int32_t No, float *work, mirec_stream_t stream) {
+  return gemm_tn(A, Amask, B, B2, Ns, C, colsum, n, M, No, work, stream);
 }

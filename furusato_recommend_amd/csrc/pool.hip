@@ -247,6 +247,71 @@ __global__ __launch_bounds__(256) void slice_norm_final_kernel(const float *__re
   }
 }
 
+// Parameter-norm term of the GraphSAGE loss (model/graphsage.py:326-337:
+// all_param = 2 all_param + |p| over the parameters, i.e. the weighted sum
+// Σ 2^(K-1-k) |p_k|) over a few small tensors plus norms already on the
+// device (the id table's slices).  One 1024-thread workgroup: each tensor's
+// sum of squares in a fixed order (strided partials, then a tree), total
+// accumulated in term order after the extra terms (deterministic).
+constexpr int kMaxNormTerms = MIREC_NORM_TERMS_MAX;
+struct NormTermArgs {
+  const float *x[kMaxNormTerms];
+  float *g[kMaxNormTerms];
+  int64_t off[kMaxNormTerms + 1];
+  float w[kMaxNormTerms];
+  float ew[kMaxNormTerms];
+  int32_t count, n_extra;
+};
+
+__global__ __launch_bounds__(1024) void norm_terms_kernel(NormTermArgs a,
+                                                          const float *__restrict__ extra,
+                                                          float *__restrict__ norms,
+                                                          float *__restrict__ total) {
+  __shared__ float red[1024];
+  float tot = 0.f;
+  for (int j = 0; j < a.n_extra; ++j) tot += a.ew[j] * extra[j];
+  for (int k = 0; k < a.count; ++k) {
+    const int64_t n = a.off[k + 1] - a.off[k];
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += 1024) {
+      const float v = a.x[k][i];
+      s += v * v;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int h = 512; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+      __syncthreads();
+    }
+    const float nk = sqrtf(red[0]);
+    tot += a.w[k] * nk;
+    if (threadIdx.x == 0) norms[k] = nk;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) total[0] = tot;
+}
+
+// g_k[i] = g * w_k * x_k[i] / |x_k| (0 where |x_k| = 0, as torch's norm
+// backward); extra_grad[j] = g * ew_j.  One thread per element of the
+// concatenation (+ n_extra).
+__global__ __launch_bounds__(256) void norm_terms_bwd_kernel(NormTermArgs a,
+                                                             const float *__restrict__ norms,
+                                                             const float *__restrict__ g_total,
+                                                             float *__restrict__ extra_grad) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const float g = g_total[0];
+  const int64_t tot = a.off[a.count];
+  if (i < tot) {
+    int k = 0;
+    while (a.off[k + 1] <= i) ++k;
+    const int64_t j = i - a.off[k];
+    const float nk = norms[k];
+    a.g[k][j] = nk > 0.f ? g * a.w[k] * (a.x[k][j] / nk) : 0.f;
+  } else if (i < tot + a.n_extra) {
+    extra_grad[i - tot] = g * a.ew[i - tot];
+  }
+}
+
 }  // namespace mirec
 
 using namespace mirec;
@@ -309,6 +374,58 @@ extern "C" int mirec_bpr_rows_loss_bwd(const float *u, const float *p, const flo
   const int64_t total = B * d;
   hipLaunchKernelGGL(bpr_rows_loss_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
                      0, (hipStream_t)stream, u, p, n, x, B, d, g_loss, coef, du, dp, dn, g_extra);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+static int norm_args(const float *const *xs, float *const *grads, const int64_t *numel,
+                     const float *weights, int32_t count, const float *extra_w, int32_t n_extra,
+                     NormTermArgs *a) {
+  MIREC_CHECK_ARG(count >= 0 && count <= kMaxNormTerms && n_extra >= 0 &&
+                  n_extra <= kMaxNormTerms && (count == 0 || (xs && numel && weights)) &&
+                  (n_extra == 0 || extra_w));
+  *a = NormTermArgs{};
+  a->count = count;
+  a->n_extra = n_extra;
+  for (int k = 0; k < count; ++k) {
+    MIREC_CHECK_ARG(xs[k] && numel[k] >= 0);
+    a->x[k] = xs[k];
+    a->g[k] = grads ? grads[k] : nullptr;
+    a->w[k] = weights[k];
+    a->off[k + 1] = a->off[k] + numel[k];
+  }
+  for (int j = 0; j < n_extra; ++j) a->ew[j] = extra_w[j];
+  return MIREC_OK;
+}
+
+extern "C" int mirec_norm_terms(const float *const *xs, const int64_t *numel, const float *weights,
+                                int32_t count, const float *extra, const float *extra_w,
+                                int32_t n_extra, float *norms, float *total,
+                                mirec_stream_t stream) {
+  NormTermArgs a;
+  const int rc = norm_args(xs, nullptr, numel, weights, count, extra_w, n_extra, &a);
+  if (rc != MIREC_OK) return rc;
+  MIREC_CHECK_ARG(total && (count == 0 || norms) && (n_extra == 0 || extra));
+  hipLaunchKernelGGL(norm_terms_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, extra,
+                     norms, total);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_norm_terms_bwd(const float *const *xs, float *const *grads,
+                                    const int64_t *numel, const float *weights, int32_t count,
+                                    const float *norms, const float *g_total,
+                                    const float *extra_w, int32_t n_extra, float *extra_grad,
+                                    mirec_stream_t stream) {
+  NormTermArgs a;
+  const int rc = norm_args(xs, grads, numel, weights, count, extra_w, n_extra, &a);
+  if (rc != MIREC_OK) return rc;
+  MIREC_CHECK_ARG(g_total && (count == 0 || (grads && norms)) && (n_extra == 0 || extra_grad));
+  for (int k = 0; k < count; ++k) MIREC_CHECK_ARG(grads[k]);
+  const int64_t tot = a.off[count] + n_extra;
+  if (tot == 0) return MIREC_OK;
+  hipLaunchKernelGGL(norm_terms_bwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, a, norms, g_total, extra_grad);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -77,11 +77,9 @@ __device__ __forceinline__ void adam_elem(float &p, float &m, float &v, float g,
                                           const mirec_adam_hparams_t &h) {
   // torch.optim.Adam single-tensor path (torch/optim/adam.py:457-547):
   // exp_avg.lerp_(g, 1-b1); exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
-  // denom = sqrt(v)/sqrt(bc2) + eps; p.addcdiv_(m, denom, -lr/bc1)
-  m = m + h.one_minus_beta1 * (g - m);
-  v = v * h.beta2 + h.one_minus_beta2 * g * g;
-  const float denom = sqrtf(v) / h.bc2_sqrt + h.eps;
-  p = p + h.neg_step_size * (m / denom);
+  // denom = sqrt(v)/sqrt(bc2) + eps; p.addcdiv_(m, denom, -lr/bc1) — the
+  // shared expression of every Adam kernel (common.h)
+  adam1(p, m, v, g, h);
 }
 
 // Sum of the input rows listed in col[beg, end) (pre-scaled / raw x dinv_j /

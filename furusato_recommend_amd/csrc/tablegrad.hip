@@ -238,16 +238,23 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
   if (beg >= n) return;
   const int64_t end = beg + kCh;
   if (end >= n) return;  // no next chunk
+  // one round of key loads decides the common cases
   const int32_t klast = keys[end - 1];
-  if (klast >= n_rows || keys[end] != klast) return;  // last segment stays inside
-  if (beg > 0 && keys[beg - 1] == klast) return;       // the run's head is earlier
+  const int32_t kn = keys[end];
+  const int32_t kp = beg > 0 ? keys[beg - 1] : -1;
+  const int32_t kn2 = end + kCh < n ? keys[end + kCh] : -1;
+  if (klast >= n_rows || kn != klast) return;  // last segment stays inside
+  if (kp == klast) return;                      // the run's head is earlier
   const unsigned long long gmask = low_bits<LPR>() << base;
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
-    float4 sum = act ? ld4(part + (2 * chunk + 1) * (int64_t)d + col) : f4_zero();
-    int64_t cc = chunk + 1;  // chunks cc.. hold the run's continuation
-    while (true) {
+    // this chunk's tail segment + the next chunk's head segment
+    const float4 a = act ? ld4(part + (2 * chunk + 1) * (int64_t)d + col) : f4_zero();
+    const float4 b = act ? ld4(part + (2 * chunk + 2) * (int64_t)d + col) : f4_zero();
+    float4 sum = f4_add(a, b);
+    int64_t cc = chunk + 2;  // chunks cc.. hold the rest of the run (if any)
+    while (kn2 == klast) {   // the run covers chunk + 1 entirely and goes on
       // lane j: does the run cover all of chunk cc + j and continue past it?
       const int64_t cj = cc + sub;
       const int64_t ej = (cj + 1) * kCh;
@@ -518,6 +525,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
     MIREC_LAUNCH_CHECK();                                                                    \
     break;
   switch (lpr) {
+    MIREC_TG_LAUNCH(8)
     MIREC_TG_LAUNCH(16)
     MIREC_TG_LAUNCH(32)
     MIREC_TG_LAUNCH(64)
@@ -534,8 +542,11 @@ static int32_t pow2_shift(int32_t d4) {
   return -1;
 }
 
+#ifndef MIREC_TG_ADAM_BLOCKS
+#define MIREC_TG_ADAM_BLOCKS 65536
+#endif
 static unsigned tg_blocks(int64_t n4) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 65536));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, MIREC_TG_ADAM_BLOCKS));
 }
 
 extern "C" int64_t mirec_adam_table_sumsq_floats(int64_t n_rows, int32_t dim) {

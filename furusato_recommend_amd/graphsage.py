@@ -33,8 +33,8 @@ from . import engine as _engine
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamGroup, AdamState, sample_triples
 from .graph import DEFAULT_SPLIT, Graph
-from .linear import Linear
-from .rows import slice_norms
+from .linear import Linear, sage_linear
+from .rows import slice_norms2
 
 
 # The id table's backward: the deterministic sorted form (True: every row
@@ -147,29 +147,29 @@ class _TableTerms(torch.autograd.Function):
                                                float(p), ctypes.c_uint64(seed), out.data_ptr(),
                                                st), "fanout_mean_gather")
             aggrs.append(out)
-        if norms is None:
-            nu, ni = slice_norms(table, n_user)  # both slices in one pass
-        else:
-            nu, ni = norms[0], norms[1]
-        ctx.save_for_backward(table, ids, nu, ni, *[l[0] for l in leaves])
+        # both slices' norms in one pass (or the previous step's fused Adam's)
+        norms2 = slice_norms2(table, n_user) if norms is None else norms.clone()
+        ctx.save_for_backward(table, ids, norms2, *[l[0] for l in leaves])
         ctx.leaf_cfg = [(k, p, seed) for _, k, p, seed in leaves]
         ctx.n_user = n_user
         ctx.sink = sink
-        return (rows, nu.clone(), ni.clone(), *aggrs)
+        return (rows, norms2, *aggrs)
 
     @staticmethod
-    def backward(ctx, g_rows, g_nu, g_ni, *g_aggrs):
-        table, ids, nu, ni, *leaf_ids = ctx.saved_tensors
+    def backward(ctx, g_rows, g_norms, *g_aggrs):
+        table, ids, norms2, *leaf_ids = ctx.saved_tensors
         k = ctx.n_user
         d = table.shape[1]
         st = _lib.stream_handle()
-        zero = torch.zeros_like(nu)
         # d|x|/dx = x/|x| (0 for a zero slice, as torch's norm backward)
-        cu = zero if g_nu is None else torch.where(nu > 0, g_nu / nu, zero)
-        ci = zero if g_ni is None else torch.where(ni > 0, g_ni / ni, zero)
+        if g_norms is None:
+            coef = torch.zeros_like(norms2)
+        else:
+            coef = torch.where(norms2 > 0, g_norms / norms2, torch.zeros_like(norms2))
+        cu, ci = coef[0], coef[1]
         sink = ctx.sink
         if sink is not None:
-            torch.stack([cu, ci], out=sink.coef)
+            sink.coef.copy_(coef)
             groups = []
             if g_rows is not None:
                 groups.append((ids, g_rows, 1, 0, 0.0, 0))
@@ -198,6 +198,71 @@ class _TableTerms(torch.autograd.Function):
                                                    grad.data_ptr(), st),
                   "fanout_mean_gather_bwd")
         return grad, None, None, None, None, None
+
+
+class _SageLoss(torch.autograd.Function):
+    """The GraphSAGE BPR loss (model/graphsage.py:326-337) in two launches:
+    mean softplus(<u,n> - <u,p>) over the seed embeddings out3 = [u ; p ; n]
+    plus decay / B * all_param, where the reference's doubling accumulation
+    all_param = 2 all_param + |p_k| over (user ids, item ids, w_0, b_0, ...)
+    is the weighted sum Σ_k 2^(K-1-k) |p_k| (mirec_norm_terms: the table
+    slices' norms come in as ``norms2``, the small parameters' are computed
+    in the same launch), then mirec_bpr_rows_loss.  Backward: the row
+    gradients of out3 in one buffer, the small parameters' gradients and the
+    table slices' norm gradients in one launch."""
+
+    @staticmethod
+    def forward(ctx, out3, norms2, decay: float, *small):
+        B = out3.shape[0] // 3
+        d = out3.shape[1]
+        K = 2 + len(small)
+        st = _lib.stream_handle()
+        dev = out3.device
+        w_small = [float(2 ** (K - 3 - k)) for k in range(len(small))]
+        w_extra = [float(2 ** (K - 1)), float(2 ** (K - 2))]
+        xs = (ctypes.c_void_p * max(1, len(small)))(*[t.data_ptr() for t in small])
+        numel = (ctypes.c_int64 * max(1, len(small)))(*[t.numel() for t in small])
+        wk = (ctypes.c_float * max(1, len(small)))(*w_small)
+        we = (ctypes.c_float * 2)(*w_extra)
+        norms = torch.empty(max(1, len(small)), device=dev)
+        total = torch.empty(1, device=dev)
+        check(lib.mirec_norm_terms(xs, numel, wk, len(small), norms2.data_ptr(), we, 2,
+                                   norms.data_ptr(), total.data_ptr(), st), "norm_terms")
+        x = torch.empty(2 * B, device=dev)
+        loss = torch.empty(1, device=dev)
+        coef = float(decay) / B
+        check(lib.mirec_bpr_rows_loss(out3.data_ptr(), out3[B:].data_ptr(),
+                                      out3[2 * B:].data_ptr(), B, d, total.data_ptr(), coef,
+                                      x.data_ptr(), loss.data_ptr(), st), "bpr_rows_loss")
+        ctx.save_for_backward(out3, x, norms, *small)
+        ctx.cfg = (B, d, coef, w_small, w_extra)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        out3, x, norms, *small = ctx.saved_tensors
+        B, d, coef, w_small, w_extra = ctx.cfg
+        st = _lib.stream_handle()
+        g = g.reshape(1).contiguous()
+        d_out3 = torch.empty_like(out3)
+        g_extra = torch.empty(1, device=out3.device)
+        check(lib.mirec_bpr_rows_loss_bwd(out3.data_ptr(), out3[B:].data_ptr(),
+                                          out3[2 * B:].data_ptr(), x.data_ptr(), B, d,
+                                          g.data_ptr(), coef, d_out3.data_ptr(),
+                                          d_out3[B:].data_ptr(), d_out3[2 * B:].data_ptr(),
+                                          g_extra.data_ptr(), st), "bpr_rows_loss_bwd")
+        grads = [torch.empty_like(t) for t in small]
+        n = max(1, len(small))
+        xs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in small])
+        gs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in grads])
+        numel = (ctypes.c_int64 * n)(*[t.numel() for t in small])
+        wk = (ctypes.c_float * n)(*w_small)
+        we = (ctypes.c_float * 2)(*w_extra)
+        g_norms2 = torch.empty(2, device=out3.device)
+        check(lib.mirec_norm_terms_bwd(xs, gs, numel, wk, len(small), norms.data_ptr(),
+                                       g_extra.data_ptr(), we, 2, g_norms2.data_ptr(), st),
+              "norm_terms_bwd")
+        return (d_out3, g_norms2, None, *grads)
 
 
 class _FanoutMean(torch.autograd.Function):
@@ -380,9 +445,9 @@ class GraphSAGE(nn.Module):
                        for ci in leaf)
         ids = torch.cat([groups[gi][0] for gi in inner])
         sink = self._tg if SORTED_LEAF_BACKWARD else None
-        rows, nu, ni, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves, sink,
+        rows, norms2, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves, sink,
                                                  self._cached_norms())
-        self._slice_norms = (nu, ni)  # consumed by loss()
+        self._slice_norms2 = norms2  # consumed by loss() / the fused loss
         # one split node: its backward concatenates the group gradients once
         # (per-slice views would each materialise a full-size zero tensor)
         h = [None] * len(groups)
@@ -401,8 +466,8 @@ class GraphSAGE(nn.Module):
                     aggr = leaf_aggr[gi]  # children at hop L are leaves
                 else:
                     aggr = _FanoutMean.apply(h[ci], groups[ci][0], k, p, seed_of(gi, i))
-                x = self.w_linears[i](torch.cat([h[gi], aggr], dim=1))
-                new[gi] = x.relu() if i != L - 1 else x
+                lin = self.w_linears[i]
+                new[gi] = sage_linear(h[gi], aggr, lin.weight, lin.bias, relu=i != L - 1)
             h = new
         return h[0]
 
@@ -457,8 +522,9 @@ class GraphSAGE(nn.Module):
         pos_scores = torch.sum(user_emb * pos_emb, dim=1)
         neg_scores = torch.sum(user_emb * neg_emb, dim=1)
         all_param = 0
-        norms = getattr(self, "_slice_norms", None)
-        self._slice_norms = None
+        n2 = getattr(self, "_slice_norms2", None)
+        self._slice_norms2 = None
+        norms = None if n2 is None else (n2[0], n2[1])
         for k, prm in enumerate(self.reg_parameters()):
             # the two table slices' norms come from the forward's fused node
             nrm = norms[k] if (k < 2 and norms is not None) else prm.norm(2)
@@ -466,6 +532,17 @@ class GraphSAGE(nn.Module):
         all_param = all_param / user_emb.size(0)
         loss = torch.mean(F.softplus(neg_scores - pos_scores))
         return loss + all_param * self.config["decay"]
+
+    def loss_fused(self, emb: torch.Tensor) -> torch.Tensor:
+        """loss() on the forward's seed embeddings emb = [u ; p ; n] [3B, d]
+        in two launches (_SageLoss); the same value up to fp32 order."""
+        n2 = getattr(self, "_slice_norms2", None)
+        if n2 is None or not emb.is_contiguous() or emb.shape[1] % 4:
+            B = emb.shape[0] // 3
+            return self.loss(emb[:B], emb[B:2 * B], emb[2 * B:])
+        self._slice_norms2 = None
+        small = [q for w in self.w_linears for q in (w.weight, w.bias)]
+        return _SageLoss.apply(emb, n2, float(self.config["decay"]), *small)
 
     def embed_triples(self, users, pos, neg, seed: int):
         """One tree over the 3B seeds (users, pos+n_user, neg+n_user)."""
@@ -486,12 +563,10 @@ class GraphSAGE(nn.Module):
         for p in self.parameters():
             p.grad = None
         if tree is None:
-            u, pe, ne = self.embed_triples(users, pos, neg, seed)
-        else:
-            B = users.numel()
-            emb = self.forward(tree, dropout_seed=seed if self.training else None)
-            u, pe, ne = emb[:B], emb[B: 2 * B], emb[2 * B:]
-        loss = self.loss(u, pe, ne)
+            seeds = torch.cat([users.int(), pos.int() + self.n_user, neg.int() + self.n_user])
+            tree = self.sample_tree(seeds.to(self.device), seed)
+        emb = self.forward(tree, dropout_seed=seed if self.training else None)
+        loss = self.loss_fused(emb)
         (loss * loss_scale if loss_scale != 1.0 else loss).backward()
         if grad_hook is not None:
             grad_hook()

@@ -121,6 +121,65 @@ class _LinearSplitK(torch.autograd.Function):
         return dx, dw, db
 
 
+class _SageLinear(torch.autograd.Function):
+    """y = act(x_self W[:, :d]ᵀ + x_nbr W[:, d:]ᵀ + b), the GraphSAGE hop's
+    Linear over [x_self ; aggr] (model/graphsage.py:314-315) without the
+    concatenation: the GEMM reads its A rows from the two tensors
+    (mirec_gemm_nt_ex), adds the bias and applies the ReLU in its epilogue.
+    Backward: the ReLU mask is applied to dY as it is loaded; dX is written
+    straight into the two input gradients (output split at d) and
+    dW = dY'ᵀ [x_self | x_nbr], db = Σ dY' in one pass (mirec_gemm_tn_ex)."""
+
+    @staticmethod
+    def forward(ctx, xs, xn, w, b, relu: bool):
+        n, d = xs.shape
+        no = w.shape[0]
+        y = torch.empty(n, no, dtype=xs.dtype, device=xs.device)
+        check(lib.mirec_gemm_nt_ex(xs.data_ptr(), xn.data_ptr(), d, None, w.data_ptr(),
+                                   _lib.ptr(b), y.data_ptr(), None, 0, int(relu), n, 2 * d, no,
+                                   _lib.stream_handle()), "gemm_nt_ex")
+        ctx.save_for_backward(xs, xn, w, y if relu else None)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, xn, w, y = ctx.saved_tensors
+        n, d = xs.shape
+        no = w.shape[0]
+        dy = dy.contiguous()
+        st = _lib.stream_handle()
+        mask = _lib.ptr(y)
+        dxs = torch.empty_like(xs)
+        dxn = torch.empty_like(xn)
+        wt = w.t().contiguous()  # [2d, no]: B of dX = dY' W
+        check(lib.mirec_gemm_nt_ex(dy.data_ptr(), None, 0, mask, wt.data_ptr(), None,
+                                   dxs.data_ptr(), dxn.data_ptr(), d, 0, n, no, 2 * d, st),
+              "gemm_nt_ex(dX)")
+        dw = torch.empty_like(w)
+        db = torch.empty(no, dtype=w.dtype, device=w.device) if ctx.has_bias else None
+        work = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, no, 2 * d)), dtype=w.dtype,
+                           device=w.device)
+        check(lib.mirec_gemm_tn_ex(dy.data_ptr(), mask, xs.data_ptr(), xn.data_ptr(), d,
+                                   dw.data_ptr(), _lib.ptr(db), n, no, 2 * d, work.data_ptr(), st),
+              "gemm_tn_ex(dW)")
+        return dxs, dxn, dw, db, None
+
+
+def sage_linear(xs: torch.Tensor, xn: torch.Tensor, w: torch.Tensor,
+                b: torch.Tensor | None, relu: bool) -> torch.Tensor:
+    """act(Linear([xs ; xn])) for the GraphSAGE hop; the fused GEMMs when the
+    shapes are theirs (d % 128, out % 128, aligned contiguous rows), else
+    concatenation + Linear + ReLU."""
+    d = xs.shape[1]
+    if (USE_MIREC_GEMM and xs.dim() == 2 and xn.shape == xs.shape and d % 128 == 0
+            and w.shape[1] == 2 * d and w.shape[0] % 128 == 0
+            and _aligned(xs, xn, w) and (b is None or _aligned(b))):
+        return _SageLinear.apply(xs, xn, w, b, bool(relu))
+    y = _LinearSplitK.apply(torch.cat([xs, xn], dim=1), w, b)
+    return y.relu() if relu else y
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     return _LinearSplitK.apply(x, w, b)
 

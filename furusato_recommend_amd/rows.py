@@ -48,6 +48,12 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
 def slice_norms(table: torch.Tensor, split_rows: int):
     """(‖table[:split_rows]‖₂, ‖table[split_rows:]‖₂) as 0-d tensors, one
     pass over the table (mirec_slice_norms; fixed summation order)."""
+    norms = slice_norms2(table, split_rows)
+    return norms[0], norms[1]
+
+
+def slice_norms2(table: torch.Tensor, split_rows: int) -> torch.Tensor:
+    """The two slice norms as one [2] tensor."""
     if not (table.is_cuda and table.dtype == torch.float32 and table.is_contiguous()
             and table.shape[-1] % 4 == 0):
         raise ValueError("slice_norms: contiguous float32 table with rows of 4k floats")
@@ -57,7 +63,7 @@ def slice_norms(table: torch.Tensor, split_rows: int):
     check(lib.mirec_slice_norms(table.data_ptr(), table.numel(), split_rows * table.shape[-1],
                                 work.data_ptr(), norms.data_ptr(), _lib.stream_handle()),
           "slice_norms")
-    return norms[0], norms[1]
+    return norms
 
 
 class _GatherRowsNorm(torch.autograd.Function):

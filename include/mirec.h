@@ -546,6 +546,24 @@ int64_t mirec_slice_norms_work_floats(void);
 int mirec_slice_norms(const float *x, int64_t n, int64_t split, float *work, float *norms,
                       mirec_stream_t stream);
 
+/* Weighted parameter-norm term (model/graphsage.py:326-337: all_param = 2
+ * all_param + |p| over the parameters = Σ_k 2^(K-1-k) |p_k|):
+ * total[0] = Σ_j extra_w[j] * extra[j] + Σ_k weights[k] * |xs[k]|₂ (extra:
+ * norms already on the device, e.g. the id table's slices; xs: count small
+ * device tensors of numel[k] floats, host array of pointers; weights /
+ * extra_w: host arrays), norms[k] = |xs[k]|₂.  Fixed summation order.
+ * Backward: grads[k] = g * weights[k] * xs[k] / |xs[k]| (written; 0 where the
+ * norm is 0) and extra_grad[j] = g * extra_w[j], with g = g_total[0]
+ * (device).  count, n_extra <= MIREC_NORM_TERMS_MAX. */
+#define MIREC_NORM_TERMS_MAX 16
+int mirec_norm_terms(const float *const *xs, const int64_t *numel, const float *weights,
+                     int32_t count, const float *extra, const float *extra_w, int32_t n_extra,
+                     float *norms, float *total, mirec_stream_t stream);
+int mirec_norm_terms_bwd(const float *const *xs, float *const *grads, const int64_t *numel,
+                         const float *weights, int32_t count, const float *norms,
+                         const float *g_total, const float *extra_w, int32_t n_extra,
+                         float *extra_grad, mirec_stream_t stream);
+
 /* Pack a SASRec batch into a fixed token capacity (the graph-captured step,
  * model/sasrec.py:449-455's pad_sequence without the padding): users [B]
  * (device int64), items [n_users, max_len] (int32, each user's last items),
@@ -582,6 +600,23 @@ int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C, i
 int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No);
 int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n, int32_t M,
                   int32_t No, float *work, mirec_stream_t stream);
+
+/* Fused forms of the two GEMMs (the GraphSAGE hop h = relu(W [x ; aggr] + b),
+ * model/graphsage.py:314-315, without materialising the concatenation):
+ *   gemm_nt_ex: A2 != NULL: the A row is [A[r, 0:Ks) | A2[r, 0:Kr-Ks)] (row
+ *     strides Ks and Kr-Ks; Ks % 32 == 0); Amask != NULL (single A only): A
+ *     elements whose Amask element (same layout) is <= 0 read as 0 (the ReLU
+ *     backward dY * (y > 0)); C2 != NULL: output columns [0, Ns) go to C (row
+ *     stride Ns) and [Ns, No) to C2 (stride No-Ns; Ns % 128 == 0); relu != 0:
+ *     max(., 0) after the bias.
+ *   gemm_tn_ex: Amask as above on A; B2 != NULL: the B row is [B[r, 0:Ns) |
+ *     B2[r, 0:No-Ns)] (Ns % 128 == 0); colsum = Σ of the masked A. */
+int mirec_gemm_nt_ex(const float *A, const float *A2, int32_t Ks, const float *Amask,
+                     const float *B, const float *bias, float *C, float *C2, int32_t Ns,
+                     int32_t relu, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream);
+int mirec_gemm_tn_ex(const float *A, const float *Amask, const float *B, const float *B2,
+                     int32_t Ns, float *C, float *colsum, int64_t n, int32_t M, int32_t No,
+                     float *work, mirec_stream_t stream);
 
 /* Row tail of the SASRec block (model/sasrec.py:385-397 — the dropout,
  * residual add, ReLU and LayerNorm around the attention and the FFN), one

@@ -563,7 +563,7 @@ def test_sage_step_matches_reference(golden, name):
     for q in m.parameters():
         q.grad = None
     out = m.forward(tree)
-    loss_t = m.loss(out[:B], out[B:2 * B], out[2 * B:])
+    loss_t = m.loss_fused(out)  # stageOne's loss node
     loss_t.backward()
     grads = {id(m._table): m.table_grad_dense().clone()}
     for li in m.w_linears:
@@ -593,8 +593,12 @@ def test_sage_step_matches_reference(golden, name):
         assert rel(prm, ref) < 1e-6, after
 
 
+@pytest.mark.parametrize("loss_path", ["torch", "fused"])
 @pytest.mark.parametrize("name", SAGE)
-def test_sage_gradients_match_reference(golden, name):
+def test_sage_gradients_match_reference(golden, name, loss_path):
+    """Gradients of every parameter vs the reference's autograd, through the
+    torch-op loss (graphsage.py:326-337 written out) and through the fused
+    loss node stageOne uses."""
     from furusato_recommend_amd.graphsage import SampleTree
     f = golden(name)
     m = sage_from(f)
@@ -602,12 +606,41 @@ def test_sage_gradients_match_reference(golden, name):
     groups = [torch.from_numpy(g.astype(np.int32)).cuda()
               for g in np.split(f["groups"], np.cumsum(f["group_len"])[:-1])]
     out = m.forward(SampleTree.from_groups(groups, L))
-    loss = m.loss(out[:B], out[B:2 * B], out[2 * B:])
+    if loss_path == "torch":
+        loss = m.loss(out[:B], out[B:2 * B], out[2 * B:])
+    else:
+        loss = m.loss_fused(out)
+    assert abs(float(loss.detach()) - float(f["loss"])) < TOL * abs(float(f["loss"]))
     loss.backward()
     assert rel(m.table_grad_dense(), f["g_table"]) < TOL
     for k, li in enumerate(m.w_linears):
         assert rel(li.weight.grad, f[f"g_w{k}"]) < TOL
         assert rel(li.bias.grad, f[f"g_b{k}"]) < TOL
+
+
+@pytest.mark.parametrize("relu", [True, False])
+@pytest.mark.parametrize("n", [1, 300, 20_000])
+def test_sage_linear_matches_cat_linear(n, relu):
+    """The fused hop Linear (two A blocks, bias + ReLU epilogue; masked dY,
+    split dX, dW / db in one pass) == cat + Linear + ReLU in float64."""
+    from furusato_recommend_amd.linear import sage_linear
+    torch.manual_seed(n)
+    d, no = 128, 128
+    xs = torch.randn(n, d, device="cuda", requires_grad=True)
+    xn = torch.randn(n, d, device="cuda", requires_grad=True)
+    w = (torch.randn(no, 2 * d, device="cuda") * 0.05).requires_grad_(True)
+    b = (torch.randn(no, device="cuda") * 0.1).requires_grad_(True)
+    y = sage_linear(xs, xn, w, b, relu)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    ref_in = [t.detach().double().requires_grad_(True) for t in (xs, xn, w, b)]
+    yr = torch.nn.functional.linear(torch.cat(ref_in[:2], 1), ref_in[2], ref_in[3])
+    if relu:
+        yr = yr.relu()
+    yr.backward(gy.double())
+    assert rel(y, yr) < 1e-5
+    for t, r in zip((xs, xn, w, b), ref_in):
+        assert rel(t.grad, r.grad) < 1e-5
 
 
 def test_fanout_sampler_and_dropout_mean():
