@@ -75,7 +75,9 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=2020)
     ap.add_argument("--prune", type=int, default=1,
                     help="frontier pruning (1) or every layer on every row (0)")
-    ap.add_argument("--dp-mode", default="sparse", choices=["sparse", "dense", "sharded"])
+    ap.add_argument("--dp-mode", default="auto", choices=["auto", "sparse", "dense", "sharded"],
+                    help="gradient exchange (dist.DataParallel); auto = sharded from "
+                         "W = 8, else sparse")
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
@@ -304,6 +306,7 @@ def main(argv=None):
     eng = model.engine
     emb = model.all_embedding.weight.data
     dp = DataParallel(eng, emb, model.optim, mode=args.dp_mode) if world > 1 else None
+    dp_mode = dp.mode if dp is not None else "none"
     B = args.batch
     u = torch.empty(B, dtype=torch.int32, device=dev)
     p, n = torch.empty_like(u), torch.empty_like(u)
@@ -387,7 +390,7 @@ def main(argv=None):
             f"{args.items} items / {args.edges} edges ({args.kind})")
         par = (f"dp{world} rehearsal: {world} ranks on one GPU, gloo collectives"
                if args.rehearse else
-               f"dp{world} (user-sharded, RCCL {args.dp_mode} gradient exchange)")
+               f"dp{world} (user-sharded, RCCL {dp_mode} gradient exchange)")
         line = {
             "metric": f"BPR positive-edges/sec (LightGCN-{args.layers} d={args.dim}, "
                       f"{args.users} x {args.items} / {args.edges} edges)",

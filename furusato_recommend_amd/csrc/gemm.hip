@@ -197,6 +197,148 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
   }
 }
 
+// Double-buffered form: the next chunk's global loads are issued before the
+// current chunk's products, staged into the other LDS buffer after them, one
+// barrier per chunk.  XCD: the ncol column tiles of a row tile get block ids
+// 8 apart (the same XCD under round-robin placement), so the row tile's A
+// rows are read once from HBM and once more from that XCD's L2.
+template <int BM, bool XCD>
+__global__ __launch_bounds__(256, 2) void gemm_nt2_kernel(const float *__restrict__ A,
+                                                         const float *__restrict__ B,
+                                                         const float *__restrict__ bias,
+                                                         float *__restrict__ C, int64_t n,
+                                                         int Kr, int No, NtArgs fx) {
+  constexpr int TM = BM / 64;
+  constexpr int QA = BM * 8 / 256;
+  constexpr int QB = 4;
+  __shared__ __attribute__((aligned(16))) float sA[2][BM * kLdNT];
+  __shared__ __attribute__((aligned(16))) float sB[2][kTile * kLdNT];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int ncol = No / kTile;
+  int64_t rt;
+  int ct;
+  if (XCD && ncol > 1) {
+    const int64_t b = blockIdx.x, grp = b / (8 * ncol);
+    const int j = (int)(b - grp * 8 * ncol);
+    rt = grp * 8 + (j & 7);
+    ct = j >> 3;
+  } else {
+    rt = blockIdx.x / ncol;
+    ct = blockIdx.x % ncol;
+  }
+  const int64_t m0 = rt * BM;
+  if (m0 >= n) return;
+  const int n0 = ct * kTile;
+  float4 ra[QA], rb[QB];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int64_t row = m0 + r;
+      float4 v = f4_zero();
+      if (row < n) {
+        if (fx.A2 == nullptr) {
+          v = ld4(A + row * Kr + k0 + 4 * c4);
+        } else if (k0 < fx.Ks) {
+          v = ld4(A + row * fx.Ks + k0 + 4 * c4);
+        } else {
+          v = ld4(fx.A2 + row * (Kr - fx.Ks) + (k0 - fx.Ks) + 4 * c4);
+        }
+        if (fx.Amask != nullptr) {
+          const float4 mk = ld4(fx.Amask + row * Kr + k0 + 4 * c4);
+          v.x = mk.x > 0.f ? v.x : 0.f;
+          v.y = mk.y > 0.f ? v.y : 0.f;
+          v.z = mk.z > 0.f ? v.z : 0.f;
+          v.w = mk.w > 0.f ? v.w : 0.f;
+        }
+      }
+      ra[q] = v;
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      rb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
+    }
+  };
+  auto stage = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      st4(sA[buf] + r * kLdNT + 4 * c4, ra[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      st4(sB[buf] + r * kLdNT + 4 * c4, rb[q]);
+    }
+  };
+  f32x16 acc[TM][2];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  auto compute = [&](int buf) {
+#pragma unroll
+    for (int sub = 0; sub < kChunk / 8; ++sub) {
+      float4 fa[TM], fb[2];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+        fa[tm] = ld4(sA[buf] + (wm * (BM / 2) + tm * 32 + i) * kLdNT + sub * 8 + 4 * h);
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+        fb[tn] = ld4(sB[buf] + (wn * 64 + tn * 32 + i) * kLdNT + sub * 8 + 4 * h);
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          acc[tm][tn] = mfma32(fa[tm].x, fb[tn].x, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].y, fb[tn].y, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].z, fb[tn].z, acc[tm][tn]);
+          acc[tm][tn] = mfma32(fa[tm].w, fb[tn].w, acc[tm][tn]);
+        }
+    }
+  };
+  const int nc = Kr / kChunk;
+  load(0);
+  stage(0);
+  __syncthreads();
+  for (int c = 0; c < nc; ++c) {
+    if (c + 1 < nc) load((c + 1) * kChunk);  // in flight during the products
+    compute(c & 1);
+    if (c + 1 < nc) stage((c + 1) & 1);      // the other buffer: last read at c - 1
+    __syncthreads();
+  }
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn) {
+    const int col = n0 + wn * 64 + tn * 32 + i;
+    const float bv = bias ? bias[col] : 0.f;
+    float *cb = C;
+    int ldc = No, cc = col;
+    if (fx.C2 != nullptr) {
+      if (col < fx.Ns) {
+        ldc = fx.Ns;
+      } else {
+        cb = fx.C2;
+        ldc = No - fx.Ns;
+        cc = col - fx.Ns;
+      }
+    }
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float y = acc[tm][tn][r] + bv;
+        if (fx.relu) y = fmaxf(y, 0.f);
+        if (row < n) cb[row * ldc + cc] = y;
+      }
+  }
+}
+
 // ------------------------------------------------------------------ gemm_tn
 // Workgroup (slice s, tile_m, tile_n): partial C tile over rows
 // [s * rows_per_slice, +rows_per_slice) -> work[s][M][No]; with colsum, the
@@ -377,12 +519,26 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   MIREC_CHECK_ARG(Amask == nullptr || (A2 == nullptr && (uintptr_t)Amask % 16 == 0));
   MIREC_CHECK_ARG(C2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0));
   NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0};
-  // 128-row tiles, one chunk of loads ahead: 64-row tiles and two chunks
-  // ahead measured the same (29.5-30.2 us at 56 K x 128 x 128): the shape is
-  // bound by the MFMA time of the busiest CU plus fixed prologue / epilogue
   const unsigned ncol = (unsigned)(No / kTile);
+  hipStream_t st = (hipStream_t)stream;
+#ifndef MIREC_NT_V
+#define MIREC_NT_V 2
+#endif
+#ifndef MIREC_NT_BM
+#define MIREC_NT_BM 128
+#endif
+#if MIREC_NT_V == 1
+  // 128-row tiles, one chunk of loads ahead: 64-row tiles and two chunks
+  // ahead measured the same (29.5-30.2 us at 56 K x 128 x 128)
   hipLaunchKernelGGL((gemm_nt_kernel<128, 1>), dim3((unsigned)((n + 127) / 128) * ncol),
-                     dim3(256), 0, (hipStream_t)stream, A, B, bias, C, n, (int)Kr, (int)No, fx);
+                     dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx);
+#else
+  constexpr int BM = MIREC_NT_BM;
+  const int64_t nrow = (n + BM - 1) / BM;
+  const int64_t blocks = ncol > 1 ? (nrow + 7) / 8 * 8 * ncol : nrow;
+  hipLaunchKernelGGL((gemm_nt2_kernel<BM, true>), dim3((unsigned)blocks), dim3(256), 0, st, A, B,
+                     bias, C, n, (int)Kr, (int)No, fx);
+#endif
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

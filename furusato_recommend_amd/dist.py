@@ -26,7 +26,15 @@ Gradient exchange modes:
     of the 282 MB dense gradient.
   * ``dense``: SUM all-reduce of the dense gradient dE, then the dense Adam
     kernel (the textbook DDP exchange; kept for comparison).
-Both give the gradient of the union batch; replicas stay bit-identical.
+  * ``sharded``: the sparse exchange, but the last backward layer and its
+    fused Adam run only on this rank's contiguous row shard (N/W rows; the
+    optimizer state of the other rows is not touched here — ZeRO-1 style),
+    then the updated table is all-gathered (N x D x 4 bytes per step, 282 MB
+    at C2) and the next forward re-derives dinv ⊙ E.  It trades the
+    replicated full last layer + Adam (1.6 ms at C2 on every rank) for the
+    all-gather, which pays once xGMI moves the table faster than that
+    (DESIGN.md §6).
+All modes give the gradient of the union batch; replicas stay bit-identical.
 
 The initial parameters are broadcast from rank 0 (the DDP ctor broadcast,
 ddp_lgcn.py:663).  The engine is duck-typed (forward / bpr / backward /
@@ -59,10 +67,21 @@ def init_distributed(backend: str = "nccl", device: torch.device | None = None,
     dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
+# World size from which "auto" shards the last layer + Adam (DESIGN.md §6:
+# projected per-rank compute at C2, sparse vs sharded, 5.33 vs 4.95 ms at
+# W = 2, 5.72 vs 4.85 at W = 4, 5.98 vs 4.88 at W = 8; the all-gather of the
+# 282 MB table must fit in the difference — at W = 8 it does at >= 260 GB/s of
+# all-gather bandwidth, at W = 2 it would need ~360 GB/s over one xGMI link).
+SHARD_FROM_WORLD = int(os.environ.get("MIREC_SHARD_FROM_WORLD", "8"))
+
+
 class DataParallel:
-    def __init__(self, engine, emb: torch.Tensor, adam, group=None, mode: str = "sparse"):
-        if mode not in ("sparse", "dense"):
+    def __init__(self, engine, emb: torch.Tensor, adam, group=None, mode: str = "auto"):
+        if mode not in ("auto", "sparse", "dense", "sharded"):
             raise ValueError(mode)
+        if mode == "auto":
+            w = dist.get_world_size(group) if dist.is_initialized() else 1
+            mode = "sharded" if w >= SHARD_FROM_WORLD else "sparse"
         self.mode = mode
         self.engine = engine
         self.emb = emb
@@ -74,6 +93,53 @@ class DataParallel:
         self.grad = torch.empty_like(emb) if mode == "dense" else None
         if self.world > 1:
             dist.broadcast(emb.data, src=0, group=group)
+        if mode == "sharded":
+            self._init_shard()
+
+    def _init_shard(self):
+        """This rank's rows i ≡ r (mod W) — interleaved, so every shard gets
+        its share of both the short user rows and the long item rows (a
+        contiguous split would give rank 0 only users: 0.5 vs 1.3 ms of last
+        layer at W = 2) — as a static byte map + row lists for the last
+        backward layer, and the [W, S, D] staging buffer (S = ceil(N / W))
+        the shards are all-gathered into."""
+        N, D = self.emb.shape
+        W, r = self.world, self.rank
+        S = (N + W - 1) // W
+        words = (N + 15) // 16 * 4
+        bm = torch.zeros(words, dtype=torch.int32, device=self.emb.device)
+        bm.view(torch.uint8)[r:N:W] = 1
+        self._shard_bm = bm
+        self.last_rows = self.engine.static_row_lists(bm)
+        self._stage = torch.empty(W, S, D, dtype=self.emb.dtype, device=self.emb.device) \
+            if W > 1 else None
+        self._S = S
+
+    def _gather_rows(self, t: torch.Tensor):
+        """Every rank's shard rows of ``t`` [N, D] to every rank (in place):
+        pack rows r, r+W, ... into this rank's staging slot, one all-gather,
+        then scatter slot w's rows back to w, w+W, ... (strided copies)."""
+        if self.world == 1:
+            return
+        N, D = t.shape
+        W, S, st = self.world, self._S, self._stage
+        r = self.rank
+        n_r = len(range(r, N, W))
+        st[r, :n_r].copy_(t[r:N:W])
+        dist.all_gather_into_tensor(st.view(W * S, D), st[r], group=self.group)
+        full = N // W  # rows s < full hold all W ranks' entries
+        if full:
+            t[: full * W].view(full, W, D).copy_(st[:, :full].transpose(0, 1))
+        for w in range(N - full * W):  # the ragged last row block
+            t[full * W + w].copy_(st[w, full])
+
+    def gather_optimizer_state(self):
+        """``sharded``: each rank's Adam moments are current on its own rows
+        only; bring every row's moments to every rank (e.g. before a
+        checkpoint of the optimizer state)."""
+        if self.mode == "sharded" and self.adam is not None:
+            self._gather_rows(self.adam.exp_avg)
+            self._gather_rows(self.adam.exp_avg_sq)
 
     def shard(self):
         """(shard, n_shards) for the on-device sampler."""
@@ -100,12 +166,17 @@ class DataParallel:
         out = eng.forward_for_batch(self.emb, users, pos, neg)
         loss = eng.bpr(out, self.emb, users, pos, neg, decay, loss_accum,
                        grad_scale=1.0 / self.world)
-        if self.mode == "sparse":
+        if self.mode in ("sparse", "sharded"):
             keys, rows_p, rows_e = eng.export_seeds()
             if self.distributed:
                 keys, rows_p, rows_e = self._exchange(keys, rows_p, rows_e)
             eng.import_seeds(keys, rows_p, rows_e)
-            eng.backward(self.emb, adam=self.adam)
+            if self.mode == "sparse":
+                eng.backward(self.emb, adam=self.adam)
+            else:
+                eng.backward(self.emb, adam=self.adam, last_rows=self.last_rows)
+                self._gather_rows(self.emb)
+                eng.invalidate_prescaled()
         else:
             eng.backward(self.emb, grad_out=self.grad)
             if self.distributed:

@@ -426,6 +426,23 @@ class PropagationEngine:
             f = "bytemap" if self._self_cap > 3 * self.max_batch else "slot"
         return self.bm_self if f == "bytemap" else None
 
+    def static_row_lists(self, bm: torch.Tensor) -> dict:
+        """Launch arguments restricting a propagation to the rows whose byte in
+        ``bm`` (uint8-viewable, [>= n_rows]) is set: the byte map plus its
+        narrow / wide row lists, built once (a fixed row set, e.g. a
+        data-parallel rank's shard)."""
+        g = self.g
+        N = g.n_nodes
+        dev = g.device
+        nl = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
+        wl = torch.zeros(max(N, 1), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        check(lib.mirec_mask_compact(g.csr_ptr(), bm.data_ptr(), int(self.narrow_max),
+                                     nl.data_ptr(), cnt[0].data_ptr(), wl.data_ptr(),
+                                     cnt[1].data_ptr(), _lib.stream_handle()), "mask_compact")
+        return dict(row_mask=bm, row_list=nl, row_count=cnt[0], row_list_cap=N,
+                    wide_list=wl, wide_count=cnt[1])
+
     def _self_rows(self):
         return self._lists(0, self.bm_self, self.s_lists, min(self._self_cap, self.g.n_nodes))
 
@@ -566,11 +583,14 @@ class PropagationEngine:
 
     # ------------------------------------------------------------- backward
     def backward(self, emb: torch.Tensor, adam: AdamState | None = None,
-                 grad_out: torch.Tensor | None = None):
+                 grad_out: torch.Tensor | None = None, last_rows: dict | None = None):
         """Horner backward from the current seeds (g_L = d, g_l = d + Â g_{l+1}).
 
         With ``adam`` the last layer applies Adam to ``emb`` in place (fused);
-        otherwise the dense gradient dLoss/dE is written to ``grad_out``."""
+        otherwise the dense gradient dLoss/dE is written to ``grad_out``.
+        ``last_rows`` (static_row_lists) restricts the last layer — and so the
+        update — to a fixed row set (a data-parallel rank's shard); the other
+        rows of ``emb`` and of the next step's dinv ⊙ E are left alone."""
         if (adam is None) == (grad_out is None):
             raise ValueError("exactly one of adam / grad_out")
         if self._seeds is None or not self._masks_ready:
@@ -585,6 +605,8 @@ class PropagationEngine:
                 final.update(xs_out=self.x0s)
         else:
             final.update(out=grad_out)
+        if last_rows is not None:
+            final.update(last_rows)
         if L == 0:
             self._prop(in_mode=IN_NONE, seed=seed_p, **final)
         else:
@@ -615,7 +637,7 @@ class PropagationEngine:
                                        _lib.stream_handle()), "bpr_seed_reset")
         self._seeds = None
         self._masks_ready = False
-        self._x0s_token = self._token(emb) if (adam is not None and L > 0
+        self._x0s_token = self._token(emb) if (adam is not None and L > 0 and last_rows is None
                                                and self.reuse_prescaled) else None
 
     def adam_step(self, param: torch.Tensor, grad: torch.Tensor, adam: AdamState):

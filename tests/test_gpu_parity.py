@@ -346,7 +346,7 @@ def test_seed_exchange_two_ranks_in_one_process(golden):
     assert int((eng.slot != -1).sum()) == 0
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "sharded"])
 def test_data_parallel_rccl_world1(golden, mode):
     """dist.DataParallel through real RCCL collectives (world_size 1) ==
     the reference's stageOne."""
@@ -1695,7 +1695,7 @@ def _run_ranks(target, args, world=2, timeout=300):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "sharded"])
 def test_data_parallel_two_ranks_hip_engine(golden, mode):
     """2 ranks (processes) of dist.DataParallel with the real HIP engine on
     one GPU: replicas bit-identical after each step and equal to the

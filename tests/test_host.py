@@ -164,7 +164,13 @@ class OracleEngine:
         e.index_add_(0, keys[ok].long(), rows_e[ok])
         self._d, self._e = d, e
 
-    def backward(self, emb, adam=None, grad_out=None):
+    def static_row_lists(self, bm):
+        return {"rows": bm.view(torch.uint8)[: self.o.emb.shape[0]].bool()}
+
+    def invalidate_prescaled(self):
+        pass
+
+    def backward(self, emb, adam=None, grad_out=None, last_rows=None):
         if grad_out is not None:
             grad_out.copy_(self.o.grad(*self._batch) * self._scale)
             return
@@ -172,7 +178,12 @@ class OracleEngine:
         for _ in range(self.o.L):
             x = O.lgconv(x, self.o.ei, self.o.div)
             g = g + x
+        before = self.o.emb.detach().clone()
         self.adam_step(emb, g + self._e, adam)
+        if last_rows is not None:  # only this rank's shard is updated here
+            keep = ~last_rows["rows"]
+            with torch.no_grad():
+                self.o.emb[keep] = before[keep]
 
     def adam_step(self, param, grad, adam):
         self.o.emb.grad = grad.clone()
@@ -207,7 +218,7 @@ def _dp_worker(rank, world, port, fpath, q, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["sparse", "dense"])
+@pytest.mark.parametrize("mode", ["sparse", "dense", "sharded"])
 def test_data_parallel_equals_union_batch(golden, mode):
     """2 ranks on disjoint halves == one process on the union batch (the
     reference's own stageOne on all 64 triples = emb_step1/2), for both the
@@ -361,3 +372,39 @@ def test_host_threads_bounded():
     import bench
     n = bench.host_threads()
     assert 1 <= n <= (os.cpu_count() or 1)
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from furusato_recommend_amd.dist import DataParallel
+
+    class Eng:
+        def static_row_lists(self, bm):
+            return {"bm": bm}
+    N, D = 11, 3
+    emb = torch.zeros(N, D)
+    dp = DataParallel(Eng(), emb, None, mode="sharded")
+    t = torch.full((N, D), -1.0)
+    t[rank:N:world] = torch.arange(N, dtype=torch.float32)[rank:N:world, None] * 10 + rank
+    dp._gather_rows(t)
+    q.put((rank, t.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_sharded_gather_rows_ragged_world3():
+    """The sharded mode's all-gather of interleaved row shards (row i owned by
+    rank i mod W) at W = 3 with N = 11 rows (a ragged last block): every rank
+    ends with every owner's rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(3))
+    for p in procs:
+        p.join(timeout=60)
+    want = (np.arange(11) * 10 + np.arange(11) % 3).astype(np.float32)
+    for r in range(3):
+        assert np.array_equal(res[r][:, 0], want) and np.array_equal(res[r][:, 2], want)

@@ -35,6 +35,11 @@ def main():
     ap.add_argument("--batch", type=int, default=2048)
     ap.add_argument("--sparse-filters", default="auto",
                     help="comma list of engine.sparse_filter values to compare")
+    ap.add_argument("--modes", default="sparse",
+                    help="comma list of DataParallel modes: sparse (replicated last "
+                         "layer + Adam) and/or sharded (rank 0's row shard only, plus the "
+                         "local copies and re-prescale of the all-gather; the RCCL "
+                         "transfer itself is not measured)")
     args = ap.parse_args()
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     from furusato_recommend_amd.engine import sample_triples
@@ -51,9 +56,18 @@ def main():
     p, n = torch.empty_like(u), torch.empty_like(u)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
 
-    configs = [(int(w), f) for w in args.worlds.split(",") for f in args.sparse_filters.split(",")]
-    for W, filt in configs:
+    configs = [(int(w), f, m) for w in args.worlds.split(",")
+               for f in args.sparse_filters.split(",") for m in args.modes.split(",")]
+    for W, filt, mode in configs:
         eng.sparse_filter = filt
+        last_rows, stage = None, None
+        if mode == "sharded":
+            N = model.graph.n_nodes
+            S = (N + W - 1) // W
+            bm = torch.zeros((N + 15) // 16 * 4, dtype=torch.int32, device=dev)
+            bm.view(torch.uint8)[0:N:W] = 1  # rank 0's interleaved shard (dist.py)
+            last_rows = eng.static_row_lists(bm)
+            stage = torch.empty(W, S, args.dim, device=dev)
         others = []
         for r in range(1, W):
             sample_triples(model.graph, B, 0, 10**9, u, p, n, err, r, W)
@@ -74,7 +88,13 @@ def main():
             rp = torch.cat([sp] + [o[1] for o in others])
             re = torch.cat([se] + [o[2] for o in others])
             eng.import_seeds(keys, rp, re)
-            eng.backward(emb, adam=model.optim)
+            eng.backward(emb, adam=model.optim, last_rows=last_rows)
+            if mode == "sharded":  # the all-gather's local copies + re-prescale
+                N = emb.shape[0]
+                stage[0, : len(range(0, N, W))].copy_(emb[0:N:W])
+                full = N // W
+                emb[: full * W].view(full, W, -1).copy_(stage[:, :full].transpose(0, 1))
+                eng.invalidate_prescaled()
 
         for _ in range(args.warmup):
             step()
@@ -92,7 +112,8 @@ def main():
             ms = [ev[s * per + j][0].elapsed_time(ev[s * per + j][1]) for s in range(args.steps)]
             launches.append(round(sum(ms) / len(ms), 4))
         f1 = int((eng.bm_hop.view(torch.uint8)[: model.graph.n_nodes] != 0).sum())
-        print(json.dumps({"world": W, "sparse_filter": filt, "ms_per_step_rank": round(dt * 1e3, 4),
+        print(json.dumps({"world": W, "mode": mode, "sparse_filter": filt,
+                          "ms_per_step_rank": round(dt * 1e3, 4),
                           "edges_per_s_projected": round(W * B / dt, 1),
                           "launch_ms": launches, "union_F1_rows": f1}), flush=True)
 
