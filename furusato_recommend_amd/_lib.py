@@ -36,6 +36,7 @@ class CSR(Structure):
         ("_pad", c_int32), ("n_long", c_int64), ("n_seg", c_int64),
         ("long_rows", c_void_p), ("long_segptr", c_void_p),
         ("seg_row", c_void_p), ("seg_beg", c_void_p),
+        ("col_sorted", c_void_p), ("n_sorted", c_int64),
     ]
 
 
@@ -83,6 +84,7 @@ SIGNATURES = {
     "mirec_struct_sizes": (c_int, [POINTER(c_size_t), POINTER(c_size_t), POINTER(c_size_t)]),
     "mirec_csr_bipartite": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64,
                                     c_void_p, c_void_p, c_void_p]),
+    "mirec_csr_sort_rows": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "mirec_csr_from_coo": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p,
                                    c_void_p, c_void_p]),
     "mirec_parse_interactions": (c_int, [c_void_p, c_int64, c_int64, c_int32, POINTER(c_int64),
@@ -205,6 +207,11 @@ SIGNATURES = {
                                   c_void_p]),
     "mirec_topk_masked": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_int32, c_void_p, c_void_p, c_void_p]),
+    "mirec_bpr_sample_capped_workspace": (c_int, [c_int64, c_int64, POINTER(c_size_t)]),
+    "mirec_bpr_sample_capped": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_int32,
+                                        c_uint64, c_uint64, c_int32, c_int32, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,
                                  c_uint64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),

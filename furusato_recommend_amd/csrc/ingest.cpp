@@ -42,7 +42,14 @@ inline bool parse_line(const char *p, const char *e, int64_t &uid, F &&on_item, 
       return have_uid;
     }
     int64_t v = 0;
-    while (p < e && *p >= '0' && *p <= '9') v = v * 10 + (*p++ - '0');
+    while (p < e && *p >= '0' && *p <= '9') {
+      const int d = *p++ - '0';
+      if (v > (INT64_MAX - d) / 10) {  // an id that does not fit int64: malformed
+        bad = true;
+        return have_uid;
+      }
+      v = v * 10 + d;
+    }
     if (p < e && !is_space(*p)) {
       bad = true;
       return have_uid;

@@ -694,4 +694,38 @@ def sample_triples(graph: Graph, batch: int, seed: int, offset: int, users, pos,
           "bpr_sample")
 
 
+def sample_epoch_capped(graph: Graph, n_candidates: int, cap: int, seed: int, offset: int = 0,
+                        shard: int = 0, n_shards: int = 1, return_candidates: bool = False):
+    """The ddp_lgcn.py epoch sampler on device (ddp_lgcn.py:33-35, 541-582):
+    ``n_candidates`` (= TRAIN_ITERATIVE x trainDataSize) uniform users, a
+    positive each, kept while the positive item was kept fewer than ``cap``
+    (POSITIVE_NUM_LIMIT) times before in draw order.  Returns int32 device
+    (users, pos, neg) of the kept triples in draw order (+ every candidate's
+    user and positive, -1 = skipped user, with ``return_candidates``)."""
+    dev = graph.device
+    n = int(n_candidates)
+    i32 = dict(dtype=torch.int32, device=dev)
+    users, pos, neg = (torch.empty(max(n, 1), **i32) for _ in range(3))
+    count = torch.zeros(1, **i32)
+    err = torch.zeros(1, **i32)
+    cu = torch.empty(max(n, 1), **i32) if return_candidates else None
+    cp = torch.empty(max(n, 1), **i32) if return_candidates else None
+    nb = ctypes.c_size_t(0)
+    check(lib.mirec_bpr_sample_capped_workspace(n, graph.m_items, ctypes.byref(nb)),
+          "bpr_sample_capped_workspace")
+    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
+    check(lib.mirec_bpr_sample_capped(graph.csr_ptr(), graph.n_users, graph.m_items, n, int(cap),
+                                      ctypes.c_uint64(seed & (2**64 - 1)),
+                                      ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
+                                      int(n_shards), users.data_ptr(), pos.data_ptr(),
+                                      neg.data_ptr(), count.data_ptr(), err.data_ptr(), ptr(cu),
+                                      ptr(cp), ws.data_ptr(), nb.value, _lib.stream_handle()),
+          "bpr_sample_capped")
+    k = int(count.item())
+    if int(err.item()) != 0:
+        raise RuntimeError("sampler: a user has every item as a positive")
+    out = (users[:k], pos[:k], neg[:k])
+    return out + (cu[:n], cp[:n]) if return_candidates else out
+
+
 _ = math

@@ -66,8 +66,24 @@ class Graph:
                        split=self.split, _pad=0, n_long=self.n_long, n_seg=self.n_seg,
                        long_rows=self.long_rows.data_ptr(),
                        long_segptr=self.long_segptr.data_ptr(),
-                       seg_row=self.seg_row.data_ptr(), seg_beg=self.seg_beg.data_ptr())
+                       seg_row=self.seg_row.data_ptr(), seg_beg=self.seg_beg.data_ptr(),
+                       col_sorted=None, n_sorted=0)
         self.transpose = None  # set for non-symmetric graphs (from_edge_index)
+        self.col_sorted = None
+        if self.n_users > 0 and self.m_items > 0:
+            self._sort_user_rows()
+
+    def _sort_user_rows(self):
+        """A sorted copy of the user rows (the positives of every user) for the
+        samplers' binary-search membership test (negative_sample.py:121-126)."""
+        nu = self.n_users
+        n = int(self.rowptr_host[nu] - self.rowptr_host[0])
+        cs = np.empty(max(n, 1), np.int32)
+        check(lib.mirec_csr_sort_rows(self.rowptr_host.ctypes.data, self.col_host.ctypes.data,
+                                      nu, cs.ctypes.data), "csr_sort_rows")
+        self.col_sorted = torch.from_numpy(cs).to(self.device)
+        self.csr.col_sorted = self.col_sorted.data_ptr()
+        self.csr.n_sorted = nu
 
     # ------------------------------------------------------------------ build
     @classmethod

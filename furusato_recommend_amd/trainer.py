@@ -4,7 +4,10 @@ the proprietary product-name / CSV side outputs.
   train()        one epoch: UniformSample of trainDataSize triples — on device
                  (mirec_bpr_sample) instead of the host numpy loop
                  (negative_sample.py:98-134, trainer.py:56-81) — then
-                 model.OneEpoch.  The reference shuffles the sampled triples
+                 model.OneEpoch.  config["sampler"] = "ddp_capped" uses the
+                 ddp_lgcn.py variant instead (train_iterative x trainDataSize
+                 candidates, at most positive_num_limit triples per positive
+                 item: ddp_lgcn.py:33-35, 541-582; mirec_bpr_sample_capped).  The reference shuffles the sampled triples
                  (utils.shuffle); on-device draws are i.i.d., so the shuffle
                  is a distributional no-op and is skipped.
   test()         Recall / Precision / NDCG / HR @ topks (trainer.py:115-170)
@@ -34,10 +37,18 @@ class Trainer:
 
     def train(self):
         n = int(self.dataset.trainDataSize)
-        users, pos, neg = self.model.sample(n, seed=self.seed, offset=self.epoch * n)
-        loss = self.model.OneEpoch(users, pos, neg)
-        if int(self.model._sample_err.item()) != 0:
-            raise RuntimeError("sampler: a user has every item as a positive")
+        if self.config.get("sampler", "uniform") == "ddp_capped":
+            from .engine import sample_epoch_capped
+            nc = int(self.config.get("train_iterative", 3)) * n
+            users, pos, neg = sample_epoch_capped(self.model.graph, nc,
+                                                  int(self.config.get("positive_num_limit", 3000)),
+                                                  seed=self.seed, offset=self.epoch * nc)
+            loss = self.model.OneEpoch(users, pos, neg)
+        else:
+            users, pos, neg = self.model.sample(n, seed=self.seed, offset=self.epoch * n)
+            loss = self.model.OneEpoch(users, pos, neg)
+            if int(self.model._sample_err.item()) != 0:
+                raise RuntimeError("sampler: a user has every item as a positive")
         self.epoch += 1
         return loss
 

@@ -116,7 +116,18 @@ typedef struct mirec_csr {
   const int64_t *long_segptr; /* [n_long+1] */
   const int32_t *seg_row;     /* [n_seg] */
   const int64_t *seg_beg;     /* [n_seg] */
+  /* optional (NULL = none): rows [0, n_sorted) with each row's entries sorted
+   * ascending, entry rowptr[r] + j of the CSR at index rowptr[r] - rowptr[0]
+   * + j (mirec_csr_sort_rows); the samplers' membership tests binary-search
+   * them (the user rows of a bipartite graph) */
+  const int32_t *col_sorted;
+  int64_t n_sorted;
 } mirec_csr_t;
+
+/* Host: rows [0, n_rows) of (rowptr, col) with each row sorted ascending into
+ * col_sorted [rowptr[n_rows] - rowptr[0]] (the csr's col_sorted). */
+int mirec_csr_sort_rows(const int64_t *rowptr, const int32_t *col, int64_t n_rows,
+                        int32_t *col_sorted);
 
 /* ------------------------------------------------------------------------ */
 /* Propagation: one LightGCN layer (CSR segment-gather SpMM + epilogue)      */
@@ -353,6 +364,23 @@ int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
                      int32_t shard, int32_t n_shards, int32_t *users,
                      int32_t *pos, int32_t *neg, int32_t *err,
                      mirec_stream_t stream);
+
+/* The ddp_lgcn.py epoch sampler (ddp_lgcn.py:33-35, 541-582): n_candidates
+ * users drawn uniformly from the shard (users without positives are
+ * skipped), a uniform positive each, and a candidate kept only if fewer than
+ * `cap` earlier candidates (draw order) with the same positive item were kept
+ * (POSITIVE_NUM_LIMIT = 3000); the kept ones (in draw order) draw a negative
+ * not among the user's positives.  users / pos / neg: capacity n_candidates;
+ * count[0] (device) = kept triples.  cand_u / cand_p (optional, [n]): every
+ * candidate's user and positive (-1 = skipped).  Workspace:
+ * mirec_bpr_sample_capped_workspace bytes. */
+int mirec_bpr_sample_capped_workspace(int64_t n_candidates, int64_t m_items, size_t *bytes);
+int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
+                            int64_t n_candidates, int32_t cap, uint64_t seed, uint64_t offset,
+                            int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
+                            int32_t *neg, int32_t *count, int32_t *err, int32_t *cand_u,
+                            int32_t *cand_p, void *workspace, size_t workspace_bytes,
+                            mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* GraphSAGE hop ops (model/graphsage.py:311-324, neighbor_sampling.py)      */

@@ -1831,3 +1831,62 @@ def test_fused_table_adam_equals_dense_adam():
                                       float((sa.exp_avg_sq - sb.exp_avg_sq).abs().max()))
         ref = torch.stack(slice_norms(wa, nu))
         assert rel(norms, ref) < 1e-6
+
+
+# ------------------------------------------------------------------ samplers
+def test_capped_epoch_sampler_matches_sequential_rule():
+    """mirec_bpr_sample_capped == ddp_lgcn.py's loop (ddp_lgcn.py:541-582)
+    applied to the same candidate stream: users without positives skipped,
+    a candidate kept iff its positive was kept < cap times before it (draw
+    order), kept triples in draw order; negatives never positives."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.engine import sample_epoch_capped
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(3000, 400, 30_000, seed=4, kind="zipf", test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    cap = 40
+    u, p, n, cu, cp = sample_epoch_capped(g, 3 * 30_000, cap, seed=9, return_candidates=True)
+    cu, cp = cu.cpu().numpy(), cp.cpu().numpy()
+    cnt, kept = {}, []
+    for t in range(len(cp)):
+        if cp[t] < 0:
+            continue
+        if cnt.get(int(cp[t]), 0) >= cap:
+            continue
+        cnt[int(cp[t])] = cnt.get(int(cp[t]), 0) + 1
+        kept.append(t)
+    kept = np.array(kept)
+    assert len(kept) == u.numel() and len(kept) < len(cp)  # the cap bit
+    assert np.array_equal(u.cpu().numpy(), cu[kept]) and np.array_equal(p.cpu().numpy(), cp[kept])
+    assert max(np.bincount(p.cpu().numpy())) <= cap
+    rp, col = g.rowptr_host, g.col_host
+    uu, pp, nn = u.cpu().numpy(), p.cpu().numpy(), n.cpu().numpy()
+    for k in range(0, len(uu), 97):
+        row = col[rp[uu[k]]:rp[uu[k] + 1]] - g.n_users
+        assert pp[k] in row and nn[k] not in row
+
+
+def test_sampler_binary_search_equals_scan():
+    """With the sorted user rows (csr.col_sorted) the negative rejection is a
+    binary search; the triples equal the row-scan ones draw for draw."""
+    import ctypes
+
+    from furusato_recommend_amd import SyntheticBipartite, _lib
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(5000, 300, 200_000, seed=6, kind="zipf", test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    assert g.col_sorted is not None
+    outs = []
+    for sorted_rows in (True, False):
+        csr = _lib.CSR.from_buffer_copy(g.csr)
+        if not sorted_rows:
+            csr.col_sorted, csr.n_sorted = None, 0
+        t = [torch.empty(8192, dtype=torch.int32, device="cuda") for _ in range(3)]
+        err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        _lib.check(_lib.lib.mirec_bpr_sample(ctypes.byref(csr), g.n_users, g.m_items, 8192,
+                                             ctypes.c_uint64(3), ctypes.c_uint64(0), 0, 1,
+                                             t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                             err.data_ptr(), _lib.stream_handle()), "sample")
+        outs.append(torch.stack(t).cpu())
+        assert int(err.item()) == 0
+    assert torch.equal(outs[0], outs[1])

@@ -408,3 +408,45 @@ def test_sharded_gather_rows_ragged_world3():
     want = (np.arange(11) * 10 + np.arange(11) % 3).astype(np.float32)
     for r in range(3):
         assert np.array_equal(res[r][:, 0], want) and np.array_equal(res[r][:, 2], want)
+
+
+def test_csr_sort_rows_matches_numpy():
+    """mirec_csr_sort_rows (host, threaded): each user row sorted ascending,
+    multi-edges kept — the samplers' binary-search rows."""
+    from furusato_recommend_amd import _lib
+    rng = np.random.default_rng(2)
+    n_rows = 3000
+    deg = rng.integers(0, 90, n_rows)
+    rowptr = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    col = rng.integers(0, 500, int(rowptr[-1])).astype(np.int32)
+    out = np.empty_like(col)
+    _lib.check(_lib.lib.mirec_csr_sort_rows(rowptr.ctypes.data, col.ctypes.data, n_rows,
+                                            out.ctypes.data), "sort_rows")
+    for r in range(n_rows):
+        assert np.array_equal(out[rowptr[r]:rowptr[r + 1]], np.sort(col[rowptr[r]:rowptr[r + 1]]))
+
+
+def test_host_code_under_asan_ubsan(tmp_path):
+    """The host C++ of libmirec (graph build, row sort, long-row schedule,
+    text ingest) built with AddressSanitizer + UBSan and run on random and
+    malformed inputs (tests/native/host_check.cpp)."""
+    import shutil
+    import subprocess
+    from tests.conftest import ROOT
+    cxx = shutil.which("g++")
+    if cxx is None:
+        pytest.skip("no g++")
+    src = os.path.join(ROOT, "furusato_recommend_amd", "csrc")
+    exe = str(tmp_path / "host_check")
+    cmd = [cxx, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer",
+           "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-pthread",
+           "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "native", "host_check.cpp"),
+           os.path.join(src, "graph.cpp"), os.path.join(src, "ingest.cpp"), "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True, timeout=300)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    env.pop("LD_PRELOAD", None)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "host_check ok" in r.stdout
