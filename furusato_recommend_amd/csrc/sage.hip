@@ -43,6 +43,40 @@ __global__ __launch_bounds__(256) void sample_fanout_kernel(
   children[i] = out;
 }
 
+// Without replacement (PyG NeighborSampler's default, the sampler of
+// model/graphsage.py:342-365): a node with deg <= k keeps all its entries
+// (row order; the remaining slots are -1), otherwise k distinct entries by
+// Floyd's algorithm (the chosen positions are kept in the output row itself
+// while drawing, then mapped to node ids).  One thread per target node.
+__global__ __launch_bounds__(256) void sample_fanout_norep_kernel(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n_rows,
+    const int32_t *__restrict__ nodes, int64_t n, int32_t k, uint64_t seed, uint64_t offset,
+    int32_t *__restrict__ children) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int32_t *out = children + t * k;
+  const int32_t v = nodes[t];
+  const int64_t beg = (v >= 0 && v < n_rows) ? rowptr[v] : 0;
+  const int64_t deg = (v >= 0 && v < n_rows) ? rowptr[v + 1] - beg : 0;
+  if (deg <= k) {
+    for (int c = 0; c < k; ++c) out[c] = c < deg ? col[beg + c] : -1;
+    return;
+  }
+  const uint64_t key = mix64(seed);
+  int m = 0;
+  for (int64_t j = deg - k; j < deg; ++j, ++m) {
+    const uint64_t r64 = mix64(key ^ (offset + (uint64_t)(t * k + m)));
+    int32_t r = (int32_t)__umul64hi(r64, (uint64_t)(j + 1));  // uniform in [0, j]
+    for (int q = 0; q < m; ++q)
+      if (out[q] == r) {
+        r = (int32_t)j;
+        break;
+      }
+    out[m] = r;
+  }
+  for (int c = 0; c < k; ++c) out[c] = col[beg + out[c]];
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ table,
                                                           const int32_t *__restrict__ ids, int64_t n,
                                                           int32_t d4, float *__restrict__ out) {
@@ -336,6 +370,19 @@ extern "C" int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes,
   if (n == 0) return MIREC_OK;
   const int64_t tot = n * k;
   hipLaunchKernelGGL(sample_fanout_kernel, dim3((tot + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), csr->rowptr, csr->col, csr->n_rows,
+                     nodes, n, k, seed, offset, children);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_sample_fanout_norep(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
+                                         int32_t k, uint64_t seed, uint64_t offset,
+                                         int32_t *children, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(csr && csr->rowptr && csr->col && nodes && children && n >= 0 && k > 0);
+  if (n == 0) return MIREC_OK;
+  hipLaunchKernelGGL(sample_fanout_norep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), csr->rowptr, csr->col, csr->n_rows,
                      nodes, n, k, seed, offset, children);
   MIREC_LAUNCH_CHECK();

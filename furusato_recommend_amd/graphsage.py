@@ -11,8 +11,15 @@ embedding alone, so the first layer is Linear(2d -> d) instead of the
 reference's Linear(4d -> d) over [id ; feature] embeddings.
 
 Sampling tree.  PyG's NeighborSampler (graphsage.py:342-365) samples hop h
-for every node already in the batch; with replacement and a fixed fanout the
-same structure is a regular tree of node groups: every node at depth d gets
+for every node already in the batch, without replacement (all neighbours
+when the degree is at most the fanout); here every tree slot draws its own
+children — a node reached twice gets two independent draws where PyG
+samples a deduplicated node once, the same distribution per occurrence —
+and a fixed fanout with -1 in the slots a short row cannot fill makes the
+structure a regular tree of node groups (``fanout_replace=True`` draws with
+replacement, as the repo's uniform_neighbors, neighbor_sampling.py:14-30,
+except that a node without neighbours gets no children — mean 0, PyG's
+behaviour — where uniform_neighbors draws random ids): every node at depth d gets
 a child group for each hop h = d+1..L (sizes[h-1] children each), and layer
 i (hop L-i) updates every group of depth <= L-1-i from its hop-(L-i)
 children.  All groups' rows are gathered from the embedding table in ONE
@@ -358,6 +365,11 @@ class GraphSAGE(nn.Module):
         if len(self.sizes) != L:
             raise ValueError("fanouts must have one size per layer")
         self.dropout_p = float(config.get("dropout_p", 0.2))
+        # neighbour sampling: without replacement (False, default: PyG's
+        # NeighborSampler of graphsage.py:342-365 — all neighbours when the
+        # degree is <= the fanout) or with replacement (True: the repo's
+        # uniform_neighbors, neighbor_sampling.py:14-30)
+        self.fanout_replace = bool(config.get("fanout_replace", False))
         self.device = torch.device(config.get("device", "cuda:0"))
         if self.device.type != "cuda":
             raise RuntimeError("GraphSAGE (furusato_recommend_amd) runs on a HIP device only")
@@ -414,10 +426,11 @@ class GraphSAGE(nn.Module):
             for h in range(depth + 1, L + 1):
                 k = self.sizes[h - 1]
                 ch = torch.empty(ids.numel() * k, dtype=torch.int32, device=self.device)
-                check(lib.mirec_sample_fanout(self.graph.csr_ptr(), ids.data_ptr(), ids.numel(),
-                                              k, ctypes.c_uint64(seed), ctypes.c_uint64(offset),
-                                              ch.data_ptr(), _lib.stream_handle()),
-                      "sample_fanout")
+                fn = lib.mirec_sample_fanout if self.fanout_replace else \
+                    lib.mirec_sample_fanout_norep
+                check(fn(self.graph.csr_ptr(), ids.data_ptr(), ids.numel(), k,
+                         ctypes.c_uint64(seed), ctypes.c_uint64(offset), ch.data_ptr(),
+                         _lib.stream_handle()), "sample_fanout")
                 offset += ch.numel()
                 ci = tree.add(ch, h)
                 tree.children[(gi, h)] = ci

@@ -393,6 +393,16 @@ int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
                         int32_t k, uint64_t seed, uint64_t offset,
                         int32_t *children, mirec_stream_t stream);
 
+/* Fixed-fanout sampling WITHOUT replacement (PyG NeighborSampler, the
+ * sampler of model/graphsage.py:342-365): a node with at most k entries keeps
+ * all of them in row order and -1 in the remaining slots; otherwise k
+ * distinct entries of its row, uniformly (Floyd's algorithm on counter RNG
+ * (seed, offset + t*k + j)).  Nodes without neighbours get k x -1 (their
+ * mean is 0, as PyG's scatter-mean over no edges). */
+int mirec_sample_fanout_norep(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
+                              int32_t k, uint64_t seed, uint64_t offset, int32_t *children,
+                              mirec_stream_t stream);
+
 /* out[i, :] = table[ids[i], :] (zeros for ids[i] < 0); dim % 4 == 0. */
 int mirec_gather_rows(const float *table, const int32_t *ids, int64_t n,
                       int32_t dim, float *out, mirec_stream_t stream);

@@ -1890,3 +1890,43 @@ def test_sampler_binary_search_equals_scan():
         outs.append(torch.stack(t).cpu())
         assert int(err.item()) == 0
     assert torch.equal(outs[0], outs[1])
+
+
+def test_fanout_sampler_without_replacement():
+    """mirec_sample_fanout_norep (PyG NeighborSampler semantics): rows with
+    deg <= k kept whole in row order (+ -1), longer rows give k distinct
+    entries with inclusion probability k / deg each; isolated nodes -1."""
+    import ctypes
+
+    from furusato_recommend_amd import SyntheticBipartite, _lib
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(400, 40, 6000, seed=12, kind="zipf", test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    k, reps = 12, 400
+    nodes = torch.arange(g.n_nodes, dtype=torch.int32, device="cuda").repeat(reps)
+    ch = torch.empty(nodes.numel() * k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.mirec_sample_fanout_norep(g.csr_ptr(), nodes.data_ptr(), nodes.numel(), k,
+                                                  ctypes.c_uint64(5), ctypes.c_uint64(0),
+                                                  ch.data_ptr(), _lib.stream_handle()), "norep")
+    ch = ch.view(reps, g.n_nodes, k).cpu().numpy()
+    rp, col = g.rowptr_host, g.col_host
+    checked_long = 0
+    for v in range(0, g.n_nodes, 3):
+        row = col[rp[v]:rp[v + 1]]
+        d = len(row)
+        if d <= k:
+            want = np.concatenate([row, -np.ones(k - d, np.int32)])
+            assert np.all(ch[:, v] == want)
+            continue
+        # each draw: a sub-multiset of the row (distinct positions)
+        vals, cnt = np.unique(row, return_counts=True)
+        for r in range(0, reps, 50):
+            dv, dc = np.unique(ch[r, v], return_counts=True)
+            assert np.all(np.isin(dv, vals))
+            assert np.all(dc <= cnt[np.searchsorted(vals, dv)])
+        # inclusion frequency of each distinct value ~ k * mult / d
+        obs = np.array([(ch[:, v] == x).sum() for x in vals], np.float64)
+        exp = reps * k * cnt / d
+        assert np.abs(obs - exp).max() < 6 * np.sqrt(exp.max()) + 3
+        checked_long += 1
+    assert checked_long > 5
