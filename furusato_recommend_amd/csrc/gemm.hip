@@ -36,8 +36,14 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 }
 
 constexpr int kTile = 128;   // output tile edge
-constexpr int kChunk = 32;   // k per LDS stage
+#ifndef MIREC_GEMM_KC
+#define MIREC_GEMM_KC 32
+#endif
+constexpr int kChunk = MIREC_GEMM_KC;  // k per LDS stage
+constexpr int kC4 = kChunk / 4;        // float4 per staged row (gemm_nt)
 constexpr int kLdNT = kChunk + 4;   // gemm_nt LDS row stride [row][k]: 16-B reads, 4-bank groups
+constexpr int kLdO = 40;            // epilogue slab stride [row][col]: lane halves (rows
+                                    // r, r + 4) 32 banks apart, 16-B row reads
 constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two lane halves
                                     // (k and k + 4) land 32 banks apart
 
@@ -67,10 +73,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
                                                         float *__restrict__ C, int64_t n,
                                                         int Kr, int No, NtArgs fx) {
   constexpr int TM = BM / 64;        // 32-row MFMA tiles per wave
-  constexpr int QA = BM * 8 / 256;   // float4 of A per thread per chunk
-  constexpr int QB = 4;              // float4 of B per thread per chunk
-  __shared__ __attribute__((aligned(16))) float sA[BM * kLdNT];
-  __shared__ __attribute__((aligned(16))) float sB[kTile * kLdNT];
+  constexpr int QA = BM * kC4 / 256;     // float4 of A per thread per chunk
+  constexpr int QB = kTile * kC4 / 256;  // float4 of B per thread per chunk
+  __shared__ __attribute__((aligned(16))) float smem[(BM + kTile) * kLdNT];
+  static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
+  float *sA = smem, *sB = smem + BM * kLdNT;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
@@ -79,12 +86,12 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
   const int ncol = No / kTile;
   const int64_t m0 = (int64_t)(blockIdx.x / ncol) * BM;
   const int n0 = (int)(blockIdx.x % ncol) * kTile;
-  // element e = t + 256 q: row e >> 3, float4 column e & 7
+  // element e = t + 256 q: row e / kC4, float4 column e % kC4
   float4 ra[PF][QA], rb[PF][QB];
   auto load = [&](float4 (&xa)[QA], float4 (&xb)[QB], int k0) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       const int64_t row = m0 + r;
       float4 v = f4_zero();
       if (row < n) {
@@ -107,19 +114,19 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       xb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
     }
   };
   auto stage = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       st4(sA + r * kLdNT + 4 * c4, xa[q]);
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       st4(sB + r * kLdNT + 4 * c4, xb[q]);
     }
   };
@@ -168,174 +175,47 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       }
     }
   }
-  // C layout of 32x32: lane holds column i, rows (r & 3) + 8 (r >> 2) + 4 h
+  // C layout of 32x32: lane holds column i, rows (r & 3) + 8 (r >> 2) + 4 h.
+  // Stored through LDS: each 32x32 block goes to a wave-private [row][col]
+  // slab and leaves as float4 rows (4 dwordx4 per lane instead of 16 dword
+  // stores: the store tail is issue-bound, not bandwidth-bound)
+  __syncthreads();  // every wave's reads of the last chunk are done
+  float *sO = smem + w * 32 * kLdO;
 #pragma unroll
   for (int tn = 0; tn < 2; ++tn) {
     const int col = n0 + wn * 64 + tn * 32 + i;
     const float bv = bias ? bias[col] : 0.f;
-    // output block of this column (a split at Ns is tile-aligned)
+    // output block of these 32 columns (a split at Ns is tile-aligned)
+    const int cbase = n0 + wn * 64 + tn * 32;
     float *cb = C;
-    int ldc = No, cc = col;
+    int ldc = No, cc = cbase;
     if (fx.C2 != nullptr) {
-      if (col < fx.Ns) {
+      if (cbase < fx.Ns) {
         ldc = fx.Ns;
       } else {
         cb = fx.C2;
         ldc = No - fx.Ns;
-        cc = col - fx.Ns;
+        cc = cbase - fx.Ns;
       }
     }
 #pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
+    for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         float y = acc[tm][tn][r] + bv;
         if (fx.relu) y = fmaxf(y, 0.f);
-        if (row < n) cb[row * ldc + cc] = y;
+        sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLdO + i] = y;
       }
-  }
-}
-
-// Double-buffered form: the next chunk's global loads are issued before the
-// current chunk's products, staged into the other LDS buffer after them, one
-// barrier per chunk.  XCD: the ncol column tiles of a row tile get block ids
-// 8 apart (the same XCD under round-robin placement), so the row tile's A
-// rows are read once from HBM and once more from that XCD's L2.
-template <int BM, bool XCD>
-__global__ __launch_bounds__(256, 2) void gemm_nt2_kernel(const float *__restrict__ A,
-                                                         const float *__restrict__ B,
-                                                         const float *__restrict__ bias,
-                                                         float *__restrict__ C, int64_t n,
-                                                         int Kr, int No, NtArgs fx) {
-  constexpr int TM = BM / 64;
-  constexpr int QA = BM * 8 / 256;
-  constexpr int QB = 4;
-  __shared__ __attribute__((aligned(16))) float sA[2][BM * kLdNT];
-  __shared__ __attribute__((aligned(16))) float sB[2][kTile * kLdNT];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int i = lane & 31, h = lane >> 5;
-  const int wm = w >> 1, wn = w & 1;
-  const int ncol = No / kTile;
-  int64_t rt;
-  int ct;
-  if (XCD && ncol > 1) {
-    const int64_t b = blockIdx.x, grp = b / (8 * ncol);
-    const int j = (int)(b - grp * 8 * ncol);
-    rt = grp * 8 + (j & 7);
-    ct = j >> 3;
-  } else {
-    rt = blockIdx.x / ncol;
-    ct = blockIdx.x % ncol;
-  }
-  const int64_t m0 = rt * BM;
-  if (m0 >= n) return;
-  const int n0 = ct * kTile;
-  float4 ra[QA], rb[QB];
-  auto load = [&](int k0) {
+      __syncthreads();
+      const int64_t rbase = m0 + wm * (BM / 2) + tm * 32;
 #pragma unroll
-    for (int q = 0; q < QA; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
-      const int64_t row = m0 + r;
-      float4 v = f4_zero();
-      if (row < n) {
-        if (fx.A2 == nullptr) {
-          v = ld4(A + row * Kr + k0 + 4 * c4);
-        } else if (k0 < fx.Ks) {
-          v = ld4(A + row * fx.Ks + k0 + 4 * c4);
-        } else {
-          v = ld4(fx.A2 + row * (Kr - fx.Ks) + (k0 - fx.Ks) + 4 * c4);
-        }
-        if (fx.Amask != nullptr) {
-          const float4 mk = ld4(fx.Amask + row * Kr + k0 + 4 * c4);
-          v.x = mk.x > 0.f ? v.x : 0.f;
-          v.y = mk.y > 0.f ? v.y : 0.f;
-          v.z = mk.z > 0.f ? v.z : 0.f;
-          v.w = mk.w > 0.f ? v.w : 0.f;
-        }
+      for (int q = 0; q < 4; ++q) {
+        const int e = lane + 64 * q, rr = e >> 3, c4 = e & 7;
+        const float4 v = ld4(sO + rr * kLdO + 4 * c4);
+        if (rbase + rr < n) st4(cb + (rbase + rr) * ldc + cc + 4 * c4, v);
       }
-      ra[q] = v;
+      __syncthreads();  // the slab is rewritten by the next block
     }
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
-      rb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
-    }
-  };
-  auto stage = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < QA; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
-      st4(sA[buf] + r * kLdNT + 4 * c4, ra[q]);
-    }
-#pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e >> 3, c4 = e & 7;
-      st4(sB[buf] + r * kLdNT + 4 * c4, rb[q]);
-    }
-  };
-  f32x16 acc[TM][2];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  auto compute = [&](int buf) {
-#pragma unroll
-    for (int sub = 0; sub < kChunk / 8; ++sub) {
-      float4 fa[TM], fb[2];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-        fa[tm] = ld4(sA[buf] + (wm * (BM / 2) + tm * 32 + i) * kLdNT + sub * 8 + 4 * h);
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn)
-        fb[tn] = ld4(sB[buf] + (wn * 64 + tn * 32 + i) * kLdNT + sub * 8 + 4 * h);
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-          acc[tm][tn] = mfma32(fa[tm].x, fb[tn].x, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].y, fb[tn].y, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].z, fb[tn].z, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].w, fb[tn].w, acc[tm][tn]);
-        }
-    }
-  };
-  const int nc = Kr / kChunk;
-  load(0);
-  stage(0);
-  __syncthreads();
-  for (int c = 0; c < nc; ++c) {
-    if (c + 1 < nc) load((c + 1) * kChunk);  // in flight during the products
-    compute(c & 1);
-    if (c + 1 < nc) stage((c + 1) & 1);      // the other buffer: last read at c - 1
-    __syncthreads();
-  }
-#pragma unroll
-  for (int tn = 0; tn < 2; ++tn) {
-    const int col = n0 + wn * 64 + tn * 32 + i;
-    const float bv = bias ? bias[col] : 0.f;
-    float *cb = C;
-    int ldc = No, cc = col;
-    if (fx.C2 != nullptr) {
-      if (col < fx.Ns) {
-        ldc = fx.Ns;
-      } else {
-        cb = fx.C2;
-        ldc = No - fx.Ns;
-        cc = col - fx.Ns;
-      }
-    }
-#pragma unroll
-    for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t row = m0 + wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        float y = acc[tm][tn][r] + bv;
-        if (fx.relu) y = fmaxf(y, 0.f);
-        if (row < n) cb[row * ldc + cc] = y;
-      }
   }
 }
 
@@ -359,8 +239,9 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
                                                         float *__restrict__ work_cs,
                                                         int64_t n, int M, int No,
                                                         int64_t rows_per_slice, TnArgs fx) {
-  __shared__ __attribute__((aligned(16))) float sA[kChunk * kLdTN];
-  __shared__ __attribute__((aligned(16))) float sB[kChunk * kLdTN];
+  __shared__ __attribute__((aligned(16))) float smem[2 * kChunk * kLdTN];
+  static_assert(4 * 32 * kLdO <= 2 * kChunk * kLdTN, "epilogue staging fits");
+  float *sA = smem, *sB = smem + kChunk * kLdTN;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
@@ -370,10 +251,11 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
   const int64_t r_end = min(n, r_beg + rows_per_slice);
   const bool do_cs = work_cs != nullptr && blockIdx.z == 0;
   // element e = t + 256 q: chunk row e >> 5, float4 column e & 31
-  float4 ra[4], rb[4];
+  constexpr int QT = kChunk * 32 / 256;
+  float4 ra[QT], rb[QT];
   auto load = [&](int64_t r0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QT; ++q) {
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
       const int64_t r = r0 + kk;
       const bool ok = r < r_end;
@@ -399,7 +281,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
   };
   auto stage = [&]() {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < QT; ++q) {
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
       st4(sA + kk * kLdTN + 4 * c4, ra[q]);
       st4(sB + kk * kLdTN + 4 * c4, rb[q]);
@@ -440,18 +322,26 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       }
     }
   }
+  // partial tile out through a wave-private LDS slab as float4 rows (as in
+  // gemm_nt_kernel)
   float *out = work + (int64_t)s * M * No;
+  __syncthreads();
+  float *sO = smem + w * 32 * kLdO;
 #pragma unroll
-  for (int tn = 0; tn < 2; ++tn) {
-    const int col = n0 + wn * 64 + tn * 32 + i;
+  for (int tn = 0; tn < 2; ++tn)
 #pragma unroll
-    for (int tm = 0; tm < 2; ++tm)
+    for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm * 64 + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        out[(int64_t)row * No + col] = acc[tm][tn][r];
+      for (int r = 0; r < 16; ++r) sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLdO + i] = acc[tm][tn][r];
+      __syncthreads();
+      const int rbase = m0 + wm * 64 + tm * 32, cbase = n0 + wn * 64 + tn * 32;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = lane + 64 * q, rr = e >> 3, c4 = e & 7;
+        st4(out + (int64_t)(rbase + rr) * No + cbase + 4 * c4, ld4(sO + rr * kLdO + 4 * c4));
       }
-  }
+      __syncthreads();
+    }
   if (do_cs && t < kTile) work_cs[(int64_t)s * M + m0 + t] = cs;
 }
 
@@ -495,10 +385,13 @@ __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__res
 
 // Row slices of gemm_tn: enough workgroups to fill the chip twice over,
 // at least 256 rows (8 chunks) per slice.
+#ifndef MIREC_TN_MINROWS
+#define MIREC_TN_MINROWS 256
+#endif
 static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
   const int64_t want = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
-  int64_t r = std::max<int64_t>(256, (n + want - 1) / want);
+  int64_t r = std::max<int64_t>(MIREC_TN_MINROWS, (n + want - 1) / want);
   r = (r + kChunk - 1) / kChunk * kChunk;
   *rows = r;
   *slices = (int)std::max<int64_t>(1, (n + r - 1) / r);
@@ -517,28 +410,25 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   MIREC_CHECK_ARG(A2 == nullptr || (Ks > 0 && Ks < Kr && Ks % kChunk == 0 &&
                                     (uintptr_t)A2 % 16 == 0));
   MIREC_CHECK_ARG(Amask == nullptr || (A2 == nullptr && (uintptr_t)Amask % 16 == 0));
-  MIREC_CHECK_ARG(C2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0));
+  MIREC_CHECK_ARG(C2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0 &&
+                                    (uintptr_t)C2 % 16 == 0));
+  MIREC_CHECK_ARG((uintptr_t)C % 16 == 0);  // float4 row stores
   NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0};
   const unsigned ncol = (unsigned)(No / kTile);
   hipStream_t st = (hipStream_t)stream;
-#ifndef MIREC_NT_V
-#define MIREC_NT_V 2
+#ifndef MIREC_NT_PF
+#define MIREC_NT_PF 1
 #endif
-#ifndef MIREC_NT_BM
-#define MIREC_NT_BM 128
+#ifndef MIREC_NT_BM1
+#define MIREC_NT_BM1 128
 #endif
-#if MIREC_NT_V == 1
-  // 128-row tiles, one chunk of loads ahead: 64-row tiles and two chunks
-  // ahead measured the same (29.5-30.2 us at 56 K x 128 x 128)
-  hipLaunchKernelGGL((gemm_nt_kernel<128, 1>), dim3((unsigned)((n + 127) / 128) * ncol),
-                     dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx);
-#else
-  constexpr int BM = MIREC_NT_BM;
-  const int64_t nrow = (n + BM - 1) / BM;
-  const int64_t blocks = ncol > 1 ? (nrow + 7) / 8 * 8 * ncol : nrow;
-  hipLaunchKernelGGL((gemm_nt2_kernel<BM, true>), dim3((unsigned)blocks), dim3(256), 0, st, A, B,
-                     bias, C, n, (int)Kr, (int)No, fx);
-#endif
+  // 128-row tiles, one chunk of loads ahead (tools/gemm_bench.py: 64-row
+  // tiles, two chunks ahead and a double-buffered LDS form measured within
+  // noise on the C3 / C4 shapes; a persistent form streaming 64-row A tiles
+  // past B held in registers measured 15-45 % slower)
+  hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF>),
+                     dim3((unsigned)((n + MIREC_NT_BM1 - 1) / MIREC_NT_BM1) * ncol), dim3(256), 0,
+                     st, A, B, bias, C, n, (int)Kr, (int)No, fx);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

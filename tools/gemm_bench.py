@@ -75,6 +75,7 @@ def main():
         out.append({"gemm": name, "kind": "tn", "n": n, "M": m, "N": no, "us": round(us, 1),
                     "tflops": round(tf, 1), "frac_peak": round(tf / PEAK_TF, 3)})
 
+    nt("c3_small_fwd", 6144, 256, 128, dual=True, relu=True)
     n3 = 153_600
     nt("c3_l0_fwd", n3, 256, 128, dual=True, relu=True)
     nt("c3_l0_dx", n3, 128, 256, mask=True, split=True)
