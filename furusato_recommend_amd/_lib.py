@@ -158,6 +158,11 @@ SIGNATURES = {
     "mirec_adam_table": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
                                  c_void_p, c_int32, c_int64, c_int32, POINTER(AdamH), c_void_p,
                                  c_void_p, c_void_p]),
+    "mirec_adam_table_dev": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                     c_void_p, c_int32, c_int64, c_int32, c_void_p, c_void_p,
+                                     c_void_p, c_void_p]),
+    "mirec_norm_coef": (c_int, [c_void_p, c_int32, c_void_p, c_int32, c_int32, c_void_p,
+                                c_void_p]),
     "mirec_attention_fwd": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
                                     c_void_p]),
     "mirec_attention_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_int32,
@@ -170,6 +175,17 @@ SIGNATURES = {
                                              c_void_p, c_void_p]),
     "mirec_attention_bucketed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
                                              c_int32, c_void_p, c_void_p]),
+    "mirec_attention_wave_supported": (c_int, [c_int32]),
+    "mirec_attention_ordered_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                            c_int32, c_void_p, c_void_p]),
+    "mirec_attention_ordered_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                            c_int32, c_int32, c_void_p, c_void_p]),
+    "mirec_attention_length_order": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "mirec_attention_wave_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                         c_int32, c_void_p, c_void_p, c_void_p]),
+    "mirec_attention_wave_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
+                                         c_void_p, c_void_p]),
     "mirec_resnorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_int32, c_int32, c_float, c_uint64, c_void_p, c_float,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -195,6 +211,8 @@ SIGNATURES = {
     "mirec_zero_tail_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_void_p]),
     "mirec_gemm_nt": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p]),
+    "mirec_gemm_nn_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                 c_int64, c_int32, c_int32, c_void_p]),
     "mirec_gemm_nt_ex": (c_int, [c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p, c_int32, c_int32, c_int64, c_int32, c_int32,
                                  c_void_p]),

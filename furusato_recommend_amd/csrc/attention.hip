@@ -203,19 +203,21 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
   inv_out = inv;
 }
 
-// Sequence seq0 + blockIdx.x / H, head blockIdx.x % H.
+// Sequence seq0 + blockIdx.x / H (or order[seq0 + blockIdx.x / H]), head
+// blockIdx.x % H.
 template <int DPAD, int NB>
 __global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restrict__ qkv,
                                                            float *__restrict__ out, int T, int H,
                                                            int dh, float scale,
                                                            const int32_t *__restrict__ offsets,
-                                                           int64_t seq0) {
+                                                           int64_t seq0,
+                                                           const int32_t *__restrict__ order) {
   using S = AttnShape<DPAD, NB>;
   __shared__ __attribute__((aligned(16))) float sK[S::TR * S::LDK];
   __shared__ __attribute__((aligned(16))) float sV[S::TR * S::LDK];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int64_t b = seq0 + blockIdx.x / H;
+  const int64_t b = order ? (int64_t)order[seq0 + blockIdx.x / H] : seq0 + blockIdx.x / H;
   const int h = blockIdx.x % H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
@@ -260,7 +262,8 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
                                                            float *__restrict__ dqkv, int T, int H,
                                                            int dh, float scale,
                                                            const int32_t *__restrict__ offsets,
-                                                           int64_t seq0) {
+                                                           int64_t seq0,
+                                                           const int32_t *__restrict__ order) {
   using S = AttnShape<DPAD, NB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
-  const int64_t b = seq0 + blockIdx.x / H;
+  const int64_t b = order ? (int64_t)order[seq0 + blockIdx.x / H] : seq0 + blockIdx.x / H;
   const int h = blockIdx.x % H;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
@@ -413,18 +416,18 @@ static int allow_lds() {
 template <int DPAD, int NB>
 static int launch_bucket(bool bwd, const float *qkv, const float *dout, const int32_t *offsets,
                          int64_t seq0, int64_t n, int T, int heads, int dh, float *outp,
-                         hipStream_t st) {
+                         hipStream_t st, const int32_t *order) {
   if (n <= 0) return MIREC_OK;
   const float scale = 1.f / sqrtf((float)dh);
   const dim3 grid((unsigned)(n * heads)), block(64 * NB);
   if (!bwd) {
     hipLaunchKernelGGL((attn_fwd_kernel<DPAD, NB>), grid, block, 0, st, qkv, outp, T, heads, dh,
-                       scale, offsets, seq0);
+                       scale, offsets, seq0, order);
   } else {
     if (allow_lds<DPAD, NB>() != 0) return MIREC_ERR_HIP;
     constexpr int lds = AttnShape<DPAD, NB>::bwd_lds;
     hipLaunchKernelGGL((attn_bwd_kernel<DPAD, NB>), grid, block, lds, st, qkv, dout, outp, T,
-                       heads, dh, scale, offsets, seq0);
+                       heads, dh, scale, offsets, seq0, order);
   }
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
@@ -433,12 +436,12 @@ static int launch_bucket(bool bwd, const float *qkv, const float *dout, const in
 template <int DPAD>
 static int launch_nb(int nb, bool bwd, const float *qkv, const float *dout,
                      const int32_t *offsets, int64_t seq0, int64_t n, int T, int heads, int dh,
-                     float *outp, hipStream_t st) {
+                     float *outp, hipStream_t st, const int32_t *order) {
   switch (nb) {
-    case 1: return launch_bucket<DPAD, 1>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
-    case 2: return launch_bucket<DPAD, 2>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
-    case 3: return launch_bucket<DPAD, 3>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
-    default: return launch_bucket<DPAD, 4>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st);
+    case 1: return launch_bucket<DPAD, 1>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st, order);
+    case 2: return launch_bucket<DPAD, 2>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st, order);
+    case 3: return launch_bucket<DPAD, 3>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st, order);
+    default: return launch_bucket<DPAD, 4>(bwd, qkv, dout, offsets, seq0, n, T, heads, dh, outp, st, order);
   }
 }
 
@@ -446,14 +449,14 @@ static int launch_nb(int nb, bool bwd, const float *qkv, const float *dout,
 // the NB = k+1 kernel.  Uniform batches pass T and one bucket.
 static int launch(bool bwd, const float *qkv, const float *dout, const int32_t *offsets,
                   const int64_t *bucket_end, int T, int heads, int dh, float *outp,
-                  hipStream_t st) {
+                  hipStream_t st, const int32_t *order = nullptr) {
   int64_t prev = 0;
   for (int k = 0; k < 4; ++k) {
     const int64_t end = bucket_end[k];
     const int rc = dh <= 32 ? launch_nb<32>(k + 1, bwd, qkv, dout, offsets, prev, end - prev, T,
-                                            heads, dh, outp, st)
+                                            heads, dh, outp, st, order)
                             : launch_nb<64>(k + 1, bwd, qkv, dout, offsets, prev, end - prev, T,
-                                            heads, dh, outp, st);
+                                            heads, dh, outp, st, order);
     if (rc != MIREC_OK) return rc;
     prev = end;
   }
@@ -539,4 +542,27 @@ extern "C" int mirec_attention_bucketed_bwd(const float *qkv, const float *dout,
   MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64 && valid_buckets(bucket_end));
   return launch(true, qkv, dout, offsets, bucket_end, kT, heads, head_dim, dqkv,
                 reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int mirec_attention_ordered_fwd(const float *qkv, const int32_t *offsets,
+                                           const int32_t *order, int64_t batch, int32_t heads,
+                                           int32_t head_dim, float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && offsets && order && out && batch >= 0 && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
+  const int64_t be[4] = {0, 0, 0, batch};
+  return launch(false, qkv, nullptr, offsets, be, kT, heads, head_dim, out,
+                reinterpret_cast<hipStream_t>(stream), order);
+}
+
+extern "C" int mirec_attention_ordered_bwd(const float *qkv, const float *dout,
+                                           const int32_t *offsets, const int32_t *order,
+                                           int64_t batch, int32_t heads, int32_t head_dim,
+                                           float *dqkv, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(qkv && dout && offsets && order && dqkv && batch >= 0 && heads >= 1);
+  MIREC_CHECK_ARG(head_dim >= 1 && head_dim <= 64);
+  const int64_t be[4] = {0, 0, 0, batch};
+  return launch(true, qkv, dout, offsets, be, kT, heads, head_dim, dqkv,
+                reinterpret_cast<hipStream_t>(stream), order);
 }

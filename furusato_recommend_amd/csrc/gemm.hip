@@ -59,11 +59,16 @@ constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two 
 // Amask (same layout as a single A) zeroes A elements whose mask is <= 0 (the
 // ReLU backward, dY * (y > 0), applied as dY is loaded); C may be split the
 // same way at column Ns into C / C2; relu applies max(., 0) after the bias.
+//
+// B layout: [No, Kr] rows (k contiguous: C = A Bᵀ, a Linear forward with B =
+// W), or with bkn [Kr, No] rows (n contiguous: C = A B, the input gradient
+// dX = dY W of a Linear with B = W, no transposed copy); the staged LDS
+// image is [n][k] either way.
 struct NtArgs {
   const float *A2;
   const float *Amask;
   float *C2;
-  int Ks, Ns, relu;
+  int Ks, Ns, relu, bkn;
 };
 
 template <int BM, int PF>
@@ -112,10 +117,18 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       }
       xa[q] = v;
     }
+    if (fx.bkn) {  // element e: k row e / 32, float4 column e % 32 of the 128 n
 #pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-      xb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
+      for (int q = 0; q < QB; ++q) {
+        const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+        xb[q] = ld4(B + (int64_t)(k0 + kk) * No + n0 + 4 * c4);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
+        xb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
+      }
     }
   };
   auto stage = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
@@ -124,10 +137,21 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       st4(sA + r * kLdNT + 4 * c4, xa[q]);
     }
+    if (fx.bkn) {  // transpose into [n][k]
 #pragma unroll
-    for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-      st4(sB + r * kLdNT + 4 * c4, xb[q]);
+      for (int q = 0; q < QB; ++q) {
+        const int e = t + 256 * q, kk = e >> 5, n = 4 * (e & 31);
+        sB[n * kLdNT + kk] = xb[q].x;
+        sB[(n + 1) * kLdNT + kk] = xb[q].y;
+        sB[(n + 2) * kLdNT + kk] = xb[q].z;
+        sB[(n + 3) * kLdNT + kk] = xb[q].w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < QB; ++q) {
+        const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
+        st4(sB + r * kLdNT + 4 * c4, xb[q]);
+      }
     }
   };
   f32x16 acc[TM][2];
@@ -403,7 +427,8 @@ using namespace mirec;
 
 static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Amask,
                    const float *B, const float *bias, float *C, float *C2, int32_t Ns,
-                   int32_t relu, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream) {
+                   int32_t relu, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream,
+                   int bkn = 0) {
   MIREC_CHECK_ARG(n >= 0 && Kr > 0 && No > 0 && Kr % kChunk == 0 && No % kTile == 0);
   if (n == 0) return MIREC_OK;  // (empty tensors may carry null pointers)
   MIREC_CHECK_ARG(A && B && C && ((uintptr_t)A | (uintptr_t)B) % 16 == 0);
@@ -413,7 +438,7 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   MIREC_CHECK_ARG(C2 == nullptr || (Ns > 0 && Ns < No && Ns % kTile == 0 &&
                                     (uintptr_t)C2 % 16 == 0));
   MIREC_CHECK_ARG((uintptr_t)C % 16 == 0);  // float4 row stores
-  NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0};
+  NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0, bkn};
   const unsigned ncol = (unsigned)(No / kTile);
   hipStream_t st = (hipStream_t)stream;
 #ifndef MIREC_NT_PF
@@ -443,6 +468,12 @@ extern "C" int mirec_gemm_nt_ex(const float *A, const float *A2, int32_t Ks, con
                                 int32_t Ns, int32_t relu, int64_t n, int32_t Kr, int32_t No,
                                 mirec_stream_t stream) {
   return gemm_nt(A, A2, Ks, Amask, B, bias, C, C2, Ns, relu, n, Kr, No, stream);
+}
+
+extern "C" int mirec_gemm_nn_ex(const float *A, const float *Amask, const float *B, float *C,
+                                float *C2, int32_t Ns, int64_t n, int32_t Kr, int32_t No,
+                                mirec_stream_t stream) {
+  return gemm_nt(A, nullptr, 0, Amask, B, nullptr, C, C2, Ns, 0, n, Kr, No, stream, 1);
 }
 
 extern "C" int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No) {

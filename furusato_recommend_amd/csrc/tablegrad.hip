@@ -321,9 +321,11 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
                                                       const float *__restrict__ acc,
                                                       const int32_t *__restrict__ stamp,
                                                       int32_t gen, int64_t n_rows, int32_t d4,
-                                                      int32_t shift, mirec_adam_hparams_t h,
+                                                      int32_t shift, mirec_adam_hparams_t h_arg,
+                                                      const mirec_adam_hparams_t *__restrict__ h_dev,
                                                       float *__restrict__ sumsq) {
   __shared__ float red[2][256];
+  const mirec_adam_hparams_t h = h_dev != nullptr ? *h_dev : h_arg;
   const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
   const int64_t n4 = n_rows * d4;
   float su = 0.f, si = 0.f;
@@ -570,13 +572,13 @@ extern "C" int mirec_table_grad_dense(const float *table, const float *coef, int
   return MIREC_OK;
 }
 
-extern "C" int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
-                                int64_t n_user, const float *acc, const int32_t *stamp,
-                                int32_t gen, int64_t n_rows, int32_t dim,
-                                const mirec_adam_hparams_t *h, float *sumsq, float *norms,
-                                mirec_stream_t stream) {
-  MIREC_CHECK_ARG(param && exp_avg && exp_avg_sq && acc && stamp && h && n_rows >= 0 &&
-                  dim > 0 && dim % 4 == 0 && n_user >= 0 && n_user <= n_rows);
+static int adam_table(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
+                      int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
+                      int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h,
+                      const mirec_adam_hparams_t *h_dev, float *sumsq, float *norms,
+                      mirec_stream_t stream) {
+  MIREC_CHECK_ARG(param && exp_avg && exp_avg_sq && acc && stamp && (h || h_dev) &&
+                  n_rows >= 0 && dim > 0 && dim % 4 == 0 && n_user >= 0 && n_user <= n_rows);
   MIREC_CHECK_ARG(((uintptr_t)param | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq |
                    (uintptr_t)acc) % 16 == 0);
   MIREC_CHECK_ARG((sumsq == nullptr) == (norms == nullptr));
@@ -584,14 +586,59 @@ extern "C" int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq,
   hipStream_t st = (hipStream_t)stream;
   const int64_t n4 = n_rows * (dim / 4);
   const unsigned blocks = tg_blocks(n4);
+  const mirec_adam_hparams_t h0 = h ? *h : mirec_adam_hparams_t{};
   hipLaunchKernelGGL(tg_adam_kernel, dim3(blocks), dim3(256), 0, st, param, exp_avg, exp_avg_sq,
-                     coef, n_user, acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4), *h,
-                     sumsq);
+                     coef, n_user, acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4), h0,
+                     h ? nullptr : h_dev, sumsq);
   MIREC_LAUNCH_CHECK();
   if (norms) {
     hipLaunchKernelGGL(tg_norm_final_kernel, dim3(1), dim3(1024), 0, st, sumsq, (int64_t)blocks,
                        norms);
     MIREC_LAUNCH_CHECK();
   }
+  return MIREC_OK;
+}
+
+extern "C" int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
+                                int64_t n_user, const float *acc, const int32_t *stamp,
+                                int32_t gen, int64_t n_rows, int32_t dim,
+                                const mirec_adam_hparams_t *h, float *sumsq, float *norms,
+                                mirec_stream_t stream) {
+  MIREC_CHECK_ARG(h != nullptr);
+  return adam_table(param, exp_avg, exp_avg_sq, coef, n_user, acc, stamp, gen, n_rows, dim, h,
+                    nullptr, sumsq, norms, stream);
+}
+
+extern "C" int mirec_adam_table_dev(float *param, float *exp_avg, float *exp_avg_sq,
+                                    const float *coef, int64_t n_user, const float *acc,
+                                    const int32_t *stamp, int32_t gen, int64_t n_rows,
+                                    int32_t dim, const mirec_adam_hparams_t *h_device,
+                                    float *sumsq, float *norms, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(h_device != nullptr);
+  return adam_table(param, exp_avg, exp_avg_sq, coef, n_user, acc, stamp, gen, n_rows, dim,
+                    nullptr, h_device, sumsq, norms, stream);
+}
+
+// coef[i] = norm[i ns] > 0 ? g[i gs] / norm[i ns] : 0 (i < n): the norm-term
+// coefficients of a table gradient, d|x|/dx = x / |x| (0 for a zero table,
+// as torch's norm backward); g = the loss's gradient w.r.t. the norm.
+__global__ void norm_coef_kernel(const float *__restrict__ g, int gs,
+                                 const float *__restrict__ norm, int ns, int n,
+                                 float *__restrict__ coef) {
+  const int i = threadIdx.x;
+  if (i < n) {
+    const float nv = norm[i * ns];
+    coef[i] = nv > 0.f ? g[i * gs] / nv : 0.f;
+  }
+}
+
+extern "C" int mirec_norm_coef(const float *g, int32_t g_stride, const float *norm,
+                               int32_t norm_stride, int32_t n, float *coef,
+                               mirec_stream_t stream) {
+  MIREC_CHECK_ARG(g && norm && coef && n >= 0 && n <= 1024 && g_stride >= 0 && norm_stride >= 0);
+  if (n == 0) return MIREC_OK;
+  hipLaunchKernelGGL(norm_coef_kernel, dim3(1), dim3(64 * ((n + 63) / 64)), 0,
+                     (hipStream_t)stream, g, g_stride, norm, norm_stride, n, coef);
+  MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

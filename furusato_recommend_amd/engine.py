@@ -186,12 +186,13 @@ class AdamGroup:
                                        ctypes.byref(hp), _lib.stream_handle()), "adam_multi")
 
     # -- graph-captured steps: the scalars live in device memory ------------
-    def next_shared_hparams(self):
-        """Advance every state (all must have a gradient and share lr /
-        betas / eps / step count) and return the one hparams struct of this
-        step — what a captured step reads through step_device."""
+    def next_shared_hparams(self, require_grad: bool = True):
+        """Advance every state (all must share lr / betas / eps / step count
+        and, with require_grad, have a gradient) and return the one hparams
+        struct of this step — what a captured step reads through
+        step_device."""
         keys = {(s.n_steps, s.lr, s.betas, s.eps) for s in self.states}
-        if len(keys) != 1 or any(s.param.grad is None for s in self.states):
+        if len(keys) != 1 or (require_grad and any(s.param.grad is None for s in self.states)):
             raise RuntimeError("device-scalar Adam needs one shared step for every parameter")
         hps = [s.next_hparams() for s in self.states]
         return hps[0]

@@ -67,6 +67,9 @@ class TableGrad:
         self.gen = 0
         self.pending = False  # S / coef of the last backward not yet consumed
         self.dense = False
+        # static: a HIP-graph-captured step bakes the generation into its
+        # launches, so every step clears the stamps and reuses generation 1
+        self.static = False
         self._ws = None
 
     def accumulate(self, groups):
@@ -87,11 +90,23 @@ class TableGrad:
               "table_grad_workspace")
         if self._ws is None or self._ws.numel() < nb.value:
             self._ws = torch.empty(nb.value, dtype=torch.uint8, device=self.acc.device)
-        self.gen += 1
+        self._next_gen()
         check(lib.mirec_table_grad_sorted(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
                                           self.stamp.data_ptr(), self.gen, self._ws.data_ptr(),
                                           self._ws.numel(), _lib.stream_handle()),
               "table_grad_sorted")
+        self.pending = True
+
+    def _next_gen(self):
+        if self.static:
+            self.stamp.zero_()
+            self.gen = 1
+        else:
+            self.gen += 1
+
+    def skip(self):
+        """A backward with no row gradient: S = 0 (a fresh generation)."""
+        self._next_gen()
         self.pending = True
 
     def materialize(self, table: torch.Tensor) -> torch.Tensor:
@@ -103,19 +118,29 @@ class TableGrad:
                                          _lib.stream_handle()), "table_grad_dense")
         return grad
 
-    def adam(self, state: AdamState, norms: torch.Tensor | None = None):
+    def adam(self, state: AdamState, norms: torch.Tensor | None = None,
+             h_dev: torch.Tensor | None = None):
         """One Adam step of the table with G formed in the kernel; writes the
-        updated slices' norms to ``norms`` (2 floats) if given."""
-        hp = state.next_hparams()
+        updated slices' norms to ``norms`` (2 floats) if given.  With
+        ``h_dev`` the hyper-parameters are read from that device buffer when
+        the kernel runs (a captured step; the host step count is not
+        advanced)."""
         sumsq = None
         if norms is not None:
             sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(self.n_rows, self.dim)),
                                 device=self.acc.device)
-        check(lib.mirec_adam_table(state.param.data_ptr(), state.exp_avg.data_ptr(),
-                                   state.exp_avg_sq.data_ptr(), self.coef.data_ptr(), self.n_user,
-                                   self.acc.data_ptr(), self.stamp.data_ptr(), self.gen,
-                                   self.n_rows, self.dim, ctypes.byref(hp), _lib.ptr(sumsq),
-                                   _lib.ptr(norms), _lib.stream_handle()), "adam_table")
+        args = (state.param.data_ptr(), state.exp_avg.data_ptr(), state.exp_avg_sq.data_ptr(),
+                self.coef.data_ptr(), self.n_user, self.acc.data_ptr(), self.stamp.data_ptr(),
+                self.gen, self.n_rows, self.dim)
+        if h_dev is None:
+            hp = state.next_hparams()
+            check(lib.mirec_adam_table(*args, ctypes.byref(hp), _lib.ptr(sumsq), _lib.ptr(norms),
+                                       _lib.stream_handle()), "adam_table")
+        else:
+            check(lib.mirec_adam_table_dev(*args, h_dev.data_ptr(), _lib.ptr(sumsq),
+                                           _lib.ptr(norms), _lib.stream_handle()),
+                  "adam_table_dev")
+        _engine._note_raw_write()
         self.pending = False
 
 
@@ -169,14 +194,13 @@ class _TableTerms(torch.autograd.Function):
         d = table.shape[1]
         st = _lib.stream_handle()
         # d|x|/dx = x/|x| (0 for a zero slice, as torch's norm backward)
-        if g_norms is None:
-            coef = torch.zeros_like(norms2)
-        else:
-            coef = torch.where(norms2 > 0, g_norms / norms2, torch.zeros_like(norms2))
-        cu, ci = coef[0], coef[1]
         sink = ctx.sink
         if sink is not None:
-            sink.coef.copy_(coef)
+            if g_norms is None:
+                sink.coef.zero_()
+            else:
+                check(lib.mirec_norm_coef(g_norms.contiguous().data_ptr(), 1, norms2.data_ptr(), 1,
+                                          2, sink.coef.data_ptr(), st), "norm_coef")
             groups = []
             if g_rows is not None:
                 groups.append((ids, g_rows, 1, 0, 0.0, 0))
@@ -186,9 +210,13 @@ class _TableTerms(torch.autograd.Function):
             if groups:
                 sink.accumulate(groups)
             else:  # S = 0: a fresh generation stamps nothing
-                sink.gen += 1
-                sink.pending = True
+                sink.skip()
             return (sink.materialize(table) if sink.dense else None), None, None, None, None, None
+        if g_norms is None:
+            coef = torch.zeros_like(norms2)
+        else:
+            coef = torch.where(norms2 > 0, g_norms / norms2, torch.zeros_like(norms2))
+        cu, ci = coef[0], coef[1]
         grad = torch.empty_like(table)
         torch.mul(table[:k], cu, out=grad[:k])
         torch.mul(table[k:], ci, out=grad[k:])

@@ -2,8 +2,8 @@
 the input gradient and the weight + bias gradient.
 
 The packed SASRec / GraphSAGE activations are tall and thin (tens of
-thousands of rows x d = 128..384).  mirec_gemm_nt computes y = x Wᵀ + b and
-dX = dY W (B = Wᵀ, a copy of the small weight); mirec_gemm_tn computes
+thousands of rows x d = 128..384).  mirec_gemm_nt computes y = x Wᵀ + b,
+mirec_gemm_nn_ex dX = dY W (W read as stored); mirec_gemm_tn computes
 dW = dYᵀ X and db = Σ dY in one pass over dY, cutting the long row reduction
 into slices summed in a fixed order.  Shapes the kernels do not take (a
 width not a multiple of 32 / 128) go to torch's GEMMs, where the weight
@@ -44,14 +44,23 @@ def gemm_nt(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = None):
     if not (USE_MIREC_GEMM and kr % 32 == 0 and no % 128 == 0 and b.shape[1] == kr
             and _aligned(a, b) and (bias is None or _aligned(bias))):
         return None
-    if kr <= 128 and no > 128 and not FORCE_MIREC_GEMM:
-        # short reduction, wide output (the QKV projection): hipBLASLt's
-        # kernel is faster there (62 vs 76 us at 56K x 128 x 384,
-        # tools/gemm_forms.py); every other Linear shape runs faster here
-        return None
     c = torch.empty(n, no, dtype=a.dtype, device=a.device)
     check(lib.mirec_gemm_nt(a.data_ptr(), b.data_ptr(), 0 if bias is None else bias.data_ptr(),
                             c.data_ptr(), n, kr, no, _lib.stream_handle()), "gemm_nt")
+    return c
+
+
+def gemm_nn(a: torch.Tensor, b: torch.Tensor):
+    """a [n, Kr] · b [Kr, No] on mirec_gemm_nn_ex (b as stored: the weight of
+    dX = dY W), or None if the shapes are not the kernel's."""
+    n, kr = a.shape
+    no = b.shape[1]
+    if not (USE_MIREC_GEMM and kr % 32 == 0 and no % 128 == 0 and b.shape[0] == kr
+            and _aligned(a, b)):
+        return None
+    c = torch.empty(n, no, dtype=a.dtype, device=a.device)
+    check(lib.mirec_gemm_nn_ex(a.data_ptr(), None, b.data_ptr(), c.data_ptr(), None, 0, n, kr, no,
+                               _lib.stream_handle()), "gemm_nn")
     return c
 
 
@@ -107,7 +116,7 @@ class _LinearSplitK(torch.autograd.Function):
         need = ctx.needs_input_grad
         dx = dw = db = None
         if need[0]:
-            dx = gemm_nt(dy2, w.t().contiguous())
+            dx = gemm_nn(dy2, w)
             dx = (dy2 @ w if dx is None else dx).view(shape)
         want_db = ctx.has_bias and need[2]
         if need[1]:
@@ -126,8 +135,8 @@ class _SageLinear(torch.autograd.Function):
     Linear over [x_self ; aggr] (model/graphsage.py:314-315) without the
     concatenation: the GEMM reads its A rows from the two tensors
     (mirec_gemm_nt_ex), adds the bias and applies the ReLU in its epilogue.
-    Backward: the ReLU mask is applied to dY as it is loaded; dX is written
-    straight into the two input gradients (output split at d) and
+    Backward: the ReLU mask is applied to dY as it is loaded; dX = dY' W is
+    written straight into the two input gradients (output split at d) and
     dW = dY'ᵀ [x_self | x_nbr], db = Σ dY' in one pass (mirec_gemm_tn_ex)."""
 
     @staticmethod
@@ -152,10 +161,8 @@ class _SageLinear(torch.autograd.Function):
         mask = _lib.ptr(y)
         dxs = torch.empty_like(xs)
         dxn = torch.empty_like(xn)
-        wt = w.t().contiguous()  # [2d, no]: B of dX = dY' W
-        check(lib.mirec_gemm_nt_ex(dy.data_ptr(), None, 0, mask, wt.data_ptr(), None,
-                                   dxs.data_ptr(), dxn.data_ptr(), d, 0, n, no, 2 * d, st),
-              "gemm_nt_ex(dX)")
+        check(lib.mirec_gemm_nn_ex(dy.data_ptr(), mask, w.data_ptr(), dxs.data_ptr(),
+                                   dxn.data_ptr(), d, n, no, 2 * d, st), "gemm_nn_ex(dX)")
         dw = torch.empty_like(w)
         db = torch.empty(no, dtype=w.dtype, device=w.device) if ctx.has_bias else None
         work = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, no, 2 * d)), dtype=w.dtype,

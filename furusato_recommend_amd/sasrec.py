@@ -52,27 +52,77 @@ def _timed(kind, shape, launch, offsets=None):
     return r
 
 
+# Attention core implementation: "wave" (csrc/attn_wave.hip, one wave per
+# (sequence, head), head_dim 16 / 32 / 64), "block" (csrc/attention.hip, one
+# workgroup per (sequence, head): any head_dim <= 64, length buckets) or
+# "hybrid" (default): the wave forward and the workgroup backward, both on
+# the longest-first sequence order.  At C4 (tools/attn_bench.py, 57 K
+# tokens): forward wave 31 us / workgroup 38; backward wave (two passes)
+# 95 us / workgroup 77.
+ATTN_IMPL = "hybrid"
+
+
+def _use_wave(dh: int) -> bool:
+    return ATTN_IMPL in ("wave", "hybrid") and bool(lib.mirec_attention_wave_supported(dh))
+
+
+def _wave_fwd(qkv, offsets, B, T, heads, dh, out):
+    """mirec_attention_wave_fwd; returns (lse [n_rows, heads], order): packed
+    sequences run longest first (mirec_attention_length_order)."""
+    lse = torch.empty(qkv.shape[0] if offsets is not None else B * T, heads, dtype=qkv.dtype,
+                      device=qkv.device)
+    order = None
+    if offsets is not None and B > 0:
+        order = torch.empty(B, dtype=torch.int32, device=qkv.device)
+        check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
+                                               _lib.stream_handle()), "attention_length_order")
+    _timed("fwd", (B, T if offsets is None else -1, heads, dh), lambda: check(
+        lib.mirec_attention_wave_fwd(qkv.data_ptr(), _ptr(offsets), _ptr(order), B, T, heads, dh,
+                                     out.data_ptr(), lse.data_ptr(), _lib.stream_handle()),
+        "attention_wave_fwd"), offsets)
+    return lse, order
+
+
+def _wave_bwd(qkv, out, lse, order, dout, offsets, B, T, heads, dh, dqkv):
+    delta = torch.empty_like(lse)
+    _timed("bwd", (B, T if offsets is None else -1, heads, dh), lambda: check(
+        lib.mirec_attention_wave_bwd(qkv.data_ptr(), out.data_ptr(), lse.data_ptr(),
+                                     dout.data_ptr(), _ptr(offsets), _ptr(order), B, T, heads,
+                                     dh, dqkv.data_ptr(), delta.data_ptr(),
+                                     _lib.stream_handle()),
+        "attention_wave_bwd"), offsets)
+
+
 class _CausalAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, heads: int):
         B, T, d3 = qkv.shape
         d = d3 // 3
+        dh = d // heads
         qkv = qkv.contiguous()
         out = torch.empty(B, T, d, dtype=qkv.dtype, device=qkv.device)
-        _timed("fwd", (B, T, heads, d // heads), lambda: check(lib.mirec_attention_fwd(
-            qkv.data_ptr(), B, T, heads, d // heads, out.data_ptr(), _lib.stream_handle()),
+        ctx.heads = heads
+        if _use_wave(dh):
+            lse, _ = _wave_fwd(qkv, None, B, T, heads, dh, out)
+            ctx.save_for_backward(qkv, out, lse)
+            return out
+        _timed("fwd", (B, T, heads, dh), lambda: check(lib.mirec_attention_fwd(
+            qkv.data_ptr(), B, T, heads, dh, out.data_ptr(), _lib.stream_handle()),
             "attention_fwd"))
         ctx.save_for_backward(qkv)
-        ctx.heads = heads
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (qkv,) = ctx.saved_tensors
+        qkv = ctx.saved_tensors[0]
         B, T, d3 = qkv.shape
         dh = d3 // 3 // ctx.heads
         dqkv = torch.empty_like(qkv)
         dout = dout.contiguous()
+        if len(ctx.saved_tensors) == 3:
+            _, out, lse = ctx.saved_tensors
+            _wave_bwd(qkv, out, lse, None, dout, None, B, T, ctx.heads, dh, dqkv)
+            return dqkv, None
         _timed("bwd", (B, T, ctx.heads, dh), lambda: check(lib.mirec_attention_bwd(
             qkv.data_ptr(), dout.data_ptr(), B, T, ctx.heads, dh, dqkv.data_ptr(),
             _lib.stream_handle()), "attention_bwd"))
@@ -92,37 +142,43 @@ class Packing(NamedTuple):
 
 class _CausalAttentionVarlen(torch.autograd.Function):
     """Packed sequences: qkv [n_tok, 3d], sequence b = rows offsets[b] ..
-    offsets[b+1]-1 (mirec_attention_varlen_*, or mirec_attention_bucketed_*
-    given the length buckets)."""
+    offsets[b+1]-1 (mirec_attention_wave_*; or, with ATTN_IMPL "block",
+    mirec_attention_varlen_* / mirec_attention_bucketed_* given the length
+    buckets)."""
 
     @staticmethod
     def forward(ctx, qkv, offsets, heads: int, bucket_end=None, padded: bool = False):
         n, d3 = qkv.shape
         d = d3 // 3
+        dh = d // heads
         B = offsets.numel() - 1
         qkv = qkv.contiguous()
         out = torch.empty(n, d, dtype=qkv.dtype, device=qkv.device)
         if padded:  # rows outside every sequence: not written by the kernels
             _zero_tail(out, offsets)
+        ctx.heads = heads
+        ctx.bucket_end = bucket_end
+        ctx.padded = padded
+        if _use_wave(dh):
+            lse, order = _wave_fwd(qkv, offsets, B, 0, heads, dh, out)
+            ctx.save_for_backward(qkv, offsets, out, lse, order)
+            return out
         if bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_fwd(  # noqa: E731
-                qkv.data_ptr(), offsets.data_ptr(), B, heads, d // heads, out.data_ptr(),
+                qkv.data_ptr(), offsets.data_ptr(), B, heads, dh, out.data_ptr(),
                 _lib.stream_handle()), "attention_varlen_fwd")
         else:
             be = _bucket_array(bucket_end, B)
             launch = lambda: check(lib.mirec_attention_bucketed_fwd(  # noqa: E731
-                qkv.data_ptr(), offsets.data_ptr(), be, heads, d // heads, out.data_ptr(),
+                qkv.data_ptr(), offsets.data_ptr(), be, heads, dh, out.data_ptr(),
                 _lib.stream_handle()), "attention_bucketed_fwd")
-        _timed("fwd", (B, -1, heads, d // heads), launch, offsets)
+        _timed("fwd", (B, -1, heads, dh), launch, offsets)
         ctx.save_for_backward(qkv, offsets)
-        ctx.heads = heads
-        ctx.bucket_end = bucket_end
-        ctx.padded = padded
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, offsets = ctx.saved_tensors
+        qkv, offsets = ctx.saved_tensors[:2]
         n, d3 = qkv.shape
         B = offsets.numel() - 1
         dh = d3 // 3 // ctx.heads
@@ -130,6 +186,18 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         if ctx.padded:
             _zero_tail(dqkv, offsets)
         dout = dout.contiguous()
+        if len(ctx.saved_tensors) == 5:
+            out, lse, order = ctx.saved_tensors[2:]
+            if ATTN_IMPL == "wave" or order is None:
+                _wave_bwd(qkv, out, lse, order, dout, offsets, B, 0, ctx.heads, dh, dqkv)
+            else:
+                _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(
+                    lib.mirec_attention_ordered_bwd(qkv.data_ptr(), dout.data_ptr(),
+                                                    offsets.data_ptr(), order.data_ptr(), B,
+                                                    ctx.heads, dh, dqkv.data_ptr(),
+                                                    _lib.stream_handle()),
+                    "attention_ordered_bwd"), offsets)
+            return dqkv, None, None, None, None
         if ctx.bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_bwd(  # noqa: E731
                 qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), B, ctx.heads, dh,
@@ -421,6 +489,16 @@ class SASRec(nn.Module):
             sequences = SequenceData(dataset.allPos, dev)
         self.seq = sequences
         self.optims = AdamGroup(AdamState(p, lr=config["lr"]) for p in self.parameters())
+        # the item table's gradient in the sorted form, its Adam fused with
+        # forming it (graphsage.TableGrad; config "table_grad": "dense" = the
+        # materialised gradient + dense Adam)
+        self._table_state = next(s for s in self.optims
+                                 if s.param is self.item_id_embedding.weight)
+        self._rest_optims = AdamGroup(s for s in self.optims if s is not self._table_state)
+        self._tg = None
+        if config.get("table_grad", "sorted") == "sorted":
+            from .graphsage import TableGrad
+            self._tg = TableGrad(self.m_item, 0, d, dev)
 
     # ------------------------------------------------------------- blocks
     def oneblock(self, x, layer, offsets=None):
@@ -600,9 +678,37 @@ class SASRec(nn.Module):
         ids, packing, seg, length = self.packed_ids(users)
         loss = self._step_body(ids, packing, seg, length, pos, neg, loss_scale)
         if grad_hook is not None:
+            tg = self._tg
+            if tg is not None and tg.pending and self.item_id_embedding.weight.grad is None:
+                # the hook (an all-reduce, a test) sees every gradient
+                self.item_id_embedding.weight.grad = tg.materialize(
+                    self.item_id_embedding.weight.detach())
             grad_hook()
-        self.optims.step()
+        self.optimizer_step()
         return loss.detach()
+
+    @torch.no_grad()
+    def optimizer_step(self, h_dev: torch.Tensor | None = None):
+        """Adam over every parameter (sasrec.py:468-471): the item table
+        through the fused kernel from the pending sorted gradient, the rest
+        with the multi-tensor kernel; or all of them densely when the
+        table's gradient was materialised.  ``h_dev``: device hyper-parameters
+        (captured step)."""
+        tg = self._tg
+        w = self.item_id_embedding.weight
+        if tg is None or w.grad is not None or not tg.pending:
+            if tg is not None:
+                tg.pending = False
+            if h_dev is None:
+                self.optims.step()
+            else:
+                self.optims.step_device(h_dev)
+            return
+        if h_dev is None:
+            self._rest_optims.step()
+        else:
+            self._rest_optims.step_device(h_dev)
+        tg.adam(self._table_state, h_dev=h_dev)
 
     def _step_body(self, ids, packing, seg, length, pos, neg, loss_scale=1.0, n_tok=None):
         """Forward, loss and backward of one packed batch; returns the loss.
@@ -618,8 +724,8 @@ class SASRec(nn.Module):
         # table's norm (the loss's only 'emb' parameter term) comes from the
         # same node (one table gradient, written once), and the BPR score /
         # softplus / mean / norm term are one kernel each way.
-        rows, wnorm = gather_rows_norm(self.item_id_embedding.weight, ids)
-        x, pn = rows.split([n_tok, 2 * B])
+        x, pn, wnorm = gather_rows_norm(self.item_id_embedding.weight, ids, split=n_tok,
+                                        sink=self._tg)
         u = self.forward_user_packed(x, packing, seg, length)
         pe, ne = self.forward_item(pn).split(B)
         loss = _BPRRowsLoss.apply(u, pe, ne, wnorm, self.config["decay"] / B)
@@ -722,6 +828,8 @@ class _CapturedStep:
         self.stage = [torch.zeros(3 * B + 4, dtype=torch.int64).pin_memory() for _ in range(2)]
         self.events = [None, None]
         self.turn = 0
+        if model._tg is not None:
+            model._tg.static = True  # the generation is baked into the graph
         pool = model.__dict__.setdefault("_graph_pool", torch.cuda.graph_pool_handle())
         params = list(model.parameters())
         snap = [p.detach().clone() for p in params]
@@ -758,7 +866,7 @@ class _CapturedStep:
         hdev = buf[3 * B:3 * B + 3].view(torch.float32)
         ids_all, packing, seg, length = m.packed_ids_static(u, self.C, pos, neg)
         loss = m._step_body(ids_all, packing, seg, length, pos, neg, n_tok=self.C)
-        m.optims.step_device(hdev)
+        m.optimizer_step(hdev)
         return loss.detach()
 
     def run(self, u_host, pos, neg):
@@ -773,7 +881,7 @@ class _CapturedStep:
         for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
             if not dv:
                 st[(j + 1) * B:(j + 2) * B] = np.asarray(t.cpu() if torch.is_tensor(t) else t)
-        hp = self.m.optims.next_shared_hparams()
+        hp = self.m.optims.next_shared_hparams(require_grad=self.m._tg is None)
         st[3 * B:3 * B + 3] = np.frombuffer(bytes(hp), dtype=np.int64)
         st[3 * B + 3] = int(torch.randint(0, 2 ** 62, (1,)).item())  # torch's CPU generator
         self.inbuf.copy_(self.stage[k], non_blocking=True)

@@ -505,6 +505,17 @@ int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const floa
                      int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
                      int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h, float *sumsq,
                      float *norms, mirec_stream_t stream);
+/* mirec_adam_table with the hyper-parameters read from device memory when
+ * the kernel runs (capturable in a HIP graph). */
+int mirec_adam_table_dev(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
+                         int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
+                         int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h_device,
+                         float *sumsq, float *norms, mirec_stream_t stream);
+
+/* coef[i] = norm[i*norm_stride] > 0 ? g[i*g_stride] / norm[i*norm_stride] : 0
+ * for i < n (<= 1024): a table gradient's norm-term coefficients. */
+int mirec_norm_coef(const float *g, int32_t g_stride, const float *norm, int32_t norm_stride,
+                    int32_t n, float *coef, mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* SASRec causal self-attention (model/sasrec.py:385-397), f32 MFMA          */
@@ -549,6 +560,35 @@ int mirec_attention_bucketed_fwd(const float *qkv, const int32_t *offsets,
 int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
                                  const int64_t *bucket_end, int32_t heads, int32_t head_dim,
                                  float *dqkv, mirec_stream_t stream);
+
+/* Packed form with the workgroups in a given sequence order (device int32
+ * [batch], e.g. mirec_attention_length_order: longest first). */
+int mirec_attention_ordered_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
+                                int64_t batch, int32_t heads, int32_t head_dim, float *out,
+                                mirec_stream_t stream);
+int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                                const int32_t *order, int64_t batch, int32_t heads,
+                                int32_t head_dim, float *dqkv, mirec_stream_t stream);
+
+/* One wave per (sequence, head) (csrc/attn_wave.hip): no LDS, no barriers,
+ * every operand loaded straight into its MFMA lane layout; head_dim 16, 32
+ * or 64 (mirec_attention_wave_supported).  offsets == NULL: uniform batch
+ * [batch, T, ...] (1 <= T <= 64); else packed as in the varlen form.  The
+ * forward also writes lse [n_rows, heads] (log-sum-exp of each query's scaled
+ * scores); the backward takes out and lse from it and writes dqkv and delta
+ * [n_rows, heads] (rowsum(dout ⊙ out), scratch), in two launches.  order
+ * (optional, packed form): the sequences in the order their units run, from
+ * mirec_attention_length_order (longest first, device int32 [batch]). */
+int mirec_attention_wave_supported(int32_t head_dim);
+int mirec_attention_length_order(const int32_t *offsets, int64_t batch, int32_t *order,
+                                 mirec_stream_t stream);
+int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
+                             int64_t batch, int32_t T, int32_t heads, int32_t head_dim, float *out,
+                             float *lse, mirec_stream_t stream);
+int mirec_attention_wave_bwd(const float *qkv, const float *out, const float *lse,
+                             const float *dout, const int32_t *offsets, const int32_t *order,
+                             int64_t batch, int32_t T, int32_t heads, int32_t head_dim,
+                             float *dqkv, float *delta, mirec_stream_t stream);
 
 /* Masked mean pool of the SASRec user tower (model/sasrec.py:399-413) on
  * packed sequences: out[b] = Σ_{r in [offsets[b], offsets[b+1])} x[r] /
@@ -652,6 +692,11 @@ int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64
 int mirec_gemm_nt_ex(const float *A, const float *A2, int32_t Ks, const float *Amask,
                      const float *B, const float *bias, float *C, float *C2, int32_t Ns,
                      int32_t relu, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream);
+/* C = A B with B [Kr, No] row-major (the input gradient dX = dY W of a
+ * Linear, W used as stored: no transposed copy); Amask and the C / C2 split
+ * as in gemm_nt_ex. */
+int mirec_gemm_nn_ex(const float *A, const float *Amask, const float *B, float *C, float *C2,
+                     int32_t Ns, int64_t n, int32_t Kr, int32_t No, mirec_stream_t stream);
 int mirec_gemm_tn_ex(const float *A, const float *Amask, const float *B, const float *B2,
                      int32_t Ns, float *C, float *colsum, int64_t n, int32_t M, int32_t No,
                      float *work, mirec_stream_t stream);

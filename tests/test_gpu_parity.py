@@ -745,8 +745,18 @@ def sasrec_from(f):
     return m
 
 
+@pytest.fixture(params=["hybrid", "wave", "block"])
+def attn_impl(request, monkeypatch):
+    """Every attention core: one wave per (sequence, head), one workgroup per
+    (sequence, head), and the wave forward + ordered workgroup backward
+    (sasrec.ATTN_IMPL)."""
+    from furusato_recommend_amd import sasrec as S
+    monkeypatch.setattr(S, "ATTN_IMPL", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("name", ["sasrec_d64_h8.npz", "sasrec_d128_h2.npz"])
-def test_sasrec_attention_block_matches_reference(golden, name):
+def test_sasrec_attention_block_matches_reference(golden, name, attn_impl):
     """The SASRec block with the MFMA attention core (fwd + bwd) == the
     reference's forward_user over torch.nn.MultiheadAttention: outputs and
     the gradients of the input and of every block parameter."""
@@ -768,7 +778,7 @@ def test_sasrec_attention_block_matches_reference(golden, name):
             assert rel(prm.grad, f[f"g_{key}{i}"]) < TOL, (key, i)
 
 
-def test_sasrec_attention_kernel_vs_torch_sdpa():
+def test_sasrec_attention_kernel_vs_torch_sdpa(attn_impl):
     """Raw kernel vs torch's causal SDPA (fp32) over every supported head dim
     and T up to 64, fwd and bwd."""
     import torch.nn.functional as F
@@ -790,7 +800,7 @@ def test_sasrec_attention_kernel_vs_torch_sdpa():
         assert rel(g1, g2) < TOL
 
 
-def test_sasrec_varlen_attention_matches_padded():
+def test_sasrec_varlen_attention_matches_padded(attn_impl):
     """Packed (varlen) kernels == padded kernels on every real row, fwd and
     bwd (padding rows carry zero output gradient, as under the pooled loss),
     incl. lengths 1 and 64 and a zero-length sequence."""
@@ -820,6 +830,16 @@ def test_sasrec_bucketed_attention_matches_varlen():
     packed kernels, fwd and bwd, at every bucket edge (0, 1, 16, 17, 32, 33,
     48, 49, 64), with empty buckets, odd head dims and dh = 64; malformed
     bucket counts are rejected."""
+    from furusato_recommend_amd import sasrec as S
+    from furusato_recommend_amd.sasrec import _CausalAttentionVarlen, length_buckets
+    prev, S.ATTN_IMPL = S.ATTN_IMPL, "block"
+    try:
+        _bucketed_vs_varlen()
+    finally:
+        S.ATTN_IMPL = prev
+
+
+def _bucketed_vs_varlen():
     from furusato_recommend_amd.sasrec import _CausalAttentionVarlen, length_buckets
     torch.manual_seed(2)
     edge = [0, 1, 16, 17, 32, 33, 48, 49, 64, 5, 50, 40, 23, 9]
@@ -843,6 +863,41 @@ def test_sasrec_bucketed_attention_matches_varlen():
         assert rel(o2, o1) < TOL and rel(g2, g1) < TOL
     with pytest.raises(ValueError):
         _CausalAttentionVarlen.apply(qkv, offsets, heads, (0, 2, 1, B))
+
+
+def test_attention_wave_matches_block_and_repeats(monkeypatch):
+    """The wave-per-(sequence, head) core == the workgroup core on packed
+    sequences at every block edge (0, 1, 16, 17, ..., 64 positions), fwd and
+    bwd, for head dims 16 / 32 / 64; reruns are bitwise equal; head dims it
+    does not take (20) fall back to the workgroup core."""
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd import sasrec as S
+    from furusato_recommend_amd.sasrec import _CausalAttentionVarlen
+    assert [int(_lib.lib.mirec_attention_wave_supported(x)) for x in (8, 16, 20, 32, 64)] == \
+        [0, 1, 0, 1, 1]
+    monkeypatch.setattr(S, "ATTN_IMPL", "hybrid")  # restored after the test
+    torch.manual_seed(3)
+    lens = [0, 1, 16, 17, 32, 33, 48, 49, 64, 5, 50, 40, 23, 9]
+    offsets = torch.zeros(len(lens) + 1, dtype=torch.int32, device="cuda")
+    offsets[1:] = torch.cumsum(torch.tensor(lens), 0).int().cuda()
+    n = sum(lens)
+    for heads, dh in ((2, 64), (8, 16), (4, 32), (3, 20)):
+        d = heads * dh
+        qkv = torch.randn(n, 3 * d, device="cuda")
+        go = torch.randn(n, d, device="cuda")
+        res = {}
+        for impl in ("block", "wave", "wave", "hybrid"):
+            S.ATTN_IMPL = impl
+            q = qkv.clone().requires_grad_(True)
+            o = _CausalAttentionVarlen.apply(q, offsets, heads)
+            g, = torch.autograd.grad(o, q, go)
+            if impl in res:
+                assert torch.equal(o, res[impl][0]) and torch.equal(g, res[impl][1])
+            res[impl] = (o, g)
+        S.ATTN_IMPL = "wave"
+        for impl in ("wave", "hybrid"):
+            assert rel(res[impl][0], res["block"][0]) < TOL, (impl, heads, dh)
+            assert rel(res[impl][1], res["block"][1]) < TOL, (impl, heads, dh)
 
 
 def test_sasrec_packed_path_equals_padded():
@@ -1011,6 +1066,46 @@ def test_sasrec_stage_one_equals_unfused_composition():
         # above the noise floor are compared
         diff = (pa - pb).abs()[live[name]]
         assert diff.numel() == 0 or float(diff.max()) < 1e-2 * cfg["lr"], name
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_sasrec_sorted_table_step_matches_dense(graph):
+    """The item table's sorted gradient + fused table Adam (TableGrad, the
+    default) == the materialised gradient + dense Adam, over three steps,
+    eager and captured: every parameter within 1e-2 lr of the dense run (the
+    only difference is the summation order of repeated ids)."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    ds = SyntheticBipartite(500, 300, 10_000, seed=4)
+    cfg = {"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+           "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0, "graph": graph}
+    torch.manual_seed(9)
+    a = SASRec(cfg, ds)
+    torch.manual_seed(9)
+    b = SASRec(dict(cfg, table_grad="dense"), ds)
+    assert a._tg is not None and b._tg is None
+    rng = np.random.default_rng(2)
+    live = {n: True for n, _ in b.named_parameters()}
+
+    def mark():  # elements whose dense gradient is above the rounding floor
+        top = max(float(q.grad.abs().max()) for q in b.parameters())
+        for n, q in b.named_parameters():
+            floor = max(1e-5 * float(q.grad.abs().max()), 1e-6 * top)
+            live[n] = live[n] & (q.grad.abs() > floor)
+    for _ in range(3):
+        users = rng.integers(0, 500, 128)
+        pos = torch.as_tensor(rng.integers(0, 300, 128), device="cuda")
+        neg = torch.as_tensor(rng.integers(0, 300, 128), device="cuda")
+        la = float(a.stageOne(users, pos, neg))
+        b.config["graph"] = False  # the hook runs in the eager step
+        lb = float(b.stageOne(users, pos, neg, grad_hook=mark))
+        assert abs(la - lb) <= 1e-5 * abs(lb)
+    for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
+        # a zero gradient's rounding noise becomes a full lr step under Adam
+        # (the key bias, item_last_proj.bias): compare the live elements
+        diff = (pa - pb).abs()[live[name]]
+        assert diff.numel() == 0 or float(diff.max()) < 1e-2 * cfg["lr"], name
+    for sa, sb in zip(a.optims, b.optims):
+        assert sa.n_steps == sb.n_steps == 3
 
 
 def test_sasrec_trains():
@@ -1274,8 +1369,10 @@ def test_sasrec_graph_step_equals_eager():
     learning with dropout on and draws a fresh mask each replay."""
     from furusato_recommend_amd import SASRec, SyntheticBipartite
     ds = SyntheticBipartite(700, 300, 14_000, seed=6)
+    # the table's gradient materialised (.grad) to compare it; the sorted
+    # form in the captured step: test_sasrec_sorted_table_step_matches_dense
     cfg = {"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
-           "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0}
+           "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0, "table_grad": "dense"}
     torch.manual_seed(3)
     a = SASRec(dict(cfg, graph=True), ds)
     torch.manual_seed(3)
@@ -1297,7 +1394,7 @@ def test_sasrec_graph_step_equals_eager():
     # dropout on: same batch twice -> different losses (fresh masks), and
     # repeated steps on one batch lower its loss
     torch.manual_seed(3)
-    c = SASRec(dict(cfg, dropout_p=0.3, lr=1e-2), ds)
+    c = SASRec(dict(cfg, dropout_p=0.3, lr=1e-2, table_grad="sorted"), ds)
     users = rng.integers(0, 700, 128)
     pos, neg = rng.integers(0, 300, 128), rng.integers(0, 300, 128)
     losses = [float(c.stageOne(users, pos, neg)) for _ in range(30)]
@@ -1322,6 +1419,31 @@ def test_gemm_nt_matches_fp64(n, kr, no):
         ref = a.double() @ b.double().t() + (0 if bb is None else bb.double())
         assert c is not None and rel(c, ref) < 1e-6
     LN.FORCE_MIREC_GEMM = False
+
+
+@pytest.mark.parametrize("n,kr,no", [(1, 32, 128), (100, 384, 128), (56_321, 384, 128),
+                                     (3000, 128, 256), (777, 256, 384)])
+def test_gemm_nn_matches_fp64(n, kr, no):
+    """mirec_gemm_nn_ex (dX = dY W with W as stored, [Kr, No]) vs float64,
+    plain and with the ReLU mask on A and the output split at a 128-column
+    boundary (the GraphSAGE hop's input gradient)."""
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd.linear import gemm_nn
+    torch.manual_seed(n + kr)
+    a = torch.randn(n, kr, device="cuda")
+    b = torch.randn(kr, no, device="cuda")
+    c = gemm_nn(a, b)
+    assert c is not None and rel(c, a.double() @ b.double()) < 1e-6
+    mask = torch.randn(n, kr, device="cuda")
+    am = torch.where(mask > 0, a, torch.zeros_like(a))
+    ref = am.double() @ b.double()
+    if no >= 256:
+        c1 = torch.empty(n, 128, device="cuda")
+        c2 = torch.empty(n, no - 128, device="cuda")
+        _lib.check(_lib.lib.mirec_gemm_nn_ex(a.data_ptr(), mask.data_ptr(), b.data_ptr(),
+                                             c1.data_ptr(), c2.data_ptr(), 128, n, kr, no,
+                                             _lib.stream_handle()), "gemm_nn_ex")
+        assert rel(torch.cat([c1, c2], 1), ref) < 1e-6
 
 
 @pytest.mark.parametrize("n,m,no", [(0, 128, 128), (1, 128, 128), (100, 384, 128),

@@ -105,11 +105,15 @@ def main():
                     help="1: replay the captured HIP graph of the step; 0: eager step")
     ap.add_argument("--attn-buckets", type=int, default=0,
                     help="0: every packed sequence on the 64-row attention kernel (A/B)")
+    ap.add_argument("--attn-impl", default="hybrid", choices=["hybrid", "wave", "block"],
+                    help="attention core (sasrec.ATTN_IMPL): wave forward + workgroup "
+                         "backward (default), one wave, or one workgroup per (sequence, head)")
     ap.add_argument("--fused-rows", type=int, default=1,
                     help="0: the torch composition of dropout / residual / LayerNorm (A/B)")
     args = ap.parse_args()
     from furusato_recommend_amd import SASRec, sasrec as S
     from furusato_recommend_amd.sasrec import SequenceData
+    S.ATTN_IMPL = args.attn_impl
     dev = torch.device("cuda:0")
     torch.manual_seed(2020)
     seq = SequenceData.synthetic(args.users, args.items, dev, max_len=args.maxlen, min_len=5,
