@@ -62,8 +62,8 @@ constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two 
 //
 // B layout: [No, Kr] rows (k contiguous: C = A Bᵀ, a Linear forward with B =
 // W), or with bkn [Kr, No] rows (n contiguous: C = A B, the input gradient
-// dX = dY W of a Linear with B = W, no transposed copy); the staged LDS
-// image is [n][k] either way.
+// dX = dY W of a Linear with B = W, no transposed copy), staged in LDS as
+// [n][k] or [k][n] respectively.
 struct NtArgs {
   const float *A2;
   const float *Amask;
@@ -71,8 +71,11 @@ struct NtArgs {
   int Ks, Ns, relu, bkn;
 };
 
-template <int BM, int PF>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict__ A,
+template <int BM, int PF, bool BKN>
+#ifndef MIREC_NT_OCC
+#define MIREC_NT_OCC 2
+#endif
+__global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         const float *__restrict__ bias,
                                                         float *__restrict__ C, int64_t n,
@@ -80,6 +83,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
   constexpr int TM = BM / 64;        // 32-row MFMA tiles per wave
   constexpr int QA = BM * kC4 / 256;     // float4 of A per thread per chunk
   constexpr int QB = kTile * kC4 / 256;  // float4 of B per thread per chunk
+  static_assert(kChunk * kLdTN <= kTile * kLdNT, "[k][n] B image fits the [n][k] region");
   __shared__ __attribute__((aligned(16))) float smem[(BM + kTile) * kLdNT];
   static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
   float *sA = smem, *sB = smem + BM * kLdNT;
@@ -117,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       }
       xa[q] = v;
     }
-    if (fx.bkn) {  // element e: k row e / 32, float4 column e % 32 of the 128 n
+    if constexpr (BKN) {  // element e: k row e / 32, float4 column e % 32 of the 128 n
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
         const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
@@ -137,14 +141,11 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       st4(sA + r * kLdNT + 4 * c4, xa[q]);
     }
-    if (fx.bkn) {  // transpose into [n][k]
+    if constexpr (BKN) {  // [k][n] as in memory (row stride kLdTN)
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
-        const int e = t + 256 * q, kk = e >> 5, n = 4 * (e & 31);
-        sB[n * kLdNT + kk] = xb[q].x;
-        sB[(n + 1) * kLdNT + kk] = xb[q].y;
-        sB[(n + 2) * kLdNT + kk] = xb[q].z;
-        sB[(n + 3) * kLdNT + kk] = xb[q].w;
+        const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+        st4(sB + kk * kLdTN + 4 * c4, xb[q]);
       }
     } else {
 #pragma unroll
@@ -169,8 +170,15 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       for (int tm = 0; tm < TM; ++tm)
         fa[tm] = ld4(sA + (wm * (BM / 2) + tm * 32 + i) * kLdNT + sub * 8 + 4 * h);
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn)
-        fb[tn] = ld4(sB + (wn * 64 + tn * 32 + i) * kLdNT + sub * 8 + 4 * h);
+      for (int tn = 0; tn < 2; ++tn) {
+        const int col = wn * 64 + tn * 32 + i;
+        if constexpr (BKN) {  // k rows 4 apart land 32 banks apart (kLdTN)
+          const float *bp = sB + (sub * 8 + 4 * h) * kLdTN + col;
+          fb[tn] = make_float4(bp[0], bp[kLdTN], bp[2 * kLdTN], bp[3 * kLdTN]);
+        } else {
+          fb[tn] = ld4(sB + col * kLdNT + sub * 8 + 4 * h);
+        }
+      }
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
@@ -451,9 +459,13 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   // tiles, two chunks ahead and a double-buffered LDS form measured within
   // noise on the C3 / C4 shapes; a persistent form streaming 64-row A tiles
   // past B held in registers measured 15-45 % slower)
-  hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF>),
-                     dim3((unsigned)((n + MIREC_NT_BM1 - 1) / MIREC_NT_BM1) * ncol), dim3(256), 0,
-                     st, A, B, bias, C, n, (int)Kr, (int)No, fx);
+  const dim3 grid((unsigned)((n + MIREC_NT_BM1 - 1) / MIREC_NT_BM1) * ncol);
+  if (bkn)
+    hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF, true>), grid, dim3(256), 0, st,
+                       A, B, bias, C, n, (int)Kr, (int)No, fx);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF, false>), grid, dim3(256), 0,
+                       st, A, B, bias, C, n, (int)Kr, (int)No, fx);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

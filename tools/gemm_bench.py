@@ -58,6 +58,20 @@ def main():
         out.append({"gemm": name, "kind": "nt", "n": n, "K": kr, "N": no, "us": round(us, 1),
                     "tflops": round(tf, 1), "frac_peak": round(tf / PEAK_TF, 3)})
 
+    def nn(name, n, kr, no, mask=False, split=False):
+        A = torch.randn(n, kr, device=dev)
+        B = torch.randn(kr, no, device=dev) * 0.05
+        M = torch.randn(n, kr, device=dev) if mask else None
+        C = torch.empty(n, no if not split else no // 2, device=dev)
+        C2 = torch.empty(n, no // 2, device=dev) if split else None
+        def f():
+            chk(lib.mirec_gemm_nn_ex(A.data_ptr(), _lib.ptr(M), B.data_ptr(), C.data_ptr(),
+                                     _lib.ptr(C2), no // 2 if split else 0, n, kr, no, st), name)
+        us = timed(f, a.reps)
+        tf = 2.0 * n * kr * no / us / 1e6
+        out.append({"gemm": name, "kind": "nn", "n": n, "K": kr, "N": no, "us": round(us, 1),
+                    "tflops": round(tf, 1), "frac_peak": round(tf / PEAK_TF, 3)})
+
     def tn(name, n, m, no, dual=False, mask=False):
         A = torch.randn(n, m, device=dev)
         Bf = torch.randn(n, no, device=dev)
@@ -79,11 +93,14 @@ def main():
     n3 = 153_600
     nt("c3_l0_fwd", n3, 256, 128, dual=True, relu=True)
     nt("c3_l0_dx", n3, 128, 256, mask=True, split=True)
+    nn("c3_l0_dx_nn", n3, 128, 256, mask=True, split=True)
     tn("c3_l0_dw", n3, 128, 256, dual=True, mask=True)
     n4 = 56_320
     nt("c4_qkv_fwd", n4, 128, 384)
     nt("c4_proj_fwd", n4, 128, 128)
     nt("c4_qkv_dx", n4, 384, 128)
+    nn("c4_qkv_dx_nn", n4, 384, 128)
+    nn("c4_proj_dx_nn", n4, 128, 128)
     tn("c4_qkv_dw", n4, 384, 128)
     tn("c4_proj_dw", n4, 128, 128)
     nt("sq_4096", 4096, 4096, 4096)
