@@ -401,6 +401,278 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   }
 }
 
+// ------------------------------------------------------------ packed backward
+// The backward above with several short sequences in one workgroup: the
+// sequences come in packs (mirec_attention_length_order: longest first,
+// one pack = one sequence of 3-4 blocks, two of 2 blocks or four of 1
+// block), so no wave idles on a short sequence and a 4-block workgroup's
+// LDS serves up to four sequences.  Pack p, head h = workgroup p*H + h;
+// wave w is block w of the pack's block list: sequence i = slot(w), local
+// block w - lo (lo = the sequence's first block in the pack).  LDS row R
+// holds local row 16 (R/16 - lo) + R%16 of its block's sequence.
+// scores_softmax of a pack's query block: local key blocks 0..lw of the
+// sequence starting at LDS block lo (keys and the query ql numbered within
+// the sequence); s[kb] holds local key block kb.
+template <int DPAD, int NB>
+__device__ __forceinline__ void scores_softmax_local(const float *sK, const float (&q)[DPAD / 4],
+                                                     int lo, int lw, int ql, int T, float scale,
+                                                     f32x4 (&s)[NB], float &m_out,
+                                                     float &inv_out) {
+  scores_softmax<DPAD, NB>(sK + kB * lo * AttnShape<DPAD, NB>::LDK, q, lw, T, scale, s, m_out,
+                           inv_out);
+  (void)ql;
+}
+
+struct PackSeqs {
+  int64_t row0[4];
+  int T[4], lo[4], n;  // n = the pack's block count
+};
+
+__device__ __forceinline__ void read_pack(const int32_t *packs, const int32_t *offsets, int64_t pk,
+                                          PackSeqs &ps) {
+  int nb = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int32_t b = packs[1 + 4 * pk + i];
+    int T = 0;
+    int64_t r0 = 0;
+    if (b >= 0) {
+      r0 = offsets[b];
+      T = min(offsets[b + 1] - offsets[b], kT);
+    }
+    ps.row0[i] = r0;
+    ps.T[i] = T;
+    ps.lo[i] = nb;
+    nb += (T + kB - 1) / kB;
+  }
+  ps.n = nb;
+}
+
+// (T, first block, first row) of the sequence holding block w (w < ps.n),
+// by selects (no dynamic register indexing).
+__device__ __forceinline__ void seq_of(const PackSeqs &ps, int w, int &T, int &lo,
+                                       int64_t &row0) {
+  T = ps.T[0];
+  lo = ps.lo[0];
+  row0 = ps.row0[0];
+#pragma unroll
+  for (int k = 1; k < 4; ++k)
+    if (w >= ps.lo[k] && ps.T[k] > 0) {
+      T = ps.T[k];
+      lo = ps.lo[k];
+      row0 = ps.row0[k];
+    }
+}
+
+// K / V rows of every block of the pack into LDS (rows past a sequence's
+// length and dims past dh zero), all loads issued before the first store.
+template <int DPAD, int LD>
+__device__ __forceinline__ void load_pack(float *d0, float *d1, const float *qkv, int64_t rs,
+                                          int coff, const PackSeqs &ps, int dh) {
+  constexpr int C4 = DPAD / 4, TR = 4 * kB, PER = TR * C4 / 256;
+  float4 v0[PER], v1[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4, w = R / kB;
+    bool ok = w < ps.n && 4 * c < dh;
+    int64_t row = 0;
+    if (ok) {
+      int T, lo;
+      int64_t r0;
+      seq_of(ps, w, T, lo, r0);
+      const int loc = kB * (w - lo) + R % kB;
+      ok = loc < T;
+      row = r0 + loc;
+    }
+    const float *src = qkv + row * rs + coff + 4 * c;
+    v0[q] = ok ? ld4(src) : f4_zero();
+    v1[q] = ok ? ld4(src + rs / 3) : f4_zero();
+  }
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4;
+    st4(d0 + R * LD + 4 * c, v0[q]);
+    st4(d1 + R * LD + 4 * c, v1[q]);
+  }
+}
+
+// waves_per_eu(4): at most 128 registers, so four workgroups (the LDS
+// limit) fit per CU.  dh % 4 == 0.
+template <int DPAD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_packed_kernel(
+    const float *__restrict__ qkv, const float *__restrict__ dout, float *__restrict__ dqkv,
+    int H, int dh, float scale, const int32_t *__restrict__ offsets,
+    const int32_t *__restrict__ packs) {
+  constexpr int NB = 4;
+  using S = AttnShape<DPAD, NB>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
+  float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
+  float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
+  const int64_t pk = blockIdx.x / H;
+  if (pk >= packs[0]) return;
+  const int h = blockIdx.x % H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = lane & 15, g = lane >> 4;
+  const int d = H * dh;
+  const int64_t rs = 3 * (int64_t)d;
+  PackSeqs ps;
+  read_pack(packs, offsets, pk, ps);
+  load_pack<DPAD, S::LDK>(sK, sV, qkv, rs, d + h * dh, ps, dh);
+  // this wave's sequence
+  const bool act = w < ps.n;
+  int T = 0, lo = 0;
+  int64_t row0 = 0;
+  if (act) seq_of(ps, w, T, lo, row0);
+  lo &= 3;                                           // (0 <= lo <= w)
+  const int hi = act ? lo + (T + kB - 1) / kB : 0;  // one past the sequence's last block
+  const float *base = qkv + row0 * rs + h * dh;
+  float *gbase = dqkv + row0 * rs + h * dh;
+  const int ql = kB * (w - lo) + j;  // local query row of phase A
+  const int qa = kB * w + j;         // its LDS row
+  const bool qvalid = act && ql < T;
+  float q[S::Q4], dov[S::Q4];
+  load_seg<S::Q4>(base + (int64_t)ql * rs, g, dh, qvalid, q);
+  load_seg<S::Q4>(dout + (row0 + ql) * d + h * dh, g, dh, qvalid, dov);
+  __syncthreads();
+  // ---------------------------------------------------- phase A: query block w
+  float kr[S::Q4], vr[S::Q4];
+  if (act) {
+    f32x4 p[NB], dp[NB];
+    float m, inv;
+    // local key blocks kb = 0..lw (LDS block lo + kb); the masks tell the
+    // compiler lw, lo < 4 (as the plain kernel's w), which keeps the
+    // unrolled block loops from holding every block's operands at once
+    const int lw = (w - lo) & 3;
+    const float *sKl = sK + kB * lo * S::LDK, *sVl = sV + kB * lo * S::LDK;  // lo < 4
+    scores_softmax_local<DPAD, NB>(sK, q, lo, lw, ql, T, scale, p, m, inv);
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
+#pragma unroll
+    for (int t = 0; t < S::Q4; ++t) {
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+        if (kb <= lw) dp[kb] = mfma16(sVl[(kB * kb + j) * S::LDK + 4 * t + g], dov[t], dp[kb]);
+    }
+    float delta = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb > lw) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) delta += p[kb][r] * dp[kb][r];
+    }
+    delta += __shfl_xor(delta, 16);
+    delta += __shfl_xor(delta, 32);
+    if (g == 0) {
+      sM[qa] = m;
+      sL[qa] = inv;
+      sD[qa] = delta;
+    }
+    f32x4 dq[S::NCB];
+#pragma unroll
+    for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = zero4();
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb > lw) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dp[kb][r] = p[kb][r] * (dp[kb][r] - delta) * scale;
+        const float *krow = sKl + (kB * kb + 4 * g + r) * S::LDK + j;
+#pragma unroll
+        for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = mfma16(krow[kB * cb], dp[kb][r], dq[cb]);
+      }
+    }
+    if (ql < T) {
+      float *row = gbase + (int64_t)ql * rs;
+#pragma unroll
+      for (int cb = 0; cb < S::NCB; ++cb) store4(row, kB * cb + 4 * g, dh, dq[cb]);
+    }
+#pragma unroll
+    for (int t = 0; t < S::Q4; ++t) {
+      kr[t] = sK[qa * S::LDK + 4 * t + g];
+      vr[t] = sV[qa * S::LDK + 4 * t + g];
+    }
+  }
+  __syncthreads();  // K / V no longer read from LDS; statistics complete
+  if (act) {
+#pragma unroll
+    for (int t = 0; t < S::Q4; ++t) {
+      sQ[qa * S::LDK + 4 * t + g] = q[t];
+      sDO[qa * S::LDK + 4 * t + g] = dov[t];
+    }
+  }
+  __syncthreads();
+  // ------------------------------------------------------ phase B: key block w
+  if (act) {
+    const int key = kB * (w - lo) + j;  // local
+    f32x4 dv[S::NCB], dk[S::NCB];
+#pragma unroll
+    for (int cb = 0; cb < S::NCB; ++cb) {
+      dv[cb] = zero4();
+      dk[cb] = zero4();
+    }
+    // local query blocks lw..nbs-1 of the sequence (LDS block lo + qb)
+    const int lw = (w - lo) & 3, nbs = hi - lo, o = kB * (lo & 3);
+    const float *sQl = sQ + o * S::LDK, *sDOl = sDO + o * S::LDK;
+    const float *sMl = sM + o, *sLl = sL + o, *sDl = sD + o;
+    for (int qb = lw; qb < nbs; ++qb) {
+      f32x4 sc = zero4(), dpc = zero4();
+      const float *qrow = sQl + (kB * qb + j) * S::LDK + g;
+      const float *orow = sDOl + (kB * qb + j) * S::LDK + g;
+#pragma unroll
+      for (int t = 0; t < S::Q4; ++t) {
+        sc = mfma16(qrow[4 * t], kr[t], sc);
+        dpc = mfma16(orow[4 * t], vr[t], dpc);
+      }
+      float pr[4], dsr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = kB * qb + 4 * g + r;  // local query = its local LDS row
+        const bool ok = key <= qq && qq < T;
+        const float pv = ok ? expf(sc[r] * scale - sMl[qq]) * sLl[qq] : 0.f;
+        pr[r] = pv;
+        dsr[r] = pv * (dpc[r] - sDl[qq]) * scale;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = kB * qb + 4 * g + r;
+        const float *dorow = sDOl + qq * S::LDK + j;
+        const float *qrr = sQl + qq * S::LDK + j;
+#pragma unroll
+        for (int cb = 0; cb < S::NCB; ++cb) {
+          dv[cb] = mfma16(dorow[kB * cb], pr[r], dv[cb]);
+          dk[cb] = mfma16(qrr[kB * cb], dsr[r], dk[cb]);
+        }
+      }
+    }
+    if (key < T) {
+      float *row = gbase + (int64_t)key * rs;
+#pragma unroll
+      for (int cb = 0; cb < S::NCB; ++cb) {
+        store4(row + d, kB * cb + 4 * g, dh, dk[cb]);
+        store4(row + 2 * d, kB * cb + 4 * g, dh, dv[cb]);
+      }
+    }
+  }
+}
+
+template <int DPAD>
+static int launch_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                             const int32_t *packs, int64_t batch, int heads, int dh, float *dqkv,
+                             hipStream_t st) {
+  constexpr int lds = AttnShape<DPAD, 4>::bwd_lds;
+  static int rc = -1;
+  if (rc < 0)
+    rc = hipFuncSetAttribute((const void *)attn_bwd_packed_kernel<DPAD>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess ? 0 : 1;
+  if (rc != 0) return MIREC_ERR_HIP;
+  hipLaunchKernelGGL((attn_bwd_packed_kernel<DPAD>), dim3((unsigned)(batch * heads)), dim3(256),
+                     lds, st, qkv, dout, dqkv, heads, dh,
+                     1.f / sqrtf((float)dh), offsets, packs);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
 // Dynamic LDS above 64 KiB needs an explicit opt-in per kernel (once).
 template <int DPAD, int NB>
 static int allow_lds() {
@@ -565,4 +837,20 @@ extern "C" int mirec_attention_ordered_bwd(const float *qkv, const float *dout,
   const int64_t be[4] = {0, 0, 0, batch};
   return launch(true, qkv, dout, offsets, be, kT, heads, head_dim, dqkv,
                 reinterpret_cast<hipStream_t>(stream), order);
+}
+
+extern "C" int mirec_attention_packed_bwd(const float *qkv, const float *dout,
+                                          const int32_t *offsets, const int32_t *packs,
+                                          int64_t batch, int32_t heads, int32_t head_dim,
+                                          float *dqkv, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(batch >= 0 && heads >= 1 && head_dim >= 4 && head_dim <= 64 &&
+                  head_dim % 4 == 0);
+  if (batch == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(qkv && dout && offsets && packs && dqkv);
+  MIREC_CHECK_ARG(((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return head_dim <= 32
+             ? launch_packed_bwd<32>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv, st)
+             : launch_packed_bwd<64>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv, st);
 }

@@ -365,11 +365,18 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dkdv_kernel(
 
 // order = the sequences by length, longest first (counting sort over the 65
 // clamped lengths; the order among equal lengths is arbitrary — it changes
-// no result, every unit is independent).
+// no result, every unit is independent).  packs (optional, int32 [1 + 4
+// batch]): packs[0] = the pack count, packs[1 + 4p + s] = sequence in slot s
+// of pack p or -1.  Over the same order, each sequence of 49-64 or 33-48
+// positions (4 / 3 blocks of 16) is a pack of its own, those of 17-32 go
+// two to a pack and those of 1-16 four to a pack (empty sequences in none):
+// mirec_attention_packed_bwd's workgroups.
 __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__restrict__ offsets,
                                                            int64_t batch,
-                                                           int32_t *__restrict__ order) {
+                                                           int32_t *__restrict__ order,
+                                                           int32_t *__restrict__ packs) {
   __shared__ int cnt[kMaxT + 1], start[kMaxT + 1];
+  __shared__ int cls_start[5], cls_count[5], pack_base[5];
   for (int i = threadIdx.x; i <= kMaxT; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
   for (int64_t b = threadIdx.x; b < batch; b += blockDim.x)
@@ -381,10 +388,46 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
       start[L] = acc;
       acc += cnt[L];
     }
+    // classes by block count k = ceil(L / 16), contiguous in the order
+    for (int k = 0; k <= 4; ++k) cls_count[k] = 0;
+    for (int L = 0; L <= kMaxT; ++L) cls_count[(L + kBlk - 1) / kBlk] += cnt[L];
+    int pos = 0, pb = 0;
+    for (int k = 4; k >= 1; --k) {
+      const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
+      cls_start[k] = pos;
+      pack_base[k] = pb;
+      pos += cls_count[k];
+      pb += (cls_count[k] + per - 1) / per;
+    }
+    cls_start[0] = pos;
+    pack_base[0] = pb;  // = the pack count
   }
   __syncthreads();
-  for (int64_t b = threadIdx.x; b < batch; b += blockDim.x)
-    order[atomicAdd(&start[min(offsets[b + 1] - offsets[b], kMaxT)], 1)] = (int32_t)b;
+  if (packs != nullptr) {
+    const int n_packs = pack_base[0];
+    if (threadIdx.x == 0) packs[0] = n_packs;
+    // slots no sequence fills: -1 (written before, and disjoint from, the
+    // sequence slots below)
+    for (int p = threadIdx.x; p < n_packs; p += blockDim.x) {
+      // class of pack p: the k with pack_base[k] <= p < pack_base[k - 1]
+      int k = 4;
+      while (k > 1 && p >= pack_base[k - 1]) --k;
+      const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
+      const int used = min(per, cls_count[k] - (p - pack_base[k]) * per);
+      for (int sl = used; sl < 4; ++sl) packs[1 + 4 * (int64_t)p + sl] = -1;
+    }
+  }
+  for (int64_t b = threadIdx.x; b < batch; b += blockDim.x) {
+    const int L = min(offsets[b + 1] - offsets[b], kMaxT);
+    const int pos = atomicAdd(&start[L], 1);
+    order[pos] = (int32_t)b;
+    const int k = (L + kBlk - 1) / kBlk;
+    if (packs != nullptr && k > 0) {
+      const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
+      const int i = pos - cls_start[k];
+      packs[1 + 4 * (int64_t)(pack_base[k] + i / per) + i % per] = (int32_t)b;
+    }
+  }
 }
 
 template <int DH>
@@ -426,12 +469,18 @@ extern "C" int mirec_attention_wave_supported(int32_t head_dim) {
 }
 
 extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batch,
-                                            int32_t *order, mirec_stream_t stream) {
-  MIREC_CHECK_ARG(batch >= 0 && batch <= INT32_MAX);
-  if (batch == 0) return MIREC_OK;
+                                            int32_t *order, int32_t *packs,
+                                            mirec_stream_t stream) {
+  MIREC_CHECK_ARG(batch >= 0 && batch <= INT32_MAX / 4);
+  if (batch == 0) {
+    if (packs != nullptr) return hipMemsetAsync(packs, 0, sizeof(int32_t),
+                                                reinterpret_cast<hipStream_t>(stream)) ==
+                                           hipSuccess ? MIREC_OK : MIREC_ERR_HIP;
+    return MIREC_OK;
+  }
   MIREC_CHECK_ARG(offsets && order);
   hipLaunchKernelGGL(length_order_kernel, dim3(1), dim3(1024), 0,
-                     reinterpret_cast<hipStream_t>(stream), offsets, batch, order);
+                     reinterpret_cast<hipStream_t>(stream), offsets, batch, order, packs);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

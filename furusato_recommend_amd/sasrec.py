@@ -73,9 +73,11 @@ def _wave_fwd(qkv, offsets, B, T, heads, dh, out):
                       device=qkv.device)
     order = None
     if offsets is not None and B > 0:
-        order = torch.empty(B, dtype=torch.int32, device=qkv.device)
+        # [order (B) | packs (1 + 4B)]
+        order = torch.empty(5 * B + 1, dtype=torch.int32, device=qkv.device)
         check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
-                                               _lib.stream_handle()), "attention_length_order")
+                                               order[B:].data_ptr(), _lib.stream_handle()),
+              "attention_length_order")
     _timed("fwd", (B, T if offsets is None else -1, heads, dh), lambda: check(
         lib.mirec_attention_wave_fwd(qkv.data_ptr(), _ptr(offsets), _ptr(order), B, T, heads, dh,
                                      out.data_ptr(), lse.data_ptr(), _lib.stream_handle()),
@@ -190,13 +192,13 @@ class _CausalAttentionVarlen(torch.autograd.Function):
             out, lse, order = ctx.saved_tensors[2:]
             if ATTN_IMPL == "wave" or order is None:
                 _wave_bwd(qkv, out, lse, order, dout, offsets, B, 0, ctx.heads, dh, dqkv)
-            else:
+            else:  # sequences packed into workgroups, longest first
                 _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(
-                    lib.mirec_attention_ordered_bwd(qkv.data_ptr(), dout.data_ptr(),
-                                                    offsets.data_ptr(), order.data_ptr(), B,
-                                                    ctx.heads, dh, dqkv.data_ptr(),
-                                                    _lib.stream_handle()),
-                    "attention_ordered_bwd"), offsets)
+                    lib.mirec_attention_packed_bwd(qkv.data_ptr(), dout.data_ptr(),
+                                                   offsets.data_ptr(), order[B:].data_ptr(), B,
+                                                   ctx.heads, dh, dqkv.data_ptr(),
+                                                   _lib.stream_handle()),
+                    "attention_packed_bwd"), offsets)
             return dqkv, None, None, None, None
         if ctx.bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_bwd(  # noqa: E731

@@ -561,6 +561,13 @@ int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int3
                                  const int64_t *bucket_end, int32_t heads, int32_t head_dim,
                                  float *dqkv, mirec_stream_t stream);
 
+/* Backward with short sequences sharing a workgroup (one wave per 16-row
+ * block, up to 4 blocks per workgroup): packs from
+ * mirec_attention_length_order; head_dim % 4 == 0, <= 64. */
+int mirec_attention_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
+                               const int32_t *packs, int64_t batch, int32_t heads,
+                               int32_t head_dim, float *dqkv, mirec_stream_t stream);
+
 /* Packed form with the workgroups in a given sequence order (device int32
  * [batch], e.g. mirec_attention_length_order: longest first). */
 int mirec_attention_ordered_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
@@ -578,10 +585,13 @@ int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32
  * scores); the backward takes out and lse from it and writes dqkv and delta
  * [n_rows, heads] (rowsum(dout ⊙ out), scratch), in two launches.  order
  * (optional, packed form): the sequences in the order their units run, from
- * mirec_attention_length_order (longest first, device int32 [batch]). */
+ * mirec_attention_length_order (longest first, device int32 [batch]; with
+ * packs (optional, int32 [1 + 4 batch]) it also groups that order into
+ * packs of at most 4 blocks of 16 positions for mirec_attention_packed_bwd:
+ * packs[0] = count, packs[1 + 4p + s] = sequence or -1). */
 int mirec_attention_wave_supported(int32_t head_dim);
 int mirec_attention_length_order(const int32_t *offsets, int64_t batch, int32_t *order,
-                                 mirec_stream_t stream);
+                                 int32_t *packs, mirec_stream_t stream);
 int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
                              int64_t batch, int32_t T, int32_t heads, int32_t head_dim, float *out,
                              float *lse, mirec_stream_t stream);
