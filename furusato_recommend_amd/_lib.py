@@ -180,9 +180,10 @@ SIGNATURES = {
                                             c_int32, c_void_p, c_void_p]),
     "mirec_attention_ordered_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                             c_int32, c_int32, c_void_p, c_void_p]),
-    "mirec_attention_length_order": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mirec_attention_length_order": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
+                                             c_int64, c_int32, c_void_p]),
     "mirec_attention_packed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                           c_int32, c_int32, c_void_p, c_void_p]),
+                                           c_int32, c_int32, c_void_p, c_int64, c_void_p]),
     "mirec_attention_wave_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                          c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_attention_wave_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

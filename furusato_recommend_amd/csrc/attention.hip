@@ -502,7 +502,7 @@ template <int DPAD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_packed_kernel(
     const float *__restrict__ qkv, const float *__restrict__ dout, float *__restrict__ dqkv,
     int H, int dh, float scale, const int32_t *__restrict__ offsets,
-    const int32_t *__restrict__ packs) {
+    const int32_t *__restrict__ packs, int64_t batch, int64_t n_rows) {
   constexpr int NB = 4;
   using S = AttnShape<DPAD, NB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -510,7 +510,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
   float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
   const int64_t pk = blockIdx.x / H;
-  if (pk >= packs[0]) return;
+  const int64_t busy = (int64_t)packs[0] * H;
+  if ((int64_t)blockIdx.x >= busy) {
+    // a spare workgroup: zero its share of the capacity padding rows
+    const int64_t w4 = 3 * (int64_t)H * dh / 4;
+    const int64_t e0 = (int64_t)offsets[batch] * w4, e1 = n_rows * w4;
+    const int64_t stride = ((int64_t)gridDim.x - busy) * 256;
+    for (int64_t e = e0 + ((int64_t)blockIdx.x - busy) * 256 + threadIdx.x; e < e1; e += stride)
+      st4(dqkv + 4 * e, f4_zero());
+    return;
+  }
   const int h = blockIdx.x % H;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
@@ -659,16 +668,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
 template <int DPAD>
 static int launch_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
                              const int32_t *packs, int64_t batch, int heads, int dh, float *dqkv,
-                             hipStream_t st) {
+                             int64_t n_rows, hipStream_t st) {
   constexpr int lds = AttnShape<DPAD, 4>::bwd_lds;
   static int rc = -1;
   if (rc < 0)
     rc = hipFuncSetAttribute((const void *)attn_bwd_packed_kernel<DPAD>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess ? 0 : 1;
   if (rc != 0) return MIREC_ERR_HIP;
-  hipLaunchKernelGGL((attn_bwd_packed_kernel<DPAD>), dim3((unsigned)(batch * heads)), dim3(256),
-                     lds, st, qkv, dout, dqkv, heads, dh,
-                     1.f / sqrtf((float)dh), offsets, packs);
+  // at most batch packs per head, plus spare workgroups for the padding rows
+  hipLaunchKernelGGL((attn_bwd_packed_kernel<DPAD>), dim3((unsigned)(batch * heads + 256)),
+                     dim3(256), lds, st, qkv, dout, dqkv, heads, dh, 1.f / sqrtf((float)dh),
+                     offsets, packs, batch, n_rows);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -842,15 +852,17 @@ extern "C" int mirec_attention_ordered_bwd(const float *qkv, const float *dout,
 extern "C" int mirec_attention_packed_bwd(const float *qkv, const float *dout,
                                           const int32_t *offsets, const int32_t *packs,
                                           int64_t batch, int32_t heads, int32_t head_dim,
-                                          float *dqkv, mirec_stream_t stream) {
+                                          float *dqkv, int64_t n_rows, mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(batch >= 0 && heads >= 1 && head_dim >= 4 && head_dim <= 64 &&
-                  head_dim % 4 == 0);
+                  head_dim % 4 == 0 && n_rows >= 0);
   if (batch == 0) return MIREC_OK;
   MIREC_CHECK_ARG(qkv && dout && offsets && packs && dqkv);
   MIREC_CHECK_ARG(((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return head_dim <= 32
-             ? launch_packed_bwd<32>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv, st)
-             : launch_packed_bwd<64>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv, st);
+             ? launch_packed_bwd<32>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv,
+                                     n_rows, st)
+             : launch_packed_bwd<64>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv,
+                                     n_rows, st);
 }

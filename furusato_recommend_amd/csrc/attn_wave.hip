@@ -374,7 +374,13 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dkdv_kernel(
 __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__restrict__ offsets,
                                                            int64_t batch,
                                                            int32_t *__restrict__ order,
-                                                           int32_t *__restrict__ packs) {
+                                                           int32_t *__restrict__ packs,
+                                                           float *__restrict__ zero_buf,
+                                                           int64_t zero_rows, int32_t zero_w4) {
+  if (zero_buf != nullptr) {  // capacity padding rows of the output
+    const int64_t e0 = (int64_t)offsets[batch] * zero_w4, e1 = zero_rows * zero_w4;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) st4(zero_buf + 4 * e, f4_zero());
+  }
   __shared__ int cnt[kMaxT + 1], start[kMaxT + 1];
   __shared__ int cls_start[5], cls_count[5], pack_base[5];
   for (int i = threadIdx.x; i <= kMaxT; i += blockDim.x) cnt[i] = 0;
@@ -469,9 +475,13 @@ extern "C" int mirec_attention_wave_supported(int32_t head_dim) {
 }
 
 extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batch,
-                                            int32_t *order, int32_t *packs,
+                                            int32_t *order, int32_t *packs, float *zero_buf,
+                                            int64_t zero_rows, int32_t zero_width,
                                             mirec_stream_t stream) {
   MIREC_CHECK_ARG(batch >= 0 && batch <= INT32_MAX / 4);
+  MIREC_CHECK_ARG(zero_buf == nullptr ||
+                  (zero_rows >= 0 && zero_width > 0 && zero_width % 4 == 0 &&
+                   (uintptr_t)zero_buf % 16 == 0));
   if (batch == 0) {
     if (packs != nullptr) return hipMemsetAsync(packs, 0, sizeof(int32_t),
                                                 reinterpret_cast<hipStream_t>(stream)) ==
@@ -480,7 +490,8 @@ extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batc
   }
   MIREC_CHECK_ARG(offsets && order);
   hipLaunchKernelGGL(length_order_kernel, dim3(1), dim3(1024), 0,
-                     reinterpret_cast<hipStream_t>(stream), offsets, batch, order, packs);
+                     reinterpret_cast<hipStream_t>(stream), offsets, batch, order, packs,
+                     zero_buf, zero_rows, zero_width / 4);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -10,17 +10,36 @@
 namespace mirec {
 
 // 64 lanes x float4 = 256 columns per pass; d <= 1024.
-__global__ __launch_bounds__(64) void segment_mean_kernel(const float *__restrict__ x,
-                                                          const int32_t *__restrict__ offsets,
-                                                          const int64_t *__restrict__ length,
-                                                          int32_t d, float *__restrict__ out) {
-  const int64_t b = blockIdx.x;
+// One wave per sequence: lanes 0-31 sum the even rows and lanes 32-63 the
+// odd rows of a 128-column slice (4 rows of each in flight per lane), then
+// the two partials are added — a fixed order, so reruns are bitwise equal.
+__global__ __launch_bounds__(256) void segment_mean_kernel(const float *__restrict__ x,
+                                                           const int32_t *__restrict__ offsets,
+                                                           const int64_t *__restrict__ length,
+                                                           int64_t B, int32_t d,
+                                                           float *__restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
   const int r0 = offsets[b], r1 = offsets[b + 1];
   const float inv = 1.f / (float)length[b];
-  for (int c = 4 * threadIdx.x; c < d; c += 256) {
+  for (int c0 = 0; c0 < d; c0 += 128) {
+    const int c = c0 + 4 * (lane & 31);
+    const bool on = c < d;
     float4 a = f4_zero();
-    for (int r = r0; r < r1; ++r) a = f4_add(a, ld4(x + (int64_t)r * d + c));
-    st4(out + b * d + c, make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv));
+    for (int r = r0 + half; r < r1; r += 8) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[u] = (on && r + 2 * u < r1) ? ld4(x + (int64_t)(r + 2 * u) * d + c) : f4_zero();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a = f4_add(a, v[u]);
+    }
+    a.x += __shfl_xor(a.x, 32);
+    a.y += __shfl_xor(a.y, 32);
+    a.z += __shfl_xor(a.z, 32);
+    a.w += __shfl_xor(a.w, 32);
+    if (on && half == 0) st4(out + b * d + c, make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv));
   }
 }
 
@@ -446,8 +465,8 @@ extern "C" int mirec_segment_mean(const float *x, const int32_t *offsets, const 
   MIREC_CHECK_ARG(B >= 0 && d > 0 && d % 4 == 0 && d <= 1024);
   if (B == 0) return MIREC_OK;
   MIREC_CHECK_ARG(x && offsets && length && out);
-  hipLaunchKernelGGL(segment_mean_kernel, dim3((unsigned)B), dim3(64), 0, (hipStream_t)stream,
-                     x, offsets, length, d, out);
+  hipLaunchKernelGGL(segment_mean_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, x, offsets, length, B, d, out);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -66,9 +66,10 @@ def _use_wave(dh: int) -> bool:
     return ATTN_IMPL in ("wave", "hybrid") and bool(lib.mirec_attention_wave_supported(dh))
 
 
-def _wave_fwd(qkv, offsets, B, T, heads, dh, out):
+def _wave_fwd(qkv, offsets, B, T, heads, dh, out, padded=False):
     """mirec_attention_wave_fwd; returns (lse [n_rows, heads], order): packed
-    sequences run longest first (mirec_attention_length_order)."""
+    sequences run longest first (mirec_attention_length_order, which also
+    zeroes out's capacity-padding rows when ``padded``)."""
     lse = torch.empty(qkv.shape[0] if offsets is not None else B * T, heads, dtype=qkv.dtype,
                       device=qkv.device)
     order = None
@@ -76,8 +77,12 @@ def _wave_fwd(qkv, offsets, B, T, heads, dh, out):
         # [order (B) | packs (1 + 4B)]
         order = torch.empty(5 * B + 1, dtype=torch.int32, device=qkv.device)
         check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
-                                               order[B:].data_ptr(), _lib.stream_handle()),
+                                               order[B:].data_ptr(),
+                                               out.data_ptr() if padded else None,
+                                               out.shape[0], out.shape[1], _lib.stream_handle()),
               "attention_length_order")
+    elif padded:
+        _zero_tail(out, offsets)
     _timed("fwd", (B, T if offsets is None else -1, heads, dh), lambda: check(
         lib.mirec_attention_wave_fwd(qkv.data_ptr(), _ptr(offsets), _ptr(order), B, T, heads, dh,
                                      out.data_ptr(), lse.data_ptr(), _lib.stream_handle()),
@@ -156,15 +161,17 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         B = offsets.numel() - 1
         qkv = qkv.contiguous()
         out = torch.empty(n, d, dtype=qkv.dtype, device=qkv.device)
-        if padded:  # rows outside every sequence: not written by the kernels
-            _zero_tail(out, offsets)
         ctx.heads = heads
         ctx.bucket_end = bucket_end
         ctx.padded = padded
+        # rows outside every sequence (capacity padding) are not written by
+        # the attention kernels: zeroed by the ordering pass or here
         if _use_wave(dh):
-            lse, order = _wave_fwd(qkv, offsets, B, 0, heads, dh, out)
+            lse, order = _wave_fwd(qkv, offsets, B, 0, heads, dh, out, padded)
             ctx.save_for_backward(qkv, offsets, out, lse, order)
             return out
+        if padded:
+            _zero_tail(out, offsets)
         if bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_fwd(  # noqa: E731
                 qkv.data_ptr(), offsets.data_ptr(), B, heads, dh, out.data_ptr(),
@@ -185,21 +192,25 @@ class _CausalAttentionVarlen(torch.autograd.Function):
         B = offsets.numel() - 1
         dh = d3 // 3 // ctx.heads
         dqkv = torch.empty_like(qkv)
-        if ctx.padded:
-            _zero_tail(dqkv, offsets)
         dout = dout.contiguous()
         if len(ctx.saved_tensors) == 5:
             out, lse, order = ctx.saved_tensors[2:]
             if ATTN_IMPL == "wave" or order is None:
+                if ctx.padded:
+                    _zero_tail(dqkv, offsets)
                 _wave_bwd(qkv, out, lse, order, dout, offsets, B, 0, ctx.heads, dh, dqkv)
-            else:  # sequences packed into workgroups, longest first
+            else:  # sequences packed into workgroups, longest first; its spare
+                # workgroups zero the capacity padding rows
                 _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(
                     lib.mirec_attention_packed_bwd(qkv.data_ptr(), dout.data_ptr(),
                                                    offsets.data_ptr(), order[B:].data_ptr(), B,
                                                    ctx.heads, dh, dqkv.data_ptr(),
+                                                   n if ctx.padded else 0,
                                                    _lib.stream_handle()),
                     "attention_packed_bwd"), offsets)
             return dqkv, None, None, None, None
+        if ctx.padded:
+            _zero_tail(dqkv, offsets)
         if ctx.bucket_end is None:
             launch = lambda: check(lib.mirec_attention_varlen_bwd(  # noqa: E731
                 qkv.data_ptr(), dout.data_ptr(), offsets.data_ptr(), B, ctx.heads, dh,

@@ -563,10 +563,12 @@ int mirec_attention_bucketed_bwd(const float *qkv, const float *dout, const int3
 
 /* Backward with short sequences sharing a workgroup (one wave per 16-row
  * block, up to 4 blocks per workgroup): packs from
- * mirec_attention_length_order; head_dim % 4 == 0, <= 64. */
+ * mirec_attention_length_order; head_dim % 4 == 0, <= 64.  Rows
+ * [offsets[batch], n_rows) of dqkv (capacity padding) are zeroed. */
 int mirec_attention_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
                                const int32_t *packs, int64_t batch, int32_t heads,
-                               int32_t head_dim, float *dqkv, mirec_stream_t stream);
+                               int32_t head_dim, float *dqkv, int64_t n_rows,
+                               mirec_stream_t stream);
 
 /* Packed form with the workgroups in a given sequence order (device int32
  * [batch], e.g. mirec_attention_length_order: longest first). */
@@ -588,10 +590,13 @@ int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32
  * mirec_attention_length_order (longest first, device int32 [batch]; with
  * packs (optional, int32 [1 + 4 batch]) it also groups that order into
  * packs of at most 4 blocks of 16 positions for mirec_attention_packed_bwd:
- * packs[0] = count, packs[1 + 4p + s] = sequence or -1). */
+ * packs[0] = count, packs[1 + 4p + s] = sequence or -1); with zero_buf it
+ * also zeroes rows [offsets[batch], zero_rows) of that [zero_rows,
+ * zero_width] buffer (the capacity padding of a packed batch's output). */
 int mirec_attention_wave_supported(int32_t head_dim);
 int mirec_attention_length_order(const int32_t *offsets, int64_t batch, int32_t *order,
-                                 int32_t *packs, mirec_stream_t stream);
+                                 int32_t *packs, float *zero_buf, int64_t zero_rows,
+                                 int32_t zero_width, mirec_stream_t stream);
 int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
                              int64_t batch, int32_t T, int32_t heads, int32_t head_dim, float *out,
                              float *lse, mirec_stream_t stream);
@@ -602,7 +607,7 @@ int mirec_attention_wave_bwd(const float *qkv, const float *out, const float *ls
 
 /* Masked mean pool of the SASRec user tower (model/sasrec.py:399-413) on
  * packed sequences: out[b] = Σ_{r in [offsets[b], offsets[b+1])} x[r] /
- * length[b] (rows summed in order), x [n, d], out [B, d], d % 4 == 0,
+ * length[b] (rows summed in a fixed order), x [n, d], out [B, d], d % 4 == 0,
  * d <= 1024.  Backward: grad_x[t] = grad_out[seg[t]] / length[seg[t]] for
  * the n_rows rows (0 where seg[t] is outside [0, B): capacity padding). */
 int mirec_segment_mean(const float *x, const int32_t *offsets, const int64_t *length, int64_t B,

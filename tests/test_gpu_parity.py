@@ -900,6 +900,32 @@ def test_attention_wave_matches_block_and_repeats(monkeypatch):
             assert rel(res[impl][1], res["block"][1]) < TOL, (impl, heads, dh)
 
 
+def test_attention_capacity_padding_rows_zero(attn_impl):
+    """A capacity-padded packed batch (the captured step's form): the rows
+    past the last sequence come out zero in the output and in dqkv, even when
+    the buffers held NaN before (the zeroing is folded into the ordering
+    pass and the packed backward's spare workgroups)."""
+    from furusato_recommend_amd.sasrec import _CausalAttentionVarlen
+    torch.manual_seed(4)
+    heads, dh = 2, 64
+    d = heads * dh
+    lens = torch.tensor([5, 50, 17, 33, 1, 64, 16, 0, 40])
+    n_tok, cap = int(lens.sum()), int(lens.sum()) + 1500
+    offsets = torch.zeros(len(lens) + 1, dtype=torch.int32, device="cuda")
+    offsets[1:] = torch.cumsum(lens, 0).int().cuda()
+    qkv = torch.randn(cap, 3 * d, device="cuda")
+    for _ in range(2):
+        junk = torch.full((cap, 3 * d), float("nan"), device="cuda")  # freed: reused below
+        del junk
+        q = qkv.clone().requires_grad_(True)
+        out = _CausalAttentionVarlen.apply(q, offsets, heads, None, True)
+        go = torch.randn_like(out)
+        go[n_tok:] = 0
+        g, = torch.autograd.grad(out, q, go)
+        assert torch.isfinite(out).all() and float(out[n_tok:].abs().max()) == 0.0
+        assert torch.isfinite(g).all() and float(g[n_tok:].abs().max()) == 0.0
+
+
 def test_sasrec_packed_path_equals_padded():
     """The training path (packed sequences) gives the padded path's user
     embeddings and parameter gradients (dropout off)."""

@@ -61,7 +61,7 @@ def main():
             delta = torch.empty_like(lse)
             order = torch.empty(5 * B + 1, dtype=torch.int32, device="cuda")
             chk(lib.mirec_attention_length_order(offs.data_ptr(), B, order.data_ptr(),
-                                                 order[B:].data_ptr(), st), "ord")
+                                                 order[B:].data_ptr(), None, 0, 0, st), "ord")
             op = order.data_ptr() if a.order else None
             t2 = float((lens.double() ** 2).sum())
             by_f = 4.0 * n * 4 * d
@@ -87,7 +87,7 @@ def main():
                     dqkv.data_ptr(), st), "blko_bwd"),
                 "packed_bwd": lambda: chk(lib.mirec_attention_packed_bwd(
                     qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(), order[B:].data_ptr(), B, H,
-                    dh, dqkv.data_ptr(), st), "packed_bwd"),
+                    dh, dqkv.data_ptr(), n, st), "packed_bwd"),
             }
             for name, fn in runs.items():
                 if name == "wave_bwd":
