@@ -377,9 +377,13 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
                                                            int32_t *__restrict__ packs,
                                                            float *__restrict__ zero_buf,
                                                            int64_t zero_rows, int32_t zero_w4) {
-  if (zero_buf != nullptr) {  // capacity padding rows of the output
+  if (blockIdx.x > 0) {  // workgroups 1..: the capacity padding rows of the output
     const int64_t e0 = (int64_t)offsets[batch] * zero_w4, e1 = zero_rows * zero_w4;
-    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) st4(zero_buf + 4 * e, f4_zero());
+    const int64_t stride = (int64_t)(gridDim.x - 1) * blockDim.x;
+    for (int64_t e = e0 + (int64_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; e < e1;
+         e += stride)
+      st4(zero_buf + 4 * e, f4_zero());
+    return;
   }
   __shared__ int cnt[kMaxT + 1], start[kMaxT + 1];
   __shared__ int cls_start[5], cls_count[5], pack_base[5];
@@ -489,7 +493,8 @@ extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batc
     return MIREC_OK;
   }
   MIREC_CHECK_ARG(offsets && order);
-  hipLaunchKernelGGL(length_order_kernel, dim3(1), dim3(1024), 0,
+  // workgroup 0 orders and packs; with zero_buf, 32 more zero the padding
+  hipLaunchKernelGGL(length_order_kernel, dim3(zero_buf != nullptr ? 33 : 1), dim3(1024), 0,
                      reinterpret_cast<hipStream_t>(stream), offsets, batch, order, packs,
                      zero_buf, zero_rows, zero_width / 4);
   MIREC_LAUNCH_CHECK();

@@ -187,6 +187,53 @@ def sage_linear(xs: torch.Tensor, xn: torch.Tensor, w: torch.Tensor,
     return y.relu() if relu else y
 
 
+class _LinearReLU(torch.autograd.Function):
+    """relu(x Wᵀ + b) with the bias and ReLU in the GEMM epilogue
+    (mirec_gemm_nt_ex); backward: the ReLU mask applied to dY as it is loaded
+    by dX = dY' W (mirec_gemm_nn_ex) and by dW = dY'ᵀ x, db = Σ dY'
+    (mirec_gemm_tn_ex) — no elementwise kernels either way."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        n, k = x.shape
+        no = w.shape[0]
+        y = torch.empty(n, no, dtype=x.dtype, device=x.device)
+        check(lib.mirec_gemm_nt_ex(x.data_ptr(), None, 0, None, w.data_ptr(), _lib.ptr(b),
+                                   y.data_ptr(), None, 0, 1, n, k, no, _lib.stream_handle()),
+              "gemm_nt_ex(relu)")
+        ctx.save_for_backward(x, w, y)
+        ctx.has_bias = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        n, k = x.shape
+        no = w.shape[0]
+        dy = dy.contiguous()
+        st = _lib.stream_handle()
+        dx = torch.empty_like(x)
+        check(lib.mirec_gemm_nn_ex(dy.data_ptr(), y.data_ptr(), w.data_ptr(), dx.data_ptr(), None,
+                                   0, n, no, k, st), "gemm_nn_ex(relu dX)")
+        dw = torch.empty_like(w)
+        db = torch.empty(no, dtype=w.dtype, device=w.device) if ctx.has_bias else None
+        work = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, no, k)), dtype=w.dtype,
+                           device=w.device)
+        check(lib.mirec_gemm_tn_ex(dy.data_ptr(), y.data_ptr(), x.data_ptr(), None, 0,
+                                   dw.data_ptr(), _lib.ptr(db), n, no, k, work.data_ptr(), st),
+              "gemm_tn_ex(relu dW)")
+        return dx, dw, db
+
+
+def linear_relu(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """relu(F.linear(x, w, b)) — fused on the mirec GEMMs when the shapes are
+    theirs (2-D aligned contiguous x, in and out widths multiples of 128)."""
+    if (USE_MIREC_GEMM and x.dim() == 2 and x.shape[1] % 128 == 0 and w.shape[0] % 128 == 0
+            and _aligned(x, w) and (b is None or _aligned(b))):
+        return _LinearReLU.apply(x, w, b)
+    return _LinearSplitK.apply(x, w, b).relu()
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     return _LinearSplitK.apply(x, w, b)
 

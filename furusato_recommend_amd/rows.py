@@ -80,12 +80,13 @@ class _GatherRowsNorm(torch.autograd.Function):
     the rows with float atomics."""
 
     @staticmethod
-    def forward(ctx, table, ids, split: int, sink):
+    def forward(ctx, table, ids, split: int, sink, norm_in):
         n, d = ids.numel(), table.shape[1]
         out = torch.empty(n, d, dtype=table.dtype, device=table.device)
         check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
                                     _lib.stream_handle()), "gather_rows")
-        norm = slice_norms(table, table.shape[0])[0]
+        # the table's norm: given (kept from the last fused Adam) or one pass
+        norm = slice_norms(table, table.shape[0])[0] if norm_in is None else norm_in.view(())
         ctx.save_for_backward(table, ids, norm)
         ctx.split, ctx.sink = split, sink
         ctx.set_materialize_grads(False)
@@ -108,7 +109,7 @@ class _GatherRowsNorm(torch.autograd.Function):
                 sink.accumulate([(i, g, 1, 0, 0.0, 0) for i, g in parts])
             else:
                 sink.skip()
-            return (sink.materialize(table) if sink.dense else None), None, None, None
+            return (sink.materialize(table) if sink.dense else None), None, None, None, None
         if g_norm is None:
             g = torch.zeros_like(table)
         else:
@@ -118,21 +119,23 @@ class _GatherRowsNorm(torch.autograd.Function):
             check(lib.mirec_scatter_add_rows(gr.data_ptr(), i.data_ptr(), i.numel(),
                                              table.shape[1], g.data_ptr(), st),
                   "scatter_add_rows")
-        return g, None, None, None
+        return g, None, None, None, None
 
 
 def gather_rows_norm(table: torch.Tensor, ids: torch.Tensor, split: int | None = None,
-                     sink=None):
+                     sink=None, norm: torch.Tensor | None = None):
     """(gather_rows(table, ids), table.norm(2)) with one fused backward; with
     ``split`` the rows come back as the two groups ids[:split], ids[split:]
-    ((rows_a, rows_b, norm)); ``sink``: see _GatherRowsNorm."""
+    ((rows_a, rows_b, norm)); ``sink``: see _GatherRowsNorm; ``norm``: the
+    table's norm when the caller already holds it (a 1-element device
+    tensor, read when the kernels run)."""
     if table.dtype != torch.float32 or table.dim() != 2 or table.shape[1] % 4:
         raise ValueError("gather_rows_norm: float32 [n, d] table with d % 4 == 0")
     flat = ids.reshape(-1).to(torch.int32).contiguous()
     k = flat.numel() if split is None else int(split)
     if not 0 <= k <= flat.numel():
         raise ValueError("gather_rows_norm: split outside the ids")
-    a, b, norm = _GatherRowsNorm.apply(table.contiguous(), flat, k, sink)
+    a, b, norm = _GatherRowsNorm.apply(table.contiguous(), flat, k, sink, norm)
     if split is None:
         return a.view(*ids.shape, table.shape[1]), norm
     return a, b, norm

@@ -30,7 +30,7 @@ import torch.nn.functional as F
 from . import _lib
 from ._lib import check, lib
 from .engine import AdamGroup, AdamState, _note_raw_write
-from .linear import Linear, blas_backend, linear
+from .linear import Linear, blas_backend, linear, linear_relu
 from .rows import gather_rows, gather_rows_norm
 
 
@@ -258,23 +258,28 @@ class _BPRRowsLoss(torch.autograd.Function):
     'emb' parameter: the doubling accumulation leaves the norm itself)."""
 
     @staticmethod
-    def forward(ctx, u, pe, ne, extra, coef: float):
-        u, pe, ne = u.contiguous(), pe.contiguous(), ne.contiguous()
+    def forward(ctx, u, pn, extra, coef: float):
+        """pn = [pe ; ne] ([2B, d]): one input, so its gradient is one tensor
+        (no concatenation of the two halves' gradients in the backward)."""
+        u, pn = u.contiguous(), pn.contiguous()
         B, d = u.shape
+        pe, ne = pn[:B], pn[B:]
         x = torch.empty(2 * B, dtype=u.dtype, device=u.device)  # x, then scratch
         loss = torch.empty((), dtype=u.dtype, device=u.device)
         check(lib.mirec_bpr_rows_loss(u.data_ptr(), pe.data_ptr(), ne.data_ptr(), B, d,
                                       extra.data_ptr(), float(coef), x.data_ptr(),
                                       loss.data_ptr(), _lib.stream_handle()), "bpr_rows_loss")
-        ctx.save_for_backward(u, pe, ne, x)
+        ctx.save_for_backward(u, pn, x)
         ctx.coef = float(coef)
         return loss
 
     @staticmethod
     def backward(ctx, g):
-        u, pe, ne, x = ctx.saved_tensors
+        u, pn, x = ctx.saved_tensors
         B, d = u.shape
-        du, dpe, dne = torch.empty_like(u), torch.empty_like(pe), torch.empty_like(ne)
+        pe, ne = pn[:B], pn[B:]
+        du, dpn = torch.empty_like(u), torch.empty_like(pn)
+        dpe, dne = dpn[:B], dpn[B:]
         g_extra = torch.empty((), dtype=u.dtype, device=u.device)
         g = g.contiguous()
         check(lib.mirec_bpr_rows_loss_bwd(u.data_ptr(), pe.data_ptr(), ne.data_ptr(),
@@ -282,7 +287,7 @@ class _BPRRowsLoss(torch.autograd.Function):
                                           du.data_ptr(), dpe.data_ptr(), dne.data_ptr(),
                                           g_extra.data_ptr(), _lib.stream_handle()),
               "bpr_rows_loss_bwd")
-        return du, dpe, dne, g_extra, None
+        return du, dpn, g_extra, None
 
 
 class _SegmentMean(torch.autograd.Function):
@@ -333,7 +338,8 @@ class _ResNorm(torch.autograd.Function):
     beta, eps) of an nn.LayerNorm."""
 
     @staticmethod
-    def forward(ctx, res, z, bias, gamma, beta, relu: bool, p: float, eps: float, norm: bool):
+    def forward(ctx, res, z, bias, gamma, beta, relu: bool, p: float, eps: float, norm: bool,
+                keep_out: bool = False):
         n, d = z.shape
         pure = res is None and bias is None and not relu and p == 0
         seed = _dropout_seed(p)
@@ -353,6 +359,10 @@ class _ResNorm(torch.autograd.Function):
         ctx.cfg = (relu, float(p), seed, res is not None, bias is not None, norm)
         ctx.seed_base = base
         ctx.set_materialize_grads(False)
+        if pure and keep_out:
+            # out = z, as a view: a later use of it (a residual) sends its
+            # gradient back as g_out, added inside the backward kernel
+            out = z.view_as(z)
         return out, y
 
     @staticmethod
@@ -386,13 +396,16 @@ class _ResNorm(torch.autograd.Function):
         if norm and g_y is None:  # y unused downstream: no LayerNorm gradients
             d_gamma = torch.zeros_like(gamma) if need[3] and gamma is not None else None
             d_beta = torch.zeros(d, dtype=out.dtype, device=out.device) if need[4] else None
-        return d_res, d_z, d_bias, d_gamma, d_beta, None, None, None, None
+        return d_res, d_z, d_bias, d_gamma, d_beta, None, None, None, None, None
 
 
 def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
-            p: float = 0.0):
+            p: float = 0.0, keep_out: bool = False):
     """(out, y) of _ResNorm for rows of width d = z.shape[-1] (any leading
-    shape); ``norm`` an nn.LayerNorm over d or None."""
+    shape); ``norm`` an nn.LayerNorm over d or None.  ``keep_out``: in the
+    pure-LayerNorm form return out (= z) too, so that z's other use (the
+    block's residual) is taken from it and its gradient joins this node's
+    backward (no separate gradient accumulation)."""
     shape = z.shape
     d = shape[-1]
     if d % 4 or not 4 <= d <= 1024:
@@ -404,7 +417,7 @@ def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = Fa
     else:
         gamma = beta = None
         eps = 0.0
-    out, y = _ResNorm.apply(r2, z2, bias, gamma, beta, relu, p, eps, norm is not None)
+    out, y = _ResNorm.apply(r2, z2, bias, gamma, beta, relu, p, eps, norm is not None, keep_out)
     return (None if out is None else out.view(shape)), (None if y is None else y.view(shape))
 
 
@@ -512,6 +525,11 @@ class SASRec(nn.Module):
         if config.get("table_grad", "sorted") == "sorted":
             from .graphsage import TableGrad
             self._tg = TableGrad(self.m_item, 0, d, dev)
+        # the table's norm after the last fused Adam ([1] of the kernel's two
+        # slice norms; the one-slice table is slice 1) and the table state it
+        # belongs to: the next forward reads it instead of a pass over the table
+        self._norm_buf = torch.zeros(2, device=dev)
+        self._norm_tok = None
 
     # ------------------------------------------------------------- blocks
     def oneblock(self, x, layer, offsets=None):
@@ -537,8 +555,9 @@ class SASRec(nn.Module):
                 x = self.oneblock(x, i, offsets)
             return x
         p = self.dropout.p if self.training else 0.0
-        _, y = resnorm(None, x, norm=self.attn_norm_layers[0])
-        res = x
+        # the first residual is taken from the LayerNorm node (keep_out): its
+        # gradient and the LayerNorm's meet inside one backward kernel
+        res, y = resnorm(None, x, norm=self.attn_norm_layers[0], keep_out=True)
         L = self.num_layers
         for i in range(L):
             attn = self.attn_layers[i]
@@ -638,7 +657,7 @@ class SASRec(nn.Module):
     def forward_item(self, x):
         """sasrec.py:415-421."""
         for lin in self.item_linears:
-            x = lin(x).relu()
+            x = linear_relu(x, lin.weight, lin.bias)
         return self.item_last_proj(x)
 
     def sequence_input(self, users):
@@ -716,12 +735,29 @@ class SASRec(nn.Module):
                 self.optims.step()
             else:
                 self.optims.step_device(h_dev)
+            self._norm_tok = None
             return
         if h_dev is None:
             self._rest_optims.step()
         else:
             self._rest_optims.step_device(h_dev)
-        tg.adam(self._table_state, h_dev=h_dev)
+        tg.adam(self._table_state, norms=self._norm_buf, h_dev=h_dev)
+        self._norm_tok = self._norm_token()
+
+    def _norm_token(self):
+        from . import engine as _engine
+        return (self.item_id_embedding.weight._version, _engine._raw_writes)
+
+    def _norm_valid(self) -> bool:
+        return self._norm_tok is not None and self._norm_tok == self._norm_token()
+
+    @torch.no_grad()
+    def _refresh_norm(self):
+        """_norm_buf[1] = the table's current norm (before a replay whose
+        forward reads it, when the table changed outside the fused Adam)."""
+        from .rows import slice_norms2
+        self._norm_buf.copy_(slice_norms2(self.item_id_embedding.weight.detach(), 0))
+        self._norm_tok = self._norm_token()
 
     def _step_body(self, ids, packing, seg, length, pos, neg, loss_scale=1.0, n_tok=None):
         """Forward, loss and backward of one packed batch; returns the loss.
@@ -738,11 +774,15 @@ class SASRec(nn.Module):
         # same node (one table gradient, written once), and the BPR score /
         # softplus / mean / norm term are one kernel each way.
         x, pn, wnorm = gather_rows_norm(self.item_id_embedding.weight, ids, split=n_tok,
-                                        sink=self._tg)
+                                        sink=self._tg,
+                                        norm=self._norm_buf[1:] if self._norm_valid() else None)
         u = self.forward_user_packed(x, packing, seg, length)
-        pe, ne = self.forward_item(pn).split(B)
-        loss = _BPRRowsLoss.apply(u, pe, ne, wnorm, self.config["decay"] / B)
-        (loss * loss_scale if loss_scale != 1.0 else loss).backward()
+        loss = _BPRRowsLoss.apply(u, self.forward_item(pn), wnorm, self.config["decay"] / B)
+        # the backward seed from a kept tensor (no fill kernel per step)
+        seed = self.__dict__.get("_loss_seed")
+        if seed is None or seed.device != loss.device:
+            seed = self._loss_seed = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(seed if loss_scale == 1.0 else seed * loss_scale)
         return loss
 
     # ------------------------------------------------------- graph capture
@@ -860,6 +900,9 @@ class _CapturedStep:
                 torch.cuda.current_stream().wait_stream(side)
                 for p in params:
                     p.grad = None
+                # the captured forward reads the kept table norm iff it is
+                # valid now (the warm-up's fused Adam wrote it)
+                self.norm_from_buf = model._norm_valid()
                 with torch.cuda.graph(self.graph, pool=pool):
                     self.loss = self._body()
         finally:
@@ -904,6 +947,11 @@ class _CapturedStep:
         for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
             if dv:  # device ids: copied after the staging copy (stream order)
                 self.inbuf[(j + 1) * B:(j + 2) * B].copy_(t)
+        m = self.m
+        if self.norm_from_buf and not m._norm_valid():
+            m._refresh_norm()  # the table changed outside the step
         _note_raw_write()
         self.graph.replay()
+        if m._tg is not None:  # the replayed fused Adam wrote the next norm
+            m._norm_tok = m._norm_token()
         return self.loss.clone()
