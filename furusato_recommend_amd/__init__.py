@@ -11,6 +11,7 @@ from .dataloader import FiveCore, Loader, SyntheticBipartite  # noqa: F401
 from .graph import Graph  # noqa: F401
 from .graphsage import GraphSAGE  # noqa: F401
 from .lgconv import LGConv  # noqa: F401
+from . import ops  # noqa: F401  (registers torch.ops.mirec.*)
 from .lightgcn import LightGCN  # noqa: F401
 from .mf import MF  # noqa: F401
 from .sasrec import SASRec  # noqa: F401

@@ -467,6 +467,79 @@ extern "C" int mirec_table_grad_workspace(const mirec_row_grad_group_t *groups, 
   return MIREC_OK;
 }
 
+// Atomic form (plain groups: k = 1, no mean, no dropout): pass 1 stamps every
+// touched row with gen and zeroes its acc row (idempotent, so repeated ids
+// are harmless), pass 2 adds every entry's gradient row with float atomics.
+// Two short launches instead of the sort; the summation order of a repeated
+// id is not fixed (reruns can differ in the last bits).
+__global__ __launch_bounds__(256) void tg_claim_kernel(GroupArgs ga, int64_t n_ent, int32_t d4,
+                                                       int32_t n_rows, float *__restrict__ acc,
+                                                       int32_t *__restrict__ stamp, int32_t gen) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ent * d4) return;
+  const int64_t e = i / d4;
+  const int c4 = (int)(i - e * d4);
+  const int g = group_of(ga.ent_off, ga.n_groups, e);
+  const int32_t id = pick(ga.ids, g)[e - pick(ga.ent_off, g)];
+  if (id < 0 || id >= n_rows) return;
+  if (c4 == 0) stamp[id] = gen;
+  st4(acc + (int64_t)id * 4 * d4 + 4 * c4, f4_zero());
+}
+
+__global__ __launch_bounds__(256) void tg_atomic_add_kernel(GroupArgs ga, int64_t n_ent, int32_t d4,
+                                                            int32_t n_rows,
+                                                            float *__restrict__ acc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_ent * d4) return;
+  const int64_t e = i / d4;
+  const int c4 = (int)(i - e * d4);
+  const int g = group_of(ga.ent_off, ga.n_groups, e);
+  const int64_t le = e - pick(ga.ent_off, g);
+  const int32_t id = pick(ga.ids, g)[le];
+  if (id < 0 || id >= n_rows) return;
+  const float4 v = ld4(pick(ga.grad, g) + le * 4 * d4 + 4 * c4);
+  float *dst = acc + (int64_t)id * 4 * d4 + 4 * c4;
+  atomicAdd(dst, v.x);
+  atomicAdd(dst + 1, v.y);
+  atomicAdd(dst + 2, v.z);
+  atomicAdd(dst + 3, v.w);
+}
+
+extern "C" int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                                       int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
+                                       int32_t gen, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(groups && n_groups >= 1 && n_groups <= kMaxGroups && n_rows >= 0 && dim > 0 &&
+                  dim % 4 == 0 && acc && stamp && (uintptr_t)acc % 16 == 0);
+  GroupArgs ga = {};
+  ga.n_groups = n_groups;
+  for (int g = 0; g < kMaxGroups; ++g) {
+    const bool real = g < n_groups;
+    const mirec_row_grad_group_t *q = real ? &groups[g] : nullptr;
+    if (real) {
+      MIREC_CHECK_ARG(q->n_targets >= 0 && q->k == 1 && q->mean == 0 && q->dropout_p == 0.f);
+      MIREC_CHECK_ARG(q->n_targets == 0 ||
+                      (q->ids && q->grad_out && (uintptr_t)q->grad_out % 16 == 0));
+    }
+    ga.ent_off[g + 1] = ga.ent_off[g] + (real ? q->n_targets : 0);
+    ga.tgt_off[g + 1] = ga.ent_off[g + 1];
+    ga.ids[g] = real ? q->ids : nullptr;
+    ga.grad[g] = real ? q->grad_out : nullptr;
+    ga.k[g] = 1;
+  }
+  const int64_t n_ent = ga.ent_off[kMaxGroups];
+  if (n_ent == 0) return MIREC_OK;
+  const int32_t d4 = dim / 4;
+  const int64_t total = n_ent * d4;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(tg_claim_kernel, grid, dim3(256), 0, st, ga, n_ent, d4, n_rows, acc, stamp,
+                     gen);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(tg_atomic_add_kernel, grid, dim3(256), 0, st, ga, n_ent, d4, n_rows, acc);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
 extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
                                        int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
                                        int32_t gen, void *workspace, size_t workspace_bytes,

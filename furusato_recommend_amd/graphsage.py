@@ -70,6 +70,9 @@ class TableGrad:
         # static: a HIP-graph-captured step bakes the generation into its
         # launches, so every step clears the stamps and reuses generation 1
         self.static = False
+        # atomic: S by float atomics (plain groups only; no sort, order of a
+        # repeated id's sum not fixed) instead of the sorted segmented sums
+        self.atomic = False
         self._ws = None
 
     def accumulate(self, groups):
@@ -85,6 +88,13 @@ class TableGrad:
             a.ids, a.grad_out = ids.data_ptr(), g.data_ptr()
             a.n_targets, a.k, a.mean = ids.numel() // k, int(k), int(mean)
             a.dropout_p, a.seed = float(p), int(seed)
+        if self.atomic:
+            self._next_gen()
+            check(lib.mirec_table_grad_atomic(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
+                                              self.stamp.data_ptr(), self.gen,
+                                              _lib.stream_handle()), "table_grad_atomic")
+            self.pending = True
+            return
         nb = ctypes.c_size_t()
         check(lib.mirec_table_grad_workspace(arr, n, self.n_rows, self.dim, ctypes.byref(nb)),
               "table_grad_workspace")

@@ -7,7 +7,9 @@ on any graph (not only the user–item bipartite one), with PyG's semantics:
 flow source_to_target, degree = in-degree at the target with multi-edges
 counted, isolated nodes give 0, ``normalize=False`` is the plain neighbour
 sum.  Differentiable: the backward x̄ = Âᵀ ȳ is the same HIP SpMM on the
-transposed CSR (the same CSR when the edge multiset is symmetric).
+transposed CSR (the same CSR when the edge multiset is symmetric).  The call
+goes through the registered operator ``torch.ops.mirec.lgcn_propagate``
+(ops.py).
 
 The CSR (and its transpose) is built once per ``edge_index`` and cached on
 the module, keyed by the tensor's storage, shape and version; ``x`` may
@@ -90,7 +92,8 @@ class LGConv(nn.Module):
         if x.dim() != 2 or x.dtype != torch.float32:
             raise ValueError("LGConv: x must be a float32 [N, D] tensor")
         g = self.graph_for(edge_index, x.shape[0], x.device)
-        return _LGConvFn.apply(x, g)
+        from .ops import handle  # torch.ops.mirec.lgcn_propagate (autograd registered)
+        return torch.ops.mirec.lgcn_propagate(x, handle(g))
 
     def __repr__(self) -> str:
         return f"LGConv(normalize={self.normalize})"

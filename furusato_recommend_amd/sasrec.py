@@ -522,9 +522,13 @@ class SASRec(nn.Module):
                                  if s.param is self.item_id_embedding.weight)
         self._rest_optims = AdamGroup(s for s in self.optims if s is not self._table_state)
         self._tg = None
-        if config.get("table_grad", "sorted") == "sorted":
+        mode = config.get("table_grad", "sorted")
+        if mode not in ("sorted", "atomic", "dense"):
+            raise ValueError(f"table_grad: sorted | atomic | dense, not {mode!r}")
+        if mode != "dense":
             from .graphsage import TableGrad
             self._tg = TableGrad(self.m_item, 0, d, dev)
+            self._tg.atomic = mode == "atomic"
         # the table's norm after the last fused Adam ([1] of the kernel's two
         # slice norms; the one-slice table is slice 1) and the table state it
         # belongs to: the next forward reads it instead of a pass over the table

@@ -490,6 +490,14 @@ int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_grou
                             int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
                             void *workspace, size_t workspace_bytes, mirec_stream_t stream);
 
+/* The same S in the atomic form, for plain groups only (k = 1, mean = 0,
+ * dropout_p = 0): touched rows stamped and zeroed, then every gradient row
+ * added with float atomics — two launches, no workspace; the summation
+ * order of a repeated id is not fixed. */
+int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                            int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
+                            mirec_stream_t stream);
+
 /* grad = G materialised (coef may be NULL = 0), [n_rows, dim]. */
 int mirec_table_grad_dense(const float *table, const float *coef, int64_t n_user,
                            const float *acc, const int32_t *stamp, int32_t gen, int64_t n_rows,

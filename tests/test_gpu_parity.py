@@ -1094,8 +1094,8 @@ def test_sasrec_stage_one_equals_unfused_composition():
         assert diff.numel() == 0 or float(diff.max()) < 1e-2 * cfg["lr"], name
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_sasrec_sorted_table_step_matches_dense(graph):
+@pytest.mark.parametrize("graph,mode", [(False, "sorted"), (True, "sorted"), (True, "atomic")])
+def test_sasrec_sorted_table_step_matches_dense(graph, mode):
     """The item table's sorted gradient + fused table Adam (TableGrad, the
     default) == the materialised gradient + dense Adam, over three steps,
     eager and captured: every parameter within 1e-2 lr of the dense run (the
@@ -1105,10 +1105,10 @@ def test_sasrec_sorted_table_step_matches_dense(graph):
     cfg = {"recdim": 64, "layer": 2, "heads": 2, "lr": 1e-3, "decay": 1e-4,
            "device": "cuda:0", "bpr_batch_size": 128, "dropout_p": 0.0, "graph": graph}
     torch.manual_seed(9)
-    a = SASRec(cfg, ds)
+    a = SASRec(dict(cfg, table_grad=mode), ds)
     torch.manual_seed(9)
     b = SASRec(dict(cfg, table_grad="dense"), ds)
-    assert a._tg is not None and b._tg is None
+    assert a._tg is not None and b._tg is None and a._tg.atomic == (mode == "atomic")
     rng = np.random.default_rng(2)
     live = {n: True for n, _ in b.named_parameters()}
 
@@ -2078,3 +2078,26 @@ def test_fanout_sampler_without_replacement():
         assert np.abs(obs - exp).max() < 6 * np.sqrt(exp.max()) + 3
         checked_long += 1
     assert checked_long > 5
+
+
+def test_torch_ops_lgcn_propagate_matches_module_and_autograd():
+    """torch.ops.mirec.lgcn_propagate == the engine's propagation and its
+    registered backward == Âᵀ ȳ (a non-symmetric edge list: the transposed
+    CSR), against a dense float64 reference."""
+    from furusato_recommend_amd import ops
+    from furusato_recommend_amd.graph import Graph
+    rng = np.random.default_rng(0)
+    n, nnz = 300, 2000
+    ei = rng.integers(0, n, (2, nnz))
+    g = Graph.from_edge_index(ei, n, "cuda")
+    x = torch.randn(n, 64, device="cuda", dtype=torch.float32, requires_grad=True)
+    y = torch.ops.mirec.lgcn_propagate(x, ops.handle(g))
+    deg = np.bincount(ei[1], minlength=n).astype(np.float64)
+    dinv = np.where(deg > 0, deg ** -0.5, 0.0)
+    A = np.zeros((n, n))
+    np.add.at(A, (ei[1], ei[0]), dinv[ei[1]] * dinv[ei[0]])
+    ref = A @ x.detach().double().cpu().numpy()
+    assert rel(y, torch.from_numpy(ref)) < 1e-5
+    gy = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    assert rel(gx, torch.from_numpy(A.T @ gy.double().cpu().numpy())) < 1e-5

@@ -450,3 +450,29 @@ def test_host_code_under_asan_ubsan(tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "host_check ok" in r.stdout
+
+
+def test_torch_ops_registration_and_fake_tracing():
+    """torch.ops.mirec.lgcn_propagate / _t are registered operators with
+    autograd and fake (meta) implementations: shape propagation under
+    FakeTensorMode runs no kernel (SURVEY §8b operator API)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    import furusato_recommend_amd  # noqa: F401  (registers the ops)
+    from furusato_recommend_amd import ops
+    assert hasattr(torch.ops.mirec, "lgcn_propagate") and hasattr(torch.ops.mirec, "lgcn_propagate_t")
+
+    class _G:
+        n_nodes, symmetric = 7, True
+    g = _G()
+    h = ops.handle(g)
+    assert ops.handle(g) == h
+    with FakeTensorMode():
+        x = torch.empty(7, 16)
+        y = torch.ops.mirec.lgcn_propagate(x, h)
+        yt = torch.ops.mirec.lgcn_propagate_t(x, h)
+    assert y.shape == (7, 16) and yt.shape == (7, 16)
+    import pytest
+    with pytest.raises(ValueError):
+        torch.ops.mirec.lgcn_propagate(torch.empty(7, 16), h)  # not on the HIP device

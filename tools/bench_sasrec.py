@@ -108,6 +108,9 @@ def main():
     ap.add_argument("--attn-impl", default="hybrid", choices=["hybrid", "wave", "block"],
                     help="attention core (sasrec.ATTN_IMPL): wave forward + workgroup "
                          "backward (default), one wave, or one workgroup per (sequence, head)")
+    ap.add_argument("--table-grad", default="sorted", choices=["sorted", "atomic", "dense"],
+                    help="item table gradient: sorted (deterministic) / atomic S + fused "
+                         "table Adam, or the materialised gradient + dense Adam")
     ap.add_argument("--fused-rows", type=int, default=1,
                     help="0: the torch composition of dropout / residual / LayerNorm (A/B)")
     args = ap.parse_args()
@@ -122,7 +125,8 @@ def main():
                 "decay": 1e-4, "device": "cuda:0", "bpr_batch_size": args.batch,
                 "dropout_p": 0.2, **({"blas": args.blas} if args.blas else {}),
                 "fused_rows": bool(args.fused_rows), "attn_buckets": bool(args.attn_buckets),
-                "graph": bool(args.graph)}, _DS(args.users, args.items),
+                "graph": bool(args.graph), "table_grad": args.table_grad},
+               _DS(args.users, args.items),
                sequences=seq)
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(7)
