@@ -230,6 +230,10 @@ SIGNATURES = {
                                   c_int64, c_int32, c_int32, c_float, c_uint64, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                   c_void_p]),
+    "mirec_score_topk_workspace": (c_int64, [c_int64, c_int64, c_int32]),
+    "mirec_score_topk": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int32, c_void_p,
+                                 c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p,
+                                 c_size_t, c_void_p]),
     "mirec_topk_masked": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_int64,
                                   c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_bpr_sample_capped_workspace": (c_int, [c_int64, c_int64, POINTER(c_size_t)]),

@@ -9,6 +9,9 @@
 // insert, taken only when a score beats the lane's current k-th); the 64
 // lane lists are then merged pairwise in LDS (6 rounds).  Order: score
 // descending, ties to the lower item id (deterministic).
+#include <algorithm>
+#include <climits>
+
 #include "common.h"
 
 namespace mirec {
@@ -134,6 +137,286 @@ __global__ __launch_bounds__(64) void topk_masked_kernel(
   }
 }
 
+// ------------------------------------------------------- streaming score top-k
+// SURVEY K8 without the [n_eval x M] rating matrix: scores U_b · Iᵀ are
+// produced tile by tile on MFMA (v_mfma_f32_32x32x2_f32) and filtered into
+// per-user candidate buffers as they are made; nothing of the score matrix
+// reaches HBM.
+//
+// Stage 1, workgroup (64 users, one chunk of the items), two waves of 32
+// users.  Lane (i, h) of a wave: user i, k-slice h of every MFMA; the user's
+// embedding stays in registers (the B operand, D/2 floats), item tiles of 32
+// rows stream through LDS (double-buffered, the A operand), so the
+// accumulator lane (i, h) holds 16 item scores of user i.  A score enters the
+// user's LDS candidate buffer (64 entries, LDS atomic slot) only if it beats
+// the user's current k-th best (kept per lane after each compaction); a
+// train positive scores -1024 (trainer.py:132-137), checked by binary search
+// in the user's sorted CSR row only for a score that would otherwise enter.
+// When a user's buffer could overflow on the next tile, the wave sorts it
+// (bitonic across the 64 lanes), keeps the best k and raises the threshold;
+// at the chunk's end every user's best k go to the partial list
+// [n_eval][n_chunks][k].  Expected insertions per user ~ k (1 + ln(M/k)).
+// Stage 2: one wave per user merges its n_chunks x k partial entries (as
+// mirec_topk_masked's lane lists).  Order: score descending, ties to the
+// lower item id — deterministic, independent of insertion order.
+constexpr int kStUsers = 64;  // users per workgroup (2 waves of 32)
+constexpr int kStCap = 64;    // candidate slots per user
+constexpr int kStTile = 32;   // items per MFMA tile
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Is item node `node` in user u's train row?  (sorted copy of the row when
+// the CSR carries one, else a scan)
+__device__ __forceinline__ bool user_has(const int64_t *__restrict__ rowptr,
+                                         const int32_t *__restrict__ col,
+                                         const int32_t *__restrict__ sorted, int64_t n_sorted,
+                                         int64_t u, int32_t node) {
+  const int64_t beg = rowptr[u], deg = rowptr[u + 1] - beg;
+  if (sorted != nullptr && u < n_sorted) {
+    const int32_t *a = sorted + (beg - rowptr[0]);
+    int64_t lo = 0, hi = deg;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (a[mid] < node) lo = mid + 1;
+      else hi = mid;
+    }
+    return lo < deg && a[lo] == node;
+  }
+  for (int64_t e = 0; e < deg; ++e)
+    if (col[beg + e] == node) return true;
+  return false;
+}
+
+// Bitonic sort of one (value, index) pair per lane over the wave, best first.
+__device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const float ov = __shfl_xor(v, stride);
+      const int oi = __shfl_xor(ix, stride);
+      const bool up = ((lane & size) == 0);    // this lane's block sorts best-first
+      const bool lower = (lane & stride) == 0;  // the lane keeps the better of the pair
+      const bool mine_better = better(v, ix, ov, oi);
+      const bool keep_mine = (lower == up) ? mine_better : !mine_better;
+      if (!keep_mine) {
+        v = ov;
+        ix = oi;
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(128) void score_topk_kernel(
+    const float *__restrict__ U, int64_t n_eval, const float *__restrict__ I, int64_t m_items,
+    const int32_t *__restrict__ users, const int64_t *__restrict__ rowptr,
+    const int32_t *__restrict__ col, const int32_t *__restrict__ sorted, int64_t n_sorted,
+    int64_t n_users, int k, int64_t chunk, float *__restrict__ part_val,
+    int32_t *__restrict__ part_idx) {
+  constexpr int LD = D + 4;
+  constexpr int KS = D / 2;  // MFMA steps (k = 2 s + h)
+  __shared__ __attribute__((aligned(16))) float sI[2][kStTile * LD];
+  __shared__ float cv[kStUsers][kStCap];
+  __shared__ int ci[kStUsers][kStCap];
+  __shared__ int cnt[kStUsers];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int ul = 32 * w + i;  // user slot in the workgroup
+  const int64_t ub = (int64_t)blockIdx.x * kStUsers + ul;
+  const bool uok = ub < n_eval;
+  const int64_t it0 = (int64_t)blockIdx.y * chunk;
+  const int64_t it1 = min(m_items, it0 + chunk);
+  // the user's embedding as the B operand: ue[s] = U[ub][2 s + h]
+  float ue[KS];
+#pragma unroll
+  for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
+  const int64_t uid = (uok && users != nullptr) ? (int64_t)users[ub] : -1;
+  if (t < kStUsers) cnt[t] = 0;
+  float thr = -INFINITY;  // the user's k-th best so far (after the last compaction)
+  int thr_i = INT_MAX;
+  // item tile loader: 32 rows x D floats, float4 per thread (D % 4 == 0)
+  constexpr int PER = (kStTile * D / 4 + 127) / 128;
+  auto load = [&](int64_t base, float4 (&r)[PER]) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 128 * q, row = e / (D / 4), c4 = e % (D / 4);
+      r[q] = (e < kStTile * D / 4 && base + row < it1) ? ld4(I + (base + row) * D + 4 * c4)
+                                                         : f4_zero();
+    }
+  };
+  auto stage = [&](int buf, const float4 (&r)[PER]) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int e = t + 128 * q, row = e / (D / 4), c4 = e % (D / 4);
+      if (e < kStTile * D / 4) st4(sI[buf] + row * LD + 4 * c4, r[q]);
+    }
+  };
+  // keep the best k of user slot `u` (one wave, lanes = entries)
+  auto compact = [&](int u) {
+    const int n = cnt[u];
+    float v = lane < n ? cv[u][lane] : -INFINITY;
+    int ix = lane < n ? ci[u][lane] : INT_MAX;
+    wave_sort_desc(v, ix);
+    if (lane < k) {
+      cv[u][lane] = v;
+      ci[u][lane] = ix;
+    }
+    const float kv = __shfl(v, k - 1);
+    const int ki = __shfl(ix, k - 1);
+    if (lane == 0) cnt[u] = min(n, k);
+    return make_float2(kv, __int_as_float(n >= k ? ki : INT_MAX));
+  };
+  float4 rg[PER];
+  int cur = 0;
+  if (it0 < it1) {
+    load(it0, rg);
+    stage(0, rg);
+  }
+  __syncthreads();
+  for (int64_t base = it0; base < it1; base += kStTile) {
+    const bool more = base + kStTile < it1;
+    if (more) load(base + kStTile, rg);  // in flight during the products
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const float *arow = sI[cur] + i * LD + h;
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);
+    // candidates: acc[r] = score of item base + (r & 3) + 8 (r >> 2) + 4 h for user i
+    if (uok) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t item = base + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (item >= it1) continue;
+        float sc = acc[r];
+        if (!better(fmaxf(sc, -1024.f), (int)item, thr, thr_i)) continue;
+        if (rowptr != nullptr && uid >= 0 &&
+            user_has(rowptr, col, sorted, n_sorted, uid, (int32_t)(n_users + item)))
+          sc = -1024.f;
+        if (!better(sc, (int)item, thr, thr_i)) continue;
+        const int slot = atomicAdd(&cnt[ul], 1);
+        cv[ul][slot] = sc;
+        ci[ul][slot] = (int)item;
+      }
+    }
+    __syncthreads();  // candidates of this tile in; sI[cur] reads done
+    // users whose buffer could overflow on the next tile (32 new at most)
+    unsigned long long need = __ballot(h == 0 && cnt[ul] > kStCap - kStTile);
+    while (need) {
+      const int j = __ffsll(need) - 1;
+      need &= need - 1;
+      const float2 th = compact(32 * w + j);
+      if (i == j) {
+        thr = th.x;
+        thr_i = __float_as_int(th.y);
+      }
+    }
+    if (more) stage(cur ^ 1, rg);
+    __syncthreads();
+    cur ^= 1;
+  }
+  // final: every user's best k of this chunk
+  const int64_t n_chunks = gridDim.y;
+  for (int j = 0; j < 32; ++j) {
+    const int u = 32 * w + j;
+    const int64_t b = (int64_t)blockIdx.x * kStUsers + u;
+    if (b >= n_eval) break;
+    const int n = cnt[u];
+    float v = lane < n ? cv[u][lane] : -INFINITY;
+    int ix = lane < n ? ci[u][lane] : INT_MAX;
+    wave_sort_desc(v, ix);
+    if (lane < k) {
+      part_val[(b * n_chunks + blockIdx.y) * k + lane] = v;
+      part_idx[(b * n_chunks + blockIdx.y) * k + lane] = ix;
+    }
+  }
+}
+
+// Stage 2: one wave per user over its n_chunks x k partial entries.
+template <int KMAX>
+__global__ __launch_bounds__(64) void topk_merge_kernel(const float *__restrict__ part_val,
+                                                        const int32_t *__restrict__ part_idx,
+                                                        int64_t n_eval, int64_t n_part, int k,
+                                                        int32_t *__restrict__ topk_idx,
+                                                        float *__restrict__ topk_val) {
+  __shared__ float s_val[64 * KMAX];
+  __shared__ int s_idx[64 * KMAX];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  float vals[KMAX];
+  int idxs[KMAX];
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) {
+    vals[q] = -INFINITY;
+    idxs[q] = INT_MAX;
+  }
+  float thr = -INFINITY;
+  int thr_i = INT_MAX;
+  for (int64_t e = lane; e < n_part; e += 64) {
+    const float x = part_val[b * n_part + e];
+    const int j = part_idx[b * n_part + e];
+    if (better(x, j, thr, thr_i)) insert_sorted<KMAX>(vals, idxs, k, x, j, thr, thr_i);
+  }
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) {
+    s_val[lane * KMAX + q] = vals[q];
+    s_idx[lane * KMAX + q] = idxs[q];
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int active = 32; active >= 1; active >>= 1) {
+    float ov[KMAX];
+    int oi[KMAX];
+    if (lane < active) {
+      const float *av = s_val + lane * KMAX, *bv = s_val + (lane + active) * KMAX;
+      const int *ai = s_idx + lane * KMAX, *bi = s_idx + (lane + active) * KMAX;
+      int pa = 0, pb = 0;
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) {
+        if (q < k) {
+          const bool ta = better(av[pa], ai[pa], bv[pb], bi[pb]);
+          ov[q] = ta ? av[pa] : bv[pb];
+          oi[q] = ta ? ai[pa] : bi[pb];
+          pa += ta ? 1 : 0;
+          pb += ta ? 0 : 1;
+        }
+      }
+    }
+    __syncthreads();
+    if (lane < active) {
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q)
+        if (q < k) {
+          s_val[lane * KMAX + q] = ov[q];
+          s_idx[lane * KMAX + q] = oi[q];
+        }
+    }
+    __syncthreads();
+  }
+  for (int q = lane; q < k; q += 64) {
+    topk_idx[b * k + q] = s_idx[q];
+    if (topk_val != nullptr) topk_val[b * k + q] = s_val[q];
+  }
+}
+
+// chunk of items per stage-1 workgroup: enough workgroups for the chip
+// (>= 1024), at least 32 tiles each
+static void st_chunks(int64_t n_eval, int64_t m_items, int64_t *chunk, int64_t *n_chunks) {
+  const int64_t ut = (n_eval + kStUsers - 1) / kStUsers;
+  int64_t want = std::max<int64_t>(1, (1024 + ut - 1) / ut);
+  int64_t c = (m_items + want - 1) / want;
+  c = std::max<int64_t>(c, 32 * kStTile);
+  c = (c + kStTile - 1) / kStTile * kStTile;
+  *chunk = c;
+  *n_chunks = (m_items + c - 1) / c;
+}
+
 }  // namespace mirec
 
 extern "C" int mirec_topk_masked(float *scores, int64_t n_eval, int64_t m_items,
@@ -151,6 +434,59 @@ extern "C" int mirec_topk_masked(float *scores, int64_t n_eval, int64_t m_items,
   // (a KMAX=32 instantiation spills on ROCm 7.2; 64 fits in 145 VGPRs)
   hipLaunchKernelGGL((topk_masked_kernel<64>), dim3(n_eval), dim3(64), 0, st, scores, n_eval,
                      m_items, users, rp, cl, n_users, (int)k, topk_idx, topk_val);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int64_t mirec_score_topk_workspace(int64_t n_eval, int64_t m_items, int32_t k) {
+  using namespace mirec;
+  if (n_eval < 0 || m_items <= 0 || k < 1 || k > 32) return -1;
+  int64_t chunk, n_chunks;
+  st_chunks(std::max<int64_t>(n_eval, 1), m_items, &chunk, &n_chunks);
+  return n_eval * n_chunks * k * (int64_t)(sizeof(float) + sizeof(int32_t));
+}
+
+extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const float *item_emb,
+                                int64_t m_items, int32_t dim, const int32_t *users,
+                                const mirec_csr_t *csr, int64_t n_users, int32_t k,
+                                int32_t *topk_idx, float *topk_val, void *workspace,
+                                size_t workspace_bytes, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(n_eval >= 0 && m_items > 0 && m_items < INT32_MAX && k >= 1 && k <= 32 &&
+                  k <= m_items);
+  MIREC_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128);
+  MIREC_CHECK_ARG(csr == nullptr || (users && csr->rowptr && csr->col));
+  if (n_eval == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(user_emb && item_emb && topk_idx && workspace);
+  MIREC_CHECK_ARG(((uintptr_t)user_emb | (uintptr_t)item_emb) % 16 == 0);
+  const int64_t need = mirec_score_topk_workspace(n_eval, m_items, k);
+  if ((int64_t)workspace_bytes < need) return MIREC_ERR_WORKSPACE;
+  int64_t chunk, n_chunks;
+  st_chunks(n_eval, m_items, &chunk, &n_chunks);
+  float *pv = static_cast<float *>(workspace);
+  int32_t *pi = reinterpret_cast<int32_t *>(pv + n_eval * n_chunks * k);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t *rp = csr ? csr->rowptr : nullptr;
+  const int32_t *cl = csr ? csr->col : nullptr;
+  const int32_t *so = csr ? csr->col_sorted : nullptr;
+  const int64_t ns = csr ? csr->n_sorted : 0;
+  const dim3 grid((unsigned)((n_eval + kStUsers - 1) / kStUsers), (unsigned)n_chunks);
+#define MIREC_ST_CASE(DD)                                                                    \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(score_topk_kernel<DD>, grid, dim3(128), 0, st, user_emb, n_eval,      \
+                       item_emb, m_items, users, rp, cl, so, ns, n_users, (int)k, chunk, pv, \
+                       pi);                                                                  \
+    break;
+  switch (dim) {
+    MIREC_ST_CASE(16)
+    MIREC_ST_CASE(32)
+    MIREC_ST_CASE(64)
+    MIREC_ST_CASE(128)
+  }
+#undef MIREC_ST_CASE
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL((topk_merge_kernel<64>), dim3((unsigned)n_eval), dim3(64), 0, st, pv, pi,
+                     n_eval, n_chunks * k, (int)k, topk_idx, topk_val);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -2,12 +2,14 @@
 
 The layer-mean embeddings are propagated ONCE per evaluation with the HIP
 engine (the reference re-propagates per 10 000-user batch through
-getUsersRating, model/lgcn.py:120-125).  Per batch of users:
-rating = U_b · Iᵀ (library GEMM, hipBLASLt via torch.matmul, as the
-reference's torch.matmul), then one HIP launch (mirec_topk_masked) sets the
-user's train positives to -1024 in place (trainer.py:132-137) and selects the
-top-k (trainer.py:138); metric sums on the host with the reference formulas
-(metric.py:60-103).
+getUsersRating, model/lgcn.py:120-125).  Per batch of users, for a model
+with ``eval_embeddings`` (LightGCN) and k <= 32: mirec_score_topk streams
+the scores U_b · Iᵀ through MFMA tiles straight into per-user top-k
+candidates, the train positives at -1024 (trainer.py:132-138) — the
+[batch, M] rating matrix is never written.  Otherwise (MF's sigmoid
+ratings, k > 32): rating = U_b · Iᵀ (library GEMM, as the reference's
+torch.matmul), then mirec_topk_masked masks in place and selects.  Metric
+sums on the host with the reference formulas (metric.py:60-103).
 """
 from __future__ import annotations
 
@@ -36,20 +38,52 @@ def topk_masked(rating: torch.Tensor, users: torch.Tensor, graph, k: int,
     return val, idx
 
 
+STREAM_DIMS = (16, 32, 64, 128)
+STREAM_MAX_K = 32
+
+
+@torch.no_grad()
+def score_topk(user_rows: torch.Tensor, items: torch.Tensor, users: torch.Tensor, graph,
+               k: int, mask: bool = True):
+    """Top-k of user_rows · itemsᵀ per row with the users' train positives
+    at -1024, streamed (mirec_score_topk): (values, item ids) [n, k]."""
+    n, d = user_rows.shape
+    user_rows, items = user_rows.contiguous(), items.contiguous()
+    users = users.to(torch.int32).contiguous()
+    idx = torch.empty(n, k, dtype=torch.int32, device=user_rows.device)
+    val = torch.empty(n, k, dtype=torch.float32, device=user_rows.device)
+    ws = torch.empty(max(int(lib.mirec_score_topk_workspace(n, items.shape[0], k)), 1),
+                     dtype=torch.uint8, device=user_rows.device)
+    check(lib.mirec_score_topk(user_rows.data_ptr(), n, items.data_ptr(), items.shape[0], d,
+                               users.data_ptr(), graph.csr_ptr() if mask else None,
+                               graph.n_users, int(k), idx.data_ptr(), val.data_ptr(),
+                               ws.data_ptr(), ws.numel(), _lib.stream_handle()), "score_topk")
+    return val, idx
+
+
 @torch.no_grad()
 def evaluate(model, test_dict: dict, topks=(10, 20), batch: int = 10000,
-             return_topk: bool = False):
+             return_topk: bool = False, stream: bool | None = None):
     users = np.array(sorted(test_dict.keys()), dtype=np.int64)
     res = {m: np.zeros(len(topks)) for m in ("precision", "recall", "ndcg", "hr")}
     if users.size == 0:
         return res
-    ratings = model.eval_ratings()   # propagates once, returns users -> rating rows
     kmax = max(topks)
+    emb = None
+    if stream is not False and hasattr(model, "eval_embeddings") and kmax <= STREAM_MAX_K:
+        emb = model.eval_embeddings()   # propagates once
+        if emb[0].shape[1] not in STREAM_DIMS:
+            emb = None
+    if emb is None:
+        ratings = model.eval_ratings()   # propagates once, returns users -> rating rows
     tops = []
     for i in range(0, len(users), batch):
         bu = torch.from_numpy(users[i:i + batch]).to(model.device)
-        rating = ratings(bu).contiguous()
-        _, top = topk_masked(rating, bu, model.graph, kmax)
+        if emb is not None:
+            _, top = score_topk(emb[0][bu], emb[1], bu, model.graph, kmax)
+        else:
+            rating = ratings(bu).contiguous()
+            _, top = topk_masked(rating, bu, model.graph, kmax)
         top = top.cpu().numpy()
         if return_topk:
             tops.append(top)

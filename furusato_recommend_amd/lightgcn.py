@@ -129,6 +129,12 @@ class LightGCN(nn.Module):
         items = out[self.num_users:]
         return lambda users: out[users.long()] @ items.t()
 
+    def eval_embeddings(self):
+        """(user rows [n_users, D], item rows [m_items, D]) of one propagation:
+        the operands of the streaming evaluation (evaluate.score_topk)."""
+        out = self.propagated()
+        return out[: self.num_users], out[self.num_users:]
+
     def _as_i32(self, t):
         if not torch.is_tensor(t):
             t = torch.as_tensor(t)

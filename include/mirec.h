@@ -773,6 +773,20 @@ int mirec_topk_masked(float *scores, int64_t n_eval, int64_t m_items,
                       int64_t n_users, int32_t k, int32_t *topk_idx,
                       float *topk_val, mirec_stream_t stream);
 
+/* Streaming evaluation: the top-k of user_emb[b] · item_embᵀ
+ * per evaluated user b, the user's train positives (csr row users[b],
+ * entries n_users + item) scoring -1024, WITHOUT materialising the
+ * [n_eval, m_items] scores: MFMA score tiles are filtered into per-user
+ * candidate lists as they are produced (two launches).  user_emb [n_eval,
+ * dim], item_emb [m_items, dim], dim in {16, 32, 64, 128}, 1 <= k <= 32;
+ * same order and ties as mirec_topk_masked.  workspace:
+ * mirec_score_topk_workspace bytes. */
+int64_t mirec_score_topk_workspace(int64_t n_eval, int64_t m_items, int32_t k);
+int mirec_score_topk(const float *user_emb, int64_t n_eval, const float *item_emb,
+                     int64_t m_items, int32_t dim, const int32_t *users, const mirec_csr_t *csr,
+                     int64_t n_users, int32_t k, int32_t *topk_idx, float *topk_val,
+                     void *workspace, size_t workspace_bytes, mirec_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

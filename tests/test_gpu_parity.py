@@ -451,6 +451,36 @@ def test_topk_masked_matches_torch():
         assert torch.equal(val, rv)
 
 
+@pytest.mark.parametrize("d", [16, 32, 64, 128])
+def test_score_topk_streaming_matches_exact_topk(d):
+    """mirec_score_topk (scores streamed through MFMA tiles into per-user
+    candidate lists, never materialised) == the exact masked top-k: integer
+    embeddings make every score exact in f32, so the order — score
+    descending, ties to the lower item id, train positives at -1024 — is
+    compared exactly, ties included, for k = 1, 20, 32, with ragged user and
+    item counts."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.evaluate import score_topk
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(2000, 1337, 30_000, seed=7, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    gen = torch.Generator().manual_seed(d)
+    users = torch.arange(3, 2000, 11)
+    U = torch.randint(-3, 4, (len(users), d), generator=gen).float()
+    I = torch.randint(-3, 4, (ds.m_items, d), generator=gen).float()
+    ref = (U.double() @ I.double().t()).numpy()
+    for r, u in enumerate(users.tolist()):
+        ref[r, ds.allPos[u]] = -1024.0
+    for k in (1, 20, 32):
+        val, idx = score_topk(U.cuda(), I.cuda(), users.cuda(), g, k)
+        val, idx = val.cpu().numpy(), idx.cpu().numpy()
+        items = np.arange(ds.m_items)
+        for r in range(len(users)):
+            order = np.lexsort((items, -ref[r]))[:k]
+            assert np.array_equal(idx[r], order), (k, r)
+            assert np.array_equal(val[r], ref[r, order].astype(np.float32)), (k, r)
+
+
 def test_evaluate_matches_oracle():
     """Recall/Precision/NDCG/HR@{10,20} of evaluate() == the oracle's
     restatement of Trainer.test on the same propagated embeddings."""

@@ -1,0 +1,68 @@
+"""Evaluation top-k on the C2 configuration (1 M users x 100 K items, d =
+64): streamed scores (mirec_score_topk: MFMA tiles filtered into per-user
+candidates, no rating matrix) vs the dense path (library GEMM writes the
+[batch, M] ratings, mirec_topk_masked reads them).  One JSON line per path:
+ms per batch of users, and whether the two agree.
+
+    python tools/eval_bench.py [--batch 10000] [--reps 5] [--k 20]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--users", type=int, default=1_000_000)
+    ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--edges", type=int, default=20_000_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=10_000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--k", type=int, default=20)
+    a = ap.parse_args()
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from furusato_recommend_amd.evaluate import score_topk, topk_masked
+    ds = SyntheticBipartite(a.users, a.items, a.edges, seed=0, test_frac=0)
+    torch.manual_seed(0)
+    m = LightGCN({"recdim": a.dim, "layer": 3, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+                  "bpr_batch_size": 2048}, ds)
+    U, I = m.eval_embeddings()
+    bu = torch.randperm(a.users, device="cuda")[: a.batch]
+
+    def stream():
+        return score_topk(U[bu], I, bu, m.graph, a.k)
+
+    def dense():
+        return topk_masked((U[bu] @ I.t()).contiguous(), bu, m.graph, a.k)
+
+    out = {}
+    for name, fn in (("stream", stream), ("dense", dense)):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(a.reps):
+            r = fn()
+        e.record()
+        torch.cuda.synchronize()
+        out[name] = r
+        ms = s.elapsed_time(e) / a.reps
+        flop = 2.0 * a.batch * a.items * a.dim
+        print(json.dumps({"path": name, "batch_users": a.batch, "items": a.items, "dim": a.dim,
+                          "k": a.k, "ms_per_batch": round(ms, 3),
+                          "tflops_scores": round(flop / ms / 1e9, 1),
+                          "rating_matrix_bytes": 0 if name == "stream" else 4 * a.batch * a.items}),
+              flush=True)
+    same = torch.equal(out["stream"][1], out["dense"][1])
+    vdiff = float((out["stream"][0] - out["dense"][0]).abs().max())
+    print(json.dumps({"agree_idx": same, "max_val_diff": vdiff}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
