@@ -128,6 +128,8 @@ SIGNATURES = {
                                      c_void_p]),
     "mirec_sample_fanout": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int32, c_uint64,
                                     c_uint64, c_void_p, c_void_p]),
+    "mirec_pack_seed_nodes": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p,
+                                      c_void_p]),
     "mirec_sample_fanout_norep": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int32, c_uint64,
                                           c_uint64, c_void_p, c_void_p]),
     "mirec_gather_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),

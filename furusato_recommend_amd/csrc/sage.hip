@@ -487,3 +487,29 @@ extern "C" int mirec_fanout_mean_gather_bwd(const float *grad_out, const int32_t
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
+
+// Seed node ids of a BPR batch for the GraphSAGE tree: out = [users ;
+// n_users + pos ; n_users + neg] (graphsage.py:326-337's user / item rows of
+// the one id table), one launch.
+__global__ __launch_bounds__(256) void pack_seed_nodes_kernel(const int32_t *__restrict__ users,
+                                                              const int32_t *__restrict__ pos,
+                                                              const int32_t *__restrict__ neg,
+                                                              int64_t B, int64_t n_users,
+                                                              int32_t *__restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 3 * B) return;
+  const int64_t part = i / B, j = i - part * B;
+  out[i] = part == 0 ? users[j] : (int32_t)(n_users + (part == 1 ? pos[j] : neg[j]));
+}
+
+extern "C" int mirec_pack_seed_nodes(const int32_t *users, const int32_t *pos, const int32_t *neg,
+                                     int64_t batch, int64_t n_users, int32_t *out,
+                                     mirec_stream_t stream) {
+  MIREC_CHECK_ARG(batch >= 0 && n_users >= 0 && n_users < INT32_MAX);
+  if (batch == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(users && pos && neg && out);
+  hipLaunchKernelGGL(pack_seed_nodes_kernel, dim3((unsigned)((3 * batch + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, users, pos, neg, batch, n_users, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

@@ -175,7 +175,7 @@ class _TableTerms(torch.autograd.Function):
     ``leaves`` = ((ids, k, dropout p, seed), ...)."""
 
     @staticmethod
-    def forward(ctx, table, ids, n_user: int, leaves, sink, norms):
+    def forward(ctx, table, ids, n_user: int, leaves, sink, norms, splits):
         n, d = ids.numel(), table.shape[1]
         st = _lib.stream_handle()
         rows = torch.empty(n, d, dtype=table.dtype, device=table.device)
@@ -189,17 +189,25 @@ class _TableTerms(torch.autograd.Function):
                                                float(p), ctypes.c_uint64(seed), out.data_ptr(),
                                                st), "fanout_mean_gather")
             aggrs.append(out)
-        # both slices' norms in one pass (or the previous step's fused Adam's)
-        norms2 = slice_norms2(table, n_user) if norms is None else norms.clone()
+        # both slices' norms in one pass (or the previous step's fused Adam's,
+        # read in place: the next Adam rewrites it only after this backward)
+        norms2 = slice_norms2(table, n_user) if norms is None else norms.view(2)
         ctx.save_for_backward(table, ids, norms2, *[l[0] for l in leaves])
         ctx.leaf_cfg = [(k, p, seed) for _, k, p, seed in leaves]
         ctx.n_user = n_user
         ctx.sink = sink
-        return (rows, norms2, *aggrs)
+        ctx.splits = tuple(int(x) for x in splits)
+        ctx.set_materialize_grads(False)
+        # the inner groups' rows as separate outputs: their gradients arrive
+        # separately (no concatenation) and become separate row groups
+        return (*rows.split(ctx.splits), norms2, *aggrs)
 
     @staticmethod
-    def backward(ctx, g_rows, g_norms, *g_aggrs):
+    def backward(ctx, *grads):
+        P = len(ctx.splits)
+        g_parts, g_norms, g_aggrs = grads[:P], grads[P], grads[P + 1:]
         table, ids, norms2, *leaf_ids = ctx.saved_tensors
+        id_parts = ids.split(ctx.splits)
         k = ctx.n_user
         d = table.shape[1]
         st = _lib.stream_handle()
@@ -211,9 +219,8 @@ class _TableTerms(torch.autograd.Function):
             else:
                 check(lib.mirec_norm_coef(g_norms.contiguous().data_ptr(), 1, norms2.data_ptr(), 1,
                                           2, sink.coef.data_ptr(), st), "norm_coef")
-            groups = []
-            if g_rows is not None:
-                groups.append((ids, g_rows, 1, 0, 0.0, 0))
+            groups = [(i, g, 1, 0, 0.0, 0) for i, g in zip(id_parts, g_parts)
+                      if g is not None and i.numel() > 0]
             for g, lid, (kk, p, seed) in zip(g_aggrs, leaf_ids, ctx.leaf_cfg):
                 if g is not None:
                     groups.append((lid, g, kk, 1, p, seed))
@@ -221,7 +228,8 @@ class _TableTerms(torch.autograd.Function):
                 sink.accumulate(groups)
             else:  # S = 0: a fresh generation stamps nothing
                 sink.skip()
-            return (sink.materialize(table) if sink.dense else None), None, None, None, None, None
+            return (sink.materialize(table) if sink.dense else None), None, None, None, None, None, \
+                None
         if g_norms is None:
             coef = torch.zeros_like(norms2)
         else:
@@ -230,10 +238,11 @@ class _TableTerms(torch.autograd.Function):
         grad = torch.empty_like(table)
         torch.mul(table[:k], cu, out=grad[:k])
         torch.mul(table[k:], ci, out=grad[k:])
-        if g_rows is not None:
-            check(lib.mirec_scatter_add_rows(g_rows.contiguous().data_ptr(), ids.data_ptr(),
-                                             ids.numel(), d, grad.data_ptr(), st),
-                  "scatter_add_rows")
+        for i, g in zip(id_parts, g_parts):
+            if g is not None and i.numel() > 0:
+                check(lib.mirec_scatter_add_rows(g.contiguous().data_ptr(), i.data_ptr(),
+                                                 i.numel(), d, grad.data_ptr(), st),
+                      "scatter_add_rows")
         for g, lid, (kk, p, seed) in zip(g_aggrs, leaf_ids, ctx.leaf_cfg):
             if g is None:
                 continue
@@ -242,7 +251,7 @@ class _TableTerms(torch.autograd.Function):
                                                    n_t, kk, d, float(p), ctypes.c_uint64(seed),
                                                    grad.data_ptr(), st),
                   "fanout_mean_gather_bwd")
-        return grad, None, None, None, None, None
+        return grad, None, None, None, None, None, None
 
 
 class _SageLoss(torch.autograd.Function):
@@ -496,13 +505,15 @@ class GraphSAGE(nn.Module):
                        for ci in leaf)
         ids = torch.cat([groups[gi][0] for gi in inner])
         sink = self._tg if SORTED_LEAF_BACKWARD else None
-        rows, norms2, *aggrs = _TableTerms.apply(self._table, ids, self.n_user, leaves, sink,
-                                                 self._cached_norms())
+        splits = [groups[gi][0].numel() for gi in inner]
+        out = _TableTerms.apply(self._table, ids, self.n_user, leaves, sink,
+                                self._cached_norms(), splits)
+        parts, norms2, aggrs = out[:len(inner)], out[len(inner)], out[len(inner) + 1:]
         self._slice_norms2 = norms2  # consumed by loss() / the fused loss
-        # one split node: its backward concatenates the group gradients once
-        # (per-slice views would each materialise a full-size zero tensor)
+        # one output per inner group (the table node's backward takes their
+        # gradients as separate row groups)
         h = [None] * len(groups)
-        for gi, part in zip(inner, torch.split(rows, [groups[gi][0].numel() for gi in inner])):
+        for gi, part in zip(inner, parts):
             h[gi] = part
         leaf_aggr = {parent[ci]: a for ci, a in zip(leaf, aggrs)}
         for i in range(L):
@@ -614,11 +625,19 @@ class GraphSAGE(nn.Module):
         for p in self.parameters():
             p.grad = None
         if tree is None:
-            seeds = torch.cat([users.int(), pos.int() + self.n_user, neg.int() + self.n_user])
-            tree = self.sample_tree(seeds.to(self.device), seed)
+            u32, p32, n32 = (torch.as_tensor(t).to(device=self.device, dtype=torch.int32)
+                             .contiguous() for t in (users, pos, neg))
+            seeds = torch.empty(3 * u32.numel(), dtype=torch.int32, device=u32.device)
+            check(lib.mirec_pack_seed_nodes(u32.data_ptr(), p32.data_ptr(), n32.data_ptr(),
+                                            u32.numel(), self.n_user, seeds.data_ptr(),
+                                            _lib.stream_handle()), "pack_seed_nodes")
+            tree = self.sample_tree(seeds, seed)
         emb = self.forward(tree, dropout_seed=seed if self.training else None)
         loss = self.loss_fused(emb)
-        (loss * loss_scale if loss_scale != 1.0 else loss).backward()
+        one = self.__dict__.get("_loss_seed")  # kept: no fill kernel per step
+        if one is None or one.device != loss.device:
+            one = self._loss_seed = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(one if loss_scale == 1.0 else one * loss_scale)
         if grad_hook is not None:
             grad_hook()
         self.optimizer_step()

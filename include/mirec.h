@@ -393,6 +393,11 @@ int mirec_sample_fanout(const mirec_csr_t *csr, const int32_t *nodes, int64_t n,
                         int32_t k, uint64_t seed, uint64_t offset,
                         int32_t *children, mirec_stream_t stream);
 
+/* out[0, B) = users, out[B, 2B) = n_users + pos, out[2B, 3B) = n_users + neg
+ * (the seed node ids of a BPR batch in a [users ; items] id table). */
+int mirec_pack_seed_nodes(const int32_t *users, const int32_t *pos, const int32_t *neg,
+                          int64_t batch, int64_t n_users, int32_t *out, mirec_stream_t stream);
+
 /* Fixed-fanout sampling WITHOUT replacement (PyG NeighborSampler, the
  * sampler of model/graphsage.py:342-365): a node with at most k entries keeps
  * all of them in row order and -1 in the remaining slots; otherwise k
