@@ -1660,8 +1660,17 @@ def test_sorted_leaf_backward_matches_atomic_and_is_deterministic():
                 g.data_ptr(), ids.data_ptr(), n_t, k, d, p, ctypes.c_uint64(5), n_rows,
                 b.data_ptr(), ws.data_ptr(), nb.value, st), "sorted")
             outs.append(b)
-        assert rel(outs[0], a) < 1e-5
+        # two fp32 summation orders of a 43 K-entry hub row: ~sqrt(n) eps apart
+        assert rel(outs[0], a) < 5e-5
         assert torch.equal(outs[0], outs[1])
+        if p == 0.0:  # both against the exact sum
+            idc = ids.view(n_t, k).long()
+            cnt = (idc >= 0).sum(1).clamp(min=1).double()
+            ref = base.double().clone()
+            ok = idc >= 0
+            rows = torch.arange(n_t, device="cuda").view(-1, 1).expand(n_t, k)[ok]
+            ref.index_add_(0, idc[ok], (g.double() / cnt[:, None])[rows])
+            assert rel(outs[0], ref) < 1e-5 and rel(a, ref) < 1e-5
 
 
 # ------------------------------------------------------------------ C5 / C3 full size
