@@ -164,6 +164,12 @@ def layer_bytes(n_nodes: int, nnz: int, d: int) -> int:
     return nnz * d * 4 + nnz * 4 + (n_nodes + 1) * 4 + n_nodes * 4 + n_nodes * d * 4
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (long legs keep a watchdog informed; the one
+    JSON line stays alone on stdout)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline(ds, args, users, pos, neg):
     """The CPU oracle (torch fp32) on a bounded sample of the same workload,
     timed per BASELINE.md §3: one warm-up training step, then the mean of K
@@ -178,12 +184,14 @@ def cpu_baseline(ds, args, users, pos, neg):
     res = {"cores": threads, "threads": threads, "os_cpu_count": os.cpu_count(),
            "kind": "port", "cpu": cpu_model(), "warmup": 1, "k": K}
     if args.cpu_baseline == "step":
+        progress("cpu baseline: warm-up step")
         o.stageOne(users, pos, neg)  # warm-up
         ts = []
-        for _ in range(K):
+        for i in range(K):
             t0 = time.perf_counter()
             o.stageOne(users, pos, neg)
             ts.append(time.perf_counter() - t0)
+            progress(f"cpu baseline: step {i + 1}/{K} {ts[-1]:.1f} s")
         t_step = sum(ts) / K
         res.update(value=round(len(users) / t_step, 3), unit="positive-edges/s",
                    step_s=round(t_step, 3), step_s_each=[round(t, 3) for t in ts],
@@ -196,10 +204,11 @@ def cpu_baseline(ds, args, users, pos, neg):
             forward(o.emb, o.ei, ds.n_users, args.layers, o.div)  # warm-up
     tf = []
     with torch.no_grad():
-        for _ in range(K):
+        for i in range(K):
             t0 = time.perf_counter()
             forward(o.emb, o.ei, ds.n_users, args.layers, o.div)
             tf.append(time.perf_counter() - t0)
+            progress(f"cpu baseline: forward {i + 1}/{K} {tf[-1]:.1f} s")
     t_fwd = sum(tf) / K
     nbytes = args.layers * layer_bytes(ds.n_users + ds.m_items, 2 * ds.trainDataSize, args.dim)
     res.update(forward_s=round(t_fwd, 3),
@@ -222,7 +231,7 @@ def pmc_traffic(args):
     kname = f"prop_kernel<{args.dim}, {({32: 2, 64: 4, 128: 4, 256: 8}).get(args.dim, 1)}, 0, false, false>"
     if (c2_workload(args) and j.get("workload") == f"C2-{args.kind}-d{args.dim}-L{args.layers}"
             and kname in j.get("kernel", "")):
-        return j.get("hbm_bytes_per_launch"), f"{PMC_FILE} ({j.get('round', 'r05')})"
+        return j.get("hbm_bytes_per_launch"), f"{PMC_FILE} ({j.get('round', j.get('tag', 'r05'))})"
     return None, None
 
 
@@ -241,8 +250,10 @@ def quality_leg(args, dev, steps: int):
     from furusato_recommend_amd.engine import sample_triples
     from furusato_recommend_amd.evaluate import evaluate
     t0 = time.perf_counter()
+    progress("quality leg: building the community graph")
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=7, kind="cluster",
                             n_clusters=args.quality_clusters, p_in=0.9, test_frac=0.1)
+    progress("quality leg: graph built")
     torch.manual_seed(args.seed)
     cfg = {"recdim": args.dim, "layer": args.layers, "lr": 1e-3, "decay": 1e-4,
            "device": str(dev), "bpr_batch_size": args.batch, "prune": bool(args.prune)}
@@ -258,8 +269,12 @@ def quality_leg(args, dev, steps: int):
     for i in range(steps):
         sample_triples(model.graph, B, args.seed + 1, i * B, u, p, n, err, 0, 1)
         eng.train_step(emb, model.optim, u, p, n, cfg["decay"])
+        if (i + 1) % 500 == 0:
+            torch.cuda.synchronize()
+            progress(f"quality leg: {i + 1}/{steps} training steps")
     torch.cuda.synchronize()
     t_train = time.perf_counter() - t_train
+    progress("quality leg: evaluating Recall@20")
     r = evaluate(model, ds.testDict, topks=(10, 20))
     mean_deg = ds.trainDataSize / ds.n_users
     return {"recall@20": float(r["recall"][1]), "ndcg@20": float(r["ndcg"][1]),
