@@ -449,23 +449,29 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   NtArgs fx{A2, Amask, C2, Ks, Ns, relu ? 1 : 0, bkn};
   const unsigned ncol = (unsigned)(No / kTile);
   hipStream_t st = (hipStream_t)stream;
-#ifndef MIREC_NT_PF
-#define MIREC_NT_PF 1
-#endif
-#ifndef MIREC_NT_BM1
-#define MIREC_NT_BM1 128
-#endif
-  // 128-row tiles, one chunk of loads ahead (tools/gemm_bench.py: 64-row
-  // tiles, two chunks ahead and a double-buffered LDS form measured within
-  // noise on the C3 / C4 shapes; a persistent form streaming 64-row A tiles
-  // past B held in registers measured 15-45 % slower)
-  const dim3 grid((unsigned)((n + MIREC_NT_BM1 - 1) / MIREC_NT_BM1) * ncol);
-  if (bkn)
-    hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF, true>), grid, dim3(256), 0, st,
-                       A, B, bias, C, n, (int)Kr, (int)No, fx);
-  else
-    hipLaunchKernelGGL((gemm_nt_kernel<MIREC_NT_BM1, MIREC_NT_PF, false>), grid, dim3(256), 0,
-                       st, A, B, bias, C, n, (int)Kr, (int)No, fx);
+  // 128- or 64-row tiles: the one whose grid needs fewer tile-rounds of the
+  // chip's workgroup slots (2 per CU), ties to 64 rows when the grid spans
+  // more than one round (tools/gemm_bench.py: 64 rows win at 48, 1200,
+  // 1320 and 2400 tiles of 128 — C3 hop 126 -> 112 us, C4 QKV forward 73 ->
+  // 64 us — and lose at 440: the N = 128 projections at 56 K rows)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t slots = 2 * (int64_t)std::max(cus, 1);
+  const int64_t t128 = (n + 127) / 128 * ncol, t64 = (n + 63) / 64 * ncol;
+  const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
+  const bool bm64 = r64 < r128 || (r64 == r128 && t128 > slots);
+#define MIREC_NT_LAUNCH(BM, BKN)                                                               \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
+                     dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx)
+  if (bm64) {
+    if (bkn) MIREC_NT_LAUNCH(64, true);
+    else MIREC_NT_LAUNCH(64, false);
+  } else {
+    if (bkn) MIREC_NT_LAUNCH(128, true);
+    else MIREC_NT_LAUNCH(128, false);
+  }
+#undef MIREC_NT_LAUNCH
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

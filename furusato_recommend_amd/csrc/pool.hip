@@ -483,3 +483,40 @@ extern "C" int mirec_segment_mean_bwd(const float *grad_out, const int64_t *seg,
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
+
+// BPR pairs of a sequence batch on the device: out[j] = a uniformly drawn
+// item of user users[j]'s sequence (items[u][0, length[u])), out[B + j] = a
+// uniform item in [0, m_items) — the (positive, negative) of UniformSample
+// over the users' interactions (the SASRec benchmark's per-step pairs).
+// Counter-based: element j's draws are mix64(key + 2 (offset + j) + {0, 1}).
+__global__ __launch_bounds__(256) void seq_sample_kernel(const int64_t *__restrict__ users,
+                                                         int64_t B,
+                                                         const int32_t *__restrict__ items,
+                                                         int32_t max_len,
+                                                         const int64_t *__restrict__ length,
+                                                         int64_t m_items, uint64_t key,
+                                                         uint64_t offset,
+                                                         int64_t *__restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B) return;
+  const uint64_t c = key + 2 * (offset + (uint64_t)j);
+  const int64_t u = users[j];
+  const int64_t len = length[u];
+  const int64_t k = len > 0 ? (int64_t)__umul64hi(mix64(c), (uint64_t)len) : 0;
+  out[j] = len > 0 ? (int64_t)items[u * max_len + k] : 0;
+  out[B + j] = (int64_t)__umul64hi(mix64(c + 1), (uint64_t)m_items);
+}
+
+extern "C" int mirec_seq_sample(const int64_t *users, int64_t B, const int32_t *items,
+                                int32_t max_len, const int64_t *length, int64_t m_items,
+                                uint64_t seed, uint64_t offset, int64_t *out,
+                                mirec_stream_t stream) {
+  MIREC_CHECK_ARG(B >= 0 && max_len > 0 && m_items > 0);
+  if (B == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(users && items && length && out);
+  hipLaunchKernelGGL(seq_sample_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, users, B, items, max_len, length, m_items,
+                     mix64(seed ^ 0x5EC5A3B1E0D7F00Dull), offset, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

@@ -658,6 +658,22 @@ class SASRec(nn.Module):
         events[k] = ev
         return out
 
+    @torch.no_grad()
+    def sample_pairs(self, users: torch.Tensor, seed: int, offset: int = 0):
+        """Device (positive, negative) item ids [2, B] (int64) for device user
+        ids: a uniform element of each user's sequence and a uniform item
+        (mirec_seq_sample, one launch)."""
+        users = users.to(device=self.device, dtype=torch.int64).contiguous()
+        items, length = self.seq.items.contiguous(), self.seq.length.contiguous()
+        if items.dtype != torch.int32 or length.dtype != torch.int64:
+            raise ValueError("SequenceData: int32 items and int64 lengths expected")
+        out = torch.empty(2, users.numel(), dtype=torch.int64, device=self.device)
+        check(lib.mirec_seq_sample(users.data_ptr(), users.numel(), items.data_ptr(),
+                                   items.shape[1], length.data_ptr(), self.m_item,
+                                   ctypes.c_uint64(seed), ctypes.c_uint64(offset),
+                                   out.data_ptr(), _lib.stream_handle()), "seq_sample")
+        return out
+
     def forward_item(self, x):
         """sasrec.py:415-421."""
         for lin in self.item_linears:
@@ -948,9 +964,16 @@ class _CapturedStep:
         ev = torch.cuda.Event()
         ev.record()
         self.events[k] = ev
-        for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
-            if dv:  # device ids: copied after the staging copy (stream order)
-                self.inbuf[(j + 1) * B:(j + 2) * B].copy_(t)
+        pair = (on_dev[0] and on_dev[1] and pos.dtype == torch.int64 and neg.dtype == torch.int64
+                and pos.dim() == 1 and neg.dim() == 1 and pos._base is not None
+                and pos._base is neg._base and pos._base.is_contiguous()
+                and neg.data_ptr() == pos.data_ptr() + 8 * B)
+        if pair:  # one [pos ; neg] block (sample_pairs): one copy
+            self.inbuf[B:3 * B].copy_(pos._base.view(-1)[:2 * B])
+        else:
+            for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
+                if dv:  # device ids: copied after the staging copy (stream order)
+                    self.inbuf[(j + 1) * B:(j + 2) * B].copy_(t)
         m = self.m
         if self.norm_from_buf and not m._norm_valid():
             m._refresh_norm()  # the table changed outside the step

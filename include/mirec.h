@@ -670,6 +670,14 @@ int mirec_norm_terms_bwd(const float *const *xs, float *const *grads, const int6
                          const float *g_total, const float *extra_w, int32_t n_extra,
                          float *extra_grad, mirec_stream_t stream);
 
+/* Per-step (positive, negative) pairs of a sequence batch: out[j] = a
+ * uniform element of user users[j]'s sequence items[u][0, length[u]) (0 for
+ * an empty one), out[B + j] = a uniform item in [0, m_items); counter-based
+ * (seed, offset + j). */
+int mirec_seq_sample(const int64_t *users, int64_t B, const int32_t *items, int32_t max_len,
+                     const int64_t *length, int64_t m_items, uint64_t seed, uint64_t offset,
+                     int64_t *out, mirec_stream_t stream);
+
 /* Pack a SASRec batch into a fixed token capacity (the graph-captured step,
  * model/sasrec.py:449-455's pad_sequence without the padding): users [B]
  * (device int64), items [n_users, max_len] (int32, each user's last items),

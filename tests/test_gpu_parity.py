@@ -1164,6 +1164,38 @@ def test_sasrec_sorted_table_step_matches_dense(graph, mode):
         assert sa.n_steps == sb.n_steps == 3
 
 
+def test_sasrec_sample_pairs():
+    """sample_pairs: every positive is an element of its user's sequence,
+    positions uniform (chi-square over one long user's positions), negatives
+    in range and uniform; same (seed, offset) -> same draws."""
+    from furusato_recommend_amd import SASRec, SyntheticBipartite
+    from furusato_recommend_amd.sasrec import SequenceData
+    ds = SyntheticBipartite(400, 300, 6000, seed=3)
+    seq = SequenceData.synthetic(400, 300, "cuda", max_len=50, min_len=5, seed=1)
+    m = SASRec({"recdim": 64, "layer": 1, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+                "device": "cuda:0", "bpr_batch_size": 64}, ds, sequences=seq)
+    users = torch.randint(0, 400, (5000,), device="cuda")
+    pn = m.sample_pairs(users, 11, 0)
+    assert torch.equal(pn, m.sample_pairs(users, 11, 0))
+    assert not torch.equal(pn, m.sample_pairs(users, 11, 5000))
+    items, length = seq.items.long(), seq.length
+    rows = items[users]
+    hit = (rows == pn[0][:, None]) & (torch.arange(50, device="cuda")[None, :] < length[users][:, None])
+    assert bool(hit.any(1).all())
+    assert int(pn[1].min()) >= 0 and int(pn[1].max()) < 300
+    u0 = int(torch.argmax(length))
+    L = int(length[u0])
+    N = L * 400
+    many = m.sample_pairs(torch.full((N,), u0, device="cuda"), 5, 0)[0].cpu().numpy()
+    vals, mult = np.unique(items[u0][:L].cpu().numpy(), return_counts=True)
+    got = np.array([(many == v).sum() for v in vals], dtype=np.float64)
+    exp = N * mult / L  # an item repeated in the sequence is drawn that much more often
+    assert got.sum() == N
+    chi2 = float(((got - exp) ** 2 / exp).sum())
+    dof = len(vals) - 1
+    assert chi2 < dof + 6 * (2 * dof) ** 0.5
+
+
 def test_sasrec_trains():
     from furusato_recommend_amd import SASRec, SyntheticBipartite
     ds = SyntheticBipartite(3000, 500, 40_000, seed=11, test_frac=0.1)

@@ -132,6 +132,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(7)
 
     rng = np.random.default_rng(7)
+    step = [0]
 
     def batch():
         # users uniform, drawn on the host like the reference's UniformSample
@@ -140,11 +141,9 @@ def main():
         # workload: no rejection of positives)
         u_h = rng.integers(0, args.users, B)
         u = m._upload(u_h)  # pinned staging: no stream sync
-        ln = seq.length[u]
-        k = (torch.rand(B, device=dev, generator=g) * ln).long()
-        p = seq.items[u, k].long()
-        n = torch.randint(0, args.items, (B,), device=dev, generator=g)
-        return u_h, p, n
+        step[0] += 1
+        pn = m.sample_pairs(u, 7, step[0] * B)  # one launch: [pos ; neg]
+        return u_h, pn[0], pn[1]
 
     for _ in range(args.warmup):
         m.stageOne(*batch())
