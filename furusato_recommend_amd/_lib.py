@@ -189,7 +189,7 @@ SIGNATURES = {
     "mirec_attention_packed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                            c_int32, c_int32, c_void_p, c_int64, c_void_p]),
     "mirec_attention_wave_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
-                                         c_int32, c_void_p, c_void_p, c_void_p]),
+                                         c_int32, c_void_p, c_void_p, c_int64, c_void_p]),
     "mirec_attention_wave_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_int64, c_int32, c_int32, c_int32, c_void_p,
                                          c_void_p, c_void_p]),

@@ -144,8 +144,18 @@ template <int DH>
 __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_fwd_kernel(
     const float *__restrict__ qkv, float *__restrict__ out, float *__restrict__ lse, int T_uniform,
     int H, float scale, const int32_t *__restrict__ offsets, const int32_t *__restrict__ order,
-    int64_t n_units) {
+    int64_t n_units, int64_t batch, int64_t n_rows) {
   constexpr int Q4 = DH / 4, NCB = DH / 16;
+  const int64_t unit_wgs = (n_units + kUnitsPerWG - 1) / kUnitsPerWG;
+  if ((int64_t)blockIdx.x >= unit_wgs) {  // the padding rows [offsets[batch], n_rows) of out
+    const int64_t w4 = (int64_t)H * DH / 4;
+    const int64_t e0 = (int64_t)offsets[batch] * w4, e1 = n_rows * w4;
+    const int64_t stride = ((int64_t)gridDim.x - unit_wgs) * blockDim.x;
+    for (int64_t e = e0 + ((int64_t)blockIdx.x - unit_wgs) * blockDim.x + threadIdx.x; e < e1;
+         e += stride)
+      st4(out + 4 * e, f4_zero());
+    return;
+  }
   Unit u;
   if (!unit_of(offsets, order, T_uniform, H, n_units, u)) return;
   const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
@@ -442,10 +452,13 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
 
 template <int DH>
 int launch_fwd(const float *qkv, const int32_t *offsets, const int32_t *order, int64_t units, int T,
-               int H, float *out, float *lse, hipStream_t st) {
-  const dim3 grid((unsigned)((units + kUnitsPerWG - 1) / kUnitsPerWG)), block(64 * kUnitsPerWG);
+               int H, float *out, float *lse, int64_t batch, int64_t n_rows, hipStream_t st) {
+  // unit workgroups, plus 32 that zero the padding rows when asked
+  const int64_t unit_wgs = (units + kUnitsPerWG - 1) / kUnitsPerWG;
+  const dim3 grid((unsigned)(unit_wgs + (n_rows > 0 && offsets ? 32 : 0))),
+      block(64 * kUnitsPerWG);
   hipLaunchKernelGGL((attnw_fwd_kernel<DH>), grid, block, 0, st, qkv, out, lse, T, H,
-                     1.f / sqrtf((float)DH), offsets, order, units);
+                     1.f / sqrtf((float)DH), offsets, order, units, batch, n_rows);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -504,7 +517,7 @@ extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batc
 extern "C" int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets,
                                         const int32_t *order, int64_t batch, int32_t T,
                                         int32_t heads, int32_t head_dim, float *out, float *lse,
-                                        mirec_stream_t stream) {
+                                        int64_t n_rows, mirec_stream_t stream) {
   MIREC_CHECK_ARG(batch >= 0 && heads >= 1 && wave_dims_ok(head_dim));
   MIREC_CHECK_ARG(offsets != nullptr || (T >= 1 && T <= kMaxT));
   if (batch == 0) return MIREC_OK;
@@ -512,9 +525,9 @@ extern "C" int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets
   const int64_t units = batch * heads;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   switch (head_dim) {
-    case 16: return launch_fwd<16>(qkv, offsets, order, units, T, heads, out, lse, st);
-    case 32: return launch_fwd<32>(qkv, offsets, order, units, T, heads, out, lse, st);
-    default: return launch_fwd<64>(qkv, offsets, order, units, T, heads, out, lse, st);
+    case 16: return launch_fwd<16>(qkv, offsets, order, units, T, heads, out, lse, batch, n_rows, st);
+    case 32: return launch_fwd<32>(qkv, offsets, order, units, T, heads, out, lse, batch, n_rows, st);
+    default: return launch_fwd<64>(qkv, offsets, order, units, T, heads, out, lse, batch, n_rows, st);
   }
 }
 

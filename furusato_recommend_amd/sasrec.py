@@ -66,26 +66,45 @@ def _use_wave(dh: int) -> bool:
     return ATTN_IMPL in ("wave", "hybrid") and bool(lib.mirec_attention_wave_supported(dh))
 
 
+_ORDER_CACHE: dict = {}
+
+
+def _length_order(offsets, B):
+    """[order (B) | packs (1 + 4B)] of a packed batch (mirec_attention_length_order),
+    computed once per offsets tensor: every layer of a step shares it (a
+    captured step launches the ordering pass once)."""
+    key = id(offsets)
+    hit = _ORDER_CACHE.get(key)
+    if hit is not None and hit[0]() is offsets and hit[1] == offsets._version:
+        return hit[2]
+    order = torch.empty(5 * B + 1, dtype=torch.int32, device=offsets.device)
+    check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
+                                           order[B:].data_ptr(), None, 0, 0,
+                                           _lib.stream_handle()), "attention_length_order")
+    import weakref
+    for k in [k for k, v in _ORDER_CACHE.items() if v[0]() is None]:
+        del _ORDER_CACHE[k]
+    _ORDER_CACHE[key] = (weakref.ref(offsets), offsets._version, order)
+    return order
+
+
 def _wave_fwd(qkv, offsets, B, T, heads, dh, out, padded=False):
     """mirec_attention_wave_fwd; returns (lse [n_rows, heads], order): packed
-    sequences run longest first (mirec_attention_length_order, which also
-    zeroes out's capacity-padding rows when ``padded``)."""
+    sequences run longest first (mirec_attention_length_order, shared by the
+    layers of a step); with ``padded`` the kernel's spare workgroups zero
+    out's capacity-padding rows."""
     lse = torch.empty(qkv.shape[0] if offsets is not None else B * T, heads, dtype=qkv.dtype,
                       device=qkv.device)
     order = None
     if offsets is not None and B > 0:
-        # [order (B) | packs (1 + 4B)]
-        order = torch.empty(5 * B + 1, dtype=torch.int32, device=qkv.device)
-        check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
-                                               order[B:].data_ptr(),
-                                               out.data_ptr() if padded else None,
-                                               out.shape[0], out.shape[1], _lib.stream_handle()),
-              "attention_length_order")
+        order = _length_order(offsets, B)
     elif padded:
         _zero_tail(out, offsets)
+    n_rows = out.shape[0] if (padded and order is not None) else 0
     _timed("fwd", (B, T if offsets is None else -1, heads, dh), lambda: check(
         lib.mirec_attention_wave_fwd(qkv.data_ptr(), _ptr(offsets), _ptr(order), B, T, heads, dh,
-                                     out.data_ptr(), lse.data_ptr(), _lib.stream_handle()),
+                                     out.data_ptr(), lse.data_ptr(), n_rows,
+                                     _lib.stream_handle()),
         "attention_wave_fwd"), offsets)
     return lse, order
 

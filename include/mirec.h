@@ -600,7 +600,9 @@ int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32
  * scores); the backward takes out and lse from it and writes dqkv and delta
  * [n_rows, heads] (rowsum(dout ⊙ out), scratch), in two launches.  order
  * (optional, packed form): the sequences in the order their units run, from
- * mirec_attention_length_order (longest first, device int32 [batch]; with
+ * mirec_attention_length_order (longest first, device int32 [batch]; the
+ * forward with offsets and n_rows > 0 also zeroes out's rows [offsets[batch],
+ * n_rows) (capacity padding); with
  * packs (optional, int32 [1 + 4 batch]) it also groups that order into
  * packs of at most 4 blocks of 16 positions for mirec_attention_packed_bwd:
  * packs[0] = count, packs[1 + 4p + s] = sequence or -1); with zero_buf it
@@ -612,7 +614,7 @@ int mirec_attention_length_order(const int32_t *offsets, int64_t batch, int32_t 
                                  int32_t zero_width, mirec_stream_t stream);
 int mirec_attention_wave_fwd(const float *qkv, const int32_t *offsets, const int32_t *order,
                              int64_t batch, int32_t T, int32_t heads, int32_t head_dim, float *out,
-                             float *lse, mirec_stream_t stream);
+                             float *lse, int64_t n_rows, mirec_stream_t stream);
 int mirec_attention_wave_bwd(const float *qkv, const float *out, const float *lse,
                              const float *dout, const int32_t *offsets, const int32_t *order,
                              int64_t batch, int32_t T, int32_t heads, int32_t head_dim,

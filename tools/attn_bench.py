@@ -69,7 +69,7 @@ def main():
             runs = {
                 "wave_fwd": lambda: chk(lib.mirec_attention_wave_fwd(
                     qkv.data_ptr(), offs.data_ptr(), op, B, 0, H, dh, out.data_ptr(), lse.data_ptr(),
-                    st), "wave_fwd"),
+                    0, st), "wave_fwd"),
                 "wave_bwd": lambda: chk(lib.mirec_attention_wave_bwd(
                     qkv.data_ptr(), out.data_ptr(), lse.data_ptr(), dout.data_ptr(),
                     offs.data_ptr(), op, B, 0, H, dh, dqkv.data_ptr(), delta.data_ptr(), st),
