@@ -141,7 +141,9 @@ __device__ __forceinline__ bool unit_of(const int32_t *offsets, const int32_t *o
 }
 
 template <int DH>
-__global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_fwd_kernel(
+// waves_per_eu(2): the preloaded unit (Q, K, V: 192 registers at dh = 64)
+// still fits two waves per SIMD
+__global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_eu(2))) void attnw_fwd_kernel(
     const float *__restrict__ qkv, float *__restrict__ out, float *__restrict__ lse, int T_uniform,
     int H, float scale, const int32_t *__restrict__ offsets, const int32_t *__restrict__ order,
     int64_t n_units, int64_t batch, int64_t n_rows) {
@@ -163,24 +165,31 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_fwd_kernel(
   const int64_t rs = 3 * (int64_t)d;
   const float *qb = qkv + u.row0 * rs + u.h * DH, *kb_ = qb + d, *vb = qb + 2 * d;
   const int nb = (T + kBlk - 1) / kBlk;
-  for (int w = 0; w < nb; ++w) {
-    const int qi = kBlk * w + j;
-    float q[Q4];
-    ld_kappa<Q4>(qb + (int64_t)qi * rs, g, qi < T, q);
-    // all K blocks of this query block in flight at once
-    float k[4][Q4];
+  // every operand of the unit in flight at once (one round trip): Q, K in
+  // the κ layout, V in the π layout, for the sequence's nb blocks
+  float qa[4][Q4], k[4][Q4], v[4][4][NCB];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      const int kr = kBlk * kb + j;
-      ld_kappa<Q4>(kb_ + (int64_t)kr * rs, g, kb <= w && kr < T, k[kb]);
+  for (int b = 0; b < 4; ++b) {
+    const int r = kBlk * b + j;
+    ld_kappa<Q4>(qb + (int64_t)r * rs, g, b < nb && r < T, qa[b]);
+    ld_kappa<Q4>(kb_ + (int64_t)r * rs, g, b < nb && r < T, k[b]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int vr = kBlk * b + 4 * g + rr;
+      ld_pi<NCB>(vb + (int64_t)vr * rs, j, b < nb && vr < T, v[b][rr]);
     }
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    if (w >= nb) break;
+    const int qi = kBlk * w + j;
     f32x4 s[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       s[kb] = zero4();
       if (kb <= w) {
 #pragma unroll
-        for (int t = 0; t < Q4; ++t) s[kb] = mfma16(k[kb][t], q[t], s[kb]);
+        for (int t = 0; t < Q4; ++t) s[kb] = mfma16(k[kb][t], qa[w][t], s[kb]);
       }
     }
     float m = -INFINITY;
@@ -211,14 +220,6 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_fwd_kernel(
     sum += __shfl_xor(sum, 16);
     sum += __shfl_xor(sum, 32);
     const float inv = 1.f / sum;
-    float v[4][4][NCB];
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int vr = kBlk * kb + 4 * g + r;
-        ld_pi<NCB>(vb + (int64_t)vr * rs, j, kb <= w && vr < T, v[kb][r]);
-      }
     f32x4 o[NCB];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) o[cb] = zero4();
