@@ -410,17 +410,82 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
 // wave w is block w of the pack's block list: sequence i = slot(w), local
 // block w - lo (lo = the sequence's first block in the pack).  LDS row R
 // holds local row 16 (R/16 - lo) + R%16 of its block's sequence.
-// scores_softmax of a pack's query block: local key blocks 0..lw of the
-// sequence starting at LDS block lo (keys and the query ql numbered within
-// the sequence); s[kb] holds local key block kb.
+// κ layout helpers of the packed backward: lane group g of a 16-row block
+// holds dims 16 c + 4 g + e (e < 4) of its row at contraction step 4 c + e;
+// dims >= dh (dh % 4 == 0) read as zero.
+template <int Q4>
+__device__ __forceinline__ void ld_kappa_dh(const float *row, int g, int dh, bool ok,
+                                            float (&v)[Q4]) {
+#pragma unroll
+  for (int c = 0; c < Q4 / 4; ++c) {
+    const int dim = 16 * c + 4 * g;
+    const float4 x = (ok && dim < dh) ? ld4(row + dim) : f4_zero();
+    v[4 * c] = x.x;
+    v[4 * c + 1] = x.y;
+    v[4 * c + 2] = x.z;
+    v[4 * c + 3] = x.w;
+  }
+}
+
+// scores_softmax with the key operand read from LDS in the κ order (float4):
+// key blocks 0..w of sK (the sequence's first block at sK), query row 16 w + j.
 template <int DPAD, int NB>
-__device__ __forceinline__ void scores_softmax_local(const float *sK, const float (&q)[DPAD / 4],
-                                                     int lo, int lw, int ql, int T, float scale,
-                                                     f32x4 (&s)[NB], float &m_out,
-                                                     float &inv_out) {
-  scores_softmax<DPAD, NB>(sK + kB * lo * AttnShape<DPAD, NB>::LDK, q, lw, T, scale, s, m_out,
-                           inv_out);
-  (void)ql;
+__device__ __forceinline__ void scores_softmax_kappa(const float *sK, const float (&q)[DPAD / 4],
+                                                     int w, int T, float scale, f32x4 (&s)[NB],
+                                                     float &m_out, float &inv_out) {
+  using S = AttnShape<DPAD, NB>;
+  const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb) s[kb] = zero4();
+#pragma unroll
+  for (int c = 0; c < S::Q4 / 4; ++c) {
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb)
+      if (kb <= w) {
+        const float4 k4 = ld4(sK + (kB * kb + j) * S::LDK + 16 * c + 4 * g);
+        s[kb] = mfma16(k4.x, q[4 * c], s[kb]);
+        s[kb] = mfma16(k4.y, q[4 * c + 1], s[kb]);
+        s[kb] = mfma16(k4.z, q[4 * c + 2], s[kb]);
+        s[kb] = mfma16(k4.w, q[4 * c + 3], s[kb]);
+      }
+  }
+  const int qi = kB * w + j;
+  float m = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb) {
+    if (kb > w) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = kB * kb + 4 * g + r;
+      const float v = (key > qi || key >= T) ? -INFINITY : s[kb][r] * scale;
+      s[kb][r] = v;
+      m = fmaxf(m, v);
+    }
+  }
+  m = fmaxf(m, __shfl_xor(m, 16));
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb) {
+    if (kb > w) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = expf(s[kb][r] - m);
+      s[kb][r] = e;
+      sum += e;
+    }
+  }
+  sum += __shfl_xor(sum, 16);
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb) {
+    if (kb > w) break;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[kb][r] *= inv;
+  }
+  m_out = m;
+  inv_out = inv;
 }
 
 struct PackSeqs {
@@ -540,9 +605,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   const int ql = kB * (w - lo) + j;  // local query row of phase A
   const int qa = kB * w + j;         // its LDS row
   const bool qvalid = act && ql < T;
+  // q / dO rows in the κ layout: lane group g holds dims 16 c + 4 g + e
+  // (float4 loads; the LDS operands are read the same way, as float4 —
+  // conflict-free at the row stride ≡ 4 mod 32)
   float q[S::Q4], dov[S::Q4];
-  load_seg<S::Q4>(base + (int64_t)ql * rs, g, dh, qvalid, q);
-  load_seg<S::Q4>(dout + (row0 + ql) * d + h * dh, g, dh, qvalid, dov);
+  ld_kappa_dh<S::Q4>(base + (int64_t)ql * rs, g, dh, qvalid, q);
+  ld_kappa_dh<S::Q4>(dout + (row0 + ql) * d + h * dh, g, dh, qvalid, dov);
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
   float kr[S::Q4], vr[S::Q4];
@@ -554,14 +622,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     // unrolled block loops from holding every block's operands at once
     const int lw = (w - lo) & 3;
     const float *sKl = sK + kB * lo * S::LDK, *sVl = sV + kB * lo * S::LDK;  // lo < 4
-    scores_softmax_local<DPAD, NB>(sK, q, lo, lw, ql, T, scale, p, m, inv);
+    scores_softmax_kappa<DPAD, NB>(sKl, q, lw, T, scale, p, m, inv);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
 #pragma unroll
-    for (int t = 0; t < S::Q4; ++t) {
+    for (int c = 0; c < S::Q4 / 4; ++c) {
 #pragma unroll
       for (int kb = 0; kb < NB; ++kb)
-        if (kb <= lw) dp[kb] = mfma16(sVl[(kB * kb + j) * S::LDK + 4 * t + g], dov[t], dp[kb]);
+        if (kb <= lw) {
+          const float4 v4 = ld4(sVl + (kB * kb + j) * S::LDK + 16 * c + 4 * g);
+          dp[kb] = mfma16(v4.x, dov[4 * c], dp[kb]);
+          dp[kb] = mfma16(v4.y, dov[4 * c + 1], dp[kb]);
+          dp[kb] = mfma16(v4.z, dov[4 * c + 2], dp[kb]);
+          dp[kb] = mfma16(v4.w, dov[4 * c + 3], dp[kb]);
+        }
     }
     float delta = 0.f;
 #pragma unroll
@@ -597,17 +671,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       for (int cb = 0; cb < S::NCB; ++cb) store4(row, kB * cb + 4 * g, dh, dq[cb]);
     }
 #pragma unroll
-    for (int t = 0; t < S::Q4; ++t) {
-      kr[t] = sK[qa * S::LDK + 4 * t + g];
-      vr[t] = sV[qa * S::LDK + 4 * t + g];
+    for (int c = 0; c < S::Q4 / 4; ++c) {
+      const float4 k4 = ld4(sK + qa * S::LDK + 16 * c + 4 * g);
+      const float4 v4 = ld4(sV + qa * S::LDK + 16 * c + 4 * g);
+      kr[4 * c] = k4.x;
+      kr[4 * c + 1] = k4.y;
+      kr[4 * c + 2] = k4.z;
+      kr[4 * c + 3] = k4.w;
+      vr[4 * c] = v4.x;
+      vr[4 * c + 1] = v4.y;
+      vr[4 * c + 2] = v4.z;
+      vr[4 * c + 3] = v4.w;
     }
   }
   __syncthreads();  // K / V no longer read from LDS; statistics complete
   if (act) {
 #pragma unroll
-    for (int t = 0; t < S::Q4; ++t) {
-      sQ[qa * S::LDK + 4 * t + g] = q[t];
-      sDO[qa * S::LDK + 4 * t + g] = dov[t];
+    for (int c = 0; c < S::Q4 / 4; ++c) {
+      st4(sQ + qa * S::LDK + 16 * c + 4 * g,
+          make_float4(q[4 * c], q[4 * c + 1], q[4 * c + 2], q[4 * c + 3]));
+      st4(sDO + qa * S::LDK + 16 * c + 4 * g,
+          make_float4(dov[4 * c], dov[4 * c + 1], dov[4 * c + 2], dov[4 * c + 3]));
     }
   }
   __syncthreads();
@@ -626,12 +710,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     const float *sMl = sM + o, *sLl = sL + o, *sDl = sD + o;
     for (int qb = lw; qb < nbs; ++qb) {
       f32x4 sc = zero4(), dpc = zero4();
-      const float *qrow = sQl + (kB * qb + j) * S::LDK + g;
-      const float *orow = sDOl + (kB * qb + j) * S::LDK + g;
+      const float *qrow = sQl + (kB * qb + j) * S::LDK + 4 * g;
+      const float *orow = sDOl + (kB * qb + j) * S::LDK + 4 * g;
 #pragma unroll
-      for (int t = 0; t < S::Q4; ++t) {
-        sc = mfma16(qrow[4 * t], kr[t], sc);
-        dpc = mfma16(orow[4 * t], vr[t], dpc);
+      for (int c = 0; c < S::Q4 / 4; ++c) {
+        const float4 q4 = ld4(qrow + 16 * c), o4 = ld4(orow + 16 * c);
+        sc = mfma16(q4.x, kr[4 * c], sc);
+        dpc = mfma16(o4.x, vr[4 * c], dpc);
+        sc = mfma16(q4.y, kr[4 * c + 1], sc);
+        dpc = mfma16(o4.y, vr[4 * c + 1], dpc);
+        sc = mfma16(q4.z, kr[4 * c + 2], sc);
+        dpc = mfma16(o4.z, vr[4 * c + 2], dpc);
+        sc = mfma16(q4.w, kr[4 * c + 3], sc);
+        dpc = mfma16(o4.w, vr[4 * c + 3], dpc);
       }
       float pr[4], dsr[4];
 #pragma unroll
