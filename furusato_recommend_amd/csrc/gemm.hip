@@ -35,6 +35,14 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// LDS visibility among the lanes of one wave (the epilogue slabs are
+// wave-private: no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 constexpr int kTile = 128;   // output tile edge
 #ifndef MIREC_GEMM_KC
 #define MIREC_GEMM_KC 32
@@ -238,7 +246,7 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
         if (fx.relu) y = fmaxf(y, 0.f);
         sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLdO + i] = y;
       }
-      __syncthreads();
+      wave_sync();  // the slab is wave-private
       const int64_t rbase = m0 + wm * (BM / 2) + tm * 32;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -246,7 +254,7 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
         const float4 v = ld4(sO + rr * kLdO + 4 * c4);
         if (rbase + rr < n) st4(cb + (rbase + rr) * ldc + cc + 4 * c4, v);
       }
-      __syncthreads();  // the slab is rewritten by the next block
+      wave_sync();  // the slab is wave-private
     }
   }
 }
@@ -326,17 +334,16 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  float cs = 0.f;  // column sum of A (column m0 + t, threads t < 128)
+  // column sums of A from the MFMA operands themselves: lane (i, h) sees
+  // column wm 64 + tm 32 + i at the chunk rows 8 sub + 4 h + st; the two
+  // lane halves are added at the end (waves wn == 0 own the sums)
+  float cs[2] = {0.f, 0.f};
   if (r_beg < r_end) load(r_beg);
   for (int64_t r0 = r_beg; r0 < r_end; r0 += kChunk) {
     __syncthreads();
     stage();
     __syncthreads();
     if (r0 + kChunk < r_end) load(r0 + kChunk);
-    if (do_cs && t < kTile) {
-#pragma unroll 8
-      for (int kk = 0; kk < kChunk; ++kk) cs += sA[kk * kLdTN + t];
-    }
 #pragma unroll
     for (int sub = 0; sub < kChunk / 8; ++sub) {
 #pragma unroll
@@ -351,9 +358,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
         for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
           for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma32(fa[tm], fb[tn], acc[tm][tn]);
+        if (do_cs) {
+          cs[0] += fa[0];
+          cs[1] += fa[1];
+        }
       }
     }
   }
+  cs[0] += __shfl_xor(cs[0], 32);
+  cs[1] += __shfl_xor(cs[1], 32);
   // partial tile out through a wave-private LDS slab as float4 rows (as in
   // gemm_nt_kernel)
   float *out = work + (int64_t)s * M * No;
@@ -365,16 +378,19 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     for (int tm = 0; tm < 2; ++tm) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLdO + i] = acc[tm][tn][r];
-      __syncthreads();
+      wave_sync();  // the slab is wave-private
       const int rbase = m0 + wm * 64 + tm * 32, cbase = n0 + wn * 64 + tn * 32;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e = lane + 64 * q, rr = e >> 3, c4 = e & 7;
         st4(out + (int64_t)(rbase + rr) * No + cbase + 4 * c4, ld4(sO + rr * kLdO + 4 * c4));
       }
-      __syncthreads();
+      wave_sync();  // the slab is wave-private
     }
-  if (do_cs && t < kTile) work_cs[(int64_t)s * M + m0 + t] = cs;
+  if (do_cs && wn == 0 && h == 0) {
+    work_cs[(int64_t)s * M + m0 + wm * 64 + i] = cs[0];
+    work_cs[(int64_t)s * M + m0 + wm * 64 + 32 + i] = cs[1];
+  }
 }
 
 // C[e] = Σ_s work[s][e] (float4 e), colsum[m] = Σ_s work_cs[s][m].  A
