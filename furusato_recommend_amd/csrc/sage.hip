@@ -77,6 +77,51 @@ __global__ __launch_bounds__(256) void sample_fanout_norep_kernel(
   for (int c = 0; c < k; ++c) out[c] = col[beg + out[c]];
 }
 
+// The same draws (same counter stream, same Floyd positions) with the chosen
+// positions held in registers: k <= KMAX, the draw loop unrolled so the
+// membership test is a chain of compares against earlier registers instead
+// of re-reading the output row from global memory (the k (k-1) / 2 dependent
+// loads per target made the 6144 x 25 root hop latency-bound: 67 us), and
+// the k column loads of the final mapping issued together.
+template <int KMAX>
+__global__ __launch_bounds__(256) void sample_fanout_norep_reg_kernel(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col, int64_t n_rows,
+    const int32_t *__restrict__ nodes, int64_t n, int32_t k, uint64_t seed, uint64_t offset,
+    int32_t *__restrict__ children) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int32_t *out = children + t * k;
+  const int32_t v = nodes[t];
+  const int64_t beg = (v >= 0 && v < n_rows) ? rowptr[v] : 0;
+  const int64_t deg = (v >= 0 && v < n_rows) ? rowptr[v + 1] - beg : 0;
+  int32_t sel[KMAX];
+  if (deg <= k) {
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c)
+      if (c < k) sel[c] = c < deg ? col[beg + c] : -1;
+  } else {
+    const uint64_t key = mix64(seed);
+#pragma unroll
+    for (int m = 0; m < KMAX; ++m) {
+      if (m < k) {
+        const int64_t j = deg - k + m;
+        const uint64_t r64 = mix64(key ^ (offset + (uint64_t)(t * k + m)));
+        int32_t r = (int32_t)__umul64hi(r64, (uint64_t)(j + 1));  // uniform in [0, j]
+        bool hit = false;
+#pragma unroll
+        for (int q = 0; q < m; ++q) hit |= sel[q] == r;
+        sel[m] = hit ? (int32_t)j : r;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < KMAX; ++c)
+      if (c < k) sel[c] = col[beg + sel[c]];
+  }
+#pragma unroll
+  for (int c = 0; c < KMAX; ++c)
+    if (c < k) out[c] = sel[c];
+}
+
 __global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ table,
                                                           const int32_t *__restrict__ ids, int64_t n,
                                                           int32_t d4, float *__restrict__ out) {
@@ -382,9 +427,18 @@ extern "C" int mirec_sample_fanout_norep(const mirec_csr_t *csr, const int32_t *
   using namespace mirec;
   MIREC_CHECK_ARG(csr && csr->rowptr && csr->col && nodes && children && n >= 0 && k > 0);
   if (n == 0) return MIREC_OK;
-  hipLaunchKernelGGL(sample_fanout_norep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), csr->rowptr, csr->col, csr->n_rows,
-                     nodes, n, k, seed, offset, children);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define MIREC_NOREP(KM)                                                                         \
+  hipLaunchKernelGGL(sample_fanout_norep_reg_kernel<KM>, grid, dim3(256), 0, st, csr->rowptr,  \
+                     csr->col, csr->n_rows, nodes, n, k, seed, offset, children)
+  if (k <= 8) MIREC_NOREP(8);
+  else if (k <= 16) MIREC_NOREP(16);
+  else if (k <= 32) MIREC_NOREP(32);
+  else
+    hipLaunchKernelGGL(sample_fanout_norep_kernel, grid, dim3(256), 0, st, csr->rowptr, csr->col,
+                       csr->n_rows, nodes, n, k, seed, offset, children);
+#undef MIREC_NOREP
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

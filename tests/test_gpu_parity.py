@@ -2151,6 +2151,57 @@ def test_fanout_sampler_without_replacement():
     assert checked_long > 5
 
 
+def _mix64(x: int) -> int:
+    m = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return x ^ (x >> 31)
+
+
+@pytest.mark.parametrize("k", [3, 10, 25, 40])
+def test_fanout_sampler_without_replacement_exact_draws(k):
+    """Every row of mirec_sample_fanout_norep equals Floyd's algorithm on the
+    documented counter stream (draw m of target t: mix64(mix64(seed) ^
+    (offset + t k + m)), mapped to [0, j] by the high product), restated
+    here in Python — the register form (k <= 32) and the generic form
+    (k = 40) give the same rows."""
+    import ctypes
+
+    from furusato_recommend_amd import SyntheticBipartite, _lib
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(300, 60, 9000, seed=4, kind="zipf", test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    rng = np.random.default_rng(k)
+    nodes_h = rng.integers(-1, g.n_nodes + 1, 700).astype(np.int32)  # out-of-range ids too
+    nodes = torch.from_numpy(nodes_h).cuda()
+    seed, offset = 77, 12345
+    ch = torch.empty(nodes.numel() * k, dtype=torch.int32, device="cuda")
+    _lib.check(_lib.lib.mirec_sample_fanout_norep(g.csr_ptr(), nodes.data_ptr(), nodes.numel(), k,
+                                                  ctypes.c_uint64(seed), ctypes.c_uint64(offset),
+                                                  ch.data_ptr(), _lib.stream_handle()), "norep")
+    got = ch.view(-1, k).cpu().numpy()
+    rp, col = g.rowptr_host, g.col_host
+    key = _mix64(seed)
+    n_long = 0
+    for t, v in enumerate(nodes_h):
+        ok = 0 <= v < g.n_nodes
+        beg = int(rp[v]) if ok else 0
+        deg = int(rp[v + 1]) - beg if ok else 0
+        if deg <= k:
+            want = [int(col[beg + c]) if c < deg else -1 for c in range(k)]
+        else:
+            n_long += 1
+            pos = []
+            for m in range(k):
+                j = deg - k + m
+                r = (_mix64(key ^ (offset + t * k + m)) * (j + 1)) >> 64
+                pos.append(j if r in pos else r)
+            want = [int(col[beg + p]) for p in pos]
+        assert got[t].tolist() == want, (t, v, deg)
+    assert n_long > 20
+
+
 def test_torch_ops_lgcn_propagate_matches_module_and_autograd():
     """torch.ops.mirec.lgcn_propagate == the engine's propagation and its
     registered backward == Âᵀ ȳ (a non-symmetric edge list: the transposed
