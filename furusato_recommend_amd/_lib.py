@@ -196,6 +196,10 @@ SIGNATURES = {
     "mirec_resnorm_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                   c_int32, c_int32, c_float, c_uint64, c_void_p, c_float,
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mirec_gemm_resnorm": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_int32, c_float, c_uint64,
+                                   c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p]),
     "mirec_resnorm_work_floats": (c_int64, [c_int64, c_int32]),
     "mirec_segment_mean": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
                                    c_void_p]),

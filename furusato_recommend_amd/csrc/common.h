@@ -114,6 +114,12 @@ __device__ __forceinline__ float4 drop4(float4 v, uint64_t key, uint64_t idx, ui
   return drop4_hq(v, key + (idx >> 2), thresh, scale);
 }
 
+// The mask key of a launch: the host key, mixed with *key_base (device, a
+// captured graph's per-replay seed base) when given.
+__device__ __forceinline__ uint64_t run_key(uint64_t key, const uint64_t *key_base) {
+  return key_base ? mix64(key ^ *key_base) : key;
+}
+
 static inline bool dropout_params(float p, uint64_t seed, uint64_t *key, uint32_t *thresh, float *scale) {
   if (!(p >= 0.f && p < 1.f)) return false;
   *key = mix64(seed ^ 0xA24BAED4963EE407ull);

@@ -79,30 +79,22 @@ struct NtArgs {
   int Ks, Ns, relu, bkn;
 };
 
+// The k loop of gemm_nt (shared by the plain and the LayerNorm epilogues):
+// acc[TM][2] of wave (wm, wn) over output rows [m0, +BM), columns [n0, +128);
+// smem holds (BM + 128) * kLdNT floats.
 template <int BM, int PF, bool BKN>
-#ifndef MIREC_NT_OCC
-#define MIREC_NT_OCC 2
-#endif
-__global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float *__restrict__ A,
-                                                        const float *__restrict__ B,
-                                                        const float *__restrict__ bias,
-                                                        float *__restrict__ C, int64_t n,
-                                                        int Kr, int No, NtArgs fx) {
+__device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict__ A,
+                                            const float *__restrict__ B, int64_t n, int Kr,
+                                            int No, const NtArgs &fx, int64_t m0, int n0,
+                                            f32x16 (&acc)[BM / 64][2]) {
   constexpr int TM = BM / 64;        // 32-row MFMA tiles per wave
   constexpr int QA = BM * kC4 / 256;     // float4 of A per thread per chunk
   constexpr int QB = kTile * kC4 / 256;  // float4 of B per thread per chunk
   static_assert(kChunk * kLdTN <= kTile * kLdNT, "[k][n] B image fits the [n][k] region");
-  __shared__ __attribute__((aligned(16))) float smem[(BM + kTile) * kLdNT];
-  static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
   float *sA = smem, *sB = smem + BM * kLdNT;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
-  // column tile fastest: the column tiles of one row tile run together and
-  // share its A rows through L2
-  const int ncol = No / kTile;
-  const int64_t m0 = (int64_t)(blockIdx.x / ncol) * BM;
-  const int n0 = (int)(blockIdx.x % ncol) * kTile;
   // element e = t + 256 q: row e / kC4, float4 column e % kC4
   float4 ra[PF][QA], rb[PF][QB];
   auto load = [&](float4 (&xa)[QA], float4 (&xb)[QB], int k0) {
@@ -163,7 +155,6 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
       }
     }
   };
-  f32x16 acc[TM][2];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -215,6 +206,30 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
       }
     }
   }
+}
+
+template <int BM, int PF, bool BKN>
+#ifndef MIREC_NT_OCC
+#define MIREC_NT_OCC 2
+#endif
+__global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float *__restrict__ A,
+                                                        const float *__restrict__ B,
+                                                        const float *__restrict__ bias,
+                                                        float *__restrict__ C, int64_t n,
+                                                        int Kr, int No, NtArgs fx) {
+  constexpr int TM = BM / 64;
+  __shared__ __attribute__((aligned(16))) float smem[(BM + kTile) * kLdNT];
+  static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  // column tile fastest: the column tiles of one row tile run together and
+  // share its A rows through L2
+  const int ncol = No / kTile;
+  const int64_t m0 = (int64_t)(blockIdx.x / ncol) * BM;
+  const int n0 = (int)(blockIdx.x % ncol) * kTile;
+  f32x16 acc[TM][2];
+  nt_mainloop<BM, PF, BKN>(smem, A, B, n, Kr, No, fx, m0, n0, acc);
   // C layout of 32x32: lane holds column i, rows (r & 3) + 8 (r >> 2) + 4 h.
   // Stored through LDS: each 32x32 block goes to a wave-private [row][col]
   // slab and leaves as float4 rows (4 dwordx4 per lane instead of 16 dword
@@ -255,6 +270,96 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
         if (rbase + rr < n) st4(cb + (rbase + rr) * ldc + cc + 4 * c4, v);
       }
       wave_sync();  // the slab is wave-private
+    }
+  }
+}
+
+// ------------------------------------------------------- gemm + row tail
+// z = A Bᵀ over the whole row (No = d = 128: one column tile) followed in the
+// same workgroup by the SASRec block's row tail of mirec_resnorm_fwd
+// (model/sasrec.py:385-397): pre = res + dropout(z + bias), out = relu?(pre),
+// y = LayerNorm(out).  z never leaves the chip (the unfused pair writes and
+// re-reads it: 2 x 28.8 MB and a launch per stage at C4).  The tile goes
+// to LDS as [row][132]; then 32 lanes per row, one float4 each, with the
+// arithmetic of resnorm_fwd_kernel<32, 1> (same sums in the same order:
+// identical out / y / mean / rstd).
+struct RnArgs {
+  const float *res, *bias, *gamma, *beta;
+  float *out, *y, *mean, *rstd;
+  int relu;
+  uint64_t key;
+  uint32_t thresh;
+  float scale, eps;
+  const uint64_t *key_base;
+};
+
+constexpr int kLdRow = kTile + 4;  // [row][col] stride of the tile image
+
+template <int BM>
+constexpr int rn_lds_floats() {
+  return (BM + kTile) * kLdNT > BM * kLdRow ? (BM + kTile) * kLdNT : BM * kLdRow;
+}
+
+template <int BM>
+__global__ __launch_bounds__(256, 2) void gemm_resnorm_kernel(const float *__restrict__ A,
+                                                              const float *__restrict__ B,
+                                                              int64_t n, int Kr, RnArgs a) {
+  constexpr int TM = BM / 64;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 0};
+  // the residual rows of this thread's lane group (32 lanes per row, one
+  // float4 each) are loaded before the k loop: in flight behind the products
+  const int g = t >> 5, c = 4 * (t & 31);
+  constexpr int RPG = BM / 8;
+  float4 rv[RPG];
+#pragma unroll
+  for (int q = 0; q < RPG; ++q) {
+    const int64_t r = m0 + g + 8 * q;
+    rv[q] = (a.res && r < n) ? ld4(a.res + r * kTile + c) : f4_zero();
+  }
+  f32x16 acc[TM][2];
+  nt_mainloop<BM, 1, false>(smem, A, B, n, Kr, kTile, fx, m0, 0, acc);
+  __syncthreads();  // every wave's reads of the last chunk are done
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * kLdRow + wn * 64 +
+             tn * 32 + i] = acc[tm][tn][r];
+  __syncthreads();
+  const uint64_t key = a.thresh != 0u ? run_key(a.key, a.key_base) : 0ull;
+  const float inv_d = 1.f / (float)kTile;
+  const float4 bia = a.bias ? ld4(a.bias + c) : f4_zero();
+  const float4 gam = a.gamma ? ld4(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+  const float4 bet = a.beta ? ld4(a.beta + c) : f4_zero();
+#pragma unroll
+  for (int q = 0; q < RPG; ++q) {
+    const int rr = g + 8 * q;
+    const int64_t r = m0 + rr;
+    if (r >= n) break;  // whole 32-lane groups (a row each) leave together
+    const int64_t e = r * kTile + c;
+    float4 x = f4_add(ld4(smem + rr * kLdRow + c), bia);
+    if (a.thresh != 0u) x = drop4(x, key, (uint64_t)e, a.thresh, a.scale);
+    if (a.res) x = f4_add(x, rv[q]);
+    if (a.relu)
+      x = make_float4(fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f));
+    if (a.out) st4(a.out + e, x);
+    if (a.y == nullptr) continue;
+    const float mu = group_sum<32>((x.x + x.y) + (x.z + x.w)) * inv_d;
+    const float4 tq = make_float4(x.x - mu, x.y - mu, x.z - mu, x.w - mu);
+    const float rs = rsqrtf(group_sum<32>(f4_dot(tq, tq)) * inv_d + a.eps);
+    const float4 tt = make_float4(rs * tq.x, rs * tq.y, rs * tq.z, rs * tq.w);
+    st4(a.y + e, make_float4(tt.x * gam.x + bet.x, tt.y * gam.y + bet.y, tt.z * gam.z + bet.z,
+                             tt.w * gam.w + bet.w));
+    if ((t & 31) == 0) {
+      a.mean[r] = mu;
+      a.rstd[r] = rs;
     }
   }
 }
@@ -559,4 +664,47 @@ extern "C" int mirec_gemm_tn_ex(const float *A, const float *Amask, const float 
                                 const float *B2, int32_t Ns, float *C, float *colsum, int64_t n,
                                 int32_t M, int32_t No, float *work, mirec_stream_t stream) {
   return gemm_tn(A, Amask, B, B2, Ns, C, colsum, n, M, No, work, stream);
+}
+
+template <int BM>
+static int launch_gemm_resnorm(const float *A, const float *B, int64_t n, int32_t Kr,
+                               const RnArgs &a, hipStream_t st) {
+  constexpr size_t lds = sizeof(float) * rn_lds_floats<BM>();
+  static int rc = -1;  // dynamic LDS above 64 KiB needs the opt-in (once)
+  if (rc < 0)
+    rc = hipFuncSetAttribute((const void *)gemm_resnorm_kernel<BM>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess
+             ? 0
+             : 1;
+  if (rc != 0) return MIREC_ERR_HIP;
+  hipLaunchKernelGGL(gemm_resnorm_kernel<BM>, dim3((unsigned)((n + BM - 1) / BM)), dim3(256), lds,
+                     st, A, B, n, (int)Kr, a);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_gemm_resnorm(const float *A, const float *W, int64_t n, int32_t Kr, int32_t d,
+                                  const float *res, const float *bias, const float *gamma,
+                                  const float *beta, int32_t relu, float dropout_p, uint64_t seed,
+                                  const uint64_t *seed_base, float eps, float *out, float *y,
+                                  float *mean, float *rstd, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(n >= 0 && d == kTile && Kr > 0 && Kr % kChunk == 0);
+  RnArgs a{res, bias, gamma, beta, out, y, mean, rstd, relu ? 1 : 0, 0, 0u, 1.f, eps, seed_base};
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &a.key, &a.thresh, &a.scale));
+  if (n == 0) return MIREC_OK;  // (empty tensors may carry null pointers)
+  MIREC_CHECK_ARG(A && W && out && ((uintptr_t)A | (uintptr_t)W | (uintptr_t)out) % 16 == 0);
+  MIREC_CHECK_ARG(y == nullptr || (mean && rstd && (uintptr_t)y % 16 == 0));
+  MIREC_CHECK_ARG(((uintptr_t)res | (uintptr_t)bias | (uintptr_t)gamma | (uintptr_t)beta) % 16 ==
+                  0);
+  hipStream_t st = (hipStream_t)stream;
+  // the row-tile choice of gemm_nt (one column tile: 128 rows unless that
+  // takes more rounds of the chip's workgroup slots)
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t slots = 2 * (int64_t)std::max(cus, 1);
+  const int64_t t128 = (n + 127) / 128, t64 = (n + 63) / 64;
+  const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
+  if (r64 < r128 || (r64 == r128 && t128 > slots)) return launch_gemm_resnorm<64>(A, W, n, Kr, a, st);
+  return launch_gemm_resnorm<128>(A, W, n, Kr, a, st);
 }

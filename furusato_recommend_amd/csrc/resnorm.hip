@@ -51,10 +51,6 @@ struct BwdArgs {
   const uint64_t *key_base;
 };
 
-// The mask key of a launch: the host key, mixed with *key_base when given.
-__device__ __forceinline__ uint64_t run_key(uint64_t key, const uint64_t *key_base) {
-  return key_base ? mix64(key ^ *key_base) : key;
-}
 
 __device__ __forceinline__ float4 relu_mask(float4 g, float4 v) {
   return make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f,

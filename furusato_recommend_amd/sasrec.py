@@ -20,6 +20,7 @@ The reference hard-codes 8 heads (:211); `heads` is a parameter here
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import NamedTuple
 
 import numpy as np
@@ -28,6 +29,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _lib
+from . import linear as linear_mod
 from ._lib import check, lib
 from .engine import AdamGroup, AdamState, _note_raw_write
 from .linear import Linear, blas_backend, linear, linear_relu
@@ -418,6 +420,107 @@ class _ResNorm(torch.autograd.Function):
         return d_res, d_z, d_bias, d_gamma, d_beta, None, None, None, None, None
 
 
+class _LinearResNorm(torch.autograd.Function):
+    """_ResNorm of z = x Wᵀ with the GEMM and the row tail in one kernel
+    (mirec_gemm_resnorm: z never written).  Backward: mirec_resnorm_bwd
+    (d_res, d_z, d_bias, d_gamma, d_beta — the _ResNorm backward), then the
+    Linear's dX = d_z W and dW = d_zᵀ x (mirec_gemm_nn_ex / mirec_gemm_tn).
+    Returns (out, y); y is None when ``norm`` is False."""
+
+    @staticmethod
+    def forward(ctx, x, w, res, bias, gamma, beta, relu: bool, p: float, eps: float, norm: bool):
+        n, k = x.shape
+        d = w.shape[0]
+        seed = _dropout_seed(p)
+        base = _SEED_BASE if p > 0 else None
+        out = torch.empty(n, d, dtype=x.dtype, device=x.device)
+        y = mean = rstd = None
+        if norm:
+            y = torch.empty_like(out)
+            mean = torch.empty(n, dtype=x.dtype, device=x.device)
+            rstd = torch.empty_like(mean)
+        check(lib.mirec_gemm_resnorm(x.data_ptr(), w.data_ptr(), n, k, d, _ptr(res), _ptr(bias),
+                                     _ptr(gamma), _ptr(beta), int(relu), float(p), seed,
+                                     _ptr(base), float(eps), out.data_ptr(), _ptr(y),
+                                     _ptr(mean), _ptr(rstd), _lib.stream_handle()),
+              "gemm_resnorm")
+        ctx.save_for_backward(x, w, out, mean, rstd, gamma)
+        ctx.cfg = (relu, float(p), seed, res is not None, bias is not None, norm)
+        ctx.seed_base = base
+        ctx.set_materialize_grads(False)
+        return out, y
+
+    @staticmethod
+    def backward(ctx, g_out, g_y):
+        x, w, out, mean, rstd, gamma = ctx.saved_tensors
+        relu, p, seed, has_res, has_bias, norm = ctx.cfg
+        n, d = out.shape
+        k = x.shape[1]
+        need = ctx.needs_input_grad
+        if not norm:
+            g_y = None
+        g_out = None if g_out is None else g_out.contiguous()
+        g_y = None if g_y is None else g_y.contiguous()
+        want_z = need[0] or need[1]
+        d_res = torch.empty_like(out) if (has_res and need[2]) else None
+        d_z = torch.empty_like(out) if want_z else None
+        d_bias = torch.empty(d, dtype=out.dtype, device=out.device) if (has_bias and need[3]) else None
+        d_gamma = d_beta = None
+        if g_y is not None and gamma is not None and need[4]:
+            d_gamma = torch.empty_like(gamma)
+        if g_y is not None and need[5]:
+            d_beta = torch.empty(d, dtype=out.dtype, device=out.device)
+        work = None
+        if d_gamma is not None or d_beta is not None or d_bias is not None:
+            work = torch.empty(int(lib.mirec_resnorm_work_floats(n, d)), dtype=out.dtype,
+                               device=out.device)
+        st = _lib.stream_handle()
+        check(lib.mirec_resnorm_bwd(_ptr(g_y), _ptr(g_out), out.data_ptr(), _ptr(mean),
+                                    _ptr(rstd), _ptr(gamma), n, d, int(relu), p, seed,
+                                    _ptr(ctx.seed_base),
+                                    _ptr(d_res), _ptr(d_z), _ptr(work), _ptr(d_gamma),
+                                    _ptr(d_beta), _ptr(d_bias), st), "resnorm_bwd")
+        if norm and g_y is None:  # y unused downstream: no LayerNorm gradients
+            d_gamma = torch.zeros_like(gamma) if need[4] and gamma is not None else None
+            d_beta = torch.zeros(d, dtype=out.dtype, device=out.device) if need[5] else None
+        dx = dw = None
+        if need[0]:
+            dx = torch.empty_like(x)
+            check(lib.mirec_gemm_nn_ex(d_z.data_ptr(), None, w.data_ptr(), dx.data_ptr(), None, 0,
+                                       n, d, k, st), "gemm_nn_ex(dX)")
+        if need[1]:
+            dw = torch.empty_like(w)
+            work2 = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, d, k)), dtype=w.dtype,
+                                device=w.device)
+            check(lib.mirec_gemm_tn(d_z.data_ptr(), x.data_ptr(), dw.data_ptr(), None, n, d, k,
+                                    work2.data_ptr(), st), "gemm_tn(dW)")
+        return dx, dw, d_res, d_bias, d_gamma, d_beta, None, None, None, None
+
+
+# MIREC_GEMM_RESNORM=0: the GEMM and the row tail as two kernels (A/B)
+FUSE_GEMM_RESNORM = os.environ.get("MIREC_GEMM_RESNORM", "1") != "0"
+
+
+def linear_resnorm(x, w, res, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
+                   p: float = 0.0):
+    """resnorm(res, linear(x, w), bias, norm, relu, p) — one kernel when the
+    shapes are mirec_gemm_resnorm's (2-D aligned contiguous rows, d = 128,
+    in width % 32), else the two-kernel composition."""
+    d = w.shape[0]
+    if (FUSE_GEMM_RESNORM and x.dim() == 2 and d == 128 and x.shape[1] % 32 == 0
+            and w.shape[1] == x.shape[1] and linear_mod._aligned(x, w)
+            and (res is None or (res.shape == (x.shape[0], d) and linear_mod._aligned(res)))
+            and (bias is None or linear_mod._aligned(bias))):
+        if norm is not None:
+            gamma, beta, eps = norm.weight, norm.bias, norm.eps
+        else:
+            gamma = beta = None
+            eps = 0.0
+        return _LinearResNorm.apply(x, w, res, bias, gamma, beta, bool(relu), float(p),
+                                    float(eps), norm is not None)
+    return resnorm(res, linear(x, w), bias, norm, relu=relu, p=p)
+
+
 def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
             p: float = 0.0, keep_out: bool = False):
     """(out, y) of _ResNorm for rows of width d = z.shape[-1] (any leading
@@ -584,12 +687,13 @@ class SASRec(nn.Module):
         L = self.num_layers
         for i in range(L):
             attn = self.attn_layers[i]
-            z = linear(attn.core(y, offsets), attn.out_proj.weight)
-            h, y = resnorm(res, z, attn.out_proj.bias, self.ffn_norm_layers[i], relu=True, p=p)
+            # out-projection / FFN Linear and the stage's row tail in one
+            # kernel each (the biases ride in the row tail)
+            h, y = linear_resnorm(attn.core(y, offsets), attn.out_proj.weight, res,
+                                  attn.out_proj.bias, self.ffn_norm_layers[i], relu=True, p=p)
             ffn = self.ffn_layers[i]
-            f = linear(y, ffn.weight)
             nxt = self.attn_norm_layers[i + 1] if i + 1 < L else None
-            res, y = resnorm(h, f, ffn.bias, nxt, p=p)
+            res, y = linear_resnorm(y, ffn.weight, h, ffn.bias, nxt, p=p)
         return res
 
     def forward_user(self, x, length):

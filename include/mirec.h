@@ -758,6 +758,19 @@ int mirec_resnorm_fwd(const float *res, const float *z, const float *bias, const
                       uint64_t seed, const uint64_t *seed_base, float eps, float *out, float *y,
                       float *mean, float *rstd, mirec_stream_t stream);
 
+/* mirec_resnorm_fwd with z = A Wᵀ computed in the same kernel (A [n, Kr],
+ * W [d, Kr] row-major, d = 128, Kr % 32 == 0): the Linear before a block
+ * stage's row tail (model/sasrec.py:385-397 — attention out-projection and
+ * FFN, their biases passed as `bias`), z never written.  out is required;
+ * every other argument and output as in mirec_resnorm_fwd (identical
+ * values: same per-row arithmetic); the backward is mirec_resnorm_bwd
+ * followed by the Linear's gradients (mirec_gemm_nn_ex / mirec_gemm_tn). */
+int mirec_gemm_resnorm(const float *A, const float *W, int64_t n, int32_t Kr, int32_t d,
+                       const float *res, const float *bias, const float *gamma, const float *beta,
+                       int32_t relu, float dropout_p, uint64_t seed, const uint64_t *seed_base,
+                       float eps, float *out, float *y, float *mean, float *rstd,
+                       mirec_stream_t stream);
+
 /* Floats of scratch mirec_resnorm_bwd needs for parameter gradients. */
 int64_t mirec_resnorm_work_floats(int64_t n, int32_t d);
 

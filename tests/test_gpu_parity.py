@@ -1025,6 +1025,49 @@ def test_resnorm_rows_match_torch(d):
                     assert float(a.abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("k", [128, 256])
+def test_gemm_resnorm_equals_two_kernel_path(k):
+    """mirec_gemm_resnorm (the Linear and the row tail in one kernel) ==
+    linear() then resnorm() bit for bit in the forward (same MFMA k loop,
+    same per-row arithmetic), dropout masks included; gradients of x, W,
+    res, bias, gamma, beta equal the two-node chain.  Row counts around the
+    64 / 128-row tiles, with and without ReLU / LayerNorm / dropout."""
+    from furusato_recommend_amd import sasrec as S
+    from furusato_recommend_amd.linear import linear
+    d = 128
+    for n, relu, norm, p in ((1, True, True, 0.0), (1000, True, True, 0.2),
+                             (56321, False, True, 0.2), (3000, False, False, 0.0),
+                             (70000, True, False, 0.1)):
+        torch.manual_seed(n + k)
+        x = torch.randn(n, k, device="cuda", requires_grad=True)
+        w = (torch.randn(d, k, device="cuda") * k ** -0.5).requires_grad_(True)
+        res = torch.randn(n, d, device="cuda", requires_grad=True)
+        bias = (torch.randn(d, device="cuda") * 0.1).requires_grad_(True)
+        ln = torch.nn.LayerNorm(d, device="cuda") if norm else None
+        if ln is not None:
+            with torch.no_grad():
+                ln.weight.uniform_(0.5, 1.5)
+                ln.bias.uniform_(-0.2, 0.2)
+        torch.manual_seed(7)  # the dropout seed is drawn from torch's CPU generator
+        out1, y1 = S.linear_resnorm(x, w, res, bias, ln, relu=relu, p=p)
+        torch.manual_seed(7)
+        out2, y2 = S.resnorm(res, linear(x, w), bias, ln, relu=relu, p=p)
+        assert torch.equal(out1, out2)
+        assert (y1 is None) == (y2 is None) and (y1 is None or torch.equal(y1, y2))
+        go = torch.randn(n, d, device="cuda")
+        outs1, outs2, gin = [out1], [out2], [go]
+        if norm:
+            gy = torch.randn(n, d, device="cuda")
+            outs1.append(y1)
+            outs2.append(y2)
+            gin.append(gy)
+        leaves = [x, w, res, bias] + ([ln.weight, ln.bias] if norm else [])
+        g1 = torch.autograd.grad(outs1, leaves, gin)
+        g2 = torch.autograd.grad(outs2, leaves, gin)
+        for a, b in zip(g1, g2):
+            assert torch.equal(a, b)
+
+
 def test_resnorm_dropout_mask_is_recomputed():
     """With p > 0: kept entries are scaled by 1/(1-p), the kept fraction is
     1-p, and the backward applies the same mask (d_z = keep * g / (1-p))."""
