@@ -499,11 +499,27 @@ def test_evaluate_matches_oracle():
     out = o.propagated()
     assert rel(m.propagated(), out) < TOL
     ref = oracle_evaluate(out[:ds.n_users], out[ds.n_users:], ds.testDict, ds.allPos, (10, 20))
-    # CPU vs GPU fp32 scores may swap a near-tie at the k-th place: allow one
-    # such flip (1/|test users| on recall/precision/ndcg sums per user).
+    # Every GPU top-20 item against the float64 scores of the oracle's
+    # embeddings (train positives excluded): it is in the exact top-20, or its
+    # score is within fp32 rounding of the exact 20th score (a near-tie).
+    users = np.array(sorted(ds.testDict.keys()), dtype=np.int64)
+    o64 = out.double()
+    s = (o64[users] @ o64[ds.n_users:].T).numpy()
+    for j, u in enumerate(users):
+        s[j, np.asarray(ds.allPos[u], dtype=np.int64)] = -np.inf
+    kth = -np.sort(-s, axis=1)[:, 19]
+    eps = 1e-5 * np.abs(s[np.isfinite(s)]).max()
+    picked = np.take_along_axis(s, top[:, :20].astype(np.int64), axis=1)
+    exact = picked >= kth[:, None]
+    assert np.all(picked >= kth[:, None] - eps)
     n = len(ds.testDict)
+    n_tie_users = int((~exact.all(axis=1)).sum())
+    assert n_tie_users <= max(2, n // 1000), n_tie_users
+    # so a swap can move a user's metrics by at most one hit: the batch sums
+    # agree within the near-tie users' share
     for k in res:
-        assert np.all(np.abs(res[k] - ref[k]) <= 1.5 / n + 1e-9), (k, res[k], ref[k])
+        assert np.all(np.abs(res[k] - ref[k]) <= (n_tie_users + 0.5) / n + 1e-9), (k, res[k],
+                                                                                 ref[k])
 
 
 def test_training_trajectory_and_recall_match_oracle():
@@ -528,7 +544,8 @@ def test_training_trajectory_and_recall_match_oracle():
         lg = float(m.OneEpoch(S[:, 0], S[:, 1], S[:, 2]))
         lo = o.OneEpoch(S[:, 0], S[:, 1], S[:, 2], 1024)
         assert abs(lg - lo) < 1e-4 * abs(lo)
-    assert rel(m.all_embedding.weight, o.emb.detach()) < 1e-3
+    # the north star's 1e-4 rel on the trained tables (measured 1.7e-6)
+    assert rel(m.all_embedding.weight, o.emb.detach()) < 1e-4
     res = evaluate(m, ds.testDict, (20,), batch=1000)
     out = o.propagated()
     ref = oracle_evaluate(out[:ds.n_users], out[ds.n_users:], ds.testDict, ds.allPos, (20,))
