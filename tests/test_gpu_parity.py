@@ -374,6 +374,45 @@ def test_data_parallel_rccl_world1(golden, mode):
         dist.destroy_process_group()
 
 
+def test_dense_grad_sharded_adam_rccl_world1():
+    """DenseGradDataParallel's sharded table Adam through real RCCL calls
+    (reduce_scatter_tensor, in-place all_gather_into_tensor; world_size 1,
+    sharding forced) == the GraphSAGE step with the same materialised table
+    gradient and the full-table Adam, parameters bit for bit."""
+    import socket
+
+    import torch.distributed as dist
+
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    from furusato_recommend_amd.dist import DenseGradDataParallel
+    ds = SyntheticBipartite(20_000, 2_000, 200_000, seed=2)  # table above BUCKET_MIN
+    cfg = {"recdim": 64, "layer": 2, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+           "bpr_batch_size": 256, "fanouts": [10, 5]}
+    torch.manual_seed(3)
+    a = GraphSAGE(cfg, ds)
+    b = GraphSAGE(cfg, ds)
+    b.load_state_dict(a.state_dict())
+    a._tg.dense = b._tg.dense = True  # the materialised table gradient, as under DP
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        dp = DenseGradDataParallel(a, shard_optimizer=True)
+        for i in range(3):
+            u, p, n = a.sample(256, seed=9, offset=256 * i)
+            dp.step(u, p, n)
+            b.stageOne(u, p, n)
+        torch.cuda.synchronize()
+        assert id(a._table) in dp._sharded
+        for x, y in zip(a.parameters(), b.parameters()):
+            assert torch.equal(x, y)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_pruned_step_equals_dense_step_full_size():
     """C2 size: the frontier-pruned training step (only the rows the loss
     depends on) updates E exactly like the full-graph step (fp32 summation
@@ -1906,10 +1945,10 @@ def _dp_rank_lgcn(rank, world, port, fpath, mode, q):
         dist.destroy_process_group()
 
 
-def _dp_rank_autograd(rank, world, port, kind, q):
+def _dp_rank_autograd(rank, world, port, kind, shard, q):
     """One rank of DenseGradDataParallel over the real GraphSAGE / SASRec on
     cuda:0: every rank steps on its own user shard; the gradient all-reduce
-    must keep the replicas identical."""
+    (or the sharded table Adam) must keep the replicas identical."""
     import os
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -1927,7 +1966,8 @@ def _dp_rank_autograd(rank, world, port, kind, q):
                "bpr_batch_size": 256, "heads": 2, "fanouts": [10, 5]}
         m = GraphSAGE(cfg, ds) if kind == "sage" else SASRec(cfg, ds)
         init = [x.detach().cpu().clone() for x in m.parameters()]
-        dp = DenseGradDataParallel(m)
+        dp = DenseGradDataParallel(m, shard_optimizer=shard)
+        assert dp.shard_optimizer == shard
         if rank == 0:
             init = [x.detach().cpu().clone() for x in m.parameters()]
         batches = []
@@ -1944,8 +1984,11 @@ def _dp_rank_autograd(rank, world, port, kind, q):
             batches.append([torch.as_tensor(x).cpu().numpy() for x in (u, p, n)])
             dp.step(u, p, n)
         torch.cuda.synchronize()
+        if shard:
+            dp.gather_optimizer_state()
+        mom = [s.exp_avg.detach().cpu().numpy().copy() for s in m.optims][:1]
         q.put((rank, [x.detach().cpu().numpy().copy() for x in m.parameters()], batches,
-               [x.numpy() for x in init]))
+               [x.numpy() for x in init], mom))
     finally:
         dist.destroy_process_group()
 
@@ -1987,12 +2030,15 @@ def test_data_parallel_two_ranks_hip_engine(golden, mode):
         assert rel(res[0][0][k], f[f"emb_step{k + 1}"]) < TOL
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 @pytest.mark.parametrize("kind", ["sage", "sasrec"])
 def test_dense_grad_data_parallel_two_ranks(kind):
     """DenseGradDataParallel over the real GraphSAGE / SASRec, 2 ranks on one
-    GPU: replicas stay bit-identical and move away from the broadcast init."""
-    res = _run_ranks(_dp_rank_autograd, (kind,))
+    GPU: replicas stay bit-identical and move away from the broadcast init;
+    the sharded table Adam (each rank steps its half of the table's rows,
+    then an in-place all-gather) gives the same parameters bit for bit as
+    the all-reduce + full Adam, and its gathered Adam moments equal theirs."""
+    res = _run_ranks(_dp_rank_autograd, (kind, False))
     p0, p1 = res[0][0], res[1][0]
     assert len(p0) == len(p1)
     for a, b in zip(p0, p1):
@@ -2000,6 +2046,11 @@ def test_dense_grad_data_parallel_two_ranks(kind):
         assert np.all(np.isfinite(a))
     init0 = res[0][2]
     assert any(not np.array_equal(a, b) for a, b in zip(p0, init0))
+    rs = _run_ranks(_dp_rank_autograd, (kind, True))
+    for r in range(2):
+        for a, b in zip(rs[r][0], p0):
+            assert np.array_equal(a, b)
+        assert np.array_equal(rs[r][3][0], res[0][3][0])
 
 
 # ------------------------------------------------------------ sorted table gradient
