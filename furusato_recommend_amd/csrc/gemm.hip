@@ -504,6 +504,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
 // order through LDS (a fixed order: deterministic).  Block 0..M/64 also
 // reduce colsum the same way.
 constexpr int kRedGroups = 16;
+constexpr int kRedU = 16;
 __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__restrict__ work,
                                                               const float *__restrict__ work_cs,
                                                               float *__restrict__ C,
@@ -516,12 +517,33 @@ __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__res
   float4 a = f4_zero();
   float c = 0.f;
   if (e < n4) {
-#pragma unroll 4
-    for (int s = g; s < slices; s += kRedGroups) a = f4_add(a, ld4(work + ((int64_t)s * n4 + e) * 4));
+    // kRedU slices' loads in flight per round (the sum order is unchanged:
+    // s = g, g + 16, ... ascending)
+    for (int s0 = g; s0 < slices; s0 += kRedGroups * kRedU) {
+      float4 x[kRedU];
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) {
+        const int s = s0 + kRedGroups * u;
+        x[u] = s < slices ? ld4(work + ((int64_t)s * n4 + e) * 4) : f4_zero();
+      }
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u)
+        if (s0 + kRedGroups * u < slices) a = f4_add(a, x[u]);
+    }
   }
   const bool do_cs = colsum != nullptr && e < M;
   if (do_cs) {
-    for (int s = g; s < slices; s += kRedGroups) c += work_cs[(int64_t)s * M + e];
+    for (int s0 = g; s0 < slices; s0 += kRedGroups * kRedU) {
+      float x[kRedU];
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u) {
+        const int s = s0 + kRedGroups * u;
+        x[u] = s < slices ? work_cs[(int64_t)s * M + e] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kRedU; ++u)
+        if (s0 + kRedGroups * u < slices) c += x[u];
+    }
   }
   part[g][lane] = a;
   pcs[g][lane] = c;

@@ -224,8 +224,18 @@ __global__ __launch_bounds__(1024) void resnorm_reduce_kernel(const float *__res
   const int cols = 3 * d;
   float acc = 0.f;
   if (j < cols) {
-#pragma unroll 4
-    for (int p = w; p < parts; p += 16) acc += partial[(int64_t)p * cols + j];
+    // 16 partials' loads in flight per round (sum order unchanged)
+    for (int p0 = w; p0 < parts; p0 += 16 * 16) {
+      float x[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int p = p0 + 16 * u;
+        x[u] = p < parts ? partial[(int64_t)p * cols + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (p0 + 16 * u < parts) acc += x[u];
+    }
   }
   red[w][lane] = acc;
   __syncthreads();
