@@ -200,6 +200,14 @@ SIGNATURES = {
                                    c_void_p, c_void_p, c_void_p, c_int32, c_float, c_uint64,
                                    c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p]),
+    "mirec_gemm_nn_resnorm_bwd_work_floats": (c_int64, [c_int64, c_int32]),
+    "mirec_gemm_nn_resnorm_bwd": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int32,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_int32, c_float, c_uint64, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                          c_void_p]),
+    "mirec_resnorm_reduce_partials": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p,
+                                              c_void_p, c_void_p]),
     "mirec_resnorm_work_floats": (c_int64, [c_int64, c_int32]),
     "mirec_segment_mean": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p,
                                    c_void_p]),

@@ -364,6 +364,113 @@ __global__ __launch_bounds__(256, 2) void gemm_resnorm_kernel(const float *__res
   }
 }
 
+// ----------------------------------------------- gemm + row tail backward
+// g_y = A W (W [Kr][d] as stored, d = 128: the input gradient of the next
+// Linear, which is the gradient of this row tail's LayerNorm output) and, in
+// the same workgroup, mirec_resnorm_bwd of that row tail: the tile goes to
+// LDS as [row][132], then 32 lanes per row with resnorm_bwd_kernel<32, 1>'s
+// per-row expressions (d_res / d_z within an ulp: the compiler contracts
+// them differently here); the column sums (d_gamma,
+// d_beta, d_bias) leave as one [3][128] partial per workgroup, added in
+// workgroup order by the resnorm reduce.  g_y never reaches HBM.  The out /
+// g_out rows and the row statistics are loaded before the k loop.
+struct RbArgs {
+  const float *g_out, *out, *mean, *rstd, *gamma;
+  float *d_res, *d_z, *partial;
+  int relu;
+  uint64_t key;
+  uint32_t thresh;
+  float scale;
+  const uint64_t *key_base;
+};
+
+template <int BM>
+constexpr int rb_lds_floats() {
+  return rn_lds_floats<BM>() > 8 * 3 * kTile ? rn_lds_floats<BM>() : 8 * 3 * kTile;
+}
+
+template <int BM>
+__global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__restrict__ A,
+                                                               const float *__restrict__ W,
+                                                               int64_t n, int Kr, RbArgs a) {
+  constexpr int TM = BM / 64;
+  constexpr int RPG = BM / 8;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int g = t >> 5, c = 4 * (t & 31);
+  float4 ov[RPG], gv[RPG];
+  float mv[RPG], sv[RPG];
+#pragma unroll
+  for (int q = 0; q < RPG; ++q) {
+    const int64_t r = m0 + g + 8 * q;
+    const bool ok = r < n;
+    ov[q] = ok ? ld4(a.out + r * kTile + c) : f4_zero();
+    gv[q] = (ok && a.g_out) ? ld4(a.g_out + r * kTile + c) : f4_zero();
+    mv[q] = ok ? a.mean[r] : 0.f;
+    sv[q] = ok ? a.rstd[r] : 0.f;
+  }
+  const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
+  f32x16 acc[TM][2];
+  nt_mainloop<BM, 1, true>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
+  __syncthreads();  // every wave's reads of the last chunk are done
+#pragma unroll
+  for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+    for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        smem[(wm * (BM / 2) + tm * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * kLdRow + wn * 64 +
+             tn * 32 + i] = acc[tm][tn][r];
+  __syncthreads();
+  const uint64_t key = a.thresh != 0u ? run_key(a.key, a.key_base) : 0ull;
+  const float inv_d = 1.f / (float)kTile;
+  const float4 gam = a.gamma ? ld4(a.gamma + c) : make_float4(1.f, 1.f, 1.f, 1.f);
+  float4 pg = f4_zero(), pb = f4_zero(), pz = f4_zero();
+#pragma unroll
+  for (int q = 0; q < RPG; ++q) {
+    const int rr = g + 8 * q;
+    const int64_t r = m0 + rr;
+    if (r >= n) break;  // whole 32-lane groups (a row each) leave together
+    const int64_t e = r * kTile + c;
+    const float4 gy = ld4(smem + rr * kLdRow + c), v = ov[q];
+    const float mu = mv[q], rs = sv[q];
+    const float4 mu4 = make_float4(mu, mu, mu, mu);
+    const float4 xh = f4_scale(rs, f4_sub(v, mu4));
+    const float4 gx = make_float4(gy.x * gam.x, gy.y * gam.y, gy.z * gam.z, gy.w * gam.w);
+    const float m1 = group_sum<32>((gx.x + gx.y) + (gx.z + gx.w)) * inv_d;
+    const float m2 = group_sum<32>(f4_dot(gx, xh)) * inv_d;
+    // dx = rstd * (gx - mean(gx) - xhat * mean(gx * xhat)) (+ g_out)
+    const float4 tq = f4_sub(f4_sub(gx, make_float4(m1, m1, m1, m1)), f4_scale(m2, xh));
+    const float4 gr = f4_fma(rs, tq, gv[q]);
+    pg = f4_add(pg, make_float4(gy.x * xh.x, gy.y * xh.y, gy.z * xh.z, gy.w * xh.w));
+    pb = f4_add(pb, gy);
+    float4 x = a.relu ? make_float4(v.x > 0.f ? gr.x : 0.f, v.y > 0.f ? gr.y : 0.f,
+                                    v.z > 0.f ? gr.z : 0.f, v.w > 0.f ? gr.w : 0.f)
+                      : gr;
+    if (a.d_res) st4(a.d_res + e, x);
+    if (a.thresh != 0u) x = drop4(x, key, (uint64_t)e, a.thresh, a.scale);
+    if (a.d_z) st4(a.d_z + e, x);
+    pz = f4_add(pz, x);
+  }
+  if (a.partial == nullptr) return;  // workgroup-uniform
+  __syncthreads();                   // the tile image is no longer read
+  float *red = smem;                 // [8 groups][3][128]
+  st4(red + (g * 3 + 0) * kTile + c, pg);
+  st4(red + (g * 3 + 1) * kTile + c, pb);
+  st4(red + (g * 3 + 2) * kTile + c, pz);
+  __syncthreads();
+  for (int k = t; k < 3 * kTile; k += 256) {
+    const int kk = k / kTile, col = k - kk * kTile;
+    float sacc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sacc += red[(q * 3 + kk) * kTile + col];
+    a.partial[(int64_t)blockIdx.x * 3 * kTile + k] = sacc;
+  }
+}
+
 // ------------------------------------------------------------------ gemm_tn
 // Workgroup (slice s, tile_m, tile_n): partial C tile over rows
 // [s * rows_per_slice, +rows_per_slice) -> work[s][M][No]; with colsum, the
@@ -729,4 +836,51 @@ extern "C" int mirec_gemm_resnorm(const float *A, const float *W, int64_t n, int
   const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
   if (r64 < r128 || (r64 == r128 && t128 > slots)) return launch_gemm_resnorm<64>(A, W, n, Kr, a, st);
   return launch_gemm_resnorm<128>(A, W, n, Kr, a, st);
+}
+
+// row tile of the fused backward: 64 rows (its preloaded out / g_out rows
+// keep 128-row tiles above the register budget)
+constexpr int kRbBM = 64;
+
+extern "C" int64_t mirec_gemm_nn_resnorm_bwd_work_floats(int64_t n, int32_t d) {
+  if (n < 0 || d != kTile) return -1;
+  return std::max<int64_t>(1, (n + kRbBM - 1) / kRbBM) * 3 * (int64_t)d;
+}
+
+extern "C" int mirec_gemm_nn_resnorm_bwd(const float *A, const float *W, int64_t n, int32_t Kr,
+                                         int32_t d, const float *g_out, const float *out,
+                                         const float *mean, const float *rstd,
+                                         const float *gamma, int32_t relu, float dropout_p,
+                                         uint64_t seed, const uint64_t *seed_base, float *d_res,
+                                         float *d_z, float *work, float *d_gamma, float *d_beta,
+                                         float *d_bias, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(n >= 0 && d == kTile && Kr > 0 && Kr % kChunk == 0);
+  RbArgs a{g_out, out, mean, rstd, gamma, d_res, d_z, work, relu ? 1 : 0, 0, 0u, 1.f, seed_base};
+  MIREC_CHECK_ARG(dropout_params(dropout_p, seed, &a.key, &a.thresh, &a.scale));
+  hipStream_t st = (hipStream_t)stream;
+  const bool sums = d_gamma || d_beta || d_bias;
+  if (n == 0) {  // empty sums; empty tensors may carry null pointers
+    if (d_gamma) MIREC_HIP(hipMemsetAsync(d_gamma, 0, sizeof(float) * d, st));
+    if (d_beta) MIREC_HIP(hipMemsetAsync(d_beta, 0, sizeof(float) * d, st));
+    if (d_bias) MIREC_HIP(hipMemsetAsync(d_bias, 0, sizeof(float) * d, st));
+    return MIREC_OK;
+  }
+  MIREC_CHECK_ARG(A && W && out && mean && rstd && (!sums || work));
+  MIREC_CHECK_ARG(((uintptr_t)A | (uintptr_t)W | (uintptr_t)out | (uintptr_t)g_out |
+                   (uintptr_t)gamma | (uintptr_t)d_res | (uintptr_t)d_z) % 16 == 0);
+  if (!sums) a.partial = nullptr;
+  constexpr size_t lds = sizeof(float) * rb_lds_floats<kRbBM>();
+  static int rc = -1;
+  if (rc < 0)
+    rc = hipFuncSetAttribute((const void *)gemm_nn_rnbwd_kernel<kRbBM>,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess
+             ? 0
+             : 1;
+  if (rc != 0) return MIREC_ERR_HIP;
+  const int64_t grid = (n + kRbBM - 1) / kRbBM;
+  hipLaunchKernelGGL(gemm_nn_rnbwd_kernel<kRbBM>, dim3((unsigned)grid), dim3(256), lds, st, A, W,
+                     n, (int)Kr, a);
+  MIREC_LAUNCH_CHECK();
+  if (sums) return mirec_resnorm_reduce_partials(work, grid, d, d_gamma, d_beta, d_bias, stream);
+  return MIREC_OK;
 }

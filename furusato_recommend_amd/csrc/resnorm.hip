@@ -354,3 +354,15 @@ extern "C" int mirec_resnorm_bwd(const float *g_y, const float *g_out, const flo
   }
   return MIREC_OK;
 }
+
+// The fixed-order column reduce of [parts][3][d] partials (shared with the
+// fused GEMM + row-tail backward, csrc/gemm.hip).
+extern "C" int mirec_resnorm_reduce_partials(const float *work, int64_t parts, int32_t d,
+                                             float *d_gamma, float *d_beta, float *d_bias,
+                                             mirec_stream_t stream) {
+  MIREC_CHECK_ARG(work && parts > 0 && parts <= INT32_MAX && d > 0);
+  resnorm_reduce_kernel<<<(unsigned)((3 * d + 63) / 64), 1024, 0, (hipStream_t)stream>>>(
+      work, (int32_t)parts, d, d_gamma, d_beta, d_bias);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}

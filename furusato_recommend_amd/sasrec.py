@@ -521,6 +521,128 @@ def linear_resnorm(x, w, res, bias=None, norm: nn.LayerNorm | None = None, relu:
     return resnorm(res, linear(x, w), bias, norm, relu=relu, p=p)
 
 
+class _BlockTail(torch.autograd.Function):
+    """Everything of a SASRec layer after the attention core (sasrec.py:
+    390-397) as one node: h, y_f = LR(o W_oᵀ; res, b_o, LN_f, ReLU) and
+    res', y' = LR(y_f W_fᵀ; h, b_f, LN_next), each forward one
+    mirec_gemm_resnorm.  h and y_f are used only inside the node, so the
+    backward can hand the FFN's input gradient straight to the first row
+    tail's backward in the same kernel (mirec_gemm_nn_resnorm_bwd: g_y_f is
+    never written): resnorm_bwd(stage 2) -> dW_f, then [g_y_f = d_z2 W_f ->
+    resnorm_bwd(stage 1)] -> dW_o, dO.  Returns (res', y' or None)."""
+
+    @staticmethod
+    def forward(ctx, o, res, w_o, b_o, g_f, be_f, w_f, b_f, g_n, be_n, p: float, eps_f: float,
+                eps_n: float, has_next: bool):
+        n, k = o.shape
+        d = w_o.shape[0]
+        st = _lib.stream_handle()
+        seeds, base = [], (_SEED_BASE if p > 0 else None)
+
+        def stage(x, w, r, b, gam, bet, relu, eps, norm):
+            seed = _dropout_seed(p)
+            seeds.append(seed)
+            out = torch.empty(n, d, dtype=x.dtype, device=x.device)
+            y = mean = rstd = None
+            if norm:
+                y = torch.empty_like(out)
+                mean = torch.empty(n, dtype=x.dtype, device=x.device)
+                rstd = torch.empty_like(mean)
+            check(lib.mirec_gemm_resnorm(x.data_ptr(), w.data_ptr(), n, x.shape[1], d, r.data_ptr(),
+                                         _ptr(b), _ptr(gam), _ptr(bet), int(relu), float(p), seed,
+                                         _ptr(base), float(eps), out.data_ptr(), _ptr(y),
+                                         _ptr(mean), _ptr(rstd), st), "gemm_resnorm")
+            return out, y, mean, rstd
+
+        h, y_f, mean1, rstd1 = stage(o, w_o, res, b_o, g_f, be_f, True, eps_f, True)
+        res2, y2, mean2, rstd2 = stage(y_f, w_f, h, b_f, g_n, be_n, False, eps_n, has_next)
+        ctx.save_for_backward(o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n)
+        ctx.cfg = (float(p), seeds, has_next, b_o is not None, b_f is not None)
+        ctx.seed_base = base
+        ctx.set_materialize_grads(False)
+        return res2, y2
+
+    @staticmethod
+    def backward(ctx, g_res2, g_y2):
+        o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n = ctx.saved_tensors
+        p, (seed1, seed2), has_next, has_bo, has_bf = ctx.cfg
+        n, d = h.shape
+        k = o.shape[1]
+        st = _lib.stream_handle()
+        base = _ptr(ctx.seed_base)
+        g_res2 = None if g_res2 is None else g_res2.contiguous()
+        g_y2 = None if (g_y2 is None or not has_next) else g_y2.contiguous()
+        f32 = dict(dtype=h.dtype, device=h.device)
+        work = torch.empty(int(lib.mirec_resnorm_work_floats(n, d)), **f32)
+        # stage 2: res' = h + drop(y_f W_fᵀ + b_f), y' = LN_next(res')
+        d_h = torch.empty_like(h)
+        d_z2 = torch.empty_like(h)
+        d_bf = torch.empty(d, **f32) if has_bf else None
+        d_gn = torch.empty(d, **f32) if (g_y2 is not None and g_n is not None) else None
+        d_ben = torch.empty(d, **f32) if g_y2 is not None else None
+        check(lib.mirec_resnorm_bwd(_ptr(g_y2), _ptr(g_res2), res2.data_ptr(), _ptr(mean2),
+                                    _ptr(rstd2), _ptr(g_n), n, d, 0, p, seed2, base,
+                                    d_h.data_ptr(), d_z2.data_ptr(), work.data_ptr(), _ptr(d_gn),
+                                    _ptr(d_ben), _ptr(d_bf), st), "resnorm_bwd(stage 2)")
+        if has_next and g_y2 is None:  # y' unused downstream: no LayerNorm gradients
+            d_gn = torch.zeros_like(g_n) if g_n is not None else None
+            d_ben = torch.zeros(d, **f32)
+        dw_f = torch.empty_like(w_f)
+        work_tn = torch.empty(max(int(lib.mirec_gemm_tn_work_floats(n, d, d)),
+                                  int(lib.mirec_gemm_tn_work_floats(n, d, k))), **f32)
+        check(lib.mirec_gemm_tn(d_z2.data_ptr(), y_f.data_ptr(), dw_f.data_ptr(), None, n, d, d,
+                                work_tn.data_ptr(), st), "gemm_tn(dW_f)")
+        # stage 1 from g_y_f = d_z2 W_f, in one kernel
+        d_res = torch.empty_like(h)
+        d_z1 = torch.empty_like(h)
+        d_bo = torch.empty(d, **f32) if has_bo else None
+        d_gf = torch.empty(d, **f32) if g_f is not None else None
+        d_bef = torch.empty(d, **f32)
+        work1 = torch.empty(int(lib.mirec_gemm_nn_resnorm_bwd_work_floats(n, d)), **f32)
+        check(lib.mirec_gemm_nn_resnorm_bwd(d_z2.data_ptr(), w_f.data_ptr(), n, d, d,
+                                            d_h.data_ptr(), h.data_ptr(), mean1.data_ptr(),
+                                            rstd1.data_ptr(), _ptr(g_f), 1, p, seed1, base,
+                                            d_res.data_ptr(), d_z1.data_ptr(), work1.data_ptr(),
+                                            _ptr(d_gf), d_bef.data_ptr(), _ptr(d_bo), st),
+              "gemm_nn_resnorm_bwd(stage 1)")
+        dw_o = torch.empty_like(w_o)
+        check(lib.mirec_gemm_tn(d_z1.data_ptr(), o.data_ptr(), dw_o.data_ptr(), None, n, d, k,
+                                work_tn.data_ptr(), st), "gemm_tn(dW_o)")
+        do = torch.empty_like(o)
+        check(lib.mirec_gemm_nn_ex(d_z1.data_ptr(), None, w_o.data_ptr(), do.data_ptr(), None, 0,
+                                   n, d, k, st), "gemm_nn_ex(dO)")
+        return (do, d_res, dw_o, d_bo, d_gf, d_bef, dw_f, d_bf, d_gn, d_ben,
+                None, None, None, None)
+
+
+# MIREC_BLOCK_TAIL=0: the two stages as separate linear_resnorm nodes (A/B)
+FUSE_BLOCK_TAIL = os.environ.get("MIREC_BLOCK_TAIL", "1") != "0"
+
+
+def block_tail(o, res, w_o, b_o, norm_f: nn.LayerNorm, w_f, b_f,
+               norm_next: nn.LayerNorm | None, p: float = 0.0):
+    """(res', y') of a layer after its attention core: h, y_f =
+    linear_resnorm(o, W_o, res, b_o, LN_f, ReLU); res', y' =
+    linear_resnorm(y_f, W_f, h, b_f, LN_next) — one autograd node with a
+    fused backward when the shapes are the kernels' (d = 128, aligned
+    contiguous rows), else the two nodes."""
+    d = w_o.shape[0]
+    al = linear_mod._aligned
+    if (FUSE_BLOCK_TAIL and FUSE_GEMM_RESNORM and o.dim() == 2 and d == 128
+            and o.shape[1] % 32 == 0 and w_o.shape[1] == o.shape[1] and w_f.shape == (d, d)
+            and res.shape == (o.shape[0], d) and al(o, w_o, w_f, res)
+            and all(t is None or al(t) for t in (b_o, b_f))):
+        g_n = be_n = None
+        eps_n = 0.0
+        if norm_next is not None:
+            g_n, be_n, eps_n = norm_next.weight, norm_next.bias, norm_next.eps
+        return _BlockTail.apply(o, res, w_o, b_o, norm_f.weight, norm_f.bias, w_f, b_f, g_n,
+                                be_n, float(p), float(norm_f.eps), float(eps_n),
+                                norm_next is not None)
+    h, y = linear_resnorm(o, w_o, res, b_o, norm_f, relu=True, p=p)
+    return linear_resnorm(y, w_f, h, b_f, norm_next, p=p)
+
+
 def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
             p: float = 0.0, keep_out: bool = False):
     """(out, y) of _ResNorm for rows of width d = z.shape[-1] (any leading
@@ -687,13 +809,14 @@ class SASRec(nn.Module):
         L = self.num_layers
         for i in range(L):
             attn = self.attn_layers[i]
-            # out-projection / FFN Linear and the stage's row tail in one
-            # kernel each (the biases ride in the row tail)
-            h, y = linear_resnorm(attn.core(y, offsets), attn.out_proj.weight, res,
-                                  attn.out_proj.bias, self.ffn_norm_layers[i], relu=True, p=p)
+            # out-projection / FFN Linear and each stage's row tail in one
+            # kernel (the biases ride in the row tails), both stages one
+            # autograd node with a fused backward
             ffn = self.ffn_layers[i]
             nxt = self.attn_norm_layers[i + 1] if i + 1 < L else None
-            res, y = linear_resnorm(y, ffn.weight, h, ffn.bias, nxt, p=p)
+            res, y = block_tail(attn.core(y, offsets), res, attn.out_proj.weight,
+                                attn.out_proj.bias, self.ffn_norm_layers[i], ffn.weight,
+                                ffn.bias, nxt, p=p)
         return res
 
     def forward_user(self, x, length):

@@ -771,6 +771,26 @@ int mirec_gemm_resnorm(const float *A, const float *W, int64_t n, int32_t Kr, in
                        float eps, float *out, float *y, float *mean, float *rstd,
                        mirec_stream_t stream);
 
+/* Backward counterpart of mirec_gemm_resnorm: g_y = A W computed in the
+ * kernel (A [n, Kr], W [Kr, d] row-major as stored — the input gradient of
+ * the Linear that consumed this row tail's y — d = 128, Kr % 32 == 0), then
+ * mirec_resnorm_bwd(g_y, g_out, out, mean, rstd, gamma, ...) (the same
+ * per-row expressions; d_gamma / d_beta / d_bias, each optional, summed per 64-row
+ * tile and then in tile order (work: mirec_gemm_nn_resnorm_bwd_work_floats
+ * floats when any sum is asked).  g_y is never written. */
+int64_t mirec_gemm_nn_resnorm_bwd_work_floats(int64_t n, int32_t d);
+int mirec_gemm_nn_resnorm_bwd(const float *A, const float *W, int64_t n, int32_t Kr, int32_t d,
+                              const float *g_out, const float *out, const float *mean,
+                              const float *rstd, const float *gamma, int32_t relu,
+                              float dropout_p, uint64_t seed, const uint64_t *seed_base,
+                              float *d_res, float *d_z, float *work, float *d_gamma,
+                              float *d_beta, float *d_bias, mirec_stream_t stream);
+/* The fixed-order sum of [parts][3][d] column partials into d_gamma /
+ * d_beta / d_bias (each optional): the second pass of the row-tail
+ * backwards. */
+int mirec_resnorm_reduce_partials(const float *work, int64_t parts, int32_t d, float *d_gamma,
+                                  float *d_beta, float *d_bias, mirec_stream_t stream);
+
 /* Floats of scratch mirec_resnorm_bwd needs for parameter gradients. */
 int64_t mirec_resnorm_work_floats(int64_t n, int32_t d);
 

@@ -1081,6 +1081,59 @@ def test_resnorm_rows_match_torch(d):
                     assert float(a.abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("has_next", [True, False])
+def test_block_tail_equals_two_linear_resnorm_nodes(has_next):
+    """The fused layer tail (one node: two mirec_gemm_resnorm forwards, the
+    FFN's input gradient handed to the first row tail's backward inside
+    mirec_gemm_nn_resnorm_bwd) == the two linear_resnorm nodes: forward bit
+    for bit; gradients to fp32 rounding (the second stage's bit for bit; the
+    first stage's row arithmetic is the same expression compiled in another
+    kernel — ~1 ulp — and its column sums run per 64-row tile)."""
+    from furusato_recommend_amd import sasrec as S
+    d = 128
+    for n in (1, 777, 56321):
+        torch.manual_seed(n)
+        o = torch.randn(n, d, device="cuda", requires_grad=True)
+        res = torch.randn(n, d, device="cuda", requires_grad=True)
+        w_o = (torch.randn(d, d, device="cuda") * d ** -0.5).requires_grad_(True)
+        w_f = (torch.randn(d, d, device="cuda") * d ** -0.5).requires_grad_(True)
+        b_o = (torch.randn(d, device="cuda") * 0.1).requires_grad_(True)
+        b_f = (torch.randn(d, device="cuda") * 0.1).requires_grad_(True)
+        ln_f = torch.nn.LayerNorm(d, device="cuda")
+        ln_n = torch.nn.LayerNorm(d, device="cuda") if has_next else None
+        with torch.no_grad():
+            for ln in (ln_f, ln_n):
+                if ln is not None:
+                    ln.weight.uniform_(0.5, 1.5)
+                    ln.bias.uniform_(-0.2, 0.2)
+        outs = []
+        for fuse in (True, False):
+            S.FUSE_BLOCK_TAIL = fuse
+            try:
+                torch.manual_seed(11)  # the dropout seeds come from torch's CPU generator
+                r2, y2 = S.block_tail(o, res, w_o, b_o, ln_f, w_f, b_f, ln_n, p=0.2)
+            finally:
+                S.FUSE_BLOCK_TAIL = True
+            outs.append((r2, y2))
+        (r_a, y_a), (r_b, y_b) = outs
+        assert torch.equal(r_a, r_b)
+        assert (y_a is None) == (y_b is None) and (y_a is None or torch.equal(y_a, y_b))
+        g_r = torch.randn(n, d, device="cuda")
+        g_y = torch.randn(n, d, device="cuda") if has_next else None
+        leaves_row = [o, res, w_o, w_f]
+        leaves_col = [b_o, b_f, ln_f.weight, ln_f.bias] + (
+            [ln_n.weight, ln_n.bias] if has_next else [])
+        grads = []
+        for r2, y2 in outs:
+            ys, gs = [r2], [g_r]
+            if has_next:
+                ys.append(y2)
+                gs.append(g_y)
+            grads.append(torch.autograd.grad(ys, leaves_row + leaves_col, gs))
+        for a, b in zip(grads[0], grads[1]):
+            assert rel(a, b) < 1e-6
+
+
 @pytest.mark.parametrize("k", [128, 256])
 def test_gemm_resnorm_equals_two_kernel_path(k):
     """mirec_gemm_resnorm (the Linear and the row tail in one kernel) ==
