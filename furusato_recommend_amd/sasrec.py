@@ -521,19 +521,97 @@ def linear_resnorm(x, w, res, bias=None, norm: nn.LayerNorm | None = None, relu:
     return resnorm(res, linear(x, w), bias, norm, relu=relu, p=p)
 
 
+def _qkv_grads(g_qkv, y, w_in, has_bias, st):
+    """dW_in = g_qkvᵀ y and db_in = Σ g_qkv (one mirec_gemm_tn pass)."""
+    n, m = g_qkv.shape
+    k = y.shape[1]
+    dw = torch.empty(m, k, dtype=y.dtype, device=y.device)
+    db = torch.empty(m, dtype=y.dtype, device=y.device) if has_bias else None
+    work = torch.empty(int(lib.mirec_gemm_tn_work_floats(n, m, k)), dtype=y.dtype,
+                       device=y.device)
+    check(lib.mirec_gemm_tn(g_qkv.data_ptr(), y.data_ptr(), dw.data_ptr(), _ptr(db), n, m, k,
+                            work.data_ptr(), st), "gemm_tn(dW_in)")
+    return dw, db
+
+
+def _qkv_forward(y, w_in, b_in, st):
+    """qkv = y W_inᵀ + b_in (mirec_gemm_nt)."""
+    n, k = y.shape
+    m = w_in.shape[0]
+    qkv = torch.empty(n, m, dtype=y.dtype, device=y.device)
+    check(lib.mirec_gemm_nt(y.data_ptr(), w_in.data_ptr(), _ptr(b_in), qkv.data_ptr(), n, k, m,
+                            st), "gemm_nt(qkv)")
+    return qkv
+
+
+class _LnQkvHead(torch.autograd.Function):
+    """The first layer's LayerNorm and QKV projection as one node:
+    y = LN_a(x) (mirec_resnorm_fwd), qkv = y W_inᵀ + b_in (mirec_gemm_nt);
+    x is also returned (a view) as the first residual, so its gradient comes
+    back here.  Backward: dW_in, db_in = g_qkvᵀ y, Σ g_qkv; then g_y = g_qkv
+    W_in and the LayerNorm backward (+ the residual's gradient) in one
+    kernel (mirec_gemm_nn_resnorm_bwd: g_y never written).  Returns
+    (x, qkv)."""
+
+    @staticmethod
+    def forward(ctx, x, g_a, b_a, w_in, b_in, eps: float):
+        n, d = x.shape
+        st = _lib.stream_handle()
+        y = torch.empty_like(x)
+        mean = torch.empty(n, dtype=x.dtype, device=x.device)
+        rstd = torch.empty_like(mean)
+        check(lib.mirec_resnorm_fwd(None, x.data_ptr(), None, _ptr(g_a), _ptr(b_a), n, d, 0, 0.0,
+                                    0, None, float(eps), None, y.data_ptr(), mean.data_ptr(),
+                                    rstd.data_ptr(), st), "resnorm_fwd(LN_a)")
+        qkv = _qkv_forward(y, w_in, b_in, st)
+        ctx.save_for_backward(x, y, mean, rstd, g_a, w_in)
+        ctx.has_bias = b_in is not None
+        ctx.set_materialize_grads(False)
+        return x.view_as(x), qkv
+
+    @staticmethod
+    def backward(ctx, g_x, g_qkv):
+        x, y, mean, rstd, g_a, w_in = ctx.saved_tensors
+        n, d = x.shape
+        st = _lib.stream_handle()
+        f32 = dict(dtype=x.dtype, device=x.device)
+        g_x = None if g_x is None else g_x.contiguous()
+        dw_in = db_in = None
+        if g_qkv is None:  # qkv unused downstream: only the residual's gradient
+            return ((torch.zeros_like(x) if g_x is None else g_x),
+                    torch.zeros_like(g_a) if g_a is not None else None,
+                    torch.zeros(d, **f32), torch.zeros_like(w_in), None, None)
+        d_ga = torch.empty_like(g_a) if g_a is not None else None
+        d_ba = torch.empty(d, **f32)
+        dx = torch.empty_like(x)
+        if g_qkv is not None:
+            g_qkv = g_qkv.contiguous()
+            dw_in, db_in = _qkv_grads(g_qkv, y, w_in, ctx.has_bias, st)
+            work = torch.empty(int(lib.mirec_gemm_nn_resnorm_bwd_work_floats(n, d)), **f32)
+            check(lib.mirec_gemm_nn_resnorm_bwd(g_qkv.data_ptr(), w_in.data_ptr(), n,
+                                                w_in.shape[0], d, _ptr(g_x), x.data_ptr(),
+                                                mean.data_ptr(), rstd.data_ptr(), _ptr(g_a), 0,
+                                                0.0, 0, None, dx.data_ptr(), None,
+                                                work.data_ptr(), _ptr(d_ga), d_ba.data_ptr(),
+                                                None, st), "gemm_nn_resnorm_bwd(LN_a)")
+        return dx, d_ga, d_ba, dw_in, db_in, None
+
+
 class _BlockTail(torch.autograd.Function):
     """Everything of a SASRec layer after the attention core (sasrec.py:
     390-397) as one node: h, y_f = LR(o W_oᵀ; res, b_o, LN_f, ReLU) and
     res', y' = LR(y_f W_fᵀ; h, b_f, LN_next), each forward one
-    mirec_gemm_resnorm.  h and y_f are used only inside the node, so the
-    backward can hand the FFN's input gradient straight to the first row
-    tail's backward in the same kernel (mirec_gemm_nn_resnorm_bwd: g_y_f is
-    never written): resnorm_bwd(stage 2) -> dW_f, then [g_y_f = d_z2 W_f ->
-    resnorm_bwd(stage 1)] -> dW_o, dO.  Returns (res', y' or None)."""
+    mirec_gemm_resnorm, and — when the next layer's projection is passed —
+    its qkv' = y' W_inᵀ + b_in.  h and y_f (and y') are used only inside the
+    node, so every input gradient of a Linear here is handed straight to the
+    row tail before it in the same kernel (mirec_gemm_nn_resnorm_bwd: g_y',
+    g_y_f never written): [g_y' = g_qkv' W_in -> resnorm_bwd(stage 2)] (or
+    resnorm_bwd(stage 2) alone) -> dW_f, then [g_y_f = d_z2 W_f ->
+    resnorm_bwd(stage 1)] -> dW_o, dO.  Returns (res', qkv' or y' or None)."""
 
     @staticmethod
-    def forward(ctx, o, res, w_o, b_o, g_f, be_f, w_f, b_f, g_n, be_n, p: float, eps_f: float,
-                eps_n: float, has_next: bool):
+    def forward(ctx, o, res, w_o, b_o, g_f, be_f, w_f, b_f, g_n, be_n, w_in, b_in, p: float,
+                eps_f: float, eps_n: float, has_next: bool):
         n, k = o.shape
         d = w_o.shape[0]
         st = _lib.stream_handle()
@@ -556,37 +634,60 @@ class _BlockTail(torch.autograd.Function):
 
         h, y_f, mean1, rstd1 = stage(o, w_o, res, b_o, g_f, be_f, True, eps_f, True)
         res2, y2, mean2, rstd2 = stage(y_f, w_f, h, b_f, g_n, be_n, False, eps_n, has_next)
-        ctx.save_for_backward(o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n)
-        ctx.cfg = (float(p), seeds, has_next, b_o is not None, b_f is not None)
+        qkv = _qkv_forward(y2, w_in, b_in, st) if w_in is not None else None
+        ctx.save_for_backward(o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n,
+                              y2 if w_in is not None else None, w_in)
+        ctx.cfg = (float(p), seeds, has_next, b_o is not None, b_f is not None,
+                   b_in is not None)
         ctx.seed_base = base
         ctx.set_materialize_grads(False)
-        return res2, y2
+        return res2, (qkv if w_in is not None else y2)
 
     @staticmethod
-    def backward(ctx, g_res2, g_y2):
-        o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n = ctx.saved_tensors
-        p, (seed1, seed2), has_next, has_bo, has_bf = ctx.cfg
+    def backward(ctx, g_res2, g_second):
+        (o, w_o, h, mean1, rstd1, g_f, y_f, w_f, res2, mean2, rstd2, g_n, y2,
+         w_in) = ctx.saved_tensors
+        p, (seed1, seed2), has_next, has_bo, has_bf, has_bin = ctx.cfg
         n, d = h.shape
         k = o.shape[1]
         st = _lib.stream_handle()
         base = _ptr(ctx.seed_base)
         g_res2 = None if g_res2 is None else g_res2.contiguous()
-        g_y2 = None if (g_y2 is None or not has_next) else g_y2.contiguous()
+        g_second = None if (g_second is None or not has_next) else g_second.contiguous()
         f32 = dict(dtype=h.dtype, device=h.device)
-        work = torch.empty(int(lib.mirec_resnorm_work_floats(n, d)), **f32)
         # stage 2: res' = h + drop(y_f W_fᵀ + b_f), y' = LN_next(res')
+        # (+ qkv' = y' W_inᵀ + b_in)
         d_h = torch.empty_like(h)
         d_z2 = torch.empty_like(h)
         d_bf = torch.empty(d, **f32) if has_bf else None
-        d_gn = torch.empty(d, **f32) if (g_y2 is not None and g_n is not None) else None
-        d_ben = torch.empty(d, **f32) if g_y2 is not None else None
-        check(lib.mirec_resnorm_bwd(_ptr(g_y2), _ptr(g_res2), res2.data_ptr(), _ptr(mean2),
-                                    _ptr(rstd2), _ptr(g_n), n, d, 0, p, seed2, base,
-                                    d_h.data_ptr(), d_z2.data_ptr(), work.data_ptr(), _ptr(d_gn),
-                                    _ptr(d_ben), _ptr(d_bf), st), "resnorm_bwd(stage 2)")
-        if has_next and g_y2 is None:  # y' unused downstream: no LayerNorm gradients
+        d_gn = torch.empty(d, **f32) if (g_second is not None and g_n is not None) else None
+        d_ben = torch.empty(d, **f32) if g_second is not None else None
+        dw_in = db_in = None
+        if w_in is not None and g_second is not None:
+            dw_in, db_in = _qkv_grads(g_second, y2, w_in, has_bin, st)
+            work2 = torch.empty(int(lib.mirec_gemm_nn_resnorm_bwd_work_floats(n, d)), **f32)
+            check(lib.mirec_gemm_nn_resnorm_bwd(g_second.data_ptr(), w_in.data_ptr(), n,
+                                                w_in.shape[0], d, _ptr(g_res2), res2.data_ptr(),
+                                                mean2.data_ptr(), rstd2.data_ptr(), _ptr(g_n), 0,
+                                                p, seed2, base, d_h.data_ptr(), d_z2.data_ptr(),
+                                                work2.data_ptr(), _ptr(d_gn), _ptr(d_ben),
+                                                _ptr(d_bf), st), "gemm_nn_resnorm_bwd(stage 2)")
+        else:
+            g_y2 = None if w_in is not None else g_second
+            work = torch.empty(int(lib.mirec_resnorm_work_floats(n, d)), **f32)
+            if g_y2 is None:
+                d_gn = d_ben = None
+            check(lib.mirec_resnorm_bwd(_ptr(g_y2), _ptr(g_res2), res2.data_ptr(), _ptr(mean2),
+                                        _ptr(rstd2), _ptr(g_n), n, d, 0, p, seed2, base,
+                                        d_h.data_ptr(), d_z2.data_ptr(), work.data_ptr(),
+                                        _ptr(d_gn), _ptr(d_ben), _ptr(d_bf), st),
+                  "resnorm_bwd(stage 2)")
+        if has_next and d_ben is None:  # y' unused downstream: no LayerNorm gradients
             d_gn = torch.zeros_like(g_n) if g_n is not None else None
             d_ben = torch.zeros(d, **f32)
+        if w_in is not None and dw_in is None:
+            dw_in = torch.zeros_like(w_in)
+            db_in = torch.zeros(w_in.shape[0], **f32) if has_bin else None
         dw_f = torch.empty_like(w_f)
         work_tn = torch.empty(max(int(lib.mirec_gemm_tn_work_floats(n, d, d)),
                                   int(lib.mirec_gemm_tn_work_floats(n, d, k))), **f32)
@@ -611,36 +712,60 @@ class _BlockTail(torch.autograd.Function):
         do = torch.empty_like(o)
         check(lib.mirec_gemm_nn_ex(d_z1.data_ptr(), None, w_o.data_ptr(), do.data_ptr(), None, 0,
                                    n, d, k, st), "gemm_nn_ex(dO)")
-        return (do, d_res, dw_o, d_bo, d_gf, d_bef, dw_f, d_bf, d_gn, d_ben,
+        return (do, d_res, dw_o, d_bo, d_gf, d_bef, dw_f, d_bf, d_gn, d_ben, dw_in, db_in,
                 None, None, None, None)
 
 
 # MIREC_BLOCK_TAIL=0: the two stages as separate linear_resnorm nodes (A/B)
 FUSE_BLOCK_TAIL = os.environ.get("MIREC_BLOCK_TAIL", "1") != "0"
+# MIREC_FUSE_QKV=0: the QKV projections as their own nodes after each LayerNorm (A/B)
+FUSE_QKV = os.environ.get("MIREC_FUSE_QKV", "1") != "0"
 
 
 def block_tail(o, res, w_o, b_o, norm_f: nn.LayerNorm, w_f, b_f,
-               norm_next: nn.LayerNorm | None, p: float = 0.0):
+               norm_next: nn.LayerNorm | None, p: float = 0.0, next_proj=None):
     """(res', y') of a layer after its attention core: h, y_f =
     linear_resnorm(o, W_o, res, b_o, LN_f, ReLU); res', y' =
     linear_resnorm(y_f, W_f, h, b_f, LN_next) — one autograd node with a
     fused backward when the shapes are the kernels' (d = 128, aligned
-    contiguous rows), else the two nodes."""
+    contiguous rows), else the two nodes.  With ``next_proj`` = (W_in, b_in)
+    of the next layer's attention (and norm_next) it returns (res', qkv' =
+    y' W_inᵀ + b_in) instead, the projection inside the same node."""
     d = w_o.shape[0]
     al = linear_mod._aligned
+    w_in, b_in = next_proj if next_proj is not None else (None, None)
+    if next_proj is not None and norm_next is None:
+        raise ValueError("next_proj needs norm_next (the projection reads LN_next's output)")
     if (FUSE_BLOCK_TAIL and FUSE_GEMM_RESNORM and o.dim() == 2 and d == 128
             and o.shape[1] % 32 == 0 and w_o.shape[1] == o.shape[1] and w_f.shape == (d, d)
             and res.shape == (o.shape[0], d) and al(o, w_o, w_f, res)
-            and all(t is None or al(t) for t in (b_o, b_f))):
+            and all(t is None or al(t) for t in (b_o, b_f))
+            and (w_in is None or (w_in.shape[1] == d and w_in.shape[0] % 128 == 0
+                                  and w_in.shape[0] % 32 == 0 and al(w_in)
+                                  and (b_in is None or al(b_in))))):
         g_n = be_n = None
         eps_n = 0.0
         if norm_next is not None:
             g_n, be_n, eps_n = norm_next.weight, norm_next.bias, norm_next.eps
         return _BlockTail.apply(o, res, w_o, b_o, norm_f.weight, norm_f.bias, w_f, b_f, g_n,
-                                be_n, float(p), float(norm_f.eps), float(eps_n),
+                                be_n, w_in, b_in, float(p), float(norm_f.eps), float(eps_n),
                                 norm_next is not None)
     h, y = linear_resnorm(o, w_o, res, b_o, norm_f, relu=True, p=p)
-    return linear_resnorm(y, w_f, h, b_f, norm_next, p=p)
+    res2, y2 = linear_resnorm(y, w_f, h, b_f, norm_next, p=p)
+    return (res2, linear(y2, w_in, b_in)) if w_in is not None else (res2, y2)
+
+
+def ln_qkv_head(x, norm: nn.LayerNorm, w_in, b_in):
+    """(x, LN(x) W_inᵀ + b_in): the first layer's LayerNorm + QKV projection
+    (x returned as the first residual) — one node with a fused backward
+    (_LnQkvHead) when the shapes are the kernels', else resnorm + linear."""
+    al = linear_mod._aligned
+    d = x.shape[-1]
+    if (FUSE_BLOCK_TAIL and x.dim() == 2 and d == 128 and al(x, w_in)
+            and w_in.shape[1] == d and w_in.shape[0] % 128 == 0 and (b_in is None or al(b_in))):
+        return _LnQkvHead.apply(x, norm.weight, norm.bias, w_in, b_in, float(norm.eps))
+    res, y = resnorm(None, x, norm=norm, keep_out=True)
+    return res, linear(y, w_in, b_in)
 
 
 def resnorm(res, z, bias=None, norm: nn.LayerNorm | None = None, relu: bool = False,
@@ -689,7 +814,10 @@ class CausalSelfAttention(nn.Module):
 
     def core(self, x, offsets=None):
         """The heads' outputs before the out-projection."""
-        qkv = linear(x, self.in_proj_weight, self.in_proj_bias)
+        return self.core_from_qkv(linear(x, self.in_proj_weight, self.in_proj_bias), offsets)
+
+    def core_from_qkv(self, qkv, offsets=None):
+        """core() after the QKV projection (qkv [.., 3d])."""
         if offsets is None:
             return _CausalAttention.apply(qkv, self.heads)
         if isinstance(offsets, Packing):
@@ -803,10 +931,29 @@ class SASRec(nn.Module):
                 x = self.oneblock(x, i, offsets)
             return x
         p = self.dropout.p if self.training else 0.0
+        L = self.num_layers
+        if FUSE_QKV and x.dim() == 2:
+            # every LayerNorm -> QKV projection pair inside one node (the head
+            # node, then each layer tail with the next layer's projection):
+            # the projection's input gradient meets the LayerNorm backward
+            # in one kernel
+            a0 = self.attn_layers[0]
+            res, qkv = ln_qkv_head(x, self.attn_norm_layers[0], a0.in_proj_weight,
+                                   a0.in_proj_bias)
+            for i in range(L):
+                attn, ffn = self.attn_layers[i], self.ffn_layers[i]
+                o = attn.core_from_qkv(qkv, offsets)
+                last = i + 1 == L
+                nxt = None if last else self.attn_norm_layers[i + 1]
+                proj = None if last else (self.attn_layers[i + 1].in_proj_weight,
+                                          self.attn_layers[i + 1].in_proj_bias)
+                res, qkv = block_tail(o, res, attn.out_proj.weight, attn.out_proj.bias,
+                                      self.ffn_norm_layers[i], ffn.weight, ffn.bias, nxt, p=p,
+                                      next_proj=proj)
+            return res
         # the first residual is taken from the LayerNorm node (keep_out): its
         # gradient and the LayerNorm's meet inside one backward kernel
         res, y = resnorm(None, x, norm=self.attn_norm_layers[0], keep_out=True)
-        L = self.num_layers
         for i in range(L):
             attn = self.attn_layers[i]
             # out-projection / FFN Linear and each stage's row tail in one

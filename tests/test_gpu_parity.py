@@ -1081,6 +1081,46 @@ def test_resnorm_rows_match_torch(d):
                     assert float(a.abs().sum()) == 0.0
 
 
+@pytest.mark.parametrize("layers", [1, 2, 3])
+def test_blocks_with_fused_qkv_equal_separate_projections(layers):
+    """SASRec.blocks with every LayerNorm -> QKV projection pair inside one
+    node (_LnQkvHead, _BlockTail with the next layer's projection: the
+    projection's input gradient meets the LayerNorm backward in one kernel)
+    == the same blocks with the projections as their own nodes: forward bit
+    for bit, every parameter and input gradient to fp32 rounding."""
+    from furusato_recommend_amd import SASRec
+    from furusato_recommend_amd import sasrec as S
+
+    class DS:
+        n_users, m_items, allPos = 50, 300, [[1, 2]] * 50
+
+    m = SASRec({"recdim": 128, "layer": layers, "heads": 2, "lr": 1e-3, "decay": 1e-4,
+                "device": "cuda:0", "dropout_p": 0.2}, DS)
+    lens = torch.randint(1, 51, (300,), generator=torch.Generator().manual_seed(layers))
+    offsets = torch.zeros(301, dtype=torch.int32)
+    offsets[1:] = torch.cumsum(lens, 0)
+    offsets = offsets.cuda()
+    n = int(lens.sum())
+    x = torch.randn(n, 128, device="cuda", requires_grad=True)
+    runs = []
+    for fuse in (True, False):
+        S.FUSE_QKV = fuse
+        try:
+            torch.manual_seed(5)  # dropout seeds
+            out = m.blocks(x, offsets)
+        finally:
+            S.FUSE_QKV = True
+        g = torch.randn(out.shape, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1))
+        grads = torch.autograd.grad(out, [x] + list(m.parameters()), g, allow_unused=True)
+        runs.append((out.detach(), grads))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1], runs[1][1]):
+        if a is None or b is None:
+            assert a is None and b is None
+            continue
+        assert rel(a, b) < 1e-6
+
+
 @pytest.mark.parametrize("has_next", [True, False])
 def test_block_tail_equals_two_linear_resnorm_nodes(has_next):
     """The fused layer tail (one node: two mirec_gemm_resnorm forwards, the
