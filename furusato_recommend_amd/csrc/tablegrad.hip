@@ -21,9 +21,10 @@
 //       kBatch rows in flight; runs wholly inside the chunk are final, a
 //       segment continuing into / from a neighbouring chunk goes to that
 //       chunk's partial slot.  Pass 2: the chunk holding a crossing run's
-//       head adds the partials of the chunks the run covers, in chunk order
-//       (a hub id in 10^5 entries is 1.5 K partial rows, read LPR at a time,
-//       not a serial walk over its entries).
+//       head adds the partials of the chunks the run covers, in chunk order,
+//       with every aligned block of 256 chunks inside the run pre-summed by
+//       its own group (pass 2a): a hub id in 1.5 M entries is ~730 block
+//       sums on the head's path, read LPR at a time, not 187 K partial rows.
 //   mirec_adam_table   Adam over the whole table with G formed on the fly
 //       (W, m, v read once, written once; S read for stamped rows only) —
 //       the dense gradient is never written.  Optionally the sums of squares
@@ -221,19 +222,64 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   }
 }
 
-// Pass 2: the group of the chunk holding a crossing run's head adds the
-// partials of the chunks the run covers, in chunk order, and stores the sum.
+// Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
+// wholly inside one run (and the run enters it from before: entries
+// G b kCh - 1 .. G (b+1) kCh - 1 share one row id) -> bsum[b] = the head
+// slots of its G chunks added in chunk order.  Pass 2b then adds one block
+// sum instead of G partial rows, so a hub run of 10^6 entries is ~500 rows
+// on the head group's path, not 10^5 (fixed positions -> fixed order).
+constexpr int kBlockChunks = 256;  // G
+
+__device__ __forceinline__ bool block_in_run(const int32_t *__restrict__ keys, int64_t n, int64_t b,
+                                             int32_t id) {
+  const int64_t e0 = b * kBlockChunks * kCh, e1 = (b + 1) * kBlockChunks * kCh;
+  return e0 >= 1 && e1 <= n && keys[e0 - 1] == id && keys[e1 - 1] == id;
+}
+
+template <int LPR>
+__global__ __launch_bounds__(256) void tg_block_kernel(const int32_t *__restrict__ keys, int64_t n,
+                                                       int32_t d, int32_t n_rows,
+                                                       const float *__restrict__ part,
+                                                       float *__restrict__ bsum) {
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const int64_t b = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  if ((b + 1) * kBlockChunks * kCh > n) return;
+  const int64_t e0 = b * kBlockChunks * kCh;
+  if (e0 < 1) return;
+  const int32_t id = keys[e0 - 1];
+  if (id >= n_rows || keys[(b + 1) * kBlockChunks * kCh - 1] != id) return;
+  for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
+    const int col = c0 + 4 * sub;
+    if (col >= d) continue;
+    float4 sum = f4_zero();
+    for (int j0 = 0; j0 < kBlockChunks; j0 += kBatch) {
+      float4 x[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        x[u] = ld4(part + 2 * (b * kBlockChunks + j0 + u) * (int64_t)d + col);
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) sum = f4_add(sum, x[u]);
+    }
+    st4(bsum + b * (int64_t)d + col, sum);
+  }
+}
+
+// Pass 2b: the group of the chunk holding a crossing run's head adds, in
+// chunk order, its tail slot and the head slots of the chunks the run
+// covers — a whole aligned block of G chunks inside the run as its block sum
+// — and stores the sum.  Lanes test LPR chunks (or blocks) per round.
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict__ keys, int64_t n,
                                                        int32_t d, int32_t n_rows,
                                                        const float *__restrict__ part,
+                                                       const float *__restrict__ bsum,
                                                        float *__restrict__ acc_out,
                                                        int32_t *__restrict__ stamp, int32_t gen) {
   const int lane = threadIdx.x & 63;
   const int sub = lane & (LPR - 1);
   const int base = lane - sub;
   const int64_t chunk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
-  const int64_t n_chunks = (n + kCh - 1) / kCh;
   const int64_t beg = chunk * kCh;
   if (beg >= n) return;
   const int64_t end = beg + kCh;
@@ -242,28 +288,56 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
   const int32_t klast = keys[end - 1];
   const int32_t kn = keys[end];
   const int32_t kp = beg > 0 ? keys[beg - 1] : -1;
-  const int32_t kn2 = end + kCh < n ? keys[end + kCh] : -1;
   if (klast >= n_rows || kn != klast) return;  // last segment stays inside
   if (kp == klast) return;                      // the run's head is earlier
   const unsigned long long gmask = low_bits<LPR>() << base;
+  const unsigned long long low = low_bits<LPR>();
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
-    // this chunk's tail segment + the next chunk's head segment
-    const float4 a = act ? ld4(part + (2 * chunk + 1) * (int64_t)d + col) : f4_zero();
-    const float4 b = act ? ld4(part + (2 * chunk + 2) * (int64_t)d + col) : f4_zero();
-    float4 sum = f4_add(a, b);
-    int64_t cc = chunk + 2;  // chunks cc.. hold the rest of the run (if any)
-    while (kn2 == klast) {   // the run covers chunk + 1 entirely and goes on
-      // lane j: does the run cover all of chunk cc + j and continue past it?
+    float4 sum = act ? ld4(part + (2 * chunk + 1) * (int64_t)d + col) : f4_zero();
+    int64_t cc = chunk + 1;  // the run continues into chunk cc
+    while (true) {
+      if (cc % kBlockChunks == 0) {
+        // block level: lane j tests block cc / G + j (inside the run, and
+        // does the run go on past it?)
+        const int64_t bj = cc / kBlockChunks + sub;
+        const bool in = block_in_run(keys, n, bj, klast);
+        const int64_t ej = (bj + 1) * kBlockChunks * kCh;
+        const bool on = in && ej < n && keys[ej] == klast;
+        const unsigned long long bal = (__ballot(on) & gmask) >> base;
+        const int nfull = bal == low ? LPR : (int)__builtin_ctzll(~bal);
+        const bool in_last = nfull < LPR && __shfl(in ? 1 : 0, base + nfull) != 0;
+        const int take = nfull + (in_last ? 1 : 0);  // + a block the run ends with
+        for (int j0 = 0; j0 < take; j0 += kBatch) {
+          float4 x[kBatch];
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u)
+            x[u] = (act && j0 + u < take)
+                       ? ld4(bsum + (cc / kBlockChunks + j0 + u) * (int64_t)d + col)
+                       : f4_zero();
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u)
+            if (j0 + u < take) sum = f4_add(sum, x[u]);
+        }
+        if (nfull == LPR) {
+          cc += (int64_t)LPR * kBlockChunks;
+          continue;
+        }
+        if (in_last) break;  // the run ends with that block
+        cc += (int64_t)nfull * kBlockChunks;  // the run ends inside block cc / G
+      }
+      // chunk level, up to the next block boundary: lane j: does the run
+      // cover all of chunk cc + j and continue past it?
+      const int64_t to_bound = kBlockChunks - cc % kBlockChunks;
+      const int lim = to_bound < LPR ? (int)to_bound : LPR;
       const int64_t cj = cc + sub;
       const int64_t ej = (cj + 1) * kCh;
-      const bool full = cj < n_chunks && ej < n && keys[ej] == klast;
+      const bool full = sub < lim && ej < n && keys[ej] == klast;
       const unsigned long long bal = (__ballot(full) & gmask) >> base;
-      const unsigned long long low = low_bits<LPR>();
-      // consecutive full chunks from cc
-      const int nfull = bal == low ? LPR : (int)__builtin_ctzll(~bal);
-      const int take = nfull < LPR ? nfull + 1 : LPR;  // + the chunk holding the tail
+      const unsigned long long lmask = lim == 64 ? ~0ull : ((1ull << lim) - 1ull);
+      const int nfull = (bal & lmask) == lmask ? lim : (int)__builtin_ctzll(~bal);
+      const int take = nfull < lim ? nfull + 1 : lim;  // + the chunk holding the tail
       for (int j0 = 0; j0 < take; j0 += kBatch) {
         float4 x[kBatch];
 #pragma unroll
@@ -274,8 +348,8 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
         for (int u = 0; u < kBatch; ++u)
           if (j0 + u < take) sum = f4_add(sum, x[u]);
       }
-      if (nfull < LPR) break;
-      cc += LPR;
+      if (nfull < lim) break;
+      cc += lim;
     }
     if (act) st4(acc_out + (int64_t)klast * d + col, sum);
   }
@@ -409,7 +483,7 @@ static int lanes_per_row(int32_t d) {
 
 struct TgLayout {
   int64_t n_ent, n_tgt, n_chunks;
-  size_t keys_in, keys_out, vals_in, vals_out, wt, part, sort, sort_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, wt, part, bsum, sort, sort_bytes, total;
   int end_bit;
 };
 
@@ -436,7 +510,8 @@ static int tg_layout(const mirec_row_grad_group_t *groups, int32_t n_groups, int
   L->vals_out = 3 * seg;
   L->wt = 4 * seg;
   L->part = L->wt + up(sizeof(float) * std::max<int64_t>(n_tgt, 1));
-  L->sort = L->part + up(sizeof(float) * 2 * std::max<int64_t>(L->n_chunks, 1) * dim);
+  L->bsum = L->part + up(sizeof(float) * 2 * std::max<int64_t>(L->n_chunks, 1) * dim);
+  L->sort = L->bsum + up(sizeof(float) * std::max<int64_t>(L->n_chunks / kBlockChunks, 1) * dim);
   int bits = 1;
   while (bits < 31 && ((int64_t)1 << bits) <= n_rows) ++bits;
   L->end_bit = bits;
@@ -580,6 +655,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   int32_t *vals_out = reinterpret_cast<int32_t *>(ws + L.vals_out);
   float *wt = reinterpret_cast<float *>(ws + L.wt);
   float *part = reinterpret_cast<float *>(ws + L.part);
+  float *bsum = reinterpret_cast<float *>(ws + L.bsum);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t nprep = std::max(L.n_ent, L.n_tgt);
   hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
@@ -589,14 +665,20 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
                                                vals_in, vals_out, (int)L.n_ent, 0, L.end_bit, st));
   const int lpr = lanes_per_row(dim);
   const int64_t threads = L.n_chunks * lpr;
+  const int64_t n_blocks = L.n_chunks / kBlockChunks;
   const dim3 grid((unsigned)((threads + 255) / 256));
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
     hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga, keys_out, vals_out, wt, \
                        L.n_ent, dim, n_rows, acc, stamp, gen, part);                          \
     MIREC_LAUNCH_CHECK();                                                                    \
+    if (n_blocks > 0) {                                                                      \
+      hipLaunchKernelGGL(tg_block_kernel<LP>, dim3((unsigned)((n_blocks * LP + 255) / 256)),  \
+                         dim3(256), 0, st, keys_out, L.n_ent, dim, n_rows, part, bsum);       \
+      MIREC_LAUNCH_CHECK();                                                                  \
+    }                                                                                        \
     hipLaunchKernelGGL(tg_fixup_kernel<LP>, grid, dim3(256), 0, st, keys_out, L.n_ent, dim,   \
-                       n_rows, part, acc, stamp, gen);                                       \
+                       n_rows, part, bsum, acc, stamp, gen);                                 \
     MIREC_LAUNCH_CHECK();                                                                    \
     break;
   switch (lpr) {

@@ -2196,6 +2196,39 @@ def _tg_reference(groups, n_rows, d):
     return acc
 
 
+def test_table_grad_hub_not_serial():
+    """Timing guard for hub rows in the sorted table gradient (the C3 leaf
+    backward on a skewed graph): 1.5 M leaf entries (150 K targets x 10, d =
+    128, dropout) all naming ONE row must cost within 4x of the same entries
+    spread uniformly over 1.1 M rows — a run is cut into fixed chunks whose
+    partials are combined in order, not walked by one wave (which is ~100x
+    slower at this size)."""
+    from furusato_recommend_amd.graphsage import TableGrad
+    n_rows, d, n_t, k = 1_100_000, 128, 150_000, 10
+    g = torch.Generator(device="cuda").manual_seed(5)
+    gr = torch.randn(n_t, d, device="cuda", generator=g)
+    times = {}
+    for kind in ("uniform", "hub"):
+        if kind == "uniform":
+            ids = torch.randint(0, n_rows, (n_t * k,), device="cuda", generator=g).int()
+        else:
+            ids = torch.full((n_t * k,), 12_345, dtype=torch.int32, device="cuda")
+        tg = TableGrad(n_rows, 1_000_000, d, "cuda")
+        groups = [(ids, gr, k, 1, 0.1, 3)]
+        tg.accumulate(groups)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            tg.accumulate(groups)
+            e.record()
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e))
+        times[kind] = sorted(ts)[2]
+    assert times["hub"] < 4.0 * times["uniform"] + 0.05, times
+
+
 @pytest.mark.parametrize("d", [16, 128, 256])
 @pytest.mark.parametrize("hub", [0, 200_000])
 def test_table_grad_sorted_matches_fp64_and_repeats(d, hub):

@@ -70,6 +70,8 @@ def main():
     ap.add_argument("--items", type=int, default=100_000)
     ap.add_argument("--edges", type=int, default=20_000_000)
     ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--kind", choices=("uniform", "zipf"), default="uniform",
+                    help="synthetic graph: uniform (C3) or Zipf item popularity (hub rows)")
     ap.add_argument("--blas", default="", help="torch BLAS backend override (cublas / cublaslt)")
     ap.add_argument("--leaf-bwd", choices=("sorted", "atomic"), default="sorted",
                     help="leaf-hop backward: radix-sorted ordered sums or float atomics")
@@ -87,7 +89,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
     from furusato_recommend_amd.dist import DenseGradDataParallel
-    ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0)
+    ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0, kind=args.kind)
     torch.manual_seed(2020)
     fan = [int(x) for x in args.fanouts.split(",")]
     m = GraphSAGE({"recdim": args.dim, "layer": len(fan), "fanouts": fan, "lr": 1e-3,
@@ -123,7 +125,8 @@ def main():
             "metric": "GraphSAGE BPR positive-edges/sec (C3)", "value": round(world * args.steps * B / dt, 1),
             "unit": "positive-edges/s", "n_gpus": world, "steps": args.steps,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "dtype": "f32",
-            "config": {"workload": "C3: GraphSAGE 2-hop fanout %s d=%d on the C2 graph" % (fan, args.dim),
+            "config": {"workload": "C3: GraphSAGE 2-hop fanout %s d=%d on the C2 graph" % (fan, args.dim)
+                        + ("" if args.kind == "uniform" else " (%s item popularity)" % args.kind),
                        "bpr_batch_per_rank": B, "parallelism": f"dp{world} (dense grad all-reduce)",
                        "leaf_bwd": args.leaf_bwd},
             "cpu_baseline": cpu}),
