@@ -124,23 +124,62 @@ __global__ __launch_bounds__(256) void seed_accum_kernel(
   if (q >= n) return;
   const int32_t node = keys_sorted[q];
   if (q > 0 && keys_sorted[q - 1] == node) return;  // not the head of its run
+  // The run is walked LPR entries per round: lane j decodes entry q0 + j
+  // (source rows and coefficients), then the group loads the rows 8 at a
+  // time and adds them in entry order — the serial walk's exact sequence of
+  // fmas (bitwise equal) without one dependent index chain per entry (a
+  // Zipf-popular item is hundreds of entries of a batch).
+  const int base = lane - sub;
+  const unsigned long long low = LPR == 64 ? ~0ull : ((1ull << LPR) - 1ull);
+  const unsigned long long gmask = low << base;
   float4 gp = f4_zero();
   int cnt = 0;
-  for (int64_t q2 = q; q2 < n && keys_sorted[q2] == node; ++q2) {
-    const int64_t occ = vals_sorted[q2];
-    const int64_t role = occ / batch;
-    const int64_t t = occ - role * batch;
-    const float c = coef[t];
-    if (role == 0) {
-      const float4 on = ld4(out + (n_users + neg[t]) * D + sub * 4);
-      const float4 op = ld4(out + (n_users + pos[t]) * D + sub * 4);
-      gp = f4_fma(c, on, gp);
-      gp = f4_fma(-c, op, gp);
-    } else {
-      const float4 ou = ld4(out + (int64_t)users[t] * D + sub * 4);
-      gp = f4_fma(role == 1 ? -c : c, ou, gp);
+  for (int64_t q0 = q;; q0 += LPR) {
+    const int64_t qj = q0 + sub;
+    const bool in = qj < n && keys_sorted[qj] == node;
+    int32_t ra = -1, rb = -1;
+    float ca = 0.f, cb = 0.f;
+    if (in) {
+      const int64_t occ = vals_sorted[qj];
+      const int64_t role = occ / batch;
+      const int64_t t = occ - role * batch;
+      const float c = coef[t];
+      if (role == 0) {  // the negative's row, then the positive's
+        ra = (int32_t)(n_users + neg[t]);
+        ca = c;
+        rb = (int32_t)(n_users + pos[t]);
+        cb = -c;
+      } else {
+        ra = users[t];
+        ca = role == 1 ? -c : c;
+      }
     }
-    ++cnt;
+    const unsigned long long bal = (__ballot(in) & gmask) >> base;
+    const int m = bal == low ? LPR : (int)__builtin_ctzll(~bal);
+    for (int u0 = 0; u0 < m; u0 += 8) {
+      float4 xa[8], xb[8];
+      float wa[8], wb[8];
+      bool hb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int src = base + ((u0 + u) & (LPR - 1));
+        const int32_t a_row = __shfl(ra, src), b_row = __shfl(rb, src);
+        wa[u] = __shfl(ca, src);
+        wb[u] = __shfl(cb, src);
+        const bool ok = u0 + u < m;
+        xa[u] = ok ? ld4(out + (int64_t)a_row * D + sub * 4) : f4_zero();
+        hb[u] = ok && b_row >= 0;
+        xb[u] = hb[u] ? ld4(out + (int64_t)b_row * D + sub * 4) : f4_zero();
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (u0 + u >= m) break;
+        gp = f4_fma(wa[u], xa[u], gp);
+        if (hb[u]) gp = f4_fma(wb[u], xb[u], gp);
+      }
+    }
+    cnt += m;
+    if (m < LPR) break;
   }
   const float4 e = ld4(emb + (int64_t)node * D + sub * 4);
   float re = decay * ((float)cnt / (float)batch);
