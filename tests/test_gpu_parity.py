@@ -115,6 +115,33 @@ def test_engine_gradient_matches_reference(golden):
     assert int((m.engine.slot != -1).sum()) == 0  # seeds reset
 
 
+def test_engine_gradient_repeated_nodes_vs_oracle(golden):
+    """A batch where one item is the positive of 90 % of the triples and one
+    user appears 40 times (a Zipf-popular item: its seed run spans many
+    rounds of the seed accumulation's LPR-entry walk): the fused backward's
+    table gradient == the CPU oracle's autograd gradient."""
+    from oracle.lightgcn_oracle import OracleLightGCN
+    f = golden("lgcn_d64_L3.npz")
+    B = 200
+    m = lgcn_from(f, batch=B)
+    n_users, m_items = int(f["n_users"]), int(f["m_items"])
+    rng = np.random.default_rng(7)
+    users = rng.integers(0, n_users, B)
+    users[:40] = 3
+    pos = np.where(rng.random(B) < 0.9, 5, rng.integers(0, m_items, B))
+    neg = rng.integers(0, m_items, B)
+    o = OracleLightGCN(f["train_user"], f["train_item"], n_users, m_items, 64, 3,
+                       float(f["lr"]), float(f["decay"]), emb=torch.from_numpy(f["emb0"]))
+    ref = o.grad(torch.from_numpy(users), torch.from_numpy(pos), torch.from_numpy(neg))
+    w = m.all_embedding.weight
+    out = m.engine.forward(w)
+    tc = [torch.from_numpy(a).cuda().int().contiguous() for a in (users, pos, neg)]
+    m.engine.bpr(out, w, *tc, float(f["decay"]))
+    g = torch.empty_like(w)
+    m.engine.backward(w, grad_out=g)
+    assert rel(g, ref) < TOL
+
+
 def test_mf(golden):
     from furusato_recommend_amd import MF
     f = golden("mf_d32.npz")
@@ -307,9 +334,11 @@ def test_full_size_properties(narrow_max):
     assert abs(lhs - rhs) < 1e-4 * max(abs(lhs), 1.0)
 
 
-def test_zipf_long_rows_match_unsplit():
-    """Skewed items force the segment path at default split; results equal
-    the unsplit kernel up to summation order."""
+@pytest.mark.parametrize("d", [32, 64, 256])
+def test_zipf_long_rows_match_unsplit(d):
+    """Skewed items force the segment path at default split (segments +
+    the one-workgroup-per-row finalize, whose lane-group count depends on
+    d); results equal the unsplit kernel up to summation order."""
     from furusato_recommend_amd import Graph, SyntheticBipartite
     from furusato_recommend_amd.engine import PropagationEngine
     ds = SyntheticBipartite(50_000, 5_000, 1_000_000, seed=2, kind="zipf", test_frac=0)
@@ -317,10 +346,10 @@ def test_zipf_long_rows_match_unsplit():
     gb = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0",
                                  split=1 << 30)
     assert ga.n_long > 0 and gb.n_long == 0
-    x = torch.randn(ga.n_nodes, 64, device="cuda")
+    x = torch.randn(ga.n_nodes, d, device="cuda")
     outs = []
     for g in (ga, gb):
-        e = PropagationEngine(g, 64, 3, 64)
+        e = PropagationEngine(g, d, 3, 64)
         outs.append(e.forward(x).clone())
     assert rel(outs[0], outs[1]) < 1e-5
 
