@@ -224,6 +224,8 @@ SIGNATURES = {
                                  c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_norm_terms_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                      c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
+    "mirec_norm_terms_bwd_acc": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32,
+                                         c_void_p, c_void_p, c_void_p]),
     "mirec_seq_sample": (c_int, [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_int64,
                                  c_uint64, c_uint64, c_void_p, c_void_p]),
     "mirec_seq_pack": (c_int, [c_void_p, c_int64, c_void_p, c_int32, c_void_p, c_void_p,

@@ -316,7 +316,8 @@ __global__ __launch_bounds__(1024) void norm_terms_kernel(NormTermArgs a,
 __global__ __launch_bounds__(256) void norm_terms_bwd_kernel(NormTermArgs a,
                                                              const float *__restrict__ norms,
                                                              const float *__restrict__ g_total,
-                                                             float *__restrict__ extra_grad) {
+                                                             float *__restrict__ extra_grad,
+                                                             int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float g = g_total[0];
   const int64_t tot = a.off[a.count];
@@ -325,7 +326,9 @@ __global__ __launch_bounds__(256) void norm_terms_bwd_kernel(NormTermArgs a,
     while (a.off[k + 1] <= i) ++k;
     const int64_t j = i - a.off[k];
     const float nk = norms[k];
-    a.g[k][j] = nk > 0.f ? g * a.w[k] * (a.x[k][j] / nk) : 0.f;
+    const float v = nk > 0.f ? g * a.w[k] * (a.x[k][j] / nk) : 0.f;
+    if (accumulate) a.g[k][j] += v;
+    else a.g[k][j] = v;
   } else if (i < tot + a.n_extra) {
     extra_grad[i - tot] = g * a.ew[i - tot];
   }
@@ -431,11 +434,10 @@ extern "C" int mirec_norm_terms(const float *const *xs, const int64_t *numel, co
   return MIREC_OK;
 }
 
-extern "C" int mirec_norm_terms_bwd(const float *const *xs, float *const *grads,
-                                    const int64_t *numel, const float *weights, int32_t count,
-                                    const float *norms, const float *g_total,
-                                    const float *extra_w, int32_t n_extra, float *extra_grad,
-                                    mirec_stream_t stream) {
+static int norm_terms_bwd(const float *const *xs, float *const *grads, const int64_t *numel,
+                          const float *weights, int32_t count, const float *norms,
+                          const float *g_total, const float *extra_w, int32_t n_extra,
+                          float *extra_grad, int accumulate, mirec_stream_t stream) {
   NormTermArgs a;
   const int rc = norm_args(xs, grads, numel, weights, count, extra_w, n_extra, &a);
   if (rc != MIREC_OK) return rc;
@@ -444,9 +446,26 @@ extern "C" int mirec_norm_terms_bwd(const float *const *xs, float *const *grads,
   const int64_t tot = a.off[count] + n_extra;
   if (tot == 0) return MIREC_OK;
   hipLaunchKernelGGL(norm_terms_bwd_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, a, norms, g_total, extra_grad);
+                     (hipStream_t)stream, a, norms, g_total, extra_grad, accumulate);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
+}
+
+extern "C" int mirec_norm_terms_bwd(const float *const *xs, float *const *grads,
+                                    const int64_t *numel, const float *weights, int32_t count,
+                                    const float *norms, const float *g_total,
+                                    const float *extra_w, int32_t n_extra, float *extra_grad,
+                                    mirec_stream_t stream) {
+  return norm_terms_bwd(xs, grads, numel, weights, count, norms, g_total, extra_w, n_extra,
+                        extra_grad, 0, stream);
+}
+
+extern "C" int mirec_norm_terms_bwd_acc(const float *const *xs, float *const *grads,
+                                        const int64_t *numel, const float *weights,
+                                        int32_t count, const float *norms, const float *g_total,
+                                        mirec_stream_t stream) {
+  return norm_terms_bwd(xs, grads, numel, weights, count, norms, g_total, nullptr, 0, nullptr, 1,
+                        stream);
 }
 
 extern "C" int mirec_zero_tail_rows(float *buf, const int32_t *offsets, int64_t B, int64_t n_rows,

@@ -290,6 +290,7 @@ class _SageLoss(torch.autograd.Function):
                                       x.data_ptr(), loss.data_ptr(), st), "bpr_rows_loss")
         ctx.save_for_backward(out3, x, norms, *small)
         ctx.cfg = (B, d, coef, w_small, w_extra)
+        ctx.small_params = small  # the leaf Parameters (their .grad gets the norm term)
         return loss.view(())
 
     @staticmethod
@@ -305,18 +306,33 @@ class _SageLoss(torch.autograd.Function):
                                           g.data_ptr(), coef, d_out3.data_ptr(),
                                           d_out3[B:].data_ptr(), d_out3[2 * B:].data_ptr(),
                                           g_extra.data_ptr(), st), "bpr_rows_loss_bwd")
-        grads = [torch.empty_like(t) for t in small]
-        n = max(1, len(small))
-        xs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in small])
-        gs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in grads])
-        numel = (ctypes.c_int64 * n)(*[t.numel() for t in small])
-        wk = (ctypes.c_float * n)(*w_small)
         we = (ctypes.c_float * 2)(*w_extra)
         g_norms2 = torch.empty(2, device=out3.device)
-        check(lib.mirec_norm_terms_bwd(xs, gs, numel, wk, len(small), norms.data_ptr(),
-                                       g_extra.data_ptr(), we, 2, g_norms2.data_ptr(), st),
-              "norm_terms_bwd")
-        return (d_out3, g_norms2, None, *grads)
+        check(lib.mirec_norm_terms_bwd(None, None, None, None, 0, None, g_extra.data_ptr(), we, 2,
+                                       g_norms2.data_ptr(), st), "norm_terms_bwd")
+        if not small:
+            return (d_out3, g_norms2, None)
+        # The small parameters' norm gradients are ADDED to their .grad once
+        # the whole backward has run (each Linear parameter also gets its
+        # GEMM gradient, the first layer's twice): one launch instead of an
+        # elementwise add per extra use.
+        params = ctx.small_params
+
+        def add_norm_grads():
+            for p in params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            n = len(params)
+            xs = (ctypes.c_void_p * n)(*[t.data_ptr() for t in small])
+            gs = (ctypes.c_void_p * n)(*[p.grad.data_ptr() for p in params])
+            numel = (ctypes.c_int64 * n)(*[t.numel() for t in small])
+            wk = (ctypes.c_float * n)(*w_small)
+            check(lib.mirec_norm_terms_bwd_acc(xs, gs, numel, wk, n, norms.data_ptr(),
+                                               g_extra.data_ptr(), _lib.stream_handle()),
+                  "norm_terms_bwd_acc")
+
+        torch.autograd.Variable._execution_engine.queue_callback(add_norm_grads)
+        return (d_out3, g_norms2, None, *[None] * len(small))
 
 
 class _FanoutMean(torch.autograd.Function):

@@ -671,6 +671,13 @@ int mirec_norm_terms_bwd(const float *const *xs, float *const *grads, const int6
                          const float *weights, int32_t count, const float *norms,
                          const float *g_total, const float *extra_w, int32_t n_extra,
                          float *extra_grad, mirec_stream_t stream);
+/* The same small-tensor gradients ADDED to grads[k] (the gradients the rest
+ * of the backward already accumulated there): g_k += g * weights[k] * xs[k] /
+ * |xs[k]|.  Run once the backward is done, so a parameter used by several
+ * nodes is not summed by a separate elementwise kernel per use. */
+int mirec_norm_terms_bwd_acc(const float *const *xs, float *const *grads, const int64_t *numel,
+                             const float *weights, int32_t count, const float *norms,
+                             const float *g_total, mirec_stream_t stream);
 
 /* Per-step (positive, negative) pairs of a sequence batch: out[j] = a
  * uniform element of user users[j]'s sequence items[u][0, length[u]) (0 for
