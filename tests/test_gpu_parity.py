@@ -2032,6 +2032,33 @@ def test_c3_full_size_sorted_vs_atomic_and_learns():
     assert torch.isfinite(m._table).all()
 
 
+def test_sage_training_steps_bitwise_repeatable():
+    """Two GraphSAGE models from the same seed, fed the same batches: every
+    parameter (the id table, its Adam moments, the Linear layers) is bitwise
+    equal after three full steps — sampling, dropout, the sorted table
+    gradient (inner rows and leaf means), the hop GEMMs' fixed-order weight
+    gradients and the end-of-backward norm-gradient launch run in fixed
+    orders (no float atomics on the step's path)."""
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    ds = SyntheticBipartite(20_000, 3_000, 300_000, seed=3, kind="zipf", test_frac=0)
+    cfg = {"recdim": 128, "layer": 2, "fanouts": [25, 10], "lr": 1e-3, "decay": 1e-4,
+           "device": "cuda:0", "bpr_batch_size": 512}
+    models = []
+    for _ in range(2):
+        torch.manual_seed(77)
+        m = GraphSAGE(cfg, ds)
+        for i in range(3):
+            u, p, n = m.sample(512, seed=5, offset=i * 512)
+            m.stageOne(u, p, n)
+        models.append(m)
+    a, b = models
+    for x, y in zip(a.parameters(), b.parameters()):
+        assert torch.equal(x, y)
+    assert torch.equal(a._table, b._table)
+    assert torch.equal(a._table_state.exp_avg, b._table_state.exp_avg)
+    assert torch.equal(a._table_state.exp_avg_sq, b._table_state.exp_avg_sq)
+
+
 # ------------------------------------------------------------ multi-rank on one GPU
 def _dp_rank_lgcn(rank, world, port, fpath, mode, q):
     """One rank of the LightGCN data-parallel step on cuda:0 (gloo
