@@ -666,12 +666,14 @@ __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__res
 }
 
 // Row slices of gemm_tn: enough workgroups to fill the chip twice over,
-// at least 128 rows (4 chunks) per slice.  (256 is 3 us faster on the
+// at least 64 rows (2 chunks) per slice.  (256 is 3 us faster on the
 // 56 K x 128 x 128 weight gradient run alone, but the C4 step, whose inputs
-// arrive from the kernels before it, runs 1.45 -> 1.43 ms with 128: two
-// same-box A/B pairs, tools/ab_tn.sh.)
+// arrive from the kernels before it, runs faster with more, shorter slices:
+// 256 -> 128 rows 1.45 -> 1.43 ms (two same-box A/B pairs), 128 -> 64 rows
+// another 1.2 % (three pairs); C3 unchanged (its large weight gradients
+// are not bound by the minimum).  tools/ab_tn.sh, tools/ab_libs.sh.)
 #ifndef MIREC_TN_MINROWS
-#define MIREC_TN_MINROWS 128
+#define MIREC_TN_MINROWS 64
 #endif
 static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
