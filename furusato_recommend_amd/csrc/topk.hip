@@ -225,8 +225,16 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     int64_t n_users, int k, int64_t chunk, float *__restrict__ part_val,
     int32_t *__restrict__ part_idx) {
   constexpr int LD = D + 4;
-  constexpr int KS = D / 2;  // MFMA steps (k = 2 s + h)
-  __shared__ __attribute__((aligned(16))) float sI[2][kStTile * LD];
+  constexpr int KS = D / 2;  // MFMA steps
+  // D > 128: the users' rows live in LDS (their register image would take
+  // D/2 VGPRs) and the B operand is read from there, four k-steps per
+  // float4; the item tile is then single-buffered (LDS 132 KB: one
+  // workgroup per CU).  k-step s of lane half h covers dim 2 s + h (D <= 128)
+  // or dim h·D/2 + s (D > 128); A and B use the same map.
+  constexpr bool UL = D > 128;
+  constexpr int NB = UL ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) float sI[NB][kStTile * LD];
+  __shared__ __attribute__((aligned(16))) float sU[UL ? kStUsers * LD : 4];
   __shared__ float cv[kStUsers][kStCap];
   __shared__ int ci[kStUsers][kStCap];
   __shared__ int cnt[kStUsers];
@@ -243,9 +251,17 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   const int64_t it0 = (int64_t)blockIdx.y * chunk;
   const int64_t it1 = min(m_items, it0 + chunk);
   // the user's embedding as the B operand: ue[s] = U[ub][2 s + h]
-  float ue[KS];
+  float ue[UL ? 1 : KS];
+  if constexpr (!UL) {
 #pragma unroll
-  for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
+    for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
+  } else {
+    for (int e = t; e < kStUsers * D / 4; e += 128) {
+      const int row = e / (D / 4), c4 = e % (D / 4);
+      const int64_t b = (int64_t)blockIdx.x * kStUsers + row;
+      st4(sU + row * LD + 4 * c4, b < n_eval ? ld4(U + b * D + 4 * c4) : f4_zero());
+    }
+  }
   if (t < kStUsers) cnt[t] = 0;
   for (int q = t; q < kStUsers * 8; q += 128) bloom[q / 8][q % 8] = 0u;
   __syncthreads();
@@ -326,9 +342,22 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const float *arow = sI[cur] + i * LD + h;
+    if constexpr (!UL) {
+      const float *arow = sI[cur] + i * LD + h;
 #pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);
+      for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);
+    } else {
+      const float *arow = sI[cur] + i * LD + h * KS;
+      const float *brow = sU + ul * LD + h * KS;
+#pragma unroll 8
+      for (int s4 = 0; s4 < KS / 4; ++s4) {
+        const float4 a = ld4(arow + 4 * s4), bq = ld4(brow + 4 * s4);
+        acc = mfma32x2(a.x, bq.x, acc);
+        acc = mfma32x2(a.y, bq.y, acc);
+        acc = mfma32x2(a.z, bq.z, acc);
+        acc = mfma32x2(a.w, bq.w, acc);
+      }
+    }
     // candidates: acc[r] = score of item base + (r & 3) + 8 (r >> 2) + 4 h for user i
     if (uok) {
 #pragma unroll
@@ -356,9 +385,9 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
         thr_i = __float_as_int(th.y);
       }
     }
-    if (more) stage(cur ^ 1, rg);
+    if (more) stage(UL ? 0 : cur ^ 1, rg);
     __syncthreads();
-    cur ^= 1;
+    if constexpr (!UL) cur ^= 1;
   }
   // final: every user's best k of this chunk
   const int64_t n_chunks = gridDim.y;
@@ -493,7 +522,7 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
   using namespace mirec;
   MIREC_CHECK_ARG(n_eval >= 0 && m_items > 0 && m_items < INT32_MAX && k >= 1 && k <= 32 &&
                   k <= m_items);
-  MIREC_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128);
+  MIREC_CHECK_ARG(dim == 16 || dim == 32 || dim == 64 || dim == 128 || dim == 256);
   MIREC_CHECK_ARG(csr == nullptr || (users && csr->rowptr && csr->col));
   if (n_eval == 0) return MIREC_OK;
   MIREC_CHECK_ARG(user_emb && item_emb && topk_idx && workspace);
@@ -521,6 +550,7 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
     MIREC_ST_CASE(32)
     MIREC_ST_CASE(64)
     MIREC_ST_CASE(128)
+    MIREC_ST_CASE(256)
   }
 #undef MIREC_ST_CASE
   MIREC_LAUNCH_CHECK();

@@ -27,13 +27,20 @@ Gradient exchange modes:
   * ``dense``: SUM all-reduce of the dense gradient dE, then the dense Adam
     kernel (the textbook DDP exchange; kept for comparison).
   * ``sharded``: the sparse exchange, but the last backward layer and its
-    fused Adam run only on this rank's contiguous row shard (N/W rows; the
-    optimizer state of the other rows is not touched here — ZeRO-1 style),
-    then the updated table is all-gathered (N x D x 4 bytes per step, 282 MB
-    at C2) and the next forward re-derives dinv ⊙ E.  It trades the
-    replicated full last layer + Adam (1.6 ms at C2 on every rank) for the
-    all-gather, which pays once xGMI moves the table faster than that
-    (DESIGN.md §6).
+    fused Adam run only on this rank's rows i ≡ rank (mod W) — interleaved,
+    not a contiguous block, so every shard holds its share of short user rows
+    and long item rows; the optimizer state of the other rows is not touched
+    here (ZeRO-1 style) — then the updated table is all-gathered (N x D x 4
+    bytes per step, 282 MB at C2; in row blocks, each block's all-gather
+    overlapping the next block's launch) and the next forward re-derives
+    dinv ⊙ E.  It trades the replicated full last layer + Adam (1.6 ms at C2
+    on every rank) for the all-gather, which pays once xGMI moves the table
+    faster than that.  (DenseGradDataParallel below shards
+    its id tables in contiguous row blocks instead: a reduce-scatter's
+    natural layout.)
+  * ``auto`` (default): ``sparse`` until ``calibrate`` has timed both
+    ``sparse`` and ``sharded`` on the job's own ranks and links, then the
+    faster of the two.
 All modes give the gradient of the union batch; replicas stay bit-identical.
 
 The initial parameters are broadcast from rank 0 (the DDP ctor broadcast,
@@ -47,6 +54,7 @@ from __future__ import annotations
 import ctypes
 import datetime
 import os
+import time
 
 import torch
 import torch.distributed as dist
@@ -68,22 +76,29 @@ def init_distributed(backend: str = "nccl", device: torch.device | None = None,
     dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
-# World size from which "auto" shards the last layer + Adam (DESIGN.md §6:
-# projected per-rank compute at C2, sparse vs sharded, 5.33 vs 4.95 ms at
-# W = 2, 5.72 vs 4.85 at W = 4, 5.98 vs 4.88 at W = 8; the all-gather of the
-# 282 MB table must fit in the difference — at W = 8 it does at >= 260 GB/s of
-# all-gather bandwidth, at W = 2 it would need ~360 GB/s over one xGMI link).
-SHARD_FROM_WORLD = int(os.environ.get("MIREC_SHARD_FROM_WORLD", "8"))
+def _elapsed_ms(events) -> float:
+    """Sum of (start, end) HIP-event intervals in ms (events recorded on the
+    stream the collectives synchronise with)."""
+    return sum(a.elapsed_time(b) for a, b in events)
 
 
 class DataParallel:
-    def __init__(self, engine, emb: torch.Tensor, adam, group=None, mode: str = "auto"):
-        if mode not in ("auto", "sparse", "dense", "sharded"):
+    """See the module docstring.  ``mode="auto"`` runs ``sparse`` until
+    ``calibrate`` has timed both ``sparse`` and ``sharded`` steps on this
+    job's ranks and links and switched to the faster one (the decision and
+    both timings are kept in ``self.calibration``).  ``chunks`` (``sharded``)
+    splits the last backward layer into that many row blocks; the finished
+    rows of each block are all-gathered (``async_op``) while the next block
+    is computed (the exchange overlapped with the last SpMM)."""
+
+    MODES = ("auto", "sparse", "dense", "sharded")
+
+    def __init__(self, engine, emb: torch.Tensor, adam, group=None, mode: str = "auto",
+                 chunks: int | None = None):
+        if mode not in self.MODES:
             raise ValueError(mode)
-        if mode == "auto":
-            w = dist.get_world_size(group) if dist.is_initialized() else 1
-            mode = "sharded" if w >= SHARD_FROM_WORLD else "sparse"
-        self.mode = mode
+        self.requested = mode
+        self.mode = "sparse" if mode == "auto" else mode
         self.engine = engine
         self.emb = emb
         self.adam = adam
@@ -91,61 +106,109 @@ class DataParallel:
         self.distributed = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
-        self.grad = torch.empty_like(emb) if mode == "dense" else None
+        self.n_chunks = max(1, int(os.environ.get("MIREC_SHARD_CHUNKS", "4")
+                                   if chunks is None else chunks))
+        self.grad = None
+        self.calibration = None
+        # HIP-event intervals of the exchange, per step, when a list (bench.py):
+        # (start, end) pairs on the current stream around every collective's
+        # exposed part (blocking calls: the whole collective; the overlapped
+        # table all-gather: from the last chunk's launch to the last unpack)
+        self.comm_events = None
         if self.world > 1:
             dist.broadcast(emb.data, src=0, group=group)
-        if mode == "sharded":
+        if mode in ("sharded", "auto"):
             self._init_shard()
+        self._mark_sharded_state(False)
 
+    # ------------------------------------------------------------ row shards
     def _init_shard(self):
         """This rank's rows i ≡ r (mod W) — interleaved, so every shard gets
         its share of both the short user rows and the long item rows (a
         contiguous split would give rank 0 only users: 0.5 vs 1.3 ms of last
-        layer at W = 2) — as a static byte map + row lists for the last
-        backward layer, and the [W, S, D] staging buffer (S = ceil(N / W))
-        the shards are all-gathered into."""
+        layer at W = 2).  Slot s of rank r is row r + s·W (S = ceil(N / W)
+        slots).  The slots are cut into ``n_chunks`` blocks [s0, s1): block c
+        covers rows [s0·W, s1·W), has its own static row lists (the last
+        backward layer's launch for that block) and its own [W, s1 - s0, D]
+        staging buffer, the output of one all-gather."""
         N, D = self.emb.shape
         W, r = self.world, self.rank
         S = (N + W - 1) // W
+        C = max(1, min(self.n_chunks, S))
+        bounds = [(c * S) // C for c in range(C + 1)]
         words = (N + 15) // 16 * 4
-        bm = torch.zeros(words, dtype=torch.int32, device=self.emb.device)
-        bm.view(torch.uint8)[r:N:W] = 1
-        self._shard_bm = bm
-        self.last_rows = self.engine.static_row_lists(bm)
-        self._stage = torch.empty(W, S, D, dtype=self.emb.dtype, device=self.emb.device) \
-            if W > 1 else None
+        dev = self.emb.device
+        stage = torch.empty(W * S * D, dtype=self.emb.dtype, device=dev) if W > 1 else None
+        self._chunks = []
+        off = 0
+        for c in range(C):
+            s0, s1 = bounds[c], bounds[c + 1]
+            bm = torch.zeros(words, dtype=torch.int32, device=dev)
+            bm.view(torch.uint8)[r + s0 * W: min(s1 * W, N): W] = 1
+            st = None
+            if stage is not None:
+                st = stage[off: off + W * (s1 - s0) * D].view(W, s1 - s0, D)
+                off += W * (s1 - s0) * D
+            self._chunks.append((s0, s1, self.engine.static_row_lists(bm), st))
         self._S = S
+        self.last_rows = [ch[2] for ch in self._chunks]
+
+    def _pack(self, c: int, t: torch.Tensor):
+        s0, s1, _, st = self._chunks[c]
+        N = t.shape[0]
+        r, W = self.rank, self.world
+        rows = t[r + s0 * W: min(s1 * W, N): W]
+        st[r, : rows.shape[0]].copy_(rows)
+
+    def _gather_chunk(self, c: int, async_op: bool):
+        _, _, _, st = self._chunks[c]
+        W, D = self.world, st.shape[2]
+        return dist.all_gather_into_tensor(st.view(-1, D), st[self.rank], group=self.group,
+                                           async_op=async_op)
+
+    def _unpack(self, c: int, t: torch.Tensor):
+        s0, s1, _, st = self._chunks[c]
+        N, D = t.shape
+        W = self.world
+        e = min(s1 * W, N)
+        full = (e - s0 * W) // W  # slots holding all W ranks' rows
+        if full:
+            t[s0 * W: s0 * W + full * W].view(full, W, D).copy_(st[:, :full].transpose(0, 1))
+        for w in range(e - s0 * W - full * W):  # the ragged last row block
+            t[s0 * W + full * W + w].copy_(st[w, full])
 
     def _gather_rows(self, t: torch.Tensor):
         """Every rank's shard rows of ``t`` [N, D] to every rank (in place):
-        pack rows r, r+W, ... into this rank's staging slot, one all-gather,
-        then scatter slot w's rows back to w, w+W, ... (strided copies)."""
+        per block, pack rows r, r+W, ... into this rank's staging slot, one
+        all-gather, then scatter slot w's rows back to w, w+W, ..."""
         if self.world == 1:
             return
-        N, D = t.shape
-        W, S, st = self.world, self._S, self._stage
-        r = self.rank
-        n_r = len(range(r, N, W))
-        st[r, :n_r].copy_(t[r:N:W])
-        dist.all_gather_into_tensor(st.view(W * S, D), st[r], group=self.group)
-        full = N // W  # rows s < full hold all W ranks' entries
-        if full:
-            t[: full * W].view(full, W, D).copy_(st[:, :full].transpose(0, 1))
-        for w in range(N - full * W):  # the ragged last row block
-            t[full * W + w].copy_(st[w, full])
+        for c in range(len(self._chunks)):
+            self._pack(c, t)
+            self._gather_chunk(c, async_op=False)
+            self._unpack(c, t)
+
+    def _mark_sharded_state(self, stale: bool):
+        """Flag the Adam state whose moments are current on this rank's rows
+        only (a state_dict() then raises instead of saving stale moments)."""
+        if self.adam is not None:
+            self.adam.stale_rows = stale
 
     def gather_optimizer_state(self):
-        """``sharded``: each rank's Adam moments are current on its own rows
-        only; bring every row's moments to every rank (e.g. before a
-        checkpoint of the optimizer state)."""
-        if self.mode == "sharded" and self.adam is not None:
+        """After ``sharded`` steps each rank's Adam moments are current on its
+        own rows only; bring every row's moments to every rank (collective:
+        call it on every rank, e.g. before a checkpoint of the optimizer
+        state)."""
+        if self.adam is not None and getattr(self.adam, "stale_rows", False):
             self._gather_rows(self.adam.exp_avg)
             self._gather_rows(self.adam.exp_avg_sq)
+            self._mark_sharded_state(False)
 
     def shard(self):
         """(shard, n_shards) for the on-device sampler."""
         return self.rank, self.world
 
+    # ------------------------------------------------------------ exchange
     def _all_gather(self, t: torch.Tensor) -> torch.Tensor:
         out = torch.empty((self.world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype,
                           device=t.device)
@@ -162,6 +225,34 @@ class DataParallel:
         return (allrec[:, 0].contiguous().view(torch.int32), allrec[:, 1:1 + D].contiguous(),
                 allrec[:, 1 + D:].contiguous())
 
+    def _event(self):
+        if self.comm_events is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _note(self, a, b):
+        if a is not None:
+            self.comm_events.append((a, b))
+
+    def exchange_bytes_per_rank(self, batch: int, mode: str | None = None) -> int:
+        """Bytes one rank receives per step in ``mode`` (default: the current
+        one): the seed records of the other W-1 ranks (3B x (1 + 2D) floats
+        each), plus in ``sharded`` the other ranks' table rows ((W-1)/W of
+        N x D floats), in ``dense`` a ring all-reduce's 2(W-1)/W of the
+        gradient."""
+        mode = mode or self.mode
+        N, D = self.emb.shape
+        W = self.world
+        table = N * D * self.emb.element_size()
+        seeds = (W - 1) * 3 * batch * (1 + 2 * D) * 4
+        if mode == "sparse":
+            return seeds
+        if mode == "sharded":
+            return seeds + (W - 1) * table // W
+        return 2 * (W - 1) * table // W
+
     def step(self, users, pos, neg, decay: float, loss_accum=None):
         eng = self.engine
         out = eng.forward_for_batch(self.emb, users, pos, neg)
@@ -170,20 +261,108 @@ class DataParallel:
         if self.mode in ("sparse", "sharded"):
             keys, rows_p, rows_e = eng.export_seeds()
             if self.distributed:
+                a = self._event()
                 keys, rows_p, rows_e = self._exchange(keys, rows_p, rows_e)
+                self._note(a, self._event())
             eng.import_seeds(keys, rows_p, rows_e)
             if self.mode == "sparse":
                 eng.backward(self.emb, adam=self.adam)
             else:
-                eng.backward(self.emb, adam=self.adam, last_rows=self.last_rows)
-                self._gather_rows(self.emb)
+                works = []
+                overlap = self.world > 1
+
+                def on_chunk(c):
+                    if overlap:
+                        self._pack(c, self.emb)
+                        works.append(self._gather_chunk(c, async_op=True))
+                eng.backward(self.emb, adam=self.adam, last_rows=self.last_rows,
+                             on_chunk=on_chunk)
+                a = self._event()
+                for c, w in enumerate(works):
+                    w.wait()
+                    self._unpack(c, self.emb)
+                self._note(a, self._event())
                 eng.invalidate_prescaled()
+                self._mark_sharded_state(self.world > 1)
         else:
+            if self.grad is None:
+                self.grad = torch.empty_like(self.emb)
             eng.backward(self.emb, grad_out=self.grad)
             if self.distributed:
+                a = self._event()
                 dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.group)
+                self._note(a, self._event())
             eng.adam_step(self.emb, self.grad, self.adam)
         return loss
+
+    # ------------------------------------------------------------ auto mode
+    def _max_over_ranks(self, x: float) -> float:
+        if not self.distributed:
+            return x
+        dev = self.emb.device if dist.get_backend(self.group) == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return float(t.item())
+
+    def time_table_allgather(self, reps: int = 3) -> float:
+        """Best-of-``reps`` ms of the sharded mode's table all-gather alone
+        (every block, blocking, no packing), max over ranks: the link rate
+        the ``sharded`` mode pays (algbw = N·D·4 B / this)."""
+        if self.world == 1:
+            return 0.0
+        best = float("inf")
+        for _ in range(reps):
+            torch.cuda.synchronize()  # (a CUDA table: time_table_allgather is GPU-only)
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record()
+            for c in range(len(self._chunks)):
+                self._gather_chunk(c, async_op=False)
+            b.record()
+            torch.cuda.synchronize()
+            best = min(best, a.elapsed_time(b))
+        return self._max_over_ranks(best)
+
+    def _measure(self, mode: str, run_step, steps: int) -> float:
+        """Wall ms per step of ``steps`` steps (after a barrier), max over ranks."""
+        torch.cuda.synchronize()
+        dist.barrier(group=self.group)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run_step()
+        torch.cuda.synchronize()
+        return self._max_over_ranks(1e3 * (time.perf_counter() - t0) / steps)
+
+    def calibrate(self, run_step, steps: int = 2, measure=None) -> dict | None:
+        """``auto``: run ``steps`` timed training steps (after one untimed
+        one) in ``sparse`` and in ``sharded`` mode — ``run_step()`` performs
+        one ``self.step`` on a fresh batch — take the max over ranks of each
+        mode's time per step, switch to the faster mode and record both, with
+        the table all-gather alone, in ``self.calibration``.  Every mode
+        computes the union batch's update, so the steps taken here are
+        ordinary training steps.  A no-op (None) unless mode was "auto" and
+        W > 1.  ``measure(mode, run_step, steps) -> ms`` replaces the wall
+        clock (tests)."""
+        if self.requested != "auto" or self.world == 1:
+            return None
+        measure = measure or self._measure
+        ms = {}
+        for m in ("sparse", "sharded"):
+            self.mode = m
+            run_step()
+            ms[m] = float(measure(m, run_step, steps))
+        choice = min(ms, key=ms.get)
+        self.mode = choice
+        self.gather_optimizer_state()  # no-op unless leaving sharded moments behind
+        ag = self.time_table_allgather() if self.emb.is_cuda else 0.0
+        table = self.emb.numel() * self.emb.element_size()
+        self.calibration = {"sparse_ms_per_step": round(ms["sparse"], 4),
+                            "sharded_ms_per_step": round(ms["sharded"], 4),
+                            "steps_per_mode": steps, "choice": choice,
+                            "table_allgather_ms": round(ag, 4),
+                            "table_allgather_algbw_GBps":
+                                round(table / (ag * 1e-3) / 1e9, 2) if ag > 0 else None}
+        return self.calibration
 
 
 class DenseGradDataParallel:
@@ -257,6 +436,7 @@ class DenseGradDataParallel:
         dist.all_gather_into_tensor(pf, pf[lo:lo + n], group=self.group)
         p.grad = None
         self._sharded.add(id(p))
+        st.stale_rows = self.world > 1
         tg = getattr(self.model, "_tg", None)
         if tg is not None:
             tg.pending = False  # the step of the table gradient is done
@@ -273,6 +453,7 @@ class DenseGradDataParallel:
                     n = f.numel() // self.world
                     dist.all_gather_into_tensor(f, f[self.rank * n:(self.rank + 1) * n].clone(),
                                                 group=self.group)
+                st.stale_rows = False
 
     def _allreduce(self):
         if not self.distributed:

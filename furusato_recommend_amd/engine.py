@@ -85,6 +85,9 @@ class AdamState:
         self.n_steps = 0
         self.exp_avg = torch.zeros_like(param)
         self.exp_avg_sq = torch.zeros_like(param)
+        # set by a data-parallel wrapper that updates this state on its own
+        # row shard only (the other rows' moments are stale until gathered)
+        self.stale_rows = False
 
     def next_hparams(self):
         self.n_steps += 1
@@ -120,6 +123,9 @@ class AdamState:
 
     def state_dict(self, param_id: int = 0) -> dict:
         """Same structure as torch.optim.Adam.state_dict() for one param."""
+        if self.stale_rows:
+            raise RuntimeError("Adam moments are sharded over the data-parallel ranks: call "
+                               "gather_optimizer_state() on every rank before state_dict()")
         return {
             "state": {param_id: {"step": torch.tensor(float(self.n_steps)),
                                  "exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq}},
@@ -302,6 +308,10 @@ class PropagationEngine:
         # for by a fused-Adam backward (which emits it for free); forward()
         # skips the prescale pass when the table is unchanged since.
         self._x0s_token = None
+        # token of the table whose FULL layer mean ``acc`` holds (None after a
+        # pruned forward or any update): repeated getUsersRating calls of one
+        # evaluation reuse it instead of re-propagating
+        self._acc_full = None
 
     # ------------------------------------------------------------ internals
     def _ensure_ws(self, batch: int):
@@ -458,8 +468,10 @@ class PropagationEngine:
         """Forget the cached dinv ⊙ E.  Needed only after writing the table
         through ``.data`` (invisible to the tensor's version counter) between
         training steps; in-place torch ops, ``load_state_dict`` and
-        re-assignment are detected."""
+        re-assignment are detected.  Also drops the cached full propagation
+        (forward_cached)."""
         self._x0s_token = None
+        self._acc_full = None
 
     def prescale(self, x: torch.Tensor, out: torch.Tensor):
         check(lib.mirec_prescale(x.data_ptr(), self.g.dinv.data_ptr(), self.g.n_nodes, self.dim,
@@ -473,8 +485,10 @@ class PropagationEngine:
         computed (valid only on S).  Returns the engine's ``acc`` buffer
         (valid until the next call)."""
         L = self.L
+        self._acc_full = None
         if L == 0:
             self.acc.copy_(emb)
+            self._acc_full = self._token(emb)
             return self.acc
         if pruned and not self._masks_ready:
             raise RuntimeError("forward(pruned=True) needs compute_frontier() first")
@@ -498,7 +512,17 @@ class PropagationEngine:
                        out=self.acc,
                        xs_out=None if last else self.xs[(l - 1) % 2],
                        **rows)
+        if not pruned:
+            self._acc_full = self._token(emb)
         return self.acc
+
+    def forward_cached(self, emb: torch.Tensor) -> torch.Tensor:
+        """``forward(emb)``, or ``acc`` as it stands when it already holds the
+        full layer mean of this table (no update, pruned forward or other
+        write since)."""
+        if self._acc_full is not None and self._acc_full == self._token(emb):
+            return self.acc
+        return self.forward(emb)
 
     def propagate_once(self, x: torch.Tensor, out: torch.Tensor, graph: Graph | None = None):
         """out = Â x (one LGConv call)."""
@@ -584,16 +608,20 @@ class PropagationEngine:
 
     # ------------------------------------------------------------- backward
     def backward(self, emb: torch.Tensor, adam: AdamState | None = None,
-                 grad_out: torch.Tensor | None = None, last_rows: dict | None = None):
+                 grad_out: torch.Tensor | None = None, last_rows=None, on_chunk=None):
         """Horner backward from the current seeds (g_L = d, g_l = d + Â g_{l+1}).
 
         With ``adam`` the last layer applies Adam to ``emb`` in place (fused);
         otherwise the dense gradient dLoss/dE is written to ``grad_out``.
         ``last_rows`` (static_row_lists) restricts the last layer — and so the
         update — to a fixed row set (a data-parallel rank's shard); the other
-        rows of ``emb`` and of the next step's dinv ⊙ E are left alone."""
+        rows of ``emb`` and of the next step's dinv ⊙ E are left alone.  A
+        list of row sets runs the last layer as one launch per set, calling
+        ``on_chunk(i)`` after launch i (dist.py overlaps the all-gather of
+        block i with the launch of block i + 1)."""
         if (adam is None) == (grad_out is None):
             raise ValueError("exactly one of adam / grad_out")
+        self._acc_full = None
         if self._seeds is None or not self._masks_ready:
             raise RuntimeError("backward() needs bpr() (or import_seeds()) first")
         L = self.L
@@ -606,10 +634,15 @@ class PropagationEngine:
                 final.update(xs_out=self.x0s)
         else:
             final.update(out=grad_out)
-        if last_rows is not None:
-            final.update(last_rows)
+        chunks = list(last_rows) if isinstance(last_rows, (list, tuple)) else [last_rows]
+
+        def last_layer(**kw):
+            for c, rows in enumerate(chunks):
+                self._prop(**kw, **final, **(rows or {}))
+                if on_chunk is not None:
+                    on_chunk(c)
         if L == 0:
-            self._prop(in_mode=IN_NONE, seed=seed_p, **final)
+            last_layer(in_mode=IN_NONE, seed=seed_p)
         else:
             for l in range(L - 1, -1, -1):
                 first = l == L - 1
@@ -628,10 +661,10 @@ class PropagationEngine:
                               in_mask=self.bm_hop if (self.prune and l == L - 2) else None)
                 kw["seed"] = seed_p
                 if l == 0:
-                    kw.update(final)
+                    last_layer(**kw)
                 else:
                     kw.update(xs_out=self.xs[(L - 1 - l) % 2])
-                self._prop(**kw)
+                    self._prop(**kw)
         if self.sparse_filter == "dense" and L > 0:
             self._dense_seeds(seed_p, 1)
         check(lib.mirec_bpr_seed_reset(self.slot.data_ptr(), keys_sorted.data_ptr(), n_keys,
@@ -643,6 +676,7 @@ class PropagationEngine:
 
     def adam_step(self, param: torch.Tensor, grad: torch.Tensor, adam: AdamState):
         _note_raw_write()  # the table changes behind its version counter
+        self._acc_full = None
         hp = adam.next_hparams()
         check(lib.mirec_adam_dense(param.data_ptr(), grad.data_ptr(), adam.exp_avg.data_ptr(),
                                    adam.exp_avg_sq.data_ptr(), param.numel(), ctypes.byref(hp),

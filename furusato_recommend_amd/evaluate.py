@@ -3,11 +3,12 @@
 The layer-mean embeddings are propagated ONCE per evaluation with the HIP
 engine (the reference re-propagates per 10 000-user batch through
 getUsersRating, model/lgcn.py:120-125).  Per batch of users, for a model
-with ``eval_embeddings`` (LightGCN) and k <= 32: mirec_score_topk streams
+with ``eval_embeddings`` (LightGCN, MF) and k <= 32: mirec_score_topk streams
 the scores U_b · Iᵀ through MFMA tiles straight into per-user top-k
 candidates, the train positives at -1024 (trainer.py:132-138) — the
-[batch, M] rating matrix is never written.  Otherwise (MF's sigmoid
-ratings, k > 32): rating = U_b · Iᵀ (library GEMM, as the reference's
+[batch, M] rating matrix is never written (MF's sigmoid ratings rank like
+its raw scores: sigmoid is monotone).  Otherwise (k > 32, or a width
+outside STREAM_DIMS): rating = U_b · Iᵀ (library GEMM, as the reference's
 torch.matmul), then mirec_topk_masked masks in place and selects.  Metric
 sums on the host with the reference formulas (metric.py:60-103).
 """
@@ -38,7 +39,7 @@ def topk_masked(rating: torch.Tensor, users: torch.Tensor, graph, k: int,
     return val, idx
 
 
-STREAM_DIMS = (16, 32, 64, 128)
+STREAM_DIMS = (16, 32, 64, 128, 256)
 STREAM_MAX_K = 32
 
 

@@ -111,11 +111,18 @@ class LightGCN(nn.Module):
 
     @torch.no_grad()
     def propagated(self) -> torch.Tensor:
-        """Full layer-mean embeddings [N, D] (no autograd)."""
-        return self.engine.forward(self.all_embedding.weight)
+        """Full layer-mean embeddings [N, D] (no autograd; the engine's
+        buffer, valid until the next engine call).  Propagates only when the
+        table changed since the last full propagation."""
+        return self.engine.forward_cached(self.all_embedding.weight)
 
     @torch.no_grad()
     def getUsersRating(self, users):
+        """model/lgcn.py:120-125.  The reference re-propagates the whole graph
+        on every call — once per 10 000-user batch of Trainer.test
+        (trainer.py:130); here the propagation is reused while the table is
+        unchanged, so an unchanged reference Trainer.test propagates once
+        per evaluation."""
         out = self.propagated()
         users_emb = out[users.long()]
         items_emb = out[self.num_users:]

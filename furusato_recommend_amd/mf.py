@@ -63,6 +63,15 @@ class MF(nn.Module):
     def propagated(self) -> torch.Tensor:
         return self._table
 
+    def eval_embeddings(self):
+        """(user rows, item rows): the operands of the streaming evaluation
+        (evaluate.score_topk).  The reference ranks sigmoid(U Iᵀ)
+        (model/MF.py:56-60); sigmoid is monotone, so the top-k of the raw
+        scores is a top-k of the ratings — where fp32 sigmoid saturates to
+        equal values, torch.topk may break the tie either way and the raw
+        score breaks it here."""
+        return self._table[: self.num_users], self._table[self.num_users:]
+
     def sample(self, n_triples: int, seed: int, offset: int = 0, shard: int = 0,
                n_shards: int = 1):
         """On-device UniformSample: int32 (users, pos, neg) device tensors."""

@@ -6,7 +6,10 @@ wrapped with its autograd formula), on top of the same C ABI
 Operator arguments must be tensors and scalars, so a graph (its CSR, the
 normalisation and the hub-row split of ``graph.Graph``) is passed as an
 integer handle: ``handle(graph)`` registers it (weakly: the entry goes when
-the Graph object does) and returns the id.
+the Graph object does) and returns the id.  The autograd node of a call keeps
+the Graph object itself alive until the backward has run (a temporary
+``LGConv()``, or one module called on a second edge_index before the first
+call's backward, would otherwise drop the only other reference).
 
     h = ops.handle(graph)
     y = torch.ops.mirec.lgcn_propagate(x, h)          # y = Â x
@@ -78,15 +81,15 @@ def _(x, graph):
 
 
 def _setup(ctx, inputs, output):
-    ctx.graph = inputs[1]
+    ctx.graph_obj = _graph(inputs[1])  # strong reference for the node's lifetime
 
 
 def _bwd(ctx, grad):
-    return torch.ops.mirec.lgcn_propagate_t(grad.contiguous(), ctx.graph), None
+    return torch.ops.mirec.lgcn_propagate_t(grad.contiguous(), handle(ctx.graph_obj)), None
 
 
 def _bwd_t(ctx, grad):
-    return torch.ops.mirec.lgcn_propagate(grad.contiguous(), ctx.graph), None
+    return torch.ops.mirec.lgcn_propagate(grad.contiguous(), handle(ctx.graph_obj)), None
 
 
 lgcn_propagate.register_autograd(_bwd, setup_context=_setup)

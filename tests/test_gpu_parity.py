@@ -519,7 +519,7 @@ def test_topk_masked_matches_torch():
         assert torch.equal(val, rv)
 
 
-@pytest.mark.parametrize("d", [16, 32, 64, 128])
+@pytest.mark.parametrize("d", [16, 32, 64, 128, 256])
 def test_score_topk_streaming_matches_exact_topk(d):
     """mirec_score_topk (scores streamed through MFMA tiles into per-user
     candidate lists, never materialised) == the exact masked top-k: integer
@@ -588,6 +588,99 @@ def test_evaluate_matches_oracle():
     for k in res:
         assert np.all(np.abs(res[k] - ref[k]) <= (n_tie_users + 0.5) / n + 1e-9), (k, res[k],
                                                                                  ref[k])
+
+
+def _near_tie_check(s, top, k, n_users_total):
+    """Every picked item of every row of ``top`` [n, >= k] is in the exact
+    top-k of the float64 scores ``s`` (train positives at -inf) or within
+    fp32 rounding of the exact k-th score; returns the number of rows with
+    such a near-tie pick (bounded by the caller)."""
+    kth = -np.sort(-s, axis=1)[:, k - 1]
+    eps = 1e-5 * np.abs(s[np.isfinite(s)]).max()
+    picked = np.take_along_axis(s, top[:, :k].astype(np.int64), axis=1)
+    assert np.all(picked >= kth[:, None] - eps)
+    return int((~(picked >= kth[:, None]).all(axis=1)).sum())
+
+
+def test_mf_c1_size_epoch_and_streamed_evaluation():
+    """BASELINE config C1 at its stated size (model/MF.py:35-112, README.md
+    5-core): 10 000 users x 1 000 items, 4 train + 1 test item per user,
+    d = 32, N(0, 1) init.  One OneEpoch over the reference sampler's triples
+    (negative_sample.py:98-134, numpy seed 2020) == OracleMF (loss, both
+    tables at 1e-4), then evaluate() — the streamed top-k of the raw scores,
+    no rating matrix — against the reference's ranking of sigmoid(U Iᵀ) with
+    train positives at -1024 (trainer.py:115-170) on the oracle's tables."""
+    from furusato_recommend_amd import MF, FiveCore
+    from furusato_recommend_amd.evaluate import evaluate
+    from oracle.lightgcn_oracle import OracleMF, get_label, ndcg_at_k, recall_precision_at_k
+    from oracle.lightgcn_oracle import uniform_sample
+    ds = FiveCore(10_000, 1_000, 5, seed=0)
+    cfg = {"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+           "bpr_batch_size": 2048}
+    torch.manual_seed(2020)
+    m = MF(cfg, ds)
+    o = OracleMF(m.embedding_user.weight.cpu(), m.embedding_item.weight.cpu(), 1e-3, 1e-4)
+    np.random.seed(2020)
+    S = uniform_sample(ds.n_users, ds.m_items, ds.allPos, ds.trainDataSize)
+    assert len(S) == 40_000
+    lg = float(m.OneEpoch(torch.from_numpy(S[:, 0]), torch.from_numpy(S[:, 1]),
+                          torch.from_numpy(S[:, 2])))
+    acc = 0.0
+    for i in range(0, len(S), 2048):
+        acc += o.stageOne(S[i:i + 2048, 0], S[i:i + 2048, 1], S[i:i + 2048, 2])
+    lo = acc / (len(S) // 2048 + 1)
+    assert abs(lg - lo) < TOL * abs(lo)
+    assert rel(m.embedding_user.weight, o.user.detach()) < TOL
+    assert rel(m.embedding_item.weight, o.item.detach()) < TOL
+    res, top = evaluate(m, ds.testDict, (10, 20), return_topk=True)
+    users = np.array(sorted(ds.testDict.keys()))
+    raw = (o.user.detach().double()[users] @ o.item.detach().double().T).numpy()
+    sig = 1.0 / (1.0 + np.exp(-raw))
+    for j, u in enumerate(users):
+        sig[j, ds.allPos[u]] = -np.inf
+    n_tie = _near_tie_check(sig, top, 20, len(users))
+    assert n_tie <= max(2, len(users) // 1000), n_tie
+    # the reference's own metric sums on the float32 sigmoid ranking
+    rating = torch.sigmoid(o.user.detach()[users] @ o.item.detach().T)
+    for j, u in enumerate(users):
+        rating[j, ds.allPos[u]] = -(1 << 10)
+    ref_top = torch.topk(rating, k=20).indices.numpy()
+    gt = [ds.testDict[u] for u in users]
+    r = get_label(gt, ref_top)
+    for j, k in enumerate((10, 20)):
+        ref_recall = recall_precision_at_k(gt, r, k)["recall"] / len(users)
+        ref_ndcg = ndcg_at_k(gt, r, k) / len(users)
+        assert abs(res["recall"][j] - ref_recall) <= (n_tie + 0.5) / len(users)
+        assert abs(res["ndcg"][j] - ref_ndcg) <= (n_tie + 0.5) / len(users)
+
+
+def test_users_rating_propagates_once_per_table_version():
+    """getUsersRating (model/lgcn.py:120-125) is called once per 10 000-user
+    batch by the reference Trainer.test (trainer.py:130): the propagation is
+    reused while the table is unchanged, recomputed after a training step
+    and after an in-place write, and always equals a fresh propagation."""
+    from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    ds = SyntheticBipartite(3000, 500, 30_000, seed=3, test_frac=0)
+    m = LightGCN({"recdim": 32, "layer": 3, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+                  "bpr_batch_size": 256}, ds)
+    calls = []
+    fwd = m.engine.forward
+    m.engine.forward = lambda *a, **k: (calls.append(1), fwd(*a, **k))[1]
+    users = torch.arange(0, 3000, 3, device="cuda")
+    r1 = m.getUsersRating(users[:500]).clone()
+    m.getUsersRating(users[500:])
+    assert len(calls) == 1
+    m.stageOne(*m.sample(256, seed=1))
+    r2 = m.getUsersRating(users[:500]).clone()
+    assert len(calls) == 3  # the step's own (pruned) forward + one full propagation
+    assert not torch.equal(r1, r2)
+    with torch.no_grad():
+        m.all_embedding.weight.mul_(0.5)
+    r3 = m.getUsersRating(users[:500])
+    assert len(calls) == 4
+    m.engine.forward = fwd
+    fresh = m.engine.forward(m.all_embedding.weight)
+    assert torch.equal(r3, fresh[users[:500]] @ fresh[ds.n_users:].t())
 
 
 def test_training_trajectory_and_recall_match_oracle():
@@ -2516,3 +2609,38 @@ def test_torch_ops_lgcn_propagate_matches_module_and_autograd():
     gy = torch.randn_like(y)
     (gx,) = torch.autograd.grad(y, x, gy)
     assert rel(gx, torch.from_numpy(A.T @ gy.double().cpu().numpy())) < 1e-5
+
+
+def test_lgconv_backward_outlives_module_and_cache():
+    """The autograd node keeps its graph alive: backward through a temporary
+    LGConv(), and through one module called on two different edge_index
+    tensors before either backward, both give Âᵀ ȳ (the graph
+    registry is weak and the module caches one graph only)."""
+    import gc
+
+    from furusato_recommend_amd import LGConv
+    rng = np.random.default_rng(1)
+    n = 200
+
+    def dense_a(ei):
+        deg = np.bincount(ei[1], minlength=n).astype(np.float64)
+        dinv = np.where(deg > 0, deg ** -0.5, 0.0)
+        A = np.zeros((n, n))
+        np.add.at(A, (ei[1], ei[0]), dinv[ei[1]] * dinv[ei[0]])
+        return A
+
+    e1, e2 = rng.integers(0, n, (2, 1500)), rng.integers(0, n, (2, 900))
+    x = torch.randn(n, 32, device="cuda", requires_grad=True)
+    y = LGConv()(x, torch.from_numpy(e1).cuda())     # temporary module
+    gc.collect()
+    gy = torch.randn_like(y)
+    (gx,) = torch.autograd.grad(y, x, gy)
+    assert rel(gx, torch.from_numpy(dense_a(e1).T @ gy.double().cpu().numpy())) < 1e-5
+    conv = LGConv()
+    y1 = conv(x, torch.from_numpy(e1).cuda())
+    y2 = conv(x, torch.from_numpy(e2).cuda())        # drops the cached first graph
+    gc.collect()
+    g1, g2 = torch.randn_like(y1), torch.randn_like(y2)
+    (gx,) = torch.autograd.grad((y1 * g1).sum() + (y2 * g2).sum(), x)
+    want = dense_a(e1).T @ g1.double().cpu().numpy() + dense_a(e2).T @ g2.double().cpu().numpy()
+    assert rel(gx, torch.from_numpy(want)) < 1e-5

@@ -170,7 +170,7 @@ class OracleEngine:
     def invalidate_prescaled(self):
         pass
 
-    def backward(self, emb, adam=None, grad_out=None, last_rows=None):
+    def backward(self, emb, adam=None, grad_out=None, last_rows=None, on_chunk=None):
         if grad_out is not None:
             grad_out.copy_(self.o.grad(*self._batch) * self._scale)
             return
@@ -181,9 +181,13 @@ class OracleEngine:
         before = self.o.emb.detach().clone()
         self.adam_step(emb, g + self._e, adam)
         if last_rows is not None:  # only this rank's shard is updated here
-            keep = ~last_rows["rows"]
+            chunks = last_rows if isinstance(last_rows, list) else [last_rows]
+            keep = ~torch.stack([c["rows"] for c in chunks]).any(0)
             with torch.no_grad():
                 self.o.emb[keep] = before[keep]
+            for c in range(len(chunks)):
+                if on_chunk is not None:
+                    on_chunk(c)
 
     def adam_step(self, param, grad, adam):
         self.o.emb.grad = grad.clone()
@@ -238,6 +242,91 @@ def test_data_parallel_equals_union_batch(golden, mode):
     assert np.array_equal(res[0], res[1])  # replicas stay identical
     ref = f["emb_step2"]
     assert np.max(np.abs(res[0] - ref)) / np.max(np.abs(ref)) < 2e-5
+
+
+def _calib_worker(rank, world, port, fpath, q, prefer):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from furusato_recommend_amd.dist import DataParallel
+    f = dict(np.load(fpath))
+    o = O.OracleLightGCN(f["train_user"], f["train_item"], int(f["n_users"]), int(f["m_items"]),
+                         64, 3, float(f["lr"]), float(f["decay"]), emb=torch.from_numpy(f["emb0"]))
+    t = f["triples"]
+    half = len(t) // world
+    mine = t[rank * half:(rank + 1) * half]
+    dp = DataParallel(OracleEngine(o, half), o.emb.data, o.optim, mode="auto", chunks=3)
+    assert dp.mode == "sparse"  # until measured
+    dp.adam = _OptimView(o)
+    seen = []
+
+    def run_step():
+        seen.append(dp.mode)
+        dp.step(mine[:, 0], mine[:, 1], mine[:, 2], float(f["decay"]))
+
+    def measure(mode, fn, steps):  # rank-dependent fake clock: max over ranks decides
+        for _ in range(steps):
+            fn()
+        fast = 1.0 if mode == prefer else 2.0
+        return dp._max_over_ranks(fast + 0.5 * rank)
+    cal = dp.calibrate(run_step, steps=1, measure=measure)
+    stale_after = dp.adam.stale_rows
+    run_step()
+    q.put((rank, o.emb.detach().numpy().copy(), cal, seen, stale_after,
+           dp.adam.exp_avg.numpy().copy()))
+    dist.destroy_process_group()
+
+
+class _OptimView:
+    """The oracle's torch.optim.Adam seen as an AdamState (moments by view)."""
+
+    def __init__(self, o):
+        self.o = o
+        self.stale_rows = False
+        o.emb.grad = torch.zeros_like(o.emb)
+        o.optim.step()  # materialise the state tensors (a zero step leaves emb unchanged) ...
+        o.emb.grad = None
+        st = o.optim.state[o.emb]
+        st["step"].zero_()  # ... and forget it happened
+        st["exp_avg"].zero_()
+        st["exp_avg_sq"].zero_()
+        self.exp_avg, self.exp_avg_sq = st["exp_avg"], st["exp_avg_sq"]
+
+
+@pytest.mark.parametrize("prefer", ["sparse", "sharded"])
+def test_data_parallel_auto_calibration(golden, prefer):
+    """mode="auto": both exchanges are timed on the ranks (max over ranks),
+    the faster one is kept, and every calibration step is an ordinary
+    training step: after 2 + 2 calibration steps and one more, both ranks
+    hold 5 union-batch steps of the reference (and, leaving ``sharded``, the
+    gathered Adam moments)."""
+    from tests.conftest import GOLDEN
+    fpath = os.path.join(GOLDEN, "lgcn_d64_L3.npz")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_calib_worker, args=(r, 2, port, fpath, q, prefer))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=180) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+    f = golden("lgcn_d64_L3.npz")
+    o = O.OracleLightGCN(f["train_user"], f["train_item"], int(f["n_users"]), int(f["m_items"]),
+                         64, 3, float(f["lr"]), float(f["decay"]), emb=torch.from_numpy(f["emb0"]))
+    t = f["triples"]
+    for _ in range(5):
+        o.stageOne(t[:, 0], t[:, 1], t[:, 2])
+    ref = o.emb.detach().numpy()
+    for r in (0, 1):
+        emb, cal, seen, stale, mom = res[r]
+        assert cal["choice"] == prefer
+        assert cal["sparse_ms_per_step"] == (1.5 if prefer == "sparse" else 2.5)
+        assert seen == ["sparse", "sparse", "sharded", "sharded", prefer]
+        assert not stale
+        assert np.max(np.abs(emb - ref)) / np.max(np.abs(ref)) < 2e-5
+    assert np.array_equal(res[0][0], res[1][0])
+    assert np.array_equal(res[0][4], res[1][4])  # moments agree on every row
 
 
 def _dense_dp_worker(rank, world, port, q):
