@@ -365,43 +365,117 @@ class DataParallel:
         return self.calibration
 
 
+def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None):
+    """all_to_all_single; CUDA tensors under gloo (CPU tests, one-GPU
+    rehearsals) travel through host copies."""
+    if inp.is_cuda and dist.get_backend(group) != "nccl":
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+        return
+    dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def route_rows(rows: torch.Tensor, vals: torch.Tensor, n_rows: int, group=None):
+    """Send every (row id, value row) to the rank owning the row — rank q
+    owns the contiguous block [q·n_rows/W, (q+1)·n_rows/W) — with one small
+    all-to-all of the counts and two uneven all-to-alls (ids, rows).
+    ``rows``: ascending int32 [n] (so each owner's rows are one contiguous
+    block), ``vals`` [n, d].  Returns (ids [m], vals [m, d], per-source
+    counts): the received blocks in source-rank order, each ascending."""
+    W = dist.get_world_size(group)
+    per = n_rows // W
+    owner = torch.div(rows.long(), per, rounding_mode="floor").clamp_(max=W - 1)
+    send = torch.bincount(owner, minlength=W)
+    recv = torch.empty_like(send)
+    _a2a(recv, send, group=group)
+    sc, rc = send.tolist(), recv.tolist()
+    m = int(sum(rc))
+    rid = torch.empty(m, dtype=rows.dtype, device=rows.device)
+    rv = torch.empty(m, vals.shape[1], dtype=vals.dtype, device=vals.device)
+    _a2a(rid, rows.contiguous(), rc, sc, group=group)
+    _a2a(rv, vals.contiguous(), rc, sc, group=group)
+    return rid, rv, rc
+
+
 class DenseGradDataParallel:
     """Data parallelism for models trained through autograd (GraphSAGE,
     SASRec; replaces ddp_sage.py:754-878, which like ddp_lgcn.py never
     synchronised gradients).  Every rank samples its own user shard; the loss
     is scaled by 1/world_size and the gradients are SUM-reduced over RCCL
     between backward and the (HIP) Adam step: the small ones as one flattened
-    all-reduce bucket; the large ones (the id tables: 563 MB at C3) either
-    all-reduced in place, or — ``shard_optimizer`` (default when the model
-    exposes its Adam states as ``optims`` and the rows divide by the world
-    size) — reduce-scattered by contiguous row shard, stepped by Adam on this
-    rank's N/W rows only, and all-gathered in place (ZeRO-1: the same bytes
-    on the wire as the all-reduce, which RCCL runs as reduce-scatter +
-    all-gather, but 1/W of the table Adam — the largest C3 kernel, 0.66 ms
-    of a 2.0 ms step — on each rank; the other rows' Adam moments are not
-    kept here, gather_optimizer_state() brings them together)."""
+    all-reduce bucket.  The id table (563 MB at C3) has three routes:
+
+    * ``table_exchange="routed"`` (default for a model with a sorted table
+      gradient, ``model._tg``, whose rows divide by W): its gradient is
+      G = c ⊙ W + S with the norm term c ⊙ W dense but identical on every
+      rank (W is replicated, c = W x this rank's coefficient) and the tree
+      term S non-zero only on the rows this rank's batch touched (~0.5 M of
+      1.1 M at C3).  Each rank sends its touched rows of S to their owners
+      (contiguous row blocks; ``route_rows``), the owner sums the received
+      blocks in source-rank order and runs the fused table Adam
+      (G formed in the kernel, mirec_adam_table) on its N/W rows, then one
+      in-place all-gather of the table.  The dense gradient is never
+      materialised; per rank ≈ (W-1)/W · (touched rows x (4 + 4d) B) in plus
+      (W-1)/W of the table — against 2 (W-1)/W of the table for the
+      reduce-scatter + all-gather of the dense gradient.
+    * ``shard_optimizer`` with a materialised gradient
+      (``table_exchange="dense"``): reduce-scatter by contiguous row shard,
+      dense Adam on this rank's N/W rows, in-place all-gather (ZeRO-1).
+    * otherwise: an in-place all-reduce and the replicated Adam.
+
+    In the sharded routes the other rows' Adam moments are not kept here:
+    ``gather_optimizer_state()`` brings them together (AdamState.state_dict
+    raises until then)."""
 
     BUCKET_MIN = 1 << 20  # elements: gradients this large are reduced in place
 
-    def __init__(self, model, group=None, shard_optimizer: bool | None = None):
+    def __init__(self, model, group=None, shard_optimizer: bool | None = None,
+                 table_exchange: str | None = None):
         self.model = model
         self.group = group
         self.distributed = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.rank = dist.get_rank(group) if self.distributed else 0
-        tg = getattr(model, "_tg", None)
-        if tg is not None and self.world > 1:
-            # the sorted table gradient: materialise it as .grad so it can be
-            # reduced (the fused table Adam needs the local S only)
-            tg.dense = True
         states = list(getattr(model, "optims", None) or [])
         self._states = {id(st.param): st for st in states if hasattr(st, "exp_avg")}
         self.shard_optimizer = (self.world > 1 and bool(self._states)
                                 if shard_optimizer is None else bool(shard_optimizer))
+        tg = getattr(model, "_tg", None)
+        tstate = getattr(model, "_table_state", None)
+        routable = (tg is not None and tstate is not None and id(tstate.param) in self._states
+                    and tg.n_rows % self.world == 0 and not tg.atomic)
+        if table_exchange is None:
+            table_exchange = "routed" if (routable and self.world > 1) else "dense"
+        if table_exchange not in ("routed", "dense"):
+            raise ValueError(table_exchange)
+        if table_exchange == "routed" and not routable:
+            raise ValueError("routed table exchange needs a sorted table gradient (model._tg) "
+                             "whose rows divide by the world size")
+        self.table_exchange = table_exchange
+        if tg is not None:
+            # dense: the sorted table gradient is materialised as .grad so it
+            # can be reduced; routed: it stays in its sparse form
+            tg.dense = self.world > 1 and table_exchange == "dense"
+            model._tg_routed = table_exchange == "routed"
         self._sharded = set()  # ids of the parameters whose Adam runs sharded
+        self._ones = None      # the routed Adam's all-stamped shard
+        self.comm_events = None  # (start, end) HIP events per collective (bench)
+        self.last_exchange_bytes = 0
         if self.world > 1:
             for p in model.parameters():
                 dist.broadcast(p.data, src=0, group=group)
+
+    def _event(self):
+        if self.comm_events is None:
+            return None
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def _note(self, a, b):
+        if a is not None:
+            self.comm_events.append((a, b))
 
     def _shardable(self, p) -> bool:
         g = p.grad
@@ -420,12 +494,14 @@ class DenseGradDataParallel:
         st = self._states[id(p)]
         n = g.numel() // self.world
         lo = self.rank * n
+        a = self._event()
         if dist.get_backend(self.group) == "nccl":
             shard = torch.empty(n, dtype=g.dtype, device=g.device)
             dist.reduce_scatter_tensor(shard, g.view(-1), op=dist.ReduceOp.SUM, group=self.group)
         else:  # gloo (CPU tests, one-GPU rehearsal): all-reduce, keep this rank's rows
             dist.all_reduce(g, op=dist.ReduceOp.SUM, group=self.group)
             shard = g.view(-1)[lo:lo + n]
+        self._note(a, self._event())
         hp = st.next_hparams()
         _note_raw_write()
         pf = p.data.view(-1)
@@ -433,13 +509,86 @@ class DenseGradDataParallel:
         check(lib.mirec_adam_dense(pf[lo:].data_ptr(), shard.data_ptr(), ea[lo:].data_ptr(),
                                    es[lo:].data_ptr(), n, ctypes.byref(hp),
                                    _lib.stream_handle()), "adam_dense(shard)")
+        a = self._event()
         dist.all_gather_into_tensor(pf, pf[lo:lo + n], group=self.group)
+        self._note(a, self._event())
+        self.last_exchange_bytes += 2 * (self.world - 1) * n * g.element_size()
         p.grad = None
         self._sharded.add(id(p))
         st.stale_rows = self.world > 1
         tg = getattr(self.model, "_tg", None)
         if tg is not None:
             tg.pending = False  # the step of the table gradient is done
+
+    @torch.no_grad()
+    def routed_export(self):
+        """This rank's touched table rows (ascending int32) and their rows of
+        S, the sparse term of the table gradient (a host sync: the count)."""
+        tg = self.model._tg
+        rows = torch.nonzero(tg.stamp == tg.gen).view(-1).to(torch.int32)
+        return rows, tg.acc.index_select(0, rows.long())
+
+    @torch.no_grad()
+    def routed_adam(self, rid, rv, counts):
+        """Owner side of the routed exchange: S of the own row block from the
+        received (ids, rows) blocks — added in source-rank order, each block's
+        rows distinct, so no two adds meet one address in a launch — then the
+        fused table Adam (G = W·c ⊙ table + S formed in the kernel) on the
+        own rows only."""
+        from . import _lib
+        from ._lib import check, lib
+        from .engine import _note_raw_write
+        tg, st = self.model._tg, self.model._table_state
+        p = st.param
+        N, d = p.shape
+        n_own = N // self.world
+        lo = self.rank * n_own
+        s_own = torch.zeros(n_own, d, dtype=p.dtype, device=p.device)
+        off = 0
+        for c in counts:
+            if c:
+                s_own.index_add_(0, (rid[off:off + c] - lo).long(), rv[off:off + c])
+            off += c
+        if self._ones is None or self._ones.numel() != n_own:
+            self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
+        coef = tg.coef * float(self.world)  # every rank's norm coefficient is the same
+        n_user = min(max(tg.n_user - lo, 0), n_own)
+        hp = st.next_hparams()
+        pf = p.data.view(-1)
+        ea, es = st.exp_avg.view(-1), st.exp_avg_sq.view(-1)
+        check(lib.mirec_adam_table(pf[lo * d:].data_ptr(), ea[lo * d:].data_ptr(),
+                                   es[lo * d:].data_ptr(), coef.data_ptr(), n_user,
+                                   s_own.data_ptr(), self._ones.data_ptr(), 1, n_own, d,
+                                   ctypes.byref(hp), None, None, _lib.stream_handle()),
+              "adam_table(shard)")
+        _note_raw_write()
+        tg.pending = False
+        self._sharded.add(id(p))
+        st.stale_rows = self.world > 1
+
+    @torch.no_grad()
+    def _routed_table_step(self):
+        """The ``routed`` exchange + fused Adam of the id table (class doc)."""
+        p = self.model._table_state.param
+        N, d = p.shape
+        W = self.world
+        n_own = N // W
+        lo = self.rank * n_own
+        rows, vals = self.routed_export()
+        a = self._event()
+        if W > 1:
+            rid, rv, counts = route_rows(rows, vals, N, self.group)
+        else:
+            rid, rv, counts = rows, vals, [rows.numel()]
+        self._note(a, self._event())
+        self.routed_adam(rid, rv, counts)
+        if W > 1:
+            pf = p.data.view(-1)
+            a = self._event()
+            dist.all_gather_into_tensor(pf, pf[lo * d:(lo + n_own) * d], group=self.group)
+            self._note(a, self._event())
+        self.last_exchange_bytes += ((sum(counts) - counts[self.rank]) * (4 + d * p.element_size())
+                                     + (W - 1) * n_own * d * p.element_size())
 
     def gather_optimizer_state(self):
         """All-gather the row shards of the sharded parameters' Adam moments
@@ -458,6 +607,10 @@ class DenseGradDataParallel:
     def _allreduce(self):
         if not self.distributed:
             return
+        self.last_exchange_bytes = 0
+        tg = getattr(self.model, "_tg", None)
+        if self.table_exchange == "routed" and tg is not None and tg.pending:
+            self._routed_table_step()
         params = [p for p in self.model.parameters() if p.grad is not None]
         # large gradients (the id tables) are reduced in place or by row shard;
         # the small ones share one flattened bucket
@@ -468,15 +621,38 @@ class DenseGradDataParallel:
             if self._shardable(p):
                 self._sharded_adam(p)
             else:
+                a = self._event()
                 dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group)
+                self._note(a, self._event())
+                self.last_exchange_bytes += 2 * (self.world - 1) * p.grad.numel() \
+                    * p.grad.element_size() // self.world
         if small:
             flat = torch.cat([g.reshape(-1) for g in small])
+            a = self._event()
             dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            self._note(a, self._event())
+            self.last_exchange_bytes += 2 * (self.world - 1) * flat.numel() * 4 // self.world
             off = 0
             for g in small:
                 g.copy_(flat[off: off + g.numel()].view_as(g))
                 off += g.numel()
 
+    def table_stepped_by_hook(self) -> bool:
+        """Whether the exchange hook itself steps the id table (routed
+        exchange, or the row-sharded dense Adam of a large table)."""
+        st = getattr(self.model, "_table_state", None)
+        if st is None:
+            return False
+        if self.table_exchange == "routed":
+            return True
+        p = st.param
+        return (self.world > 1 and self.shard_optimizer and p.numel() >= self.BUCKET_MIN
+                and p.shape[0] % self.world == 0)
+
     def step(self, users, pos, neg):
+        kw = {}
+        if getattr(self.model, "captures_dp_step", False):
+            # SASRec: the captured step, split around this exchange
+            kw["table_by_hook"] = self.table_stepped_by_hook()
         return self.model.stageOne(users, pos, neg, grad_hook=self._allreduce,
-                                   loss_scale=1.0 / self.world)
+                                   loss_scale=1.0 / self.world, **kw)

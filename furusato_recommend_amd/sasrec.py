@@ -1097,19 +1097,31 @@ class SASRec(nn.Module):
         loss = torch.mean(F.softplus(neg_scores - pos_scores))
         return loss + all_param * self.config["decay"]
 
-    def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0):
+    # DenseGradDataParallel passes table_by_hook: the captured step can be
+    # split around its gradient exchange
+    captures_dp_step = True
+
+    def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0,
+                 table_by_hook: bool | None = None):
         """One BPR step on packed sequences.  ``loss_scale`` scales the
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
         between backward and Adam (DenseGradDataParallel's all-reduce).
-        With config "graph" (default on) a single-process step (no hook, no
-        scale) replays a captured HIP graph of the whole step
-        (_CapturedStep); otherwise the step runs eagerly.  The projections
-        run on the BLAS backend of config "blas" (default: hipBLASLt in the
-        captured step, where its faster kernels win; rocBLAS in the eager
-        step, which is host-bound and rocBLAS launches cost less host time)."""
-        if (self.config.get("graph", True) and grad_hook is None and loss_scale == 1.0
-                and len(users) > 0):
-            return self._graph_step(users, pos, neg)
+        With config "graph" (default on) the step replays a captured HIP graph
+        (_CapturedStep): the whole step for a single process; under data
+        parallelism (a hook and ``table_by_hook`` — whether the hook itself
+        steps the item table — given) two graphs, the packing / forward /
+        loss / backward one and the Adam one, with the hook's collectives
+        run between the two replays.  Otherwise the step runs eagerly.  The
+        projections run on the BLAS backend of config "blas" (default:
+        hipBLASLt in the captured step, where its faster kernels win;
+        rocBLAS in the eager step, which is host-bound and rocBLAS launches
+        cost less host time)."""
+        if self.config.get("graph", True) and len(users) > 0:
+            if grad_hook is None and loss_scale == 1.0:
+                return self._graph_step(users, pos, neg)
+            if grad_hook is not None and table_by_hook is not None:
+                return self._graph_step(users, pos, neg, grad_hook, float(loss_scale),
+                                        bool(table_by_hook))
         with blas_backend(self.config.get("blas", "cublas")):
             return self._stage_one(users, pos, neg, grad_hook, loss_scale)
 
@@ -1124,7 +1136,8 @@ class SASRec(nn.Module):
         loss = self._step_body(ids, packing, seg, length, pos, neg, loss_scale)
         if grad_hook is not None:
             tg = self._tg
-            if tg is not None and tg.pending and self.item_id_embedding.weight.grad is None:
+            if (tg is not None and tg.pending and self.item_id_embedding.weight.grad is None
+                    and not getattr(self, "_tg_routed", False)):
                 # the hook (an all-reduce, a test) sees every gradient
                 self.item_id_embedding.weight.grad = tg.materialize(
                     self.item_id_embedding.weight.detach())
@@ -1224,12 +1237,15 @@ class SASRec(nn.Module):
                                  seg.data_ptr(), _lib.stream_handle()), "seq_pack")
         return ids_all, Packing(offsets, None, True), seg, length
 
-    def _graph_step(self, users, pos, neg):
+    def _graph_step(self, users, pos, neg, hook=None, loss_scale: float = 1.0,
+                    table_by_hook: bool | None = None):
         u_host = users.cpu().numpy() if torch.is_tensor(users) else np.asarray(users)
         B = len(u_host)
         n_tok = int(self.seq.length_host[u_host].sum())
         graphs = self.__dict__.setdefault("_graphs", {})
-        fits = [k for k in graphs if k[0] == B and k[2] == self.training and k[1] >= n_tok]
+        split = None if hook is None else (loss_scale, table_by_hook)
+        fits = [k for k in graphs if k[0] == B and k[2] == self.training and k[1] >= n_tok
+                and k[3] == split]
         if fits:
             g = graphs[min(fits, key=lambda k: k[1])]
         else:
@@ -1239,8 +1255,9 @@ class SASRec(nn.Module):
             lens = self.seq.length_host
             expect = B * float(lens.mean()) + 4.0 * float(lens.std()) * B ** 0.5
             cap = -(-max(n_tok, int(expect)) // 1024) * 1024
-            g = graphs[(B, cap, self.training)] = _CapturedStep(self, B, cap, u_host)
-        return g.run(u_host, pos, neg)
+            g = graphs[(B, cap, self.training, split)] = _CapturedStep(self, B, cap, u_host,
+                                                                       split)
+        return g.run(u_host, pos, neg, hook)
 
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])
@@ -1278,9 +1295,14 @@ class _CapturedStep:
     warm-up step on a side stream first (library handles, lazy autograd
     state) and restores the parameters and Adam moments it touched."""
 
-    def __init__(self, model: "SASRec", B: int, capacity: int, u_host):
+    def __init__(self, model: "SASRec", B: int, capacity: int, u_host, split=None):
+        """``split`` = (loss_scale, table_by_hook) captures the data-parallel
+        form: graph A (packing, forward, loss x loss_scale, backward) and
+        graph B (Adam over the parameters the hook does not step), replayed
+        around the hook's collectives."""
         global _SEED_BASE
         self.m, self.B, self.C = model, B, capacity
+        self.split = split
         dev = model.device
         # [users | pos | neg | Adam hparams (6 f32 = 3 int64) | seed base];
         # the warm-up runs on the first batch's users (fits the capacity)
@@ -1305,19 +1327,35 @@ class _CapturedStep:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         self.graph = torch.cuda.CUDAGraph()
+        self.graph_b = torch.cuda.CUDAGraph() if split is not None else None
         try:
             _SEED_BASE = self.inbuf[3 * B + 3:]
             with blas_backend(model.graph_blas()):
                 with torch.cuda.stream(side):
                     self._body()  # warm-up (eager, on the side stream)
+                    if split is not None:
+                        self._body_b()
                 torch.cuda.current_stream().wait_stream(side)
                 for p in params:
                     p.grad = None
+                if split is not None and model._tg is not None:
+                    # graph B may not run the fused table Adam that keeps the
+                    # norm: the forward reads it from the buffer, refreshed
+                    # by run() whenever the table changed
+                    model._refresh_norm()
                 # the captured forward reads the kept table norm iff it is
                 # valid now (the warm-up's fused Adam wrote it)
                 self.norm_from_buf = model._norm_valid()
                 with torch.cuda.graph(self.graph, pool=pool):
                     self.loss = self._body()
+                if split is not None:
+                    tg = model._tg
+                    # graph B runs the fused table Adam (which keeps the norm)
+                    # iff the table's gradient stays in its sorted form
+                    self.fused_b = (not split[1] and tg is not None and tg.pending
+                                    and model.item_id_embedding.weight.grad is None)
+                    with torch.cuda.graph(self.graph_b, pool=pool):
+                        self._body_b()
         finally:
             _SEED_BASE = None
         with torch.no_grad():
@@ -1334,11 +1372,27 @@ class _CapturedStep:
         u, pos, neg = buf[:B], buf[B:2 * B], buf[2 * B:3 * B]
         hdev = buf[3 * B:3 * B + 3].view(torch.float32)
         ids_all, packing, seg, length = m.packed_ids_static(u, self.C, pos, neg)
-        loss = m._step_body(ids_all, packing, seg, length, pos, neg, n_tok=self.C)
-        m.optimizer_step(hdev)
+        scale = 1.0 if self.split is None else self.split[0]
+        loss = m._step_body(ids_all, packing, seg, length, pos, neg, loss_scale=scale,
+                            n_tok=self.C)
+        if self.split is None:
+            m.optimizer_step(hdev)
         return loss.detach()
 
-    def run(self, u_host, pos, neg):
+    def _group_b(self):
+        """The Adam states graph B steps: all but the item table when the
+        hook steps it (routed exchange / row-sharded Adam), else all."""
+        return self.m._rest_optims if self.split[1] else self.m.optims
+
+    def _body_b(self):
+        B = self.B
+        hdev = self.inbuf[3 * B:3 * B + 3].view(torch.float32)
+        if self.split[1]:
+            self.m._rest_optims.step_device(hdev)
+        else:  # the table too: fused from its sorted gradient, or densely
+            self.m.optimizer_step(hdev)
+
+    def run(self, u_host, pos, neg, hook=None):
         B = self.B
         k = self.turn
         self.turn ^= 1
@@ -1350,7 +1404,10 @@ class _CapturedStep:
         for j, (t, dv) in enumerate(((pos, on_dev[0]), (neg, on_dev[1]))):
             if not dv:
                 st[(j + 1) * B:(j + 2) * B] = np.asarray(t.cpu() if torch.is_tensor(t) else t)
-        hp = self.m.optims.next_shared_hparams(require_grad=self.m._tg is None)
+        if self.split is None or not self.split[1]:
+            hp = self.m.optims.next_shared_hparams(require_grad=False)
+        else:
+            hp = self.m._rest_optims.next_shared_hparams(require_grad=False)
         st[3 * B:3 * B + 3] = np.frombuffer(bytes(hp), dtype=np.int64)
         st[3 * B + 3] = int(torch.randint(0, 2 ** 62, (1,)).item())  # torch's CPU generator
         self.inbuf.copy_(self.stage[k], non_blocking=True)
@@ -1372,6 +1429,18 @@ class _CapturedStep:
             m._refresh_norm()  # the table changed outside the step
         _note_raw_write()
         self.graph.replay()
+        if self.split is not None:
+            if m._tg is not None:
+                m._tg.pending = True  # the replayed backward left S / coef
+            hook()
+            if m._tg is not None:
+                m._tg.pending = False
+            self.graph_b.replay()
+            _note_raw_write()
+            # the fused table Adam of graph B wrote the next norm; otherwise
+            # the next run refreshes it
+            m._norm_tok = m._norm_token() if self.fused_b else None
+            return self.loss.clone()
         if m._tg is not None:  # the replayed fused Adam wrote the next norm
             m._norm_tok = m._norm_token()
         return self.loss.clone()

@@ -565,3 +565,42 @@ def test_torch_ops_registration_and_fake_tracing():
     import pytest
     with pytest.raises(ValueError):
         torch.ops.mirec.lgcn_propagate(torch.empty(7, 16), h)  # not on the HIP device
+
+
+def _route_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from furusato_recommend_amd.dist import route_rows
+    n_rows, d = 12, 3
+    g = torch.Generator().manual_seed(rank)
+    rows = torch.sort(torch.randperm(n_rows, generator=g)[: 4 + 2 * rank]).values.int()
+    vals = rows.float()[:, None] * 10 + rank + torch.arange(d).float()[None] / 10
+    rid, rv, counts = route_rows(rows, vals, n_rows)
+    q.put((rank, rows.numpy(), rid.numpy(), rv.numpy(), counts))
+    dist.destroy_process_group()
+
+
+def test_route_rows_to_owners_world3():
+    """route_rows (the routed table exchange of DenseGradDataParallel): at
+    W = 3 over 12 rows every (row, value) reaches the owner of its
+    contiguous block, in source-rank order, ascending within a source."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_route_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=120) for _ in range(3))}
+    for p in procs:
+        p.join(timeout=60)
+    for owner in range(3):
+        _, rid, rv, counts = res[owner]
+        want_ids, want_vals = [], []
+        for src in range(3):
+            rows = res[src][0]
+            mine = rows[(rows // 4) == owner]
+            want_ids += mine.tolist()
+            want_vals += [[r * 10 + src + k / 10 for k in range(3)] for r in mine]
+            assert counts[src] == len(mine)
+        assert rid.tolist() == want_ids
+        assert np.allclose(rv, np.array(want_vals, dtype=np.float32).reshape(-1, 3))

@@ -18,45 +18,47 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def cpu_baseline(m, B, fan):
+def cpu_baseline(m, B, fan, k=3):
     """The oracle's restatement of graphsage.py:311-337 (torch CPU fp32) on
-    one batch of the same workload: one sampled tree
-    (drawn by the GPU sampler, copied to the host), forward, loss with the
-    reference's parameter norms, backward, torch Adam over every parameter."""
-    import platform
-
+    the same workload, timed per BASELINE.md §3: one warm-up training step,
+    then the mean of ``k`` steps, each on its own sampled tree (drawn by the
+    GPU sampler, copied to the host): forward, loss with the reference's
+    parameter norms, backward, torch Adam over every parameter."""
+    import bench
     from oracle import lightgcn_oracle as O
-    # torch's default intra-op pool (OMP_NUM_THREADS: 16 on the GPU box), as
-    # bench.py's baseline
-    u, p, n = m.sample(B, seed=99, offset=0)
-    seeds = torch.cat([u, p + m.n_user, n + m.n_user])
-    tree = m.sample_tree(seeds, 12345)
-    groups = [g.cpu().numpy() for g, _ in tree.groups]
+    threads = bench.host_threads()
+    torch.set_num_threads(threads)
     table = m._table.detach().cpu().clone().requires_grad_(True)
     lin = [torch.nn.Linear(2 * m.latent_dim, m.latent_dim) for _ in m.w_linears]
     for a, b in zip(lin, m.w_linears):
-        a.load_state_dict({k: v.detach().cpu() for k, v in b.state_dict().items()})
+        a.load_state_dict({kk: v.detach().cpu() for kk, v in b.state_dict().items()})
     params = [table] + [q for layer in lin for q in layer.parameters()]
     opt = torch.optim.Adam(params, lr=1e-3)
-    t0 = time.perf_counter()
-    emb = O.sage_forward(table, lin, groups, m.num_layers, m.sizes)
-    ue, pe, ne = emb[:B], emb[B:2 * B], emb[2 * B:]
-    reg = [table[:m.n_user], table[m.n_user:]] + [q for layer in lin for q in (layer.weight,
-                                                                              layer.bias)]
-    loss = O.sage_loss(ue, pe, ne, reg, 1e-7)
-    loss.backward()
-    opt.step()
-    t = time.perf_counter() - t0
-    cpu_name = platform.processor() or "cpu"
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_name = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
-    return {"value": round(B / t, 2), "unit": "positive-edges/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu": cpu_name, "step_s": round(t, 3),
-            "sample": f"1 training step (B={B}, fanout {fan}) of the C3 workload: tree of "
-                      f"{sum(g.size for g in groups)} rows, dense Adam over the id table"}
+    times, rows = [], 0
+    for i in range(k + 1):
+        u, p, n = m.sample(B, seed=99, offset=i * B)
+        seeds = torch.cat([u, p + m.n_user, n + m.n_user])
+        groups = [g.cpu().numpy() for g, _ in m.sample_tree(seeds, 12345 + i).groups]
+        rows = sum(g.size for g in groups)
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        emb = O.sage_forward(table, lin, groups, m.num_layers, m.sizes)
+        ue, pe, ne = emb[:B], emb[B:2 * B], emb[2 * B:]
+        reg = [table[:m.n_user], table[m.n_user:]] + [q for layer in lin
+                                                      for q in (layer.weight, layer.bias)]
+        loss = O.sage_loss(ue, pe, ne, reg, 1e-7)
+        loss.backward()
+        opt.step()
+        if i:  # i = 0 is the warm-up
+            times.append(time.perf_counter() - t0)
+    t = sum(times) / len(times)
+    return {"value": round(B / t, 2), "unit": "positive-edges/s", "cores": threads,
+            "threads": threads, "os_cpu_count": os.cpu_count(), "kind": "port",
+            "cpu": bench.cpu_model(), "warmup": 1, "k": k, "step_s": round(t, 3),
+            "step_s_each": [round(x, 3) for x in times],
+            "sample": f"1 warm-up + mean of {k} training steps (B={B}, fanout {fan}) of the C3 "
+                      f"workload, each on its own sampled tree (~{rows} rows), dense Adam over "
+                      f"the id table"}
 
 
 def main():
@@ -75,6 +77,10 @@ def main():
     ap.add_argument("--blas", default="", help="torch BLAS backend override (cublas / cublaslt)")
     ap.add_argument("--leaf-bwd", choices=("sorted", "atomic"), default="sorted",
                     help="leaf-hop backward: radix-sorted ordered sums or float atomics")
+    ap.add_argument("--table-exchange", choices=("auto", "routed", "dense"), default="auto",
+                    help="data-parallel exchange of the id table (dist.DenseGradDataParallel)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
     args = ap.parse_args()
     from furusato_recommend_amd import graphsage as _gs
     _gs.SORTED_LEAF_BACKWARD = args.leaf_bwd == "sorted"
@@ -83,10 +89,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = 0 if args.rehearse else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        from furusato_recommend_amd.dist import init_distributed
+        init_distributed("gloo" if args.rehearse else "nccl", dev)
     from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
     from furusato_recommend_amd.dist import DenseGradDataParallel
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0, kind=args.kind)
@@ -94,7 +102,8 @@ def main():
     fan = [int(x) for x in args.fanouts.split(",")]
     m = GraphSAGE({"recdim": args.dim, "layer": len(fan), "fanouts": fan, "lr": 1e-3,
                    "decay": 1e-7, "device": str(dev), "bpr_batch_size": args.batch}, ds)
-    dp = DenseGradDataParallel(m)
+    dp = DenseGradDataParallel(m, table_exchange=None if args.table_exchange == "auto"
+                               else args.table_exchange)
     B = args.batch
 
     def step(i):
@@ -104,6 +113,7 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    dp.comm_events = [] if world > 1 else None
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -117,6 +127,18 @@ def main():
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    comm = None
+    if world > 1:
+        from furusato_recommend_amd.dist import _elapsed_ms
+        cm = _elapsed_ms(dp.comm_events) / args.steps
+        t = torch.tensor([cm], dtype=torch.float64, device="cpu" if args.rehearse else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        cm = float(t.item())
+        comm = {"backend": dist.get_backend(), "world_size": world,
+                "table_exchange": dp.table_exchange, "comm_ms_per_step": round(cm, 4),
+                "exchange_bytes_per_rank": dp.last_exchange_bytes,
+                "exchange_bytes_note": "bytes rank 0 received in the last step",
+                "algbw_GBps": round(dp.last_exchange_bytes / (cm * 1e-3) / 1e9, 2) if cm else None}
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(m, B, fan)
@@ -127,8 +149,12 @@ def main():
             "ms_per_step": round(1e3 * dt / args.steps, 3), "dtype": "f32",
             "config": {"workload": "C3: GraphSAGE 2-hop fanout %s d=%d on the C2 graph" % (fan, args.dim)
                         + ("" if args.kind == "uniform" else " (%s item popularity)" % args.kind),
-                       "bpr_batch_per_rank": B, "parallelism": f"dp{world} (dense grad all-reduce)",
+                       "bpr_batch_per_rank": B,
+                       "parallelism": (f"dp{world} rehearsal (gloo, one GPU)" if args.rehearse
+                                       else f"dp{world} (user-sharded, {dp.table_exchange} "
+                                            f"table exchange)"),
                        "leaf_bwd": args.leaf_bwd},
+            "comm": comm,
             "cpu_baseline": cpu}),
             flush=True)
     if world > 1:

@@ -10,8 +10,20 @@ copy standing in for the all-gather's output write).  What is NOT measured:
 the RCCL all-gather itself (W x 3B x (4 + 8D) bytes, 3.2 MB per rank at C2).
 
   python tools/bench_world_sim.py [--worlds 1,2,4,8] [--steps 20]
+
+--model sage: the same for C3 (GraphSAGE [25, 10] d = 128 on the C2 graph)
+under DenseGradDataParallel.  Rank 0's step at world W: its shard's batch,
+forward, loss x 1/W, backward, then the table exchange's LOCAL work —
+``routed``: export of its touched rows, the merge of the blocks every rank
+sends to owner 0 (the other W-1 ranks' blocks produced up front by their
+own backward passes) and the fused Adam on rows [0, N/W); ``dense``: the
+materialised gradient and the dense Adam on rows [0, N/W) — plus the small
+parameters' bucket and Adam.  Printed per W: ms per rank step (no
+transfer), the bytes rank 0 receives per step, and the projected step and
+weak-scaling efficiency at several link rates (compute + bytes / rate).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -40,7 +52,14 @@ def main():
                          "layer + Adam) and/or sharded (rank 0's row shard only, plus the "
                          "local copies and re-prescale of the all-gather; the RCCL "
                          "transfer itself is not measured)")
+    ap.add_argument("--model", choices=("lgn", "sage"), default="lgn")
+    ap.add_argument("--exchanges", default="routed,dense",
+                    help="sage: table exchanges to simulate")
+    ap.add_argument("--rates", default="100,200,300,400",
+                    help="sage: link rates (GB/s of received bytes per rank) to project at")
     args = ap.parse_args()
+    if args.model == "sage":
+        return sage_main(args)
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     from furusato_recommend_amd.engine import sample_triples
     dev = torch.device("cuda:0")
@@ -116,6 +135,106 @@ def main():
                           "ms_per_step_rank": round(dt * 1e3, 4),
                           "edges_per_s_projected": round(W * B / dt, 1),
                           "launch_ms": launches, "union_F1_rows": f1}), flush=True)
+
+
+def sage_main(args):
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    from furusato_recommend_amd.dist import DenseGradDataParallel
+    dev = torch.device("cuda:0")
+    ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0)
+    torch.manual_seed(2020)
+    d = 128 if args.dim == 64 else args.dim
+    m = GraphSAGE({"recdim": d, "layer": 2, "fanouts": [25, 10], "lr": 1e-3, "decay": 1e-7,
+                   "device": str(dev), "bpr_batch_size": args.batch}, ds)
+    B = args.batch
+    N = m._table.shape[0]
+    rates = [float(x) for x in args.rates.split(",")]
+    base = None
+    for W in [int(w) for w in args.worlds.split(",")]:
+        for ex in args.exchanges.split(","):
+            if N % W:
+                continue
+            dp = DenseGradDataParallel(m, table_exchange=ex)  # world 1: no collectives
+            dp.world, dp.rank = W, 0  # rank 0 of a world of W (local work only)
+            m._tg.dense = ex == "dense"
+            m._tg_routed = ex == "routed"
+            n_own = N // W
+            others = []  # what ranks 1..W-1 send to owner 0: (ids, rows)
+            for r in range(1, W):
+                u, p, n = m.sample(B, seed=11, offset=10**8 + r * B, shard=r, n_shards=W)
+
+                def capture():
+                    if ex == "routed":
+                        rows, vals = dp.routed_export()
+                        k = int((rows < n_own).sum())
+                        others.append((rows[:k].clone(), vals[:k].clone()))
+                    for q in m.parameters():
+                        q.grad = None
+                    m._tg.pending = False
+                m.stageOne(u, p, n, grad_hook=capture, loss_scale=1.0 / W)
+            recv_other = sum(o[0].numel() for o in others) * (4 + 4 * d)
+
+            def hook():
+                if ex == "routed":
+                    rows, vals = dp.routed_export()
+                    k = int((rows < n_own).sum())
+                    rid = torch.cat([rows[:k]] + [o[0] for o in others])
+                    rv = torch.cat([vals[:k]] + [o[1] for o in others])
+                    dp.routed_adam(rid, rv, [k] + [o[0].numel() for o in others])
+                else:  # materialised G; the reduce-scatter's output stands in as a slice
+                    g = m._table.grad
+                    st = dp._states[id(m._table)]
+                    from furusato_recommend_amd import _lib
+                    from furusato_recommend_amd._lib import check, lib
+                    hp = st.next_hparams()
+                    check(lib.mirec_adam_dense(m._table.data.data_ptr(), g.data_ptr(),
+                                               st.exp_avg.data_ptr(), st.exp_avg_sq.data_ptr(),
+                                               n_own * d, ctypes.byref(hp), _lib.stream_handle()),
+                          "adam_dense(shard)")
+                    m._table.grad = None
+                    m._tg.pending = False
+                small = [q.grad for q in m.parameters() if q.grad is not None]
+                if small:  # the bucket's flatten + copy back (its all-reduce is transfer)
+                    flat = torch.cat([g.reshape(-1) for g in small])
+                    off = 0
+                    for g in small:
+                        g.copy_(flat[off: off + g.numel()].view_as(g))
+                        off += g.numel()
+
+            step_no = [0]
+
+            def step():
+                u, p, n = m.sample(B, seed=7, offset=step_no[0] * B, shard=0, n_shards=W)
+                step_no[0] += 1
+                m.stageOne(u, p, n, grad_hook=hook if W > 1 else None, loss_scale=1.0 / W)
+
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / args.steps * 1e3
+            if W == 1:
+                base = ms
+            table_b = N * d * 4
+            if ex == "routed":
+                recv = recv_other + (W - 1) * table_b // W
+            else:
+                recv = 2 * (W - 1) * table_b // W
+            small_b = sum(q.numel() for q in m.parameters() if q is not m._table) * 4
+            recv += 2 * (W - 1) * small_b // W
+            proj = {f"{int(r)}GBps": {"ms": round(ms + recv / (r * 1e6), 3),
+                                      "efficiency": round(base / (ms + recv / (r * 1e6)), 3)
+                                      if base else None} for r in rates}
+            print(json.dumps({"model": "sage C3", "world": W, "table_exchange": ex,
+                              "ms_per_step_rank_compute": round(ms, 4),
+                              "recv_bytes_per_rank": int(recv if W > 1 else 0),
+                              "routed_rows_from_others": int(recv_other // (4 + 4 * d)),
+                              "projected": proj if W > 1 else None}), flush=True)
+            if W == 1:
+                break  # one single-GPU baseline (both exchanges are the plain step)
 
 
 if __name__ == "__main__":
