@@ -493,19 +493,18 @@ struct PackSeqs {
   int T[4], lo[4], n;  // n = the pack's block count
 };
 
-__device__ __forceinline__ void read_pack(const int32_t *packs, const int32_t *offsets, int64_t pk,
-                                          PackSeqs &ps) {
+// The pack's descriptor: (first row, length) of its four slots, written by
+// the ordering pass (mirec_attention_length_order) — two 16-byte loads, no
+// dependent load of the offsets.
+__device__ __forceinline__ void read_pack(const int32_t *packs, int64_t pk, PackSeqs &ps) {
+  const int4 *d = reinterpret_cast<const int4 *>(packs + 4 + 8 * pk);
+  const int4 a = d[0], b = d[1];
+  const int r0[4] = {a.x, a.z, b.x, b.z}, len[4] = {a.y, a.w, b.y, b.w};
   int nb = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int32_t b = packs[1 + 4 * pk + i];
-    int T = 0;
-    int64_t r0 = 0;
-    if (b >= 0) {
-      r0 = offsets[b];
-      T = min(offsets[b + 1] - offsets[b], kT);
-    }
-    ps.row0[i] = r0;
+    const int T = min(len[i], kT);
+    ps.row0[i] = r0[i];
     ps.T[i] = T;
     ps.lo[i] = nb;
     nb += (T + kB - 1) / kB;
@@ -591,7 +590,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   PackSeqs ps;
-  read_pack(packs, offsets, pk, ps);
+  read_pack(packs, pk, ps);
   load_pack<DPAD, S::LDK>(sK, sV, qkv, rs, d + h * dh, ps, dh);
   // this wave's sequence
   const bool act = w < ps.n;
@@ -948,7 +947,7 @@ extern "C" int mirec_attention_packed_bwd(const float *qkv, const float *dout,
   MIREC_CHECK_ARG(batch >= 0 && heads >= 1 && head_dim >= 4 && head_dim <= 64 &&
                   head_dim % 4 == 0 && n_rows >= 0);
   if (batch == 0) return MIREC_OK;
-  MIREC_CHECK_ARG(qkv && dout && offsets && packs && dqkv);
+  MIREC_CHECK_ARG(qkv && dout && offsets && packs && dqkv && (uintptr_t)packs % 16 == 0);
   MIREC_CHECK_ARG(((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return head_dim <= 32

@@ -376,12 +376,14 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dkdv_kernel(
 
 // order = the sequences by length, longest first (counting sort over the 65
 // clamped lengths; the order among equal lengths is arbitrary — it changes
-// no result, every unit is independent).  packs (optional, int32 [1 + 4
-// batch]): packs[0] = the pack count, packs[1 + 4p + s] = sequence in slot s
-// of pack p or -1.  Over the same order, each sequence of 49-64 or 33-48
-// positions (4 / 3 blocks of 16) is a pack of its own, those of 17-32 go
-// two to a pack and those of 1-16 four to a pack (empty sequences in none):
-// mirec_attention_packed_bwd's workgroups.
+// no result, every unit is independent).  packs (optional, int32 [4 + 8
+// batch], 16-byte aligned): packs[0] = the pack count, packs[4 + 8p + 2s],
+// packs[5 + 8p + 2s] = (first row, length) of the sequence in slot s of pack
+// p, (0, 0) for an empty slot — the descriptor the backward workgroup reads
+// with two 16-byte loads, no dependent load of the offsets.  Over the same
+// order, each sequence of 49-64 or 33-48 positions (4 / 3 blocks of 16) is a
+// pack of its own, those of 17-32 go two to a pack and those of 1-16 four to
+// a pack (empty sequences in none): mirec_attention_packed_bwd's workgroups.
 __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__restrict__ offsets,
                                                            int64_t batch,
                                                            int32_t *__restrict__ order,
@@ -426,16 +428,19 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
   __syncthreads();
   if (packs != nullptr) {
     const int n_packs = pack_base[0];
-    if (threadIdx.x == 0) packs[0] = n_packs;
-    // slots no sequence fills: -1 (written before, and disjoint from, the
-    // sequence slots below)
+    if (threadIdx.x < 4) packs[threadIdx.x] = threadIdx.x == 0 ? n_packs : 0;
+    // slots no sequence fills: (0, 0) (written before, and disjoint from,
+    // the sequence slots below)
     for (int p = threadIdx.x; p < n_packs; p += blockDim.x) {
       // class of pack p: the k with pack_base[k] <= p < pack_base[k - 1]
       int k = 4;
       while (k > 1 && p >= pack_base[k - 1]) --k;
       const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
       const int used = min(per, cls_count[k] - (p - pack_base[k]) * per);
-      for (int sl = used; sl < 4; ++sl) packs[1 + 4 * (int64_t)p + sl] = -1;
+      for (int sl = used; sl < 4; ++sl) {
+        packs[4 + 8 * (int64_t)p + 2 * sl] = 0;
+        packs[5 + 8 * (int64_t)p + 2 * sl] = 0;
+      }
     }
   }
   for (int64_t b = threadIdx.x; b < batch; b += blockDim.x) {
@@ -446,7 +451,9 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
     if (packs != nullptr && k > 0) {
       const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
       const int i = pos - cls_start[k];
-      packs[1 + 4 * (int64_t)(pack_base[k] + i / per) + i % per] = (int32_t)b;
+      const int64_t slot = 4 + 8 * (int64_t)(pack_base[k] + i / per) + 2 * (i % per);
+      packs[slot] = offsets[b];
+      packs[slot + 1] = L;
     }
   }
 }
@@ -506,7 +513,7 @@ extern "C" int mirec_attention_length_order(const int32_t *offsets, int64_t batc
                                            hipSuccess ? MIREC_OK : MIREC_ERR_HIP;
     return MIREC_OK;
   }
-  MIREC_CHECK_ARG(offsets && order);
+  MIREC_CHECK_ARG(offsets && order && (uintptr_t)packs % 16 == 0);
   // workgroup 0 orders and packs; with zero_buf, 32 more zero the padding
   hipLaunchKernelGGL(length_order_kernel, dim3(zero_buf != nullptr ? 33 : 1), dim3(1024), 0,
                      reinterpret_cast<hipStream_t>(stream), offsets, batch, order, packs,

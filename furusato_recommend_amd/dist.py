@@ -138,7 +138,10 @@ class DataParallel:
         bounds = [(c * S) // C for c in range(C + 1)]
         words = (N + 15) // 16 * 4
         dev = self.emb.device
-        stage = torch.empty(W * S * D, dtype=self.emb.dtype, device=dev) if W > 1 else None
+        # (allocated whenever a process group exists: at W = 1 the collectives
+        # still run, so a one-GPU job exercises the RCCL calls of the path)
+        stage = torch.empty(W * S * D, dtype=self.emb.dtype, device=dev) \
+            if self.distributed else None
         self._chunks = []
         off = 0
         for c in range(C):
@@ -181,7 +184,7 @@ class DataParallel:
         """Every rank's shard rows of ``t`` [N, D] to every rank (in place):
         per block, pack rows r, r+W, ... into this rank's staging slot, one
         all-gather, then scatter slot w's rows back to w, w+W, ..."""
-        if self.world == 1:
+        if not self.distributed:
             return
         for c in range(len(self._chunks)):
             self._pack(c, t)
@@ -269,7 +272,7 @@ class DataParallel:
                 eng.backward(self.emb, adam=self.adam)
             else:
                 works = []
-                overlap = self.world > 1
+                overlap = self.distributed
 
                 def on_chunk(c):
                     if overlap:
@@ -308,7 +311,7 @@ class DataParallel:
         """Best-of-``reps`` ms of the sharded mode's table all-gather alone
         (every block, blocking, no packing), max over ranks: the link rate
         the ``sharded`` mode pays (algbw = N·D·4 B / this)."""
-        if self.world == 1:
+        if not self.distributed:
             return 0.0
         best = float("inf")
         for _ in range(reps):
@@ -333,7 +336,8 @@ class DataParallel:
         torch.cuda.synchronize()
         return self._max_over_ranks(1e3 * (time.perf_counter() - t0) / steps)
 
-    def calibrate(self, run_step, steps: int = 2, measure=None) -> dict | None:
+    def calibrate(self, run_step, steps: int = 2, measure=None,
+                  force: bool = False) -> dict | None:
         """``auto``: run ``steps`` timed training steps (after one untimed
         one) in ``sparse`` and in ``sharded`` mode — ``run_step()`` performs
         one ``self.step`` on a fresh batch — take the max over ranks of each
@@ -341,9 +345,9 @@ class DataParallel:
         the table all-gather alone, in ``self.calibration``.  Every mode
         computes the union batch's update, so the steps taken here are
         ordinary training steps.  A no-op (None) unless mode was "auto" and
-        W > 1.  ``measure(mode, run_step, steps) -> ms`` replaces the wall
-        clock (tests)."""
-        if self.requested != "auto" or self.world == 1:
+        W > 1 (``force``: also at W = 1, tests).  ``measure(mode, run_step,
+        steps) -> ms`` replaces the wall clock (tests)."""
+        if self.requested != "auto" or not self.distributed or (self.world == 1 and not force):
             return None
         measure = measure or self._measure
         ms = {}
@@ -376,6 +380,22 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, 
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+def route_ids(ids: torch.Tensor, n_rows: int, group=None):
+    """Send every row id to the rank owning it (contiguous blocks of
+    n_rows/W rows; ``ids`` ascending int32).  Returns (received ids in
+    source-rank order, per-source counts, per-owner counts sent)."""
+    W = dist.get_world_size(group)
+    per = n_rows // W
+    owner = torch.div(ids.long(), per, rounding_mode="floor").clamp_(max=W - 1)
+    send = torch.bincount(owner, minlength=W)
+    recv = torch.empty_like(send)
+    _a2a(recv, send, group=group)
+    sc, rc = send.tolist(), recv.tolist()
+    rid = torch.empty(int(sum(rc)), dtype=ids.dtype, device=ids.device)
+    _a2a(rid, ids.contiguous(), rc, sc, group=group)
+    return rid, rc, sc
+
+
 def route_rows(rows: torch.Tensor, vals: torch.Tensor, n_rows: int, group=None):
     """Send every (row id, value row) to the rank owning the row — rank q
     owns the contiguous block [q·n_rows/W, (q+1)·n_rows/W) — with one small
@@ -383,17 +403,8 @@ def route_rows(rows: torch.Tensor, vals: torch.Tensor, n_rows: int, group=None):
     ``rows``: ascending int32 [n] (so each owner's rows are one contiguous
     block), ``vals`` [n, d].  Returns (ids [m], vals [m, d], per-source
     counts): the received blocks in source-rank order, each ascending."""
-    W = dist.get_world_size(group)
-    per = n_rows // W
-    owner = torch.div(rows.long(), per, rounding_mode="floor").clamp_(max=W - 1)
-    send = torch.bincount(owner, minlength=W)
-    recv = torch.empty_like(send)
-    _a2a(recv, send, group=group)
-    sc, rc = send.tolist(), recv.tolist()
-    m = int(sum(rc))
-    rid = torch.empty(m, dtype=rows.dtype, device=rows.device)
-    rv = torch.empty(m, vals.shape[1], dtype=vals.dtype, device=vals.device)
-    _a2a(rid, rows.contiguous(), rc, sc, group=group)
+    rid, rc, sc = route_ids(rows, n_rows, group)
+    rv = torch.empty(rid.numel(), vals.shape[1], dtype=vals.dtype, device=vals.device)
     _a2a(rv, vals.contiguous(), rc, sc, group=group)
     return rid, rv, rc
 
@@ -424,6 +435,19 @@ class DenseGradDataParallel:
       dense Adam on this rank's N/W rows, in-place all-gather (ZeRO-1).
     * otherwise: an in-place all-reduce and the replicated Adam.
 
+    * ``table_exchange="fetch"`` (default for GraphSAGE, whose step exposes
+      its sampled tree before the forward): the routed exchange without the
+      all-gather.  Only the owner keeps its row block current; before each
+      forward a rank fetches the current values of the rows its tree reads
+      (~0.5 M distinct rows of 1.1 M at C3) from their owners — one
+      all-to-all of row ids, one of rows back — and the table's slice norms
+      (the loss's parameter-norm term) come from the owners' Adam partials
+      (an all-gather of 2 floats per rank, summed in rank order).  Per rank
+      ≈ (W-1)/W x (touched rows + tree rows) x (4 + 4d) B in, about half of
+      the routed exchange at C3.  The local table is then stale outside the
+      own block and the tree's rows: ``gather_optimizer_state()`` (also
+      ``sync_table()``) all-gathers it before inference or a checkpoint.
+
     In the sharded routes the other rows' Adam moments are not kept here:
     ``gather_optimizer_state()`` brings them together (AdamState.state_dict
     raises until then)."""
@@ -445,19 +469,26 @@ class DenseGradDataParallel:
         tstate = getattr(model, "_table_state", None)
         routable = (tg is not None and tstate is not None and id(tstate.param) in self._states
                     and tg.n_rows % self.world == 0 and not tg.atomic)
+        fetchable = routable and hasattr(model, "sample_tree")
         if table_exchange is None:
-            table_exchange = "routed" if (routable and self.world > 1) else "dense"
-        if table_exchange not in ("routed", "dense"):
+            table_exchange = ("fetch" if fetchable else "routed" if routable else "dense") \
+                if self.world > 1 else "dense"
+        if table_exchange not in ("fetch", "routed", "dense"):
             raise ValueError(table_exchange)
-        if table_exchange == "routed" and not routable:
-            raise ValueError("routed table exchange needs a sorted table gradient (model._tg) "
-                             "whose rows divide by the world size")
+        if table_exchange != "dense" and not routable:
+            raise ValueError("routed / fetch table exchange needs a sorted table gradient "
+                             "(model._tg) whose rows divide by the world size")
+        if table_exchange == "fetch" and not fetchable:
+            raise ValueError("fetch table exchange needs a model with a sampled tree (GraphSAGE)")
         self.table_exchange = table_exchange
         if tg is not None:
             # dense: the sorted table gradient is materialised as .grad so it
-            # can be reduced; routed: it stays in its sparse form
-            tg.dense = self.world > 1 and table_exchange == "dense"
-            model._tg_routed = table_exchange == "routed"
+            # can be reduced; routed / fetch: it stays in its sparse form
+            # (world 1: left as the caller set it)
+            if self.world > 1 or table_exchange != "dense":
+                tg.dense = table_exchange == "dense"
+            model._tg_routed = table_exchange != "dense"
+        self._norms_next = None  # fetch: the table's slice norms after the last update
         self._sharded = set()  # ids of the parameters whose Adam runs sharded
         self._ones = None      # the routed Adam's all-stamped shard
         self.comm_events = None  # (start, end) HIP events per collective (bench)
@@ -529,12 +560,13 @@ class DenseGradDataParallel:
         return rows, tg.acc.index_select(0, rows.long())
 
     @torch.no_grad()
-    def routed_adam(self, rid, rv, counts):
+    def routed_adam(self, rid, rv, counts, norms: torch.Tensor | None = None):
         """Owner side of the routed exchange: S of the own row block from the
         received (ids, rows) blocks — added in source-rank order, each block's
         rows distinct, so no two adds meet one address in a launch — then the
         fused table Adam (G = W·c ⊙ table + S formed in the kernel) on the
-        own rows only."""
+        own rows only; with ``norms`` [2] the updated block's user / item slice
+        norms are written there (the kernel's fixed-order partials)."""
         from . import _lib
         from ._lib import check, lib
         from .engine import _note_raw_write
@@ -556,10 +588,15 @@ class DenseGradDataParallel:
         hp = st.next_hparams()
         pf = p.data.view(-1)
         ea, es = st.exp_avg.view(-1), st.exp_avg_sq.view(-1)
+        sumsq = None
+        if norms is not None:
+            sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(n_own, d)),
+                                device=p.device)
         check(lib.mirec_adam_table(pf[lo * d:].data_ptr(), ea[lo * d:].data_ptr(),
                                    es[lo * d:].data_ptr(), coef.data_ptr(), n_user,
                                    s_own.data_ptr(), self._ones.data_ptr(), 1, n_own, d,
-                                   ctypes.byref(hp), None, None, _lib.stream_handle()),
+                                   ctypes.byref(hp), _lib.ptr(sumsq), _lib.ptr(norms),
+                                   _lib.stream_handle()),
               "adam_table(shard)")
         _note_raw_write()
         tg.pending = False
@@ -576,25 +613,82 @@ class DenseGradDataParallel:
         lo = self.rank * n_own
         rows, vals = self.routed_export()
         a = self._event()
-        if W > 1:
-            rid, rv, counts = route_rows(rows, vals, N, self.group)
-        else:
-            rid, rv, counts = rows, vals, [rows.numel()]
+        # (the collectives run at W = 1 too: a one-GPU job exercises them)
+        rid, rv, counts = route_rows(rows, vals, N, self.group)
         self._note(a, self._event())
+        self.last_exchange_bytes += (sum(counts) - counts[self.rank]) * (4 + d * p.element_size())
+        if self.table_exchange == "fetch":
+            own = torch.empty(2, device=p.device)
+            self.routed_adam(rid, rv, counts, norms=own)
+            # the full table's slice norms: Σ over the owners' blocks of
+            # norm², in rank order (identical on every rank)
+            sq = own * own
+            allp = torch.empty(W, 2, device=p.device)
+            a = self._event()
+            dist.all_gather_into_tensor(allp.view(-1), sq, group=self.group)
+            self._note(a, self._event())
+            tot = allp[0].clone()
+            for q in range(1, W):
+                tot += allp[q]
+            self._norms_next = tot.sqrt()
+            return
         self.routed_adam(rid, rv, counts)
-        if W > 1:
+        if self.distributed:
             pf = p.data.view(-1)
             a = self._event()
             dist.all_gather_into_tensor(pf, pf[lo * d:(lo + n_own) * d], group=self.group)
             self._note(a, self._event())
-        self.last_exchange_bytes += ((sum(counts) - counts[self.rank]) * (4 + d * p.element_size())
-                                     + (W - 1) * n_own * d * p.element_size())
+        self.last_exchange_bytes += (W - 1) * n_own * d * p.element_size()
+
+    @torch.no_grad()
+    def fetch_rows(self, tree):
+        """``fetch``: before the forward, the current values of the rows the
+        tree reads that lie outside this rank's block, from their owners (one
+        all-to-all of ids, one of rows back), written into the local table;
+        and the table's slice norms of the last update for the forward."""
+        m = self.model
+        if self._norms_next is not None:
+            m._norm_cache = (self._norms_next, m._norm_token())
+            self._norms_next = None
+        if not self.distributed or self.world == 1:
+            return
+        p = m._table_state.param
+        N, d = p.shape
+        n_own = N // self.world
+        lo = self.rank * n_own
+        ids = torch.cat([g for g, _ in tree.groups])
+        uniq = torch.unique(ids[ids >= 0])
+        need = uniq[(uniq < lo) | (uniq >= lo + n_own)].to(torch.int32).contiguous()
+        a = self._event()
+        req, rc, sc = route_ids(need, N, self.group)
+        rows = p.data.index_select(0, req.long())
+        got = torch.empty(need.numel(), d, dtype=p.dtype, device=p.device)
+        _a2a(got, rows, sc, rc, group=self.group)
+        self._note(a, self._event())
+        p.data.index_copy_(0, need.long(), got)
+        self.last_exchange_bytes += need.numel() * d * p.element_size() + \
+            (sum(rc) - rc[self.rank]) * 4
+
+    @torch.no_grad()
+    def sync_table(self):
+        """``fetch``: all-gather the owners' row blocks, so every rank's table
+        is current everywhere (before inference or a checkpoint)."""
+        if self.table_exchange != "fetch" or not self.distributed:
+            return
+        p = self.model._table_state.param
+        N, d = p.shape
+        n_own = N // self.world
+        lo = self.rank * n_own
+        pf = p.data.view(-1)
+        dist.all_gather_into_tensor(pf, pf[lo * d:(lo + n_own) * d].clone(), group=self.group)
 
     def gather_optimizer_state(self):
         """All-gather the row shards of the sharded parameters' Adam moments
-        (for a checkpoint: afterwards every rank holds the full state)."""
+        (for a checkpoint: afterwards every rank holds the full state) and,
+        under ``fetch``, the table itself (sync_table)."""
         if not self.distributed:
             return
+        self.sync_table()
         for st in self._states.values():
             if id(st.param) in self._sharded:
                 for t in (st.exp_avg, st.exp_avg_sq):
@@ -607,9 +701,8 @@ class DenseGradDataParallel:
     def _allreduce(self):
         if not self.distributed:
             return
-        self.last_exchange_bytes = 0
         tg = getattr(self.model, "_tg", None)
-        if self.table_exchange == "routed" and tg is not None and tg.pending:
+        if self.table_exchange != "dense" and tg is not None and tg.pending:
             self._routed_table_step()
         params = [p for p in self.model.parameters() if p.grad is not None]
         # large gradients (the id tables) are reduced in place or by row shard;
@@ -643,14 +736,17 @@ class DenseGradDataParallel:
         st = getattr(self.model, "_table_state", None)
         if st is None:
             return False
-        if self.table_exchange == "routed":
+        if self.table_exchange != "dense":
             return True
         p = st.param
         return (self.world > 1 and self.shard_optimizer and p.numel() >= self.BUCKET_MIN
                 and p.shape[0] % self.world == 0)
 
     def step(self, users, pos, neg):
+        self.last_exchange_bytes = 0
         kw = {}
+        if self.table_exchange == "fetch":
+            kw["tree_hook"] = self.fetch_rows
         if getattr(self.model, "captures_dp_step", False):
             # SASRec: the captured step, split around this exchange
             kw["table_by_hook"] = self.table_stepped_by_hook()

@@ -632,10 +632,12 @@ class GraphSAGE(nn.Module):
 
     # ------------------------------------------------------------ training
     def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0,
-                 tree: SampleTree | None = None):
+                 tree: SampleTree | None = None, tree_hook=None):
         """One BPR step (graphsage.py:366-397).  ``loss_scale`` scales the
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
-        between backward and Adam (the gradient all-reduce)."""
+        between backward and Adam (the gradient all-reduce); ``tree_hook(tree)``
+        runs between sampling and the forward (DenseGradDataParallel's row
+        fetch)."""
         seed = self._step_seed * 7919 + self._calls
         self._calls += 1
         for p in self.parameters():
@@ -648,6 +650,8 @@ class GraphSAGE(nn.Module):
                                             u32.numel(), self.n_user, seeds.data_ptr(),
                                             _lib.stream_handle()), "pack_seed_nodes")
             tree = self.sample_tree(seeds, seed)
+        if tree_hook is not None:
+            tree_hook(tree)
         emb = self.forward(tree, dropout_seed=seed if self.training else None)
         loss = self.loss_fused(emb)
         one = self.__dict__.get("_loss_seed")  # kept: no fill kernel per step

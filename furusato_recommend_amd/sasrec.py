@@ -72,16 +72,18 @@ _ORDER_CACHE: dict = {}
 
 
 def _length_order(offsets, B):
-    """[order (B) | packs (1 + 4B)] of a packed batch (mirec_attention_length_order),
-    computed once per offsets tensor: every layer of a step shares it (a
-    captured step launches the ordering pass once)."""
+    """[order (B, padded to 4) | packs (4 + 8B)] of a packed batch
+    (mirec_attention_length_order), computed once per offsets tensor: every
+    layer of a step shares it (a captured step launches the ordering pass
+    once).  The packs start 16-byte aligned (``packs_of``)."""
     key = id(offsets)
     hit = _ORDER_CACHE.get(key)
     if hit is not None and hit[0]() is offsets and hit[1] == offsets._version:
         return hit[2]
-    order = torch.empty(5 * B + 1, dtype=torch.int32, device=offsets.device)
+    bp = -(-B // 4) * 4
+    order = torch.empty(bp + 4 + 8 * B, dtype=torch.int32, device=offsets.device)
     check(lib.mirec_attention_length_order(offsets.data_ptr(), B, order.data_ptr(),
-                                           order[B:].data_ptr(), None, 0, 0,
+                                           order[bp:].data_ptr(), None, 0, 0,
                                            _lib.stream_handle()), "attention_length_order")
     import weakref
     for k in [k for k, v in _ORDER_CACHE.items() if v[0]() is None]:
@@ -224,7 +226,8 @@ class _CausalAttentionVarlen(torch.autograd.Function):
                 # workgroups zero the capacity padding rows
                 _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(
                     lib.mirec_attention_packed_bwd(qkv.data_ptr(), dout.data_ptr(),
-                                                   offsets.data_ptr(), order[B:].data_ptr(), B,
+                                                   offsets.data_ptr(),
+                                                   order[-(-B // 4) * 4:].data_ptr(), B,
                                                    ctx.heads, dh, dqkv.data_ptr(),
                                                    n if ctx.padded else 0,
                                                    _lib.stream_handle()),

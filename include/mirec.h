@@ -603,9 +603,11 @@ int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32
  * mirec_attention_length_order (longest first, device int32 [batch]; the
  * forward with offsets and n_rows > 0 also zeroes out's rows [offsets[batch],
  * n_rows) (capacity padding); with
- * packs (optional, int32 [1 + 4 batch]) it also groups that order into
- * packs of at most 4 blocks of 16 positions for mirec_attention_packed_bwd:
- * packs[0] = count, packs[1 + 4p + s] = sequence or -1); with zero_buf it
+ * packs (optional, int32 [4 + 8 batch], 16-byte aligned) it also groups
+ * that order into packs of at most 4 blocks of 16 positions for
+ * mirec_attention_packed_bwd: packs[0] = count, packs[4 + 8p + 2s] and
+ * packs[5 + 8p + 2s] = (first row, length) of the sequence in slot s of
+ * pack p, (0, 0) when empty); with zero_buf it
  * also zeroes rows [offsets[batch], zero_rows) of that [zero_rows,
  * zero_width] buffer (the capacity padding of a packed batch's output). */
 int mirec_attention_wave_supported(int32_t head_dim);

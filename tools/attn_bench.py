@@ -59,9 +59,10 @@ def main():
             dout = torch.randn(n, d, device="cuda")
             dqkv = torch.empty_like(qkv)
             delta = torch.empty_like(lse)
-            order = torch.empty(5 * B + 1, dtype=torch.int32, device="cuda")
+            bp = -(-B // 4) * 4  # packs start 16-byte aligned
+            order = torch.empty(bp + 4 + 8 * B, dtype=torch.int32, device="cuda")
             chk(lib.mirec_attention_length_order(offs.data_ptr(), B, order.data_ptr(),
-                                                 order[B:].data_ptr(), None, 0, 0, st), "ord")
+                                                 order[bp:].data_ptr(), None, 0, 0, st), "ord")
             op = order.data_ptr() if a.order else None
             t2 = float((lens.double() ** 2).sum())
             by_f = 4.0 * n * 4 * d
@@ -86,7 +87,7 @@ def main():
                     qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(), order.data_ptr(), B, H, dh,
                     dqkv.data_ptr(), st), "blko_bwd"),
                 "packed_bwd": lambda: chk(lib.mirec_attention_packed_bwd(
-                    qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(), order[B:].data_ptr(), B, H,
+                    qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(), order[bp:].data_ptr(), B, H,
                     dh, dqkv.data_ptr(), n, st), "packed_bwd"),
             }
             for name, fn in runs.items():

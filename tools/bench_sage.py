@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--blas", default="", help="torch BLAS backend override (cublas / cublaslt)")
     ap.add_argument("--leaf-bwd", choices=("sorted", "atomic"), default="sorted",
                     help="leaf-hop backward: radix-sorted ordered sums or float atomics")
-    ap.add_argument("--table-exchange", choices=("auto", "routed", "dense"), default="auto",
+    ap.add_argument("--table-exchange", choices=("auto", "fetch", "routed", "dense"), default="auto",
                     help="data-parallel exchange of the id table (dist.DenseGradDataParallel)")
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")

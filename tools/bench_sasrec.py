@@ -125,11 +125,24 @@ def main():
                          "table Adam, or the materialised gradient + dense Adam")
     ap.add_argument("--fused-rows", type=int, default=1,
                     help="0: the torch composition of dropout / residual / LayerNorm (A/B)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="under torch.distributed.run: every rank on cuda:0, gloo collectives "
+                         "(the data-parallel path on one GPU; not a throughput measurement)")
+    ap.add_argument("--table-exchange", default="auto", choices=["auto", "routed", "dense"])
     args = ap.parse_args()
     from furusato_recommend_amd import SASRec, sasrec as S
     from furusato_recommend_amd.sasrec import SequenceData
     S.ATTN_IMPL = args.attn_impl
-    dev = torch.device("cuda:0")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    gpu = 0 if args.rehearse else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    if world > 1:
+        import torch.distributed as dist
+
+        from furusato_recommend_amd.dist import DenseGradDataParallel, init_distributed
+        init_distributed("gloo" if args.rehearse else "nccl", dev)
     torch.manual_seed(2020)
     seq = SequenceData.synthetic(args.users, args.items, dev, max_len=args.maxlen, min_len=5,
                                  seed=0)
@@ -140,6 +153,10 @@ def main():
                 "graph": bool(args.graph), "table_grad": args.table_grad},
                _DS(args.users, args.items),
                sequences=seq)
+    dp = None
+    if world > 1:
+        dp = DenseGradDataParallel(m, table_exchange=None if args.table_exchange == "auto"
+                                   else args.table_exchange)
     B = args.batch
     g = torch.Generator(device=dev).manual_seed(7)
 
@@ -151,20 +168,43 @@ def main():
         # (so the packed batch is sized without a device sync); positive = a
         # random element of the user's sequence; negative uniform (timing
         # workload: no rejection of positives)
-        u_h = rng.integers(0, args.users, B)
+        u_h = rng.integers(0, args.users // world, B) * world + rank  # the rank's user shard
         u = m._upload(u_h)  # pinned staging: no stream sync
         step[0] += 1
         pn = m.sample_pairs(u, 7, step[0] * B)  # one launch: [pos ; neg]
         return u_h, pn[0], pn[1]
 
+    run = m.stageOne if dp is None else dp.step
     for _ in range(args.warmup):
-        m.stageOne(*batch())
+        run(*batch())
     torch.cuda.synchronize()
+    if dp is not None:
+        dp.comm_events = []
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        m.stageOne(*batch())
+        run(*batch())
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    comm = None
+    if dp is not None:
+        from furusato_recommend_amd.dist import _elapsed_ms
+        cm = _elapsed_ms(dp.comm_events) / args.steps
+        dp.comm_events = None
+        t = torch.tensor([dt, cm], dtype=torch.float64, device="cpu" if args.rehearse else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, cm = float(t[0]), float(t[1])
+        comm = {"backend": dist.get_backend(), "world_size": world,
+                "table_exchange": dp.table_exchange, "comm_ms_per_step": round(cm, 4),
+                "exchange_bytes_per_rank": dp.last_exchange_bytes,
+                "step": "captured, split around the exchange" if m.config["graph"] else "eager"}
+        if rank == 0:
+            print(json.dumps({"metric": "SASRec BPR positive-edges/sec (C4), data parallel",
+                              "value": round(world * args.steps * B / dt, 1),
+                              "unit": "positive-edges/s", "ms_per_step_rank": round(1e3 * dt / args.steps, 3),
+                              "rehearsal": bool(args.rehearse), "comm": comm}), flush=True)
+        dist.destroy_process_group()
+        return
     # per-launch attention timing: a few eager steps of the same kernels
     # (events on the launch stream; a replayed graph records none)
     graph_mode = m.config["graph"]

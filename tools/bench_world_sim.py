@@ -53,7 +53,7 @@ def main():
                          "local copies and re-prescale of the all-gather; the RCCL "
                          "transfer itself is not measured)")
     ap.add_argument("--model", choices=("lgn", "sage"), default="lgn")
-    ap.add_argument("--exchanges", default="routed,dense",
+    ap.add_argument("--exchanges", default="fetch,routed,dense",
                     help="sage: table exchanges to simulate")
     ap.add_argument("--rates", default="100,200,300,400",
                     help="sage: link rates (GB/s of received bytes per rank) to project at")
@@ -157,14 +157,15 @@ def sage_main(args):
             dp = DenseGradDataParallel(m, table_exchange=ex)  # world 1: no collectives
             dp.world, dp.rank = W, 0  # rank 0 of a world of W (local work only)
             m._tg.dense = ex == "dense"
-            m._tg_routed = ex == "routed"
+            m._tg_routed = ex != "dense"
             n_own = N // W
+            fetched = [0]
             others = []  # what ranks 1..W-1 send to owner 0: (ids, rows)
             for r in range(1, W):
                 u, p, n = m.sample(B, seed=11, offset=10**8 + r * B, shard=r, n_shards=W)
 
                 def capture():
-                    if ex == "routed":
+                    if ex != "dense":
                         rows, vals = dp.routed_export()
                         k = int((rows < n_own).sum())
                         others.append((rows[:k].clone(), vals[:k].clone()))
@@ -174,13 +175,24 @@ def sage_main(args):
                 m.stageOne(u, p, n, grad_hook=capture, loss_scale=1.0 / W)
             recv_other = sum(o[0].numel() for o in others) * (4 + 4 * d)
 
+            def tree_hook(tree):
+                # fetch's local work at rank 0: the tree's distinct rows outside
+                # block 0, their gather (at the owners: the same count) and the
+                # write into the local table
+                ids = torch.cat([g for g, _ in tree.groups])
+                uniq = torch.unique(ids[ids >= 0])
+                need = uniq[uniq >= n_own].long()
+                fetched[0] = need.numel()
+                m._table.data.index_copy_(0, need, m._table.data.index_select(0, need))
+
             def hook():
-                if ex == "routed":
+                if ex != "dense":
                     rows, vals = dp.routed_export()
                     k = int((rows < n_own).sum())
                     rid = torch.cat([rows[:k]] + [o[0] for o in others])
                     rv = torch.cat([vals[:k]] + [o[1] for o in others])
-                    dp.routed_adam(rid, rv, [k] + [o[0].numel() for o in others])
+                    norms = torch.empty(2, device=dev) if ex == "fetch" else None
+                    dp.routed_adam(rid, rv, [k] + [o[0].numel() for o in others], norms=norms)
                 else:  # materialised G; the reduce-scatter's output stands in as a slice
                     g = m._table.grad
                     st = dp._states[id(m._table)]
@@ -206,7 +218,8 @@ def sage_main(args):
             def step():
                 u, p, n = m.sample(B, seed=7, offset=step_no[0] * B, shard=0, n_shards=W)
                 step_no[0] += 1
-                m.stageOne(u, p, n, grad_hook=hook if W > 1 else None, loss_scale=1.0 / W)
+                m.stageOne(u, p, n, grad_hook=hook if W > 1 else None, loss_scale=1.0 / W,
+                           tree_hook=tree_hook if (W > 1 and ex == "fetch") else None)
 
             for _ in range(args.warmup):
                 step()
@@ -219,7 +232,9 @@ def sage_main(args):
             if W == 1:
                 base = ms
             table_b = N * d * 4
-            if ex == "routed":
+            if ex == "fetch":
+                recv = recv_other + fetched[0] * (4 + 4 * d)
+            elif ex == "routed":
                 recv = recv_other + (W - 1) * table_b // W
             else:
                 recv = 2 * (W - 1) * table_b // W
@@ -232,6 +247,7 @@ def sage_main(args):
                               "ms_per_step_rank_compute": round(ms, 4),
                               "recv_bytes_per_rank": int(recv if W > 1 else 0),
                               "routed_rows_from_others": int(recv_other // (4 + 4 * d)),
+                              "fetched_rows": fetched[0] if ex == "fetch" else None,
                               "projected": proj if W > 1 else None}), flush=True)
             if W == 1:
                 break  # one single-GPU baseline (both exchanges are the plain step)
