@@ -95,6 +95,10 @@ SIGNATURES = {
                                     c_void_p]),
     "mirec_propagate": (c_int, [POINTER(CSR), POINTER(Prop), c_void_p]),
     "mirec_prescale": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "mirec_shard_pack": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int64, c_int64,
+                                 c_void_p, c_void_p]),
+    "mirec_shard_unpack": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int64,
+                                   c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mirec_frontier": (c_int, [POINTER(CSR), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p]),

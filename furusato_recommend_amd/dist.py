@@ -158,9 +158,15 @@ class DataParallel:
 
     def _pack(self, c: int, t: torch.Tensor):
         s0, s1, _, st = self._chunks[c]
-        N = t.shape[0]
+        N, D = t.shape
         r, W = self.rank, self.world
-        rows = t[r + s0 * W: min(s1 * W, N): W]
+        if t.is_cuda:
+            from . import _lib
+            from ._lib import check, lib
+            check(lib.mirec_shard_pack(t.data_ptr(), N, D, W, r, s0, s1 - s0, st[r].data_ptr(),
+                                       _lib.stream_handle()), "shard_pack")
+            return
+        rows = t[r + s0 * W: min(s1 * W, N): W]  # (host tensors: the CPU driver tests)
         st[r, : rows.shape[0]].copy_(rows)
 
     def _gather_chunk(self, c: int, async_op: bool):
@@ -169,10 +175,21 @@ class DataParallel:
         return dist.all_gather_into_tensor(st.view(-1, D), st[self.rank], group=self.group,
                                            async_op=async_op)
 
-    def _unpack(self, c: int, t: torch.Tensor):
+    def _unpack(self, c: int, t: torch.Tensor, x0s: torch.Tensor | None = None):
+        """Block c's rows of the other ranks from the staging buffer into
+        ``t`` (and, with ``x0s``, dinv ⊙ those rows into x0s: the next
+        forward's pre-scaled input)."""
         s0, s1, _, st = self._chunks[c]
         N, D = t.shape
         W = self.world
+        if t.is_cuda:
+            from . import _lib
+            from ._lib import check, lib
+            check(lib.mirec_shard_unpack(st.data_ptr(), N, D, W, self.rank, s0, s1 - s0,
+                                         _lib.ptr(None if x0s is None else self.engine.g.dinv),
+                                         t.data_ptr(), _lib.ptr(x0s), _lib.stream_handle()),
+                  "shard_unpack")
+            return
         e = min(s1 * W, N)
         full = (e - s0 * W) // W  # slots holding all W ranks' rows
         if full:
@@ -281,11 +298,17 @@ class DataParallel:
                 eng.backward(self.emb, adam=self.adam, last_rows=self.last_rows,
                              on_chunk=on_chunk)
                 a = self._event()
+                # the unpack also writes dinv ⊙ E for the other ranks' rows
+                # (the fused Adam wrote this rank's): no prescale pass follows
+                x0s = getattr(eng, "x0s", None) if self.emb.is_cuda else None
                 for c, w in enumerate(works):
                     w.wait()
-                    self._unpack(c, self.emb)
+                    self._unpack(c, self.emb, x0s)
                 self._note(a, self._event())
-                eng.invalidate_prescaled()
+                if x0s is not None and overlap and getattr(eng, "reuse_prescaled", False):
+                    eng.mark_prescaled(self.emb)
+                else:
+                    eng.invalidate_prescaled()
                 self._mark_sharded_state(self.world > 1)
         else:
             if self.grad is None:

@@ -473,6 +473,13 @@ class PropagationEngine:
         self._x0s_token = None
         self._acc_full = None
 
+    def mark_prescaled(self, emb: torch.Tensor):
+        """x0s holds dinv ⊙ emb on every row (written piecewise by the
+        caller, e.g. the sharded data-parallel unpack): the next forward
+        skips its prescale pass."""
+        self._x0s_token = self._token(emb)
+        self._acc_full = None
+
     def prescale(self, x: torch.Tensor, out: torch.Tensor):
         check(lib.mirec_prescale(x.data_ptr(), self.g.dinv.data_ptr(), self.g.n_nodes, self.dim,
                                  out.data_ptr(), _lib.stream_handle()), "prescale")

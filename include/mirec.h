@@ -214,6 +214,21 @@ int mirec_propagate(const mirec_csr_t *csr, const mirec_prop_t *p,
 int mirec_prescale(const float *x, const float *dinv, int64_t n_rows,
                    int32_t dim, float *out, mirec_stream_t stream);
 
+/* Row shards of the data-parallel `sharded` exchange (csrc/shard.hip;
+ * replaces the reference's never-synchronised DDP, ddp_lgcn.py:663-673).
+ * Rank r of W owns rows i ≡ r (mod W); slot s of rank r is row r + s·W; a
+ * block of slots [slot0, slot0 + n_slots) is all-gathered through a
+ * [W][n_slots][dim] staging buffer.  pack: stage_rank[s] = table[rank +
+ * (slot0 + s)·W] (rows past n_rows give zero rows).  unpack: table[w +
+ * (slot0 + s)·W] = stage[w][s] for every w != rank (rows past n_rows
+ * skipped) and, with x0s (and dinv), x0s[row] = dinv[row] · stage[w][s]. */
+int mirec_shard_pack(const float *table, int64_t n_rows, int32_t dim, int32_t world,
+                     int32_t rank, int64_t slot0, int64_t n_slots, float *stage_rank,
+                     mirec_stream_t stream);
+int mirec_shard_unpack(const float *stage, int64_t n_rows, int32_t dim, int32_t world,
+                       int32_t rank, int64_t slot0, int64_t n_slots, const float *dinv,
+                       float *table, float *x0s, mirec_stream_t stream);
+
 /* Frontier bitmaps of a key set S (keys[n_keys], entries outside [0, n_rows)
  * ignored; or, if keys == NULL, the 3*batch nodes of the triples users[b],
  * n_users+pos[b], n_users+neg[b]):  bm_self = S, bm_hop = S ∪ N(S).  Both

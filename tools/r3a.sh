@@ -1,7 +1,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "mf_c1 or users_rating or union_step or captured_step_equals or data_parallel or lgconv or dense_grad or score_topk or evaluate" > gpurun_out/r3a_pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "mf_c1 or users_rating or union_step or captured_step_equals or data_parallel or lgconv or dense_grad or score_topk or evaluate or routed" > gpurun_out/r3a_pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/r3a_pytest.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py --gpus 2 --rehearse --steps 5 --warmup 2 --calib-steps 2 > gpurun_out/r3a_rehearse.log 2>&1
