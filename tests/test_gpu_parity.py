@@ -2444,17 +2444,17 @@ def _dp_rank_union(rank, world, port, kind, exchange, q, over=None):
         m, ds = _union_model(kind, **(over or {}))
         dp = DenseGradDataParallel(m, table_exchange=exchange)
         assert dp.table_exchange == exchange
-        batches, states = [], []
+        batches, states, losses = [], [], []
         for i in range(3):
             u, p, n = _union_batch(m, ds, kind, i, rank, world)
             batches.append([torch.as_tensor(x).cpu().numpy() for x in (u, p, n)])
             states.append(torch.get_rng_state().numpy().copy())
-            dp.step(u, p, n)
+            losses.append(float(dp.step(u, p, n)))
         torch.cuda.synchronize()
         dp.gather_optimizer_state()
         st = m._table_state
         q.put((rank, [x.detach().cpu().numpy().copy() for x in m.parameters()], batches, states,
-               st.exp_avg.cpu().numpy().copy(), dp.last_exchange_bytes))
+               st.exp_avg.cpu().numpy().copy(), dp.last_exchange_bytes, losses))
     finally:
         dist.destroy_process_group()
 
@@ -2565,29 +2565,33 @@ def test_sasrec_data_parallel_captured_step_equals_eager(exchange):
     graph A (packing, forward, loss x 1/W, backward), the exchange between
     the replays, graph B (Adam of what the exchange does not step).  2 ranks
     on one GPU, dropout off (the captured step draws its dropout keys from a
-    device seed base): the captured run equals the eager run of the same
-    batches (the step's row-slice sums see the capacity padding rows: fp32
-    order only) and the replicas stay bit-identical."""
+    device seed base): the captured run gives the eager run's losses at every
+    step and its parameters up to fp32 order (the step's row-slice sums see
+    the capacity padding rows), and the replicas stay bit-identical."""
     cap = _run_ranks(_dp_rank_union_graph, (exchange, True))
     eag = _run_ranks(_dp_rank_union_graph, (exchange, False))
     for a, b in zip(cap[0][0], cap[1][0]):
         assert np.array_equal(a, b)
+    for r in (0, 1):  # every step's loss (as test_sasrec_graph_step_equals_eager)
+        for lc, le in zip(cap[r][5], eag[r][5]):
+            assert abs(lc - le) <= 1e-5 * abs(le), (r, lc, le)
     m, _ = _union_model("sasrec")
     for (nm, _), a, b in zip(m.named_parameters(), cap[0][0], eag[0][0]):
         a, b = torch.from_numpy(a), torch.from_numpy(b)
         # (one BLAS backend for both) the captured step's row slices see the
-        # capacity padding rows: fp32 order, which Adam's lr·m̂/(√v̂ + eps)
-        # magnifies where a gradient is small; the slices whose exact
-        # gradient is zero (the attention key bias, the item tower's last
-        # bias: see the union-step test) are bounded by the step size only
-        ok = torch.ones_like(a, dtype=torch.bool)
+        # capacity padding rows: fp32 order.  Adam's first steps are
+        # ±lr·sign(g) wherever |g| >> eps, so an element whose gradient is
+        # rounding noise — the structurally zero slices (attention key bias,
+        # the item tower's last bias) and the occasional near-cancelling
+        # table element — may step either way: every element within the 3
+        # steps' bound, all but 0.1 % of each parameter's within 1e-4
+        assert float((a - b).abs().max()) <= 2 * 3 * 1e-3 + 1e-7, nm
+        far = (a - b).abs() > 1e-4 * float(b.abs().max())
         if nm.endswith("in_proj_bias"):
-            ok[a.numel() // 3: 2 * a.numel() // 3] = False
+            far[a.numel() // 3: 2 * a.numel() // 3] = False
         if nm == "item_last_proj.bias":
-            ok[:] = False
-        assert float((a - b).abs().max()) <= 3 * 1e-3 + 1e-7, nm
-        if bool(ok.any()):
-            assert rel(a[ok], b[ok]) < 1e-4, nm
+            far[:] = False
+        assert float(far.float().mean()) <= 1e-3, (nm, int(far.sum()))
 
 
 # ------------------------------------------------------------ sorted table gradient

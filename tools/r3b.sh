@@ -11,7 +11,7 @@ run() {  # name, seconds, command...
   echo "$name rc=$rc"; tail -3 gpurun_out/r3b_$name.log
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
-run tests_attn 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "attention or sasrec or packed or c3_full"
+run tests_attn 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "attention or sasrec or packed or c3_full or shard"
 run attn_bench 200 python tools/attn_bench.py --batches 2048 --mixes c4,64
 run world_sim_c3 500 python tools/bench_world_sim.py --model sage --worlds 1,2,4,8 --steps 10 --warmup 3
 run sage_dp2_fetch 300 python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29610 tools/bench_sage.py --rehearse --steps 5 --warmup 3 --table-exchange fetch --cpu-baseline 0
