@@ -246,6 +246,8 @@ SIGNATURES = {
     "mirec_gemm_tn_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                  c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p]),
     "mirec_gemm_tn_work_floats": (c_int64, [c_int64, c_int32, c_int32]),
+    "mirec_col_sums_work_floats": (c_int64, [c_int64, c_int32]),
+    "mirec_col_sums": (c_int, [c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     "mirec_gemm_tn": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                               c_void_p, c_void_p]),
     "mirec_resnorm_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -684,9 +684,84 @@ static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   *slices = (int)std::max<int64_t>(1, (n + r - 1) / r);
 }
 
+// Column sums out[c] = Σ_r A[r, c] of a row-major [n, m] matrix in a fixed
+// order (the bias gradient db = Σ_rows dY of Linear layers whose widths the
+// GEMM tiles do not take; torch's reduction kernel gave replay-dependent
+// bias gradients inside the captured SASRec step).  Pass 1: workgroup
+// (slice s, column block) — one lane per column walks the slice's rows in
+// order with four row-interleaved partial sums added as ((p0 + p1) + (p2 +
+// p3)); pass 2: one lane per column adds the slices' partials in slice order.
+constexpr int kCsRows = 64;  // rows per slice (at least)
+__global__ __launch_bounds__(256) void col_sums_slice_kernel(const float *__restrict__ A,
+                                                             float *__restrict__ work, int64_t n,
+                                                             int m, int64_t rows) {
+  const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  if (c >= m) return;
+  const int64_t r0 = (int64_t)blockIdx.x * rows, r1 = min(n, r0 + rows);
+  float p[4] = {0.f, 0.f, 0.f, 0.f};
+  int64_t r = r0;
+  for (; r + 4 <= r1; r += 4) {
+    const float a0 = A[r * m + c], a1 = A[(r + 1) * m + c];
+    const float a2 = A[(r + 2) * m + c], a3 = A[(r + 3) * m + c];
+    p[0] += a0;
+    p[1] += a1;
+    p[2] += a2;
+    p[3] += a3;
+  }
+  for (int k = 0; r < r1; ++r, ++k) p[k] += A[r * m + c];
+  work[(int64_t)blockIdx.x * m + c] = (p[0] + p[1]) + (p[2] + p[3]);
+}
+
+__global__ __launch_bounds__(256) void col_sums_final_kernel(const float *__restrict__ work,
+                                                             float *__restrict__ out, int slices,
+                                                             int m) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= m) return;
+  float s = 0.f;
+  for (int q = 0; q < slices; ++q) s += work[(int64_t)q * m + c];
+  out[c] = s;
+}
+
+static void cs_slices(int64_t n, int m, int *slices, int64_t *rows) {
+  // about 2048 workgroups over the chip, at least kCsRows rows each
+  const int64_t cb = (m + 255) / 256;
+  const int64_t want = std::max<int64_t>(1, 2048 / cb);
+  int64_t r = std::max<int64_t>(kCsRows, (n + want - 1) / want);
+  *rows = r;
+  *slices = (int)std::max<int64_t>(1, (n + r - 1) / r);
+}
+
 }  // namespace mirec
 
 using namespace mirec;
+
+extern "C" int64_t mirec_col_sums_work_floats(int64_t n, int32_t m) {
+  if (n < 0 || m <= 0) return -1;
+  int slices;
+  int64_t rows;
+  cs_slices(std::max<int64_t>(n, 1), m, &slices, &rows);
+  return (int64_t)slices * m;
+}
+
+extern "C" int mirec_col_sums(const float *A, int64_t n, int32_t m, float *out, float *work,
+                              mirec_stream_t stream) {
+  MIREC_CHECK_ARG(n >= 0 && m > 0 && out && work && (n == 0 || A));
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) {
+    MIREC_HIP(hipMemsetAsync(out, 0, sizeof(float) * m, st));
+    return MIREC_OK;
+  }
+  int slices;
+  int64_t rows;
+  cs_slices(n, m, &slices, &rows);
+  const unsigned cb = (unsigned)((m + 255) / 256);
+  hipLaunchKernelGGL(col_sums_slice_kernel, dim3((unsigned)slices, cb), dim3(256), 0, st, A,
+                     work, n, (int)m, rows);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(col_sums_final_kernel, dim3(cb), dim3(256), 0, st, work, out, slices, (int)m);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
 
 static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Amask,
                    const float *B, const float *bias, float *C, float *C2, int32_t Ns,

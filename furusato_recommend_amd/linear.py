@@ -82,15 +82,31 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, colsum: bool):
     return c, cs
 
 
+def col_sums(a: torch.Tensor) -> torch.Tensor:
+    """Σ over the rows of a contiguous [n, m] float32 tensor, in a fixed order
+    (mirec_col_sums: deterministic and capturable — torch's reduction kernel
+    gave replay-dependent bias gradients inside the captured SASRec step)."""
+    a = a.contiguous()
+    n, m = a.shape
+    out = torch.empty(m, dtype=a.dtype, device=a.device)
+    work = torch.empty(max(int(lib.mirec_col_sums_work_floats(n, m)), 1), dtype=a.dtype,
+                       device=a.device)
+    check(lib.mirec_col_sums(a.data_ptr(), n, m, out.data_ptr(), work.data_ptr(),
+                             _lib.stream_handle()), "col_sums")
+    return out
+
+
 def weight_grad(dy: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
-    """dyᵀ x for dy [n, N], x [n, K] (contiguous rows), torch GEMMs."""
+    """dyᵀ x for dy [n, N], x [n, K] (contiguous rows), torch GEMMs (the
+    slices' products summed by col_sums)."""
     n = dy.shape[0]
     if n < SPLIT * MIN_ROWS_PER_SLICE:
         return dy.t() @ x
     m = n // SPLIT
     main = SPLIT * m
-    g = torch.bmm(dy[:main].view(SPLIT, m, dy.shape[1]).transpose(1, 2),
-                  x[:main].view(SPLIT, m, x.shape[1])).sum(0)
+    parts = torch.bmm(dy[:main].view(SPLIT, m, dy.shape[1]).transpose(1, 2),
+                      x[:main].view(SPLIT, m, x.shape[1]))
+    g = col_sums(parts.view(SPLIT, -1)).view(dy.shape[1], x.shape[1])
     if main < n:
         g = g + dy[main:].t() @ x[main:]
     return g
@@ -126,7 +142,7 @@ class _LinearSplitK(torch.autograd.Function):
             else:
                 dw, db = r
         if want_db and db is None:
-            db = dy2.sum(0)
+            db = col_sums(dy2)
         return dx, dw, db
 
 

@@ -738,6 +738,15 @@ int mirec_gemm_nt(const float *A, const float *B, const float *bias, float *C, i
  * work: mirec_gemm_tn_work_floats(n, M, No) floats (per-slice partial
  * sums, added in a fixed order: deterministic). */
 int64_t mirec_gemm_tn_work_floats(int64_t n, int32_t M, int32_t No);
+
+/* out[c] = Σ_r A[r, c] over the n rows of a row-major [n, m] matrix, summed
+ * in a fixed order (deterministic, capturable): the bias gradient db = Σ dY
+ * of a Linear whose width the GEMM tiles do not take (nn.Linear backward,
+ * model/sasrec.py:385-421), and the slice sum of the split weight gradient.
+ * work: mirec_col_sums_work_floats(n, m) floats. */
+int64_t mirec_col_sums_work_floats(int64_t n, int32_t m);
+int mirec_col_sums(const float *A, int64_t n, int32_t m, float *out, float *work,
+                   mirec_stream_t stream);
 int mirec_gemm_tn(const float *A, const float *B, float *C, float *colsum, int64_t n, int32_t M,
                   int32_t No, float *work, mirec_stream_t stream);
 

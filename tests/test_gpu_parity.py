@@ -1516,8 +1516,10 @@ def test_sasrec_stage_one_equals_unfused_composition():
     for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
         scale = float(pb.grad.abs().max())
         # item_last_proj.bias and the key part of in_proj_bias have exactly
-        # zero gradient (the bias cancels in pos - neg / in the softmax)
-        assert float((grads[name] - pb.grad).abs().max()) <= TOL * max(scale, 1e-4), name
+        # zero gradient (the bias cancels in pos - neg / in the softmax): the
+        # fused tower sums pos and neg rows in one fixed-order column sum, so
+        # that zero arrives as rounding noise (~1e-8) — floor 1e-3 x TOL
+        assert float((grads[name] - pb.grad).abs().max()) <= TOL * max(scale, 1e-3), name
         live[name] = pb.grad.abs() > 1e-5 * scale
     b.optims.step()
     for (name, pa), pb in zip(a.named_parameters(), b.parameters()):
@@ -1956,6 +1958,39 @@ def test_gemm_tn_matches_fp64(n, m, no):
     assert rel(cs, a.double().sum(0)) < 1e-6
     c2, cs2 = gemm_tn(a, b, True)
     assert torch.equal(c, c2) and torch.equal(cs, cs2)
+
+
+@pytest.mark.parametrize("n,m", [(0, 5), (1, 1), (3, 7), (63, 192), (64, 192), (7169, 192),
+                                 (70_001, 64), (32, 12_288)])
+def test_col_sums_matches_fp64_and_replays_equal(n, m):
+    """mirec_col_sums (the bias gradient of Linear widths the GEMM tiles do
+    not take, and the split weight gradient's slice sum) vs float64; bitwise
+    repeatable, and a captured HIP graph's replays give the eager bits — the
+    replacement for torch's sum(0), whose result inside the captured SASRec
+    data-parallel step depended on host timing (the layer-0 QKV bias
+    gradient differed by up to 2 between two runs of the same step)."""
+    from furusato_recommend_amd.linear import col_sums
+    torch.manual_seed(n + m)
+    a = torch.randn(n, m, device="cuda")
+    c = col_sums(a)
+    assert c.shape == (m,)
+    if n == 0:
+        assert float(c.abs().max()) == 0.0
+        return
+    assert rel(c, a.double().sum(0)) < 1e-6
+    assert torch.equal(c, col_sums(a))
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        col_sums(a)  # warm-up off the capture
+    torch.cuda.current_stream().wait_stream(side)
+    with torch.cuda.graph(g):
+        out = col_sums(a)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        assert torch.equal(out, c)
 
 
 def test_linear_on_mirec_gemms_matches_torch():
@@ -2574,7 +2609,7 @@ def test_sasrec_data_parallel_captured_step_equals_eager(exchange):
         assert np.array_equal(a, b)
     for r in (0, 1):  # every step's loss (as test_sasrec_graph_step_equals_eager)
         for lc, le in zip(cap[r][5], eag[r][5]):
-            assert abs(lc - le) <= 1e-5 * abs(le), (r, lc, le)
+            assert abs(lc - le) <= 1e-5 * abs(le), (r, cap[r][5], eag[r][5])
     m, _ = _union_model("sasrec")
     for (nm, _), a, b in zip(m.named_parameters(), cap[0][0], eag[0][0]):
         a, b = torch.from_numpy(a), torch.from_numpy(b)
