@@ -85,7 +85,11 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, colsum: bool):
 def col_sums(a: torch.Tensor) -> torch.Tensor:
     """Σ over the rows of a contiguous [n, m] float32 tensor, in a fixed order
     (mirec_col_sums: deterministic and capturable — torch's reduction kernel
-    gave replay-dependent bias gradients inside the captured SASRec step)."""
+    gave replay-dependent bias gradients inside the captured SASRec step).
+    Tensors off the HIP device or not float32 (the module used as a plain
+    nn.Linear, e.g. float64 on the host) take torch's sum."""
+    if not (a.is_cuda and a.dtype == torch.float32):
+        return a.sum(0)
     a = a.contiguous()
     n, m = a.shape
     out = torch.empty(m, dtype=a.dtype, device=a.device)
