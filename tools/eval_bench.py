@@ -59,9 +59,18 @@ def main():
                           "tflops_scores": round(flop / ms / 1e9, 1),
                           "rating_matrix_bytes": 0 if name == "stream" else 4 * a.batch * a.items}),
               flush=True)
-    same = torch.equal(out["stream"][1], out["dense"][1])
+    si, di = out["stream"][1], out["dense"][1]
+    same = torch.equal(si, di)
+    rows_same = float((si == di).all(dim=1).float().mean())
     vdiff = float((out["stream"][0] - out["dense"][0]).abs().max())
-    print(json.dumps({"agree_idx": same, "max_val_diff": vdiff}), flush=True)
+    vmax = float(out["dense"][0].abs().max())
+    # the two paths sum the d products in different orders: scores agree to
+    # fp32 rounding, so near-tied items may swap places; the position-wise
+    # scores of the two top-k lists agreeing within that rounding means
+    # both are a top-k of the same ratings
+    print(json.dumps({"agree_idx": same, "rows_identical_frac": round(rows_same, 6),
+                      "max_val_diff": vdiff, "max_score": vmax,
+                      "same_topk_values": vdiff <= 1e-6 * vmax}), flush=True)
 
 
 if __name__ == "__main__":
