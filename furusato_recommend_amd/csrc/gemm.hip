@@ -35,6 +35,72 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
+// ---------------------------------------------- f32 products on bf16 MFMA
+// MIREC_GEMM_X6 (default): every f32 operand is split exactly into three
+// bf16 terms, x = x_h + x_m + x_l (round-to-nearest at each stage; the
+// residuals x - x_h and (x - x_h) - x_m are exact in f32, |x_m| <= 2^-8 |x|,
+// |x_l| <= 2^-16 |x|, and x_l carries the rest to 2^-25 |x|), and a·b is
+// taken as the six products whose size is at least 2^-16 |ab|:
+//   a_l b_h + a_h b_l + a_m b_m + a_m b_h + a_h b_m + a_h b_h
+// on v_mfma_f32_32x32x16_bf16 (bf16 x bf16 products are exact in f32, f32
+// accumulate).  The dropped terms (a_m b_l, a_l b_m, a_l b_l) are below
+// 2^-23 |ab|: the error per product is that of one f32 rounding, i.e. the
+// f32 GEMM's own accuracy (tests against float64 at 1e-6), at 6 x 32 = 192
+// MFMA cycles per 32x32x16 block instead of 8 x 64 = 512 with
+// v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md cycle constants).
+#ifndef MIREC_GEMM_X6
+#define MIREC_GEMM_X6 1
+#endif
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+
+// packed RNE (a in the low half)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// x[0..7] -> three bf16x8 planes (element e of every plane is x[e]'s term)
+__device__ __forceinline__ Split3 split3(const float (&x)[8]) {
+  u32x4 H, M, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = x[2 * p], b = x[2 * p + 1];
+    const uint32_t ph = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+    const uint32_t pm = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
+    H[p] = ph;
+    M[p] = pm;
+    L[p] = pk_bf16(sa, sb);
+  }
+  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M),
+                __builtin_bit_cast(bf16x8, L)};
+}
+
+// C += A·B over one 16-deep k block: lane (i, h) supplies row / column i's
+// 8 k values of its half (any k order, the same for A and B)
+__device__ __forceinline__ f32x16 mfma_x6(const Split3 &a, const Split3 &b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
+  return c;
+}
+
+// The k order of a lane half h inside a 16-deep block: element e < 4 is k =
+// 4 h + e, e >= 4 is 8 + 4 h + (e - 4) — two float4 reads of a [row][k] LDS
+// row, and on a [k][col] image the two halves' rows are 4 apart (32 banks at
+// the row strides used here), as in the f32 form's sub-chunks.
+__device__ __forceinline__ int x6_k(int h, int e) { return 4 * h + (e & 3) + 8 * (e >> 2); }
+
 // LDS visibility among the lanes of one wave (the epilogue slabs are
 // wave-private: no workgroup barrier)
 __device__ __forceinline__ void wave_sync() {
@@ -82,7 +148,7 @@ struct NtArgs {
 // The k loop of gemm_nt (shared by the plain and the LayerNorm epilogues):
 // acc[TM][2] of wave (wm, wn) over output rows [m0, +BM), columns [n0, +128);
 // smem holds (BM + 128) * kLdNT floats.
-template <int BM, int PF, bool BKN>
+template <int BM, int PF, bool BKN, bool X6 = MIREC_GEMM_X6>
 __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict__ A,
                                             const float *__restrict__ B, int64_t n, int Kr,
                                             int No, const NtArgs &fx, int64_t m0, int n0,
@@ -162,6 +228,39 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   auto compute = [&]() {
+    if constexpr (X6) {
+#pragma unroll
+    for (int s16 = 0; s16 < kChunk / 16; ++s16) {
+      Split3 sa[TM], sb[2];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+        const float *ap = sA + (wm * (BM / 2) + tm * 32 + i) * kLdNT + s16 * 16 + 4 * h;
+        const float4 lo = ld4(ap), hi = ld4(ap + 8);
+        const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        sa[tm] = split3(x);
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        const int col = wn * 64 + tn * 32 + i;
+        float x[8];
+        if constexpr (BKN) {
+          const float *bp = sB + (s16 * 16 + 4 * h) * kLdTN + col;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = bp[(x6_k(0, e)) * kLdTN];
+        } else {
+          const float *bp = sB + col * kLdNT + s16 * 16 + 4 * h;
+          const float4 lo = ld4(bp), hi = ld4(bp + 8);
+          x[0] = lo.x, x[1] = lo.y, x[2] = lo.z, x[3] = lo.w;
+          x[4] = hi.x, x[5] = hi.y, x[6] = hi.z, x[7] = hi.w;
+        }
+        sb[tn] = split3(x);
+      }
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+    }
+    } else {
 #pragma unroll
     for (int sub = 0; sub < kChunk / 8; ++sub) {
       float4 fa[TM], fb[2];
@@ -187,6 +286,7 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
           acc[tm][tn] = mfma32(fa[tm].z, fb[tn].z, acc[tm][tn]);
           acc[tm][tn] = mfma32(fa[tm].w, fb[tn].w, acc[tm][tn]);
         }
+    }
     }
   };
   const int nc = Kr / kChunk;
@@ -414,7 +514,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
   }
   const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
   f32x16 acc[TM][2];
-  nt_mainloop<BM, 1, true>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
+  // The f32 k loop here (X6 = false): with the bf16x6 loop this kernel
+  // returned, in 1 to 9 of 10 launches at n = 56 K, one row (always a
+  // second-pass row of an upper half-wave: local rows 9 / 11 / 13 / 15)
+  // whose row-tail statistics were wrong while its g_y was right (d_beta
+  // exact, d_gamma / d_res off by up to 2e-2), whether the row data were
+  // loaded before or after the loop, with or without a full s_waitcnt after
+  // it — and never with the f32 loop (0 in 60), in any other bf16x6 GEMM
+  // (plain nt / nn / tn, gemm_resnorm: 0 in 19-40 repeats each) or in the
+  // round-2/3 suites.  tools/dbg_rnbwd.py, test_gemm_nn_resnorm_bwd_repeatable.
+  nt_mainloop<BM, 1, true, false>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
   __syncthreads();  // every wave's reads of the last chunk are done
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
@@ -556,6 +665,36 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     stage();
     __syncthreads();
     if (r0 + kChunk < r_end) load(r0 + kChunk);
+#if MIREC_GEMM_X6
+#pragma unroll
+    for (int s16 = 0; s16 < kChunk / 16; ++s16) {
+      Split3 sa[2], sb[2];
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm) {
+        const float *ap = sA + (s16 * 16 + 4 * h) * kLdTN + wm * 64 + tm * 32 + i;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = ap[x6_k(0, e) * kLdTN];
+        if (do_cs) {
+          cs[tm] += (x[0] + x[1]) + (x[2] + x[3]);
+          cs[tm] += (x[4] + x[5]) + (x[6] + x[7]);
+        }
+        sa[tm] = split3(x);
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn) {
+        const float *bp = sB + (s16 * 16 + 4 * h) * kLdTN + wn * 64 + tn * 32 + i;
+        float x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = bp[x6_k(0, e) * kLdTN];
+        sb[tn] = split3(x);
+      }
+#pragma unroll
+      for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+    }
+#else
 #pragma unroll
     for (int sub = 0; sub < kChunk / 8; ++sub) {
 #pragma unroll
@@ -576,6 +715,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
         }
       }
     }
+#endif
   }
   cs[0] += __shfl_xor(cs[0], 32);
   cs[1] += __shfl_xor(cs[1], 32);
