@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256, 2) void gemm_resnorm_kernel(const float *__res
 #pragma unroll
   for (int q = 0; q < RPG; ++q) {
     const int64_t r = m0 + g + 8 * q;
-    rv[q] = (a.res && r < n) ? ld4(a.res + r * kTile + c) : f4_zero();
+    rv[q] = a.res ? ld4(a.res + min(r, n - 1) * kTile + c) : f4_zero();  // (as gemm_nn_rnbwd)
   }
   f32x16 acc[TM][2];
   nt_mainloop<BM, 1, false>(smem, A, B, n, Kr, kTile, fx, m0, 0, acc);
@@ -503,27 +503,24 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
   const int g = t >> 5, c = 4 * (t & 31);
   float4 ov[RPG], gv[RPG];
   float mv[RPG], sv[RPG];
+  // unconditional loads of a clamped row index (rows past n are never
+  // stored): with exec-masked loads (r < n ? load : 0) here, the bf16x6 k
+  // loop below returned, in up to 1 of 2 launches at n = 56 K, one row whose
+  // row-tail statistics were wrong while its g_y was right (always a
+  // second-pass row of an upper half-wave, local rows 9 / 11 / 13 / 15);
+  // never with the f32 loop, never with these loads (0 in 120 launches over
+  // two builds) — tools/dbg_rnbwd.py, test_gemm_nn_resnorm_bwd_repeatable.
 #pragma unroll
   for (int q = 0; q < RPG; ++q) {
-    const int64_t r = m0 + g + 8 * q;
-    const bool ok = r < n;
-    ov[q] = ok ? ld4(a.out + r * kTile + c) : f4_zero();
-    gv[q] = (ok && a.g_out) ? ld4(a.g_out + r * kTile + c) : f4_zero();
-    mv[q] = ok ? a.mean[r] : 0.f;
-    sv[q] = ok ? a.rstd[r] : 0.f;
+    const int64_t r = min(m0 + g + 8 * q, n - 1);
+    ov[q] = ld4(a.out + r * kTile + c);
+    gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
+    mv[q] = a.mean[r];
+    sv[q] = a.rstd[r];
   }
   const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
   f32x16 acc[TM][2];
-  // The f32 k loop here (X6 = false): with the bf16x6 loop this kernel
-  // returned, in 1 to 9 of 10 launches at n = 56 K, one row (always a
-  // second-pass row of an upper half-wave: local rows 9 / 11 / 13 / 15)
-  // whose row-tail statistics were wrong while its g_y was right (d_beta
-  // exact, d_gamma / d_res off by up to 2e-2), whether the row data were
-  // loaded before or after the loop, with or without a full s_waitcnt after
-  // it — and never with the f32 loop (0 in 60), in any other bf16x6 GEMM
-  // (plain nt / nn / tn, gemm_resnorm: 0 in 19-40 repeats each) or in the
-  // round-2/3 suites.  tools/dbg_rnbwd.py, test_gemm_nn_resnorm_bwd_repeatable.
-  nt_mainloop<BM, 1, true, false>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
+  nt_mainloop<BM, 1, true>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
   __syncthreads();  // every wave's reads of the last chunk are done
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm)
