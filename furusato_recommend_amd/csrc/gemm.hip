@@ -928,8 +928,11 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   const int64_t t128 = (n + 127) / 128 * ncol, t64 = (n + 63) / 64 * ncol;
   const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
   const bool bm64 = r64 < r128 || (r64 == r128 && t128 > slots);
+#ifndef MIREC_NT_PF
+#define MIREC_NT_PF 1
+#endif
 #define MIREC_NT_LAUNCH(BM, BKN)                                                               \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, MIREC_NT_PF, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
                      dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx)
   if (bm64) {
     if (bkn) MIREC_NT_LAUNCH(64, true);
