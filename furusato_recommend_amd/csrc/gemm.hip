@@ -121,6 +121,49 @@ constexpr int kLdO = 40;            // epilogue slab stride [row][col]: lane hal
 constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two lane halves
                                     // (k and k + 4) land 32 banks apart
 
+// bf16 planes (MIREC_GEMM_PLANES, with MIREC_GEMM_X6; [row][k] operands of
+// gemm_nt only): the staging thread splits its float4s once and stores the
+// three terms as bf16 planes [3][rows][kLdP], each 16-deep k block permuted
+// so that a lane half's 8 values (x6_k order) are contiguous: one 16-byte
+// read per plane and operand.  Row stride 80 B: the 16 lanes of a read phase
+// hit distinct 4-bank groups.  Halves the split VALU of the wave-side split
+// (every element was split by both waves that read it).
+#ifndef MIREC_GEMM_PLANES
+#define MIREC_GEMM_PLANES 1
+#endif
+constexpr int kLdP = kChunk + 8;  // bf16 units
+template <int BM>
+constexpr int nt_lds_floats() {
+  return (MIREC_GEMM_X6 && MIREC_GEMM_PLANES) && 3 * (BM + kTile) * kLdP / 2 > (BM + kTile) * kLdNT
+             ? 3 * (BM + kTile) * kLdP / 2
+             : (BM + kTile) * kLdNT;
+}
+
+struct Split3x4 {
+  uint2 h, m, l;
+};
+// a float4 -> three planes of 4 packed bf16 (the split3 arithmetic)
+__device__ __forceinline__ Split3x4 split3x4(float4 v) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+  uint32_t H[2], M[2], L[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const float a = x[2 * p], b = x[2 * p + 1];
+    const uint32_t ph = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+    const uint32_t pm = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
+    H[p] = ph;
+    M[p] = pm;
+    L[p] = pk_bf16(sa, sb);
+  }
+  return Split3x4{make_uint2(H[0], H[1]), make_uint2(M[0], M[1]), make_uint2(L[0], L[1])};
+}
+// bf16 position of float4 column c4 (k = 4 c4 .. +3) of a staged chunk row
+__device__ __forceinline__ int plane_pos(int c4) {
+  return (c4 >> 2) * 16 + 8 * (c4 & 1) + 4 * ((c4 >> 1) & 1);
+}
+
 // ------------------------------------------------------------------ gemm_nt
 // Workgroup (tile_m, tile_n): rows [BM tile_m, +BM) of C, columns
 // [128 tile_n, +128); waves 2 x 2, each BM/2 x 64 (BM/64 x 2 MFMA tiles).
@@ -227,8 +270,54 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  constexpr bool PL = X6 && !BKN && MIREC_GEMM_PLANES;
+  uint16_t *pA = reinterpret_cast<uint16_t *>(smem);      // [3][BM][kLdP]
+  uint16_t *pB = pA + 3 * BM * kLdP;                        // [3][128][kLdP]
+  auto stage_planes = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
+      const Split3x4 v = split3x4(xa[q]);
+      uint16_t *d = pA + r * kLdP + plane_pos(c4);
+      *reinterpret_cast<uint2 *>(d) = v.h;
+      *reinterpret_cast<uint2 *>(d + BM * kLdP) = v.m;
+      *reinterpret_cast<uint2 *>(d + 2 * BM * kLdP) = v.l;
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
+      const Split3x4 v = split3x4(xb[q]);
+      uint16_t *d = pB + r * kLdP + plane_pos(c4);
+      *reinterpret_cast<uint2 *>(d) = v.h;
+      *reinterpret_cast<uint2 *>(d + kTile * kLdP) = v.m;
+      *reinterpret_cast<uint2 *>(d + 2 * kTile * kLdP) = v.l;
+    }
+  };
   auto compute = [&]() {
-    if constexpr (X6) {
+    if constexpr (PL) {
+#pragma unroll
+      for (int s16 = 0; s16 < kChunk / 16; ++s16) {
+        Split3 sa[TM], sb[2];
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm) {
+          const uint16_t *ap = pA + (wm * (BM / 2) + tm * 32 + i) * kLdP + s16 * 16 + 8 * h;
+          sa[tm].h = *reinterpret_cast<const bf16x8 *>(ap);
+          sa[tm].m = *reinterpret_cast<const bf16x8 *>(ap + BM * kLdP);
+          sa[tm].l = *reinterpret_cast<const bf16x8 *>(ap + 2 * BM * kLdP);
+        }
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) {
+          const uint16_t *bp = pB + (wn * 64 + tn * 32 + i) * kLdP + s16 * 16 + 8 * h;
+          sb[tn].h = *reinterpret_cast<const bf16x8 *>(bp);
+          sb[tn].m = *reinterpret_cast<const bf16x8 *>(bp + kTile * kLdP);
+          sb[tn].l = *reinterpret_cast<const bf16x8 *>(bp + 2 * kTile * kLdP);
+        }
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+      }
+    } else if constexpr (X6) {
 #pragma unroll
     for (int s16 = 0; s16 < kChunk / 16; ++s16) {
       Split3 sa[TM], sb[2];
@@ -299,7 +388,8 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
       const int c = c0 + p;
       if (c < nc) {
         __syncthreads();  // the previous chunk's LDS reads are done
-        stage(ra[p], rb[p]);
+        if constexpr (PL) stage_planes(ra[p], rb[p]);
+        else stage(ra[p], rb[p]);
         __syncthreads();
         if (c + PF < nc) load(ra[p], rb[p], (c + PF) * kChunk);  // in flight during the products
         compute();
@@ -318,7 +408,7 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
                                                         float *__restrict__ C, int64_t n,
                                                         int Kr, int No, NtArgs fx) {
   constexpr int TM = BM / 64;
-  __shared__ __attribute__((aligned(16))) float smem[(BM + kTile) * kLdNT];
+  __shared__ __attribute__((aligned(16))) float smem[BKN ? (BM + kTile) * kLdNT : nt_lds_floats<BM>()];
   static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -397,7 +487,7 @@ constexpr int kLdRow = kTile + 4;  // [row][col] stride of the tile image
 
 template <int BM>
 constexpr int rn_lds_floats() {
-  return (BM + kTile) * kLdNT > BM * kLdRow ? (BM + kTile) * kLdNT : BM * kLdRow;
+  return nt_lds_floats<BM>() > BM * kLdRow ? nt_lds_floats<BM>() : BM * kLdRow;
 }
 
 template <int BM>
@@ -485,8 +575,8 @@ struct RbArgs {
 };
 
 template <int BM>
-constexpr int rb_lds_floats() {
-  return rn_lds_floats<BM>() > 8 * 3 * kTile ? rn_lds_floats<BM>() : 8 * 3 * kTile;
+constexpr int rb_lds_floats() {  // ([k][n] B image: no bf16 planes)
+  return std::max(std::max((BM + kTile) * kLdNT, BM * kLdRow), 8 * 3 * kTile);
 }
 
 template <int BM>
