@@ -132,11 +132,14 @@ constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two 
 #define MIREC_GEMM_PLANES 1
 #endif
 constexpr int kLdP = kChunk + 8;  // bf16 units
+constexpr int kLdK = kTile + 32;  // bf16 units (k-major planes, below)
 template <int BM>
 constexpr int nt_lds_floats() {
-  return (MIREC_GEMM_X6 && MIREC_GEMM_PLANES) && 3 * (BM + kTile) * kLdP / 2 > (BM + kTile) * kLdNT
-             ? 3 * (BM + kTile) * kLdP / 2
-             : (BM + kTile) * kLdNT;
+  // [row][k] planes of A and B, or of A with the [k][n] planes of B
+  constexpr int pl = 3 * BM * kLdP / 2 +
+                     (3 * kTile * kLdP > 3 * kChunk * kLdK ? 3 * kTile * kLdP : 3 * kChunk * kLdK) / 2;
+  return (MIREC_GEMM_X6 && MIREC_GEMM_PLANES) && pl > (BM + kTile) * kLdNT ? pl
+                                                                           : (BM + kTile) * kLdNT;
 }
 
 struct Split3x4 {
@@ -162,6 +165,34 @@ __device__ __forceinline__ Split3x4 split3x4(float4 v) {
 // bf16 position of float4 column c4 (k = 4 c4 .. +3) of a staged chunk row
 __device__ __forceinline__ int plane_pos(int c4) {
   return (c4 >> 2) * 16 + 8 * (c4 & 1) + 4 * ((c4 >> 1) & 1);
+}
+
+// k-major operands ([k][n] B of gemm_nn / the fused dX kernel, both operands
+// of gemm_tn): planes [3][kChunk][kLdK] in the natural [k][col] order (a
+// float4 of 4 columns -> one 8-byte store per plane) read back with the
+// gfx950 transposing LDS read ds_read_b64_tr_b16: per 16-lane group a 4-row
+// x 16-column block arrives column-major, lane i holding column i's 4 rows —
+// two reads (rows 4h.. and 8 + 4h..) give a lane half h its 8 values in the
+// x6_k order.  Row stride 320 B (80 dwords = 16 mod 64): the 32 lanes of a
+// half (4 rows x 2 groups x 4 column quads) hit 64 distinct banks.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4i16 lds_tr16(const uint16_t *p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4i16 *)(const_cast<uint16_t *>(p)));
+}
+// the 32x32x16 operand of columns [c0, c0 + 32) of one plane, k block s16
+__device__ __forceinline__ bf16x8 tr_operand(const uint16_t *plane, int c0, int s16, int lane) {
+  const int G = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3, h = G >> 1;
+  const uint16_t *a = plane + (s16 * 16 + 4 * h + q) * kLdK + c0 + 16 * (G & 1) + 4 * pq;
+  const v4i16 x = lds_tr16(a), y = lds_tr16(a + 8 * kLdK);
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 v = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ Split3 tr_split3(const uint16_t *planes, int plane_stride, int c0,
+                                            int s16, int lane) {
+  return Split3{tr_operand(planes, c0, s16, lane), tr_operand(planes + plane_stride, c0, s16, lane),
+                tr_operand(planes + 2 * plane_stride, c0, s16, lane)};
 }
 
 // ------------------------------------------------------------------ gemm_nt
@@ -270,9 +301,10 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  constexpr bool PL = X6 && !BKN && MIREC_GEMM_PLANES;
+  constexpr bool PL = X6 && MIREC_GEMM_PLANES;
   uint16_t *pA = reinterpret_cast<uint16_t *>(smem);      // [3][BM][kLdP]
-  uint16_t *pB = pA + 3 * BM * kLdP;                        // [3][128][kLdP]
+  uint16_t *pB = pA + 3 * BM * kLdP;  // [3][128][kLdP], or [3][kChunk][kLdK] ([k][n] B)
+  constexpr int kPB = BKN ? kChunk * kLdK : kTile * kLdP;  // B plane stride
   auto stage_planes = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
@@ -285,12 +317,18 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
       const Split3x4 v = split3x4(xb[q]);
-      uint16_t *d = pB + r * kLdP + plane_pos(c4);
+      uint16_t *d;
+      if constexpr (BKN) {  // [k][n] as in memory
+        const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+        d = pB + kk * kLdK + 4 * c4;
+      } else {
+        const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
+        d = pB + r * kLdP + plane_pos(c4);
+      }
       *reinterpret_cast<uint2 *>(d) = v.h;
-      *reinterpret_cast<uint2 *>(d + kTile * kLdP) = v.m;
-      *reinterpret_cast<uint2 *>(d + 2 * kTile * kLdP) = v.l;
+      *reinterpret_cast<uint2 *>(d + kPB) = v.m;
+      *reinterpret_cast<uint2 *>(d + 2 * kPB) = v.l;
     }
   };
   auto compute = [&]() {
@@ -307,10 +345,14 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
         }
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn) {
-          const uint16_t *bp = pB + (wn * 64 + tn * 32 + i) * kLdP + s16 * 16 + 8 * h;
-          sb[tn].h = *reinterpret_cast<const bf16x8 *>(bp);
-          sb[tn].m = *reinterpret_cast<const bf16x8 *>(bp + kTile * kLdP);
-          sb[tn].l = *reinterpret_cast<const bf16x8 *>(bp + 2 * kTile * kLdP);
+          if constexpr (BKN) {
+            sb[tn] = tr_split3(pB, kPB, wn * 64 + tn * 32, s16, lane);
+          } else {
+            const uint16_t *bp = pB + (wn * 64 + tn * 32 + i) * kLdP + s16 * 16 + 8 * h;
+            sb[tn].h = *reinterpret_cast<const bf16x8 *>(bp);
+            sb[tn].m = *reinterpret_cast<const bf16x8 *>(bp + kTile * kLdP);
+            sb[tn].l = *reinterpret_cast<const bf16x8 *>(bp + 2 * kTile * kLdP);
+          }
         }
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
@@ -408,7 +450,7 @@ __global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float 
                                                         float *__restrict__ C, int64_t n,
                                                         int Kr, int No, NtArgs fx) {
   constexpr int TM = BM / 64;
-  __shared__ __attribute__((aligned(16))) float smem[BKN ? (BM + kTile) * kLdNT : nt_lds_floats<BM>()];
+  __shared__ __attribute__((aligned(16))) float smem[nt_lds_floats<BM>()];
   static_assert(4 * 32 * kLdO <= (BM + kTile) * kLdNT, "epilogue staging fits");
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -575,8 +617,8 @@ struct RbArgs {
 };
 
 template <int BM>
-constexpr int rb_lds_floats() {  // ([k][n] B image: no bf16 planes)
-  return std::max(std::max((BM + kTile) * kLdNT, BM * kLdRow), 8 * 3 * kTile);
+constexpr int rb_lds_floats() {
+  return std::max(std::max(nt_lds_floats<BM>(), BM * kLdRow), 8 * 3 * kTile);
 }
 
 template <int BM>
@@ -687,9 +729,16 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
                                                         float *__restrict__ work_cs,
                                                         int64_t n, int M, int No,
                                                         int64_t rows_per_slice, TnArgs fx) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * kChunk * kLdTN];
-  static_assert(4 * 32 * kLdO <= 2 * kChunk * kLdTN, "epilogue staging fits");
+  // TPL: both k-major operands as [k][col] bf16 planes read back with the
+  // transposing LDS read (as gemm_nt's [k][n] B); the column sums of A are
+  // then taken from the staged f32 values
+  constexpr bool TPL = MIREC_GEMM_X6 && MIREC_GEMM_PLANES;
+  constexpr int kPl = kChunk * kLdK;  // one plane (bf16 units)
+  constexpr int kTnLds = TPL ? 3 * kPl : 2 * kChunk * kLdTN;
+  __shared__ __attribute__((aligned(16))) float smem[kTnLds];
+  static_assert(4 * 32 * kLdO <= kTnLds && 8 * kTile <= kTnLds, "epilogue staging fits");
   float *sA = smem, *sB = smem + kChunk * kLdTN;
+  uint16_t *pA = reinterpret_cast<uint16_t *>(smem), *pB = pA + 3 * kPl;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
@@ -727,12 +776,25 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       }
     }
   };
+  float4 csv = f4_zero();  // TPL: this thread's column sums (columns 4 c4 ..)
   auto stage = [&]() {
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-      st4(sA + kk * kLdTN + 4 * c4, ra[q]);
-      st4(sB + kk * kLdTN + 4 * c4, rb[q]);
+      if constexpr (TPL) {
+        if (do_cs) csv = f4_add(csv, ra[q]);
+        const Split3x4 va = split3x4(ra[q]), vb = split3x4(rb[q]);
+        uint16_t *da = pA + kk * kLdK + 4 * c4, *db = pB + kk * kLdK + 4 * c4;
+        *reinterpret_cast<uint2 *>(da) = va.h;
+        *reinterpret_cast<uint2 *>(da + kPl) = va.m;
+        *reinterpret_cast<uint2 *>(da + 2 * kPl) = va.l;
+        *reinterpret_cast<uint2 *>(db) = vb.h;
+        *reinterpret_cast<uint2 *>(db + kPl) = vb.m;
+        *reinterpret_cast<uint2 *>(db + 2 * kPl) = vb.l;
+      } else {
+        st4(sA + kk * kLdTN + 4 * c4, ra[q]);
+        st4(sB + kk * kLdTN + 4 * c4, rb[q]);
+      }
     }
   };
   f32x16 acc[2][2];
@@ -753,6 +815,21 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     __syncthreads();
     if (r0 + kChunk < r_end) load(r0 + kChunk);
 #if MIREC_GEMM_X6
+    if constexpr (TPL) {
+#pragma unroll
+      for (int s16 = 0; s16 < kChunk / 16; ++s16) {
+        Split3 sa[2], sb[2];
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm) sa[tm] = tr_split3(pA, kPl, wm * 64 + tm * 32, s16, lane);
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn) sb[tn] = tr_split3(pB, kPl, wn * 64 + tn * 32, s16, lane);
+#pragma unroll
+        for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+      }
+      continue;
+    }
 #pragma unroll
     for (int s16 = 0; s16 < kChunk / 16; ++s16) {
       Split3 sa[2], sb[2];
@@ -826,7 +903,18 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       }
       wave_sync();  // the slab is wave-private
     }
-  if (do_cs && wn == 0 && h == 0) {
+  if constexpr (TPL) {
+    if (!do_cs) return;  // workgroup-uniform
+    __syncthreads();     // the slabs are no longer read
+    st4(smem + (t >> 5) * kTile + 4 * (t & 31), csv);
+    __syncthreads();
+    if (t < kTile) {  // the 8 row groups added in group order
+      float c = 0.f;
+#pragma unroll
+      for (int g8 = 0; g8 < 8; ++g8) c += smem[g8 * kTile + t];
+      work_cs[(int64_t)s * M + m0 + t] = c;
+    }
+  } else if (do_cs && wn == 0 && h == 0) {
     work_cs[(int64_t)s * M + m0 + wm * 64 + i] = cs[0];
     work_cs[(int64_t)s * M + m0 + wm * 64 + 32 + i] = cs[1];
   }
