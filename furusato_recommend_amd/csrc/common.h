@@ -142,4 +142,39 @@ __device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
   p = fmaf(h.neg_step_size, m / denom, p);
 }
 
+// ---- exact three-term bf16 split of f32 operands (gemm.hip, attention.hip)
+// x = x_h + x_m + x_l, each term rounded to nearest; the residuals are exact
+// in f32 (error analysis: gemm.hip, MIREC_GEMM_X6).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8 h, m, l;
+};
+
+// packed RNE (a in the low half)
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+
+// x[0..7] -> three bf16x8 planes (element e of every plane is x[e]'s term)
+__device__ __forceinline__ Split3 split3(const float (&x)[8]) {
+  u32x4 H, M, L;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float a = x[2 * p], b = x[2 * p + 1];
+    const uint32_t ph = pk_bf16(a, b);
+    const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+    const uint32_t pm = pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
+    H[p] = ph;
+    M[p] = pm;
+    L[p] = pk_bf16(sa, sb);
+  }
+  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M),
+                __builtin_bit_cast(bf16x8, L)};
+}
+
 }  // namespace mirec

@@ -51,37 +51,7 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 #ifndef MIREC_GEMM_X6
 #define MIREC_GEMM_X6 1
 #endif
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-struct Split3 {
-  bf16x8 h, m, l;
-};
-
-// packed RNE (a in the low half)
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
-}
-
-// x[0..7] -> three bf16x8 planes (element e of every plane is x[e]'s term)
-__device__ __forceinline__ Split3 split3(const float (&x)[8]) {
-  u32x4 H, M, L;
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float a = x[2 * p], b = x[2 * p + 1];
-    const uint32_t ph = pk_bf16(a, b);
-    const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
-    const uint32_t pm = pk_bf16(ra, rb);
-    const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
-    H[p] = ph;
-    M[p] = pm;
-    L[p] = pk_bf16(sa, sb);
-  }
-  return Split3{__builtin_bit_cast(bf16x8, H), __builtin_bit_cast(bf16x8, M),
-                __builtin_bit_cast(bf16x8, L)};
-}
+// (bf16x8, Split3, pk_bf16, split3: common.h)
 
 // C += A·B over one 16-deep k block: lane (i, h) supplies row / column i's
 // 8 k values of its half (any k order, the same for A and B)
