@@ -960,9 +960,22 @@ __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__res
 #ifndef MIREC_TN_MINROWS
 #define MIREC_TN_MINROWS 64
 #endif
+// A single 128 x 128 output tile (the d = 128 projection / FFN weight
+// gradients of C4) takes 256 slices instead: half the partial tiles for the
+// reduce, and its load-latency-bound slices lose less than the reduce saves
+// (split bf16 loop: 30.4 -> 25.7 us, C4 1.259 -> 1.232 ms/step, same box;
+// 256 workgroups in total lose on 2- and 3-tile gradients: 125 -> 172 us,
+// 49.6 -> 52.9 us).
+#ifndef MIREC_TN_WANT
+#define MIREC_TN_WANT 512
+#endif
+#ifndef MIREC_TN_WANT1
+#define MIREC_TN_WANT1 256
+#endif
 static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
-  const int64_t want = std::max<int64_t>(1, (512 + tiles - 1) / tiles);
+  const int64_t total = tiles == 1 ? MIREC_TN_WANT1 : MIREC_TN_WANT;
+  const int64_t want = std::max<int64_t>(1, (total + tiles - 1) / tiles);
   int64_t r = std::max<int64_t>(MIREC_TN_MINROWS, (n + want - 1) / want);
   r = (r + kChunk - 1) / kChunk * kChunk;
   *rows = r;
