@@ -2023,6 +2023,46 @@ def test_gemm_nn_matches_fp64(n, kr, no):
         assert rel(torch.cat([c1, c2], 1), ref) < 1e-6
 
 
+def test_gemm_split_bf16_is_f32_accurate():
+    """The GEMMs multiply f32 operands as an exact three-term bf16 split
+    (gemm.hip, MIREC_GEMM_X6).  Claim: f32-class accuracy.  Check: on
+    operands spanning twelve decades (row / column scales 10^U(-6, 6)), the
+    error of every output element relative to its own scale Σ_k |a_ik b_kj|
+    (float64) is below 1e-6 and within 4x of torch's fp32 matmul on the same
+    operands, for the nt, nn and tn forms."""
+    from furusato_recommend_amd import linear as LN
+    from furusato_recommend_amd.linear import gemm_nn, gemm_nt, gemm_tn
+    LN.FORCE_MIREC_GEMM = True
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        torch.manual_seed(5)
+        for n, k, m in ((4096, 128, 384), (20_000, 384, 128)):
+            a = torch.randn(n, k, device="cuda") * 10 ** (12 * torch.rand(n, 1, device="cuda") - 6)
+            b = torch.randn(m, k, device="cuda") * 10 ** (12 * torch.rand(m, 1, device="cuda") - 6)
+            scale = a.double().abs() @ b.double().abs().t()
+            ref = a.double() @ b.double().t()
+
+            def err(c):
+                return float(((c.double() - ref).abs() / scale).max())
+            e_torch = err(a @ b.t())
+            for name, c in (("nt", gemm_nt(a, b)), ("nn", gemm_nn(a, b.t().contiguous()))):
+                e = err(c)
+                assert e < 1e-6 and e < 4 * e_torch + 1e-8, (name, n, e, e_torch)
+            # tn: C = Aᵀ B over the n rows
+            bt = torch.randn(n, m, device="cuda") * 10 ** (12 * torch.rand(1, m, device="cuda") - 6)
+            at = a
+            scale = at.double().abs().t() @ bt.double().abs()
+            ref = at.double().t() @ bt.double()
+            e_torch = float(((at.t() @ bt).double() - ref).abs().div(scale).max())
+            c, _ = gemm_tn(at, bt, False)
+            e = float(((c.double() - ref).abs() / scale).max())
+            assert e < 1e-6 and e < 4 * e_torch + 1e-8, ("tn", n, e, e_torch)
+    finally:
+        LN.FORCE_MIREC_GEMM = False
+        torch.backends.cuda.matmul.allow_tf32 = prev
+
+
 @pytest.mark.parametrize("n,m,no", [(0, 128, 128), (1, 128, 128), (100, 384, 128),
                                     (56_321, 384, 128), (9000, 128, 256), (33, 256, 384)])
 def test_gemm_tn_matches_fp64(n, m, no):
