@@ -604,3 +604,43 @@ def test_route_rows_to_owners_world3():
             assert counts[src] == len(mine)
         assert rid.tolist() == want_ids
         assert np.allclose(rv, np.array(want_vals, dtype=np.float32).reshape(-1, 3))
+
+
+def _bf16_rne(x: np.ndarray) -> np.ndarray:
+    """f32 -> nearest bf16 (ties to even), returned as f32 — what
+    v_cvt_pk_bf16_f32 does for finite values."""
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(np.float32)
+
+
+def test_bf16_three_term_split_error_bound():
+    """The GEMMs' f32 products on bf16 MFMA (csrc/common.h split3, gemm.hip
+    MIREC_GEMM_X6), emulated on the host: x = x_h + x_m + x_l with every
+    residual exact in f32, |x_m| <= 2^-8 |x|, |x_l| <= 2^-16 |x|, the split
+    exact to 2^-24 |x|, and the six kept products (a_l b_h + a_h b_l + a_m b_m
+    + a_m b_h + a_h b_m + a_h b_h, exact in float64 as bf16 x bf16 products
+    are) within 2^-22 |a b| of the exact product — an f32 rounding's order."""
+    rng = np.random.default_rng(0)
+    x = (rng.standard_normal(200_000) * 10.0 ** rng.uniform(-30, 30, 200_000)).astype(np.float32)
+    y = (rng.standard_normal(200_000) * 10.0 ** rng.uniform(-30, 30, 200_000)).astype(np.float32)
+
+    def split(v):
+        h = _bf16_rne(v)
+        r1 = (v - h).astype(np.float32)
+        m = _bf16_rne(r1)
+        r2 = (r1 - m).astype(np.float32)
+        lo = _bf16_rne(r2)
+        # the residuals are exact: recomputing in float64 gives the same
+        assert np.array_equal(r1.astype(np.float64), v.astype(np.float64) - h.astype(np.float64))
+        assert np.array_equal(r2.astype(np.float64), r1.astype(np.float64) - m.astype(np.float64))
+        return h.astype(np.float64), m.astype(np.float64), lo.astype(np.float64)
+    xh, xm, xl = split(x)
+    yh, ym, yl = split(y)
+    ax = np.abs(x.astype(np.float64))
+    assert np.all(np.abs(xm) <= 2.0 ** -8 * ax) and np.all(np.abs(xl) <= 2.0 ** -16 * ax)
+    assert np.all(np.abs(xh + xm + xl - x.astype(np.float64)) <= 2.0 ** -24 * ax)
+    six = xl * yh + xh * yl + xm * ym + xm * yh + xh * ym + xh * yh
+    exact = x.astype(np.float64) * y.astype(np.float64)
+    rel = np.abs(six - exact) / np.abs(exact)
+    assert rel.max() <= 2.0 ** -22, rel.max()
