@@ -147,6 +147,7 @@ def main():
             "metric": "GraphSAGE BPR positive-edges/sec (C3)", "value": round(world * args.steps * B / dt, 1),
             "unit": "positive-edges/s", "n_gpus": world, "steps": args.steps,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "dtype": "f32",
+            "gemm_arith": "f32 products as an exact three-term bf16 split on bf16 MFMA (f32-class error: DESIGN.md section 4, profiles/round3c_gemm_split_accuracy.jsonl)",
             "config": {"workload": "C3: GraphSAGE 2-hop fanout %s d=%d on the C2 graph" % (fan, args.dim)
                         + ("" if args.kind == "uniform" else " (%s item popularity)" % args.kind),
                        "bpr_batch_per_rank": B,

@@ -254,6 +254,7 @@ def main():
         "value": round(args.steps * B / dt, 1), "unit": "positive-edges/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * dt / args.steps, 3),
         "dtype": "f32", "data": "synthetic sequences U[5,%d], random-init weights" % args.maxlen,
+            "gemm_arith": "f32 products as an exact three-term bf16 split on bf16 MFMA (f32-class error: DESIGN.md section 4, profiles/round3c_gemm_split_accuracy.jsonl)",
         "config": {"workload": "C4: SASRec L=%d heads=%d d=%d maxlen=%d, %d users x %d items"
                    % (args.layers, args.heads, args.dim, args.maxlen, args.users, args.items),
                    "bpr_batch": B, "step": "HIP graph replay" if graph_mode else "eager"},
