@@ -177,4 +177,24 @@ __device__ __forceinline__ Split3 split3(const float (&x)[8]) {
                 __builtin_bit_cast(bf16x8, L)};
 }
 
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// C += A·B over one 16-deep k block: lane (i, h) supplies row / column i's
+// 8 k values of its half (any k order, the same for A and B)
+__device__ __forceinline__ f32x16 mfma_x6(const Split3 &a, const Split3 &b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.l, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.l, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.m, b.h, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.m, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a.h, b.h, c, 0, 0, 0);
+  return c;
+}
+
+// The k order of a lane half h inside a 16-deep block: element e < 4 is k =
+// 4 h + e, e >= 4 is 8 + 4 h + (e - 4) — two float4 reads of a [row][k] LDS
+// row, and on a [k][col] image the two halves' rows are 4 apart (32 banks at
+// the row strides used here), as in the f32 form's sub-chunks.
+__device__ __forceinline__ int x6_k(int h, int e) { return 4 * h + (e & 3) + 8 * (e >> 2); }
+
 }  // namespace mirec
