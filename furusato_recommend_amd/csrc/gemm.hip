@@ -12,17 +12,20 @@
 //             cut into row slices (one workgroup per slice and 128 x 128
 //             output tile, partial tiles in a workspace) and the slices are
 //             summed in a fixed order by a second kernel: deterministic.
-// Every product is built from v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains,
-// 64 FLOP/clk/SIMD: the f32 matrix peak).  A 256-thread workgroup owns a
-// 128 x 128 output tile, each of its 4 waves a 64 x 64 quarter (2 x 2 MFMA
-// tiles, 64 accumulator registers); the k loop runs in chunks of 32 staged
-// through LDS with the next chunk's global loads in flight (in registers)
-// while the current chunk is multiplied.
+// The f32 products run on the bf16 MFMA pipe as an exact three-term split
+// (MIREC_GEMM_X6, below: six v_mfma_f32_32x32x16_bf16 per 16-deep block,
+// f32-class error), the operands staged once per element as bf16 planes in
+// LDS (MIREC_GEMM_PLANES); MIREC_GEMM_X6=0 builds the round-2 form on
+// v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains, 64 FLOP/clk/SIMD).  A
+// 256-thread workgroup owns a 128 x 128 output tile, each of its 4 waves a
+// 64 x 64 quarter (2 x 2 MFMA tiles, 64 accumulator registers); the k loop
+// runs in chunks of 32 staged through LDS with the next chunk's global loads
+// in flight (in registers) while the current chunk is multiplied.
 //
-// MFMA operand order: step s (0..3) of an 8-wide k sub-chunk takes, in lane
-// half h = lane >> 5, the k index 4h + s — both operands use the same
-// bijection, so the sum is unchanged — which lets a lane fetch its four
-// steps' operands with one 16-byte LDS read in gemm_nt.
+// MFMA operand order (f32 form): step s (0..3) of an 8-wide k sub-chunk
+// takes, in lane half h = lane >> 5, the k index 4h + s — both operands use
+// the same bijection, so the sum is unchanged — which lets a lane fetch its
+// four steps' operands with one 16-byte LDS read in gemm_nt.
 #include <algorithm>
 
 #include "common.h"
