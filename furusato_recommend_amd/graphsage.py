@@ -66,6 +66,7 @@ class TableGrad:
         self.coef = torch.zeros(2, device=device)
         self.gen = 0
         self.pending = False  # S / coef of the last backward not yet consumed
+        self.adam_events = None  # a list: (start, end) HIP events of each adam()
         self.dense = False
         # static: a HIP-graph-captured step bakes the generation into its
         # launches, so every step clears the stamps and reuses generation 1
@@ -142,6 +143,10 @@ class TableGrad:
         args = (state.param.data_ptr(), state.exp_avg.data_ptr(), state.exp_avg_sq.data_ptr(),
                 self.coef.data_ptr(), self.n_user, self.acc.data_ptr(), self.stamp.data_ptr(),
                 self.gen, self.n_rows, self.dim)
+        ev = self.adam_events  # bench: HIP events around the launch (its stream)
+        if ev is not None:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
         if h_dev is None:
             hp = state.next_hparams()
             check(lib.mirec_adam_table(*args, ctypes.byref(hp), _lib.ptr(sumsq), _lib.ptr(norms),
@@ -150,6 +155,9 @@ class TableGrad:
             check(lib.mirec_adam_table_dev(*args, h_dev.data_ptr(), _lib.ptr(sumsq),
                                            _lib.ptr(norms), _lib.stream_handle()),
                   "adam_table_dev")
+        if ev is not None:
+            e1.record()
+            ev.append((e0, e1))
         _engine._note_raw_write()
         self.pending = False
 

@@ -114,6 +114,8 @@ def main():
         step(i)
     torch.cuda.synchronize()
     dp.comm_events = [] if world > 1 else None
+    tg = m._tg
+    tg.adam_events = [] if world == 1 else None  # the dominant kernel, timed live
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -139,6 +141,21 @@ def main():
                 "exchange_bytes_per_rank": dp.last_exchange_bytes,
                 "exchange_bytes_note": "bytes rank 0 received in the last step",
                 "algbw_GBps": round(dp.last_exchange_bytes / (cm * 1e-3) / 1e9, 2) if cm else None}
+    roof = None
+    if tg.adam_events:
+        # tg_adam_kernel (+ its 2-float norm finalize in the same bracket):
+        # W, m, v read and written, the stamps, and the tree-sum rows of the
+        # last step (stamp == gen) read — per launch
+        ms = sum(a.elapsed_time(b) for a, b in tg.adam_events) / len(tg.adam_events)
+        touched = int((tg.stamp == tg.gen).sum())
+        nbytes = 6 * tg.n_rows * tg.dim * 4 + tg.n_rows * 4 + touched * tg.dim * 4
+        roof = {"bound": "hbm", "kernel": "tg_adam_kernel (fused table Adam)",
+                "achieved": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                "frac": round(nbytes / (ms * 1e-3) / 1e9 / 8000.0, 4),
+                "traffic": 3660805737, "traffic_source": "profiles/round3d_pmc_tg_adam.json",
+                "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
+                "launches_per_step": round(len(tg.adam_events) / args.steps, 2)}
+        tg.adam_events = None
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu = cpu_baseline(m, B, fan)
@@ -155,6 +172,7 @@ def main():
                                        else f"dp{world} (user-sharded, {dp.table_exchange} "
                                             f"table exchange)"),
                        "leaf_bwd": args.leaf_bwd},
+            "roofline": roof,
             "comm": comm,
             "cpu_baseline": cpu}),
             flush=True)
