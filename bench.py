@@ -56,6 +56,7 @@ PMC_FILE = os.path.join("profiles", "pmc_prop_kernel.json")
 # MI355X_MICROARCH.md: the achievable HBM stream rate of a read/write kernel
 # (the "HBM-honest" reference for counter bytes; the spec peak is above)
 HBM_STREAM_GBS = 6290.0
+PARITY_TOL = 1e-4  # north_star: output embeddings within 1e-4 rel fp32 of the CPU path
 # C5 (d = 256, 11.26 GB tables: no Infinity-Cache help) full launch, round 2
 C5_NO_CACHE = {"achieved_GBps": 6340.0, "frac_of_peak": 0.79,
                "source": "profiles/round2_bench_c5_1gpu.json"}
@@ -88,6 +89,10 @@ def parse(argv=None):
                     help="timed warm-up steps per exchange mode for --dp-mode auto")
     ap.add_argument("--shard-chunks", type=int, default=4,
                     help="row blocks of the sharded last layer (all-gather overlap)")
+    ap.add_argument("--parity", type=int, default=1,
+                    help="rank 0 at N=1: one more GPU step checked against the CPU oracle "
+                         "from the same table / Adam state / triples (the run fails above "
+                         "1e-4)")
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
@@ -180,22 +185,95 @@ def progress(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline(ds, args, users, pos, neg):
+def rel_err(a: torch.Tensor, b: torch.Tensor) -> float:
+    """max|a - b| / max|b| over the whole tensor (the north_star's 1e-4
+    relative fp32 bar; the same measure as tests/test_gpu_parity.py)."""
+    a, b = a.double(), b.double()
+    return float((a - b).abs().max() / b.abs().max().clamp(min=1e-30))
+
+
+def parity_snapshot(model, eng, emb, args, step_index: int, rank: int, world: int):
+    """One more training step of the benchmarked engine, with everything the
+    CPU oracle needs to take the SAME step copied to the host first: the
+    table and the Adam moments / step count as they stand after the timed
+    steps, the full layer-mean output of that table (all N rows), and the
+    step's (u, p, n).  Then the GPU step itself: its loss and the table it
+    leaves.  The oracle side runs in ``cpu_baseline``."""
+    from furusato_recommend_amd.engine import sample_triples
+    dev = emb.device
+    B = args.batch
+    u = torch.empty(B, dtype=torch.int32, device=dev)
+    p, n = torch.empty_like(u), torch.empty_like(u)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    sample_triples(model.graph, B, args.seed, step_index * B, u, p, n, err, rank, world)
+    ad = model.optim
+    snap = {"emb0": emb.detach().cpu().clone(), "exp_avg": ad.exp_avg.cpu().clone(),
+            "exp_avg_sq": ad.exp_avg_sq.cpu().clone(), "n_steps": int(ad.n_steps),
+            "lr": ad.lr, "betas": ad.betas, "eps": ad.eps}
+    out = eng.forward(emb)  # full layer mean of every row (unpruned)
+    snap["out_gpu"] = out.cpu().clone()
+    loss = eng.train_step(emb, model.optim, u, p, n, 1e-4)
+    torch.cuda.synchronize()
+    if int(err.item()) != 0:
+        raise RuntimeError("sampler retry budget exhausted")
+    snap.update(loss_gpu=float(loss.item()), emb1_gpu=emb.detach().cpu().clone(),
+                users=u.cpu().numpy(), pos=p.cpu().numpy(), neg=n.cpu().numpy(),
+                step_index=step_index)
+    return snap
+
+
+def oracle_parity(o, snap) -> dict:
+    """The oracle takes the snapshot's step (model/lgcn.py:78-133 restated):
+    same table, same Adam moments and step count, same triples.  Returns the
+    relative errors of the full output, the stepped table and the loss."""
+    with torch.no_grad():
+        o.emb.copy_(snap["emb0"])
+    o.optim.state[o.emb] = {"step": torch.tensor(float(snap["n_steps"])),
+                            "exp_avg": snap["exp_avg"].clone(),
+                            "exp_avg_sq": snap["exp_avg_sq"].clone()}
+    grp = o.optim.param_groups[0]
+    grp["lr"], grp["betas"], grp["eps"] = snap["lr"], tuple(snap["betas"]), snap["eps"]
+    progress("parity: oracle full forward")
+    out_cpu = o.propagated()
+    progress("parity: oracle training step")
+    loss_cpu = o.stageOne(snap["users"], snap["pos"], snap["neg"])
+    r = {"rel_out": rel_err(snap["out_gpu"], out_cpu),
+         "rel_emb_step": rel_err(snap["emb1_gpu"], o.emb.detach()),
+         "rel_loss": abs(snap["loss_gpu"] - loss_cpu) / max(abs(loss_cpu), 1e-30),
+         "loss_gpu": snap["loss_gpu"], "loss_cpu": loss_cpu,
+         "rows": int(snap["emb0"].shape[0]), "tol": PARITY_TOL,
+         "what": f"GPU training step {snap['step_index']} (after the timed steps) vs the CPU "
+                 "oracle from the same table, Adam moments and step count on the same "
+                 "(u, p, n): rel = max|gpu - cpu| / max|cpu| over every row of the "
+                 "layer-mean output (before the step) and of the table after it"}
+    r["ok"] = bool(max(r["rel_out"], r["rel_emb_step"], r["rel_loss"]) < PARITY_TOL)
+    return r
+
+
+def cpu_baseline(ds, args, users, pos, neg, snap=None):
     """The CPU oracle (torch fp32) on a bounded sample of the same workload,
     timed per BASELINE.md §3: one warm-up training step, then the mean of K
     full training steps (B triples each, full C2 graph); the 3-layer forward
-    the same way (warmed by the warm-up step)."""
+    the same way (warmed by the warm-up step).  With ``snap`` (parity_snapshot)
+    the oracle starts from the GPU's table and Adam state and its warm-up step
+    is the parity step: the same step the GPU took, compared element-wise."""
     from oracle.lightgcn_oracle import OracleLightGCN, forward
     threads = host_threads()
     torch.set_num_threads(threads)
     o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, args.dim,
-                       args.layers, 1e-3, 1e-4, seed=args.seed)
+                       args.layers, 1e-3, 1e-4, seed=args.seed,
+                       emb=None if snap is None else snap["emb0"])
     K = max(1, args.cpu_k)
     res = {"cores": threads, "threads": threads, "os_cpu_count": os.cpu_count(),
            "kind": "port", "cpu": cpu_model(), "warmup": 1, "k": K}
+    parity = None
+    if snap is not None:
+        parity = oracle_parity(o, snap)  # the warm-up step
+        users, pos, neg = snap["users"], snap["pos"], snap["neg"]
     if args.cpu_baseline == "step":
-        progress("cpu baseline: warm-up step")
-        o.stageOne(users, pos, neg)  # warm-up
+        if parity is None:
+            progress("cpu baseline: warm-up step")
+            o.stageOne(users, pos, neg)  # warm-up
         ts = []
         for i in range(K):
             t0 = time.perf_counter()
@@ -226,7 +304,7 @@ def cpu_baseline(ds, args, users, pos, neg):
     if args.cpu_baseline == "forward":
         res.update(value=round(1.0 / t_fwd, 4), unit="forward passes/s",
                    sample=f"1 warm-up + mean of {K} 3-layer full-graph forwards of the C2 graph")
-    return res
+    return res, parity
 
 
 def pmc_traffic(args):
@@ -450,6 +528,11 @@ def main(argv=None):
     achieved = avg_bytes / (avg_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args)
 
+    snap = None
+    if rank == 0 and world == 1 and args.parity:
+        progress("parity: GPU step from a host snapshot of the table and Adam state")
+        snap = parity_snapshot(model, eng, emb, args, t_base + args.steps, rank, world)
+
     qsteps = args.quality_steps if args.quality_steps >= 0 else (3000 if world == 1 else 0)
     recall = None
     if qsteps > 0 and rank == 0:
@@ -457,9 +540,16 @@ def main(argv=None):
         torch.cuda.empty_cache()
         recall = quality_leg(args, dev, qsteps)
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
-        cpu = cpu_baseline(ds, args, u.cpu().numpy(), p.cpu().numpy(), n.cpu().numpy())
+        cpu, parity = cpu_baseline(ds, args, u.cpu().numpy(), p.cpu().numpy(),
+                                   n.cpu().numpy(), snap)
+    elif snap is not None:
+        from oracle.lightgcn_oracle import OracleLightGCN
+        torch.set_num_threads(host_threads())
+        o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, args.dim,
+                           args.layers, 1e-3, 1e-4, emb=snap["emb0"])
+        parity = oracle_parity(o, snap)
 
     if rank == 0:
         value = world * args.steps * B / dt
@@ -508,6 +598,7 @@ def main(argv=None):
             "prune": bool(args.prune),
             "frontier_F1_rows": f1_rows,
             "recall": recall,
+            "parity": parity,
             "cpu_baseline": cpu,
             "setup_s": round(t_setup, 2),
         }
@@ -518,6 +609,8 @@ def main(argv=None):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if parity is not None and not parity["ok"]:
+        raise SystemExit(f"parity above {PARITY_TOL}: {parity}")
 
 
 if __name__ == "__main__":

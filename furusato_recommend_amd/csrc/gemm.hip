@@ -598,13 +598,28 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
   // second-pass row of an upper half-wave, local rows 9 / 11 / 13 / 15);
   // never with the f32 loop, never with these loads (0 in 120 launches over
   // two builds) — tools/dbg_rnbwd.py, test_gemm_nn_resnorm_bwd_repeatable.
+#ifndef MIREC_RNBWD_MASKED
+#define MIREC_RNBWD_MASKED 0
+#endif
 #pragma unroll
   for (int q = 0; q < RPG; ++q) {
+#if MIREC_RNBWD_MASKED
+    const int64_t r = m0 + g + 8 * q;
+    ov[q] = gv[q] = f4_zero();
+    mv[q] = sv[q] = 0.f;
+    if (r < n) {
+      ov[q] = ld4(a.out + r * kTile + c);
+      gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
+      mv[q] = a.mean[r];
+      sv[q] = a.rstd[r];
+    }
+#else
     const int64_t r = min(m0 + g + 8 * q, n - 1);
     ov[q] = ld4(a.out + r * kTile + c);
     gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
     mv[q] = a.mean[r];
     sv[q] = a.rstd[r];
+#endif
   }
   const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
   f32x16 acc[TM][2];

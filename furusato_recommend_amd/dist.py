@@ -117,9 +117,22 @@ class DataParallel:
         self.comm_events = None
         if self.world > 1:
             dist.broadcast(emb.data, src=0, group=group)
-        if mode in ("sharded", "auto"):
+        # the row shards' static lists and the N x D staging buffer: built
+        # now for "sharded", on first use for "auto" (and dropped again when
+        # the calibration keeps "sparse": 282 MB at C2, ~11 GB at C5)
+        self._chunks = None
+        self.last_rows = None
+        if mode == "sharded":
             self._init_shard()
         self._mark_sharded_state(False)
+
+    def _ensure_shard(self):
+        if self._chunks is None:
+            self._init_shard()
+
+    def _free_shard(self):
+        self._chunks = None
+        self.last_rows = None
 
     # ------------------------------------------------------------ row shards
     def _init_shard(self):
@@ -203,6 +216,7 @@ class DataParallel:
         all-gather, then scatter slot w's rows back to w, w+W, ..."""
         if not self.distributed:
             return
+        self._ensure_shard()
         for c in range(len(self._chunks)):
             self._pack(c, t)
             self._gather_chunk(c, async_op=False)
@@ -288,6 +302,7 @@ class DataParallel:
             if self.mode == "sparse":
                 eng.backward(self.emb, adam=self.adam)
             else:
+                self._ensure_shard()
                 works = []
                 overlap = self.distributed
 
@@ -336,6 +351,7 @@ class DataParallel:
         the ``sharded`` mode pays (algbw = N·D·4 B / this)."""
         if not self.distributed:
             return 0.0
+        self._ensure_shard()
         best = float("inf")
         for _ in range(reps):
             torch.cuda.synchronize()  # (a CUDA table: time_table_allgather is GPU-only)
@@ -382,6 +398,8 @@ class DataParallel:
         self.mode = choice
         self.gather_optimizer_state()  # no-op unless leaving sharded moments behind
         ag = self.time_table_allgather() if self.emb.is_cuda else 0.0
+        if choice != "sharded":
+            self._free_shard()
         table = self.emb.numel() * self.emb.element_size()
         self.calibration = {"sparse_ms_per_step": round(ms["sparse"], 4),
                             "sharded_ms_per_step": round(ms["sharded"], 4),
@@ -606,7 +624,12 @@ class DenseGradDataParallel:
             off += c
         if self._ones is None or self._ones.numel() != n_own:
             self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
-        coef = tg.coef * float(self.world)  # every rank's norm coefficient is the same
+        # the union's norm coefficient: the SUM of the ranks' (each scales with
+        # its own 1/B, graphsage.py:333-336, so ranks with uneven batches —
+        # a short last batch — differ); 2 floats
+        coef = tg.coef.clone()
+        if self.distributed:
+            dist.all_reduce(coef, op=dist.ReduceOp.SUM, group=self.group)
         n_user = min(max(tg.n_user - lo, 0), n_own)
         hp = st.next_hparams()
         pf = p.data.view(-1)
@@ -654,6 +677,8 @@ class DenseGradDataParallel:
             for q in range(1, W):
                 tot += allp[q]
             self._norms_next = tot.sqrt()
+            if self.distributed and W > 1:
+                self.model.table_stale = True  # until sync_table()
             return
         self.routed_adam(rid, rv, counts)
         if self.distributed:
@@ -704,6 +729,7 @@ class DenseGradDataParallel:
         lo = self.rank * n_own
         pf = p.data.view(-1)
         dist.all_gather_into_tensor(pf, pf[lo * d:(lo + n_own) * d].clone(), group=self.group)
+        self.model.table_stale = False
 
     def gather_optimizer_state(self):
         """All-gather the row shards of the sharded parameters' Adam moments

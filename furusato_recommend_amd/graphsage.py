@@ -466,6 +466,18 @@ class GraphSAGE(nn.Module):
         self._norm_cache = None  # (norms [2], token) of the table after the fused Adam
         self._step_seed = int(config.get("seed", 2020))
         self._calls = 0
+        # set by DenseGradDataParallel's ``fetch`` exchange: the local table
+        # is current on this rank's row block and the fetched rows only
+        # until sync_table() / gather_optimizer_state() (collectives) run
+        self.table_stale = False
+        self.register_state_dict_pre_hook(
+            lambda module, prefix, keep_vars: module._check_table_current("state_dict()"))
+
+    def _check_table_current(self, what: str):
+        if self.table_stale:
+            raise RuntimeError(f"GraphSAGE.{what}: the id table is current on this rank's row "
+                               "block only (data-parallel 'fetch' exchange); call "
+                               "sync_table() or gather_optimizer_state() on every rank first")
 
     @property
     def user_id_embeddings(self):
@@ -694,6 +706,7 @@ class GraphSAGE(nn.Module):
     def propagated(self) -> torch.Tensor:
         """Full-graph inference (getUsersRating 'all', graphsage.py:401-424):
         every node aggregates the mean of ALL its neighbours per layer."""
+        self._check_table_current("propagated() / evaluation")
         x = self._table.detach()
         for i in range(self.num_layers):
             agg = torch.empty_like(x)

@@ -1206,6 +1206,9 @@ class SASRec(nn.Module):
                                         sink=self._tg,
                                         norm=self._norm_buf[1:] if self._norm_valid() else None)
         u = self.forward_user_packed(x, packing, seg, length)
+        # the pooled user rows of the last step (B x d; in a captured step
+        # the graph's own buffer, rewritten by every replay): parity tests
+        self._user_rows = u.detach()
         loss = _BPRRowsLoss.apply(u, self.forward_item(pn), wnorm, self.config["decay"] / B)
         # the backward seed from a kept tensor (no fill kernel per step)
         seed = self.__dict__.get("_loss_seed")
@@ -1351,6 +1354,14 @@ class _CapturedStep:
                 self.norm_from_buf = model._norm_valid()
                 with torch.cuda.graph(self.graph, pool=pool):
                     self.loss = self._body()
+                self.user_rows = model._user_rows  # written by every replay
+                # the gradient tensors graph A's backward writes on every
+                # replay (AccumulateGrad assigned them during capture; replays
+                # never assign .grad again): run() re-attaches them before
+                # the hook, which may consume a .grad (the row-sharded Adam
+                # sets it to None), so every replay's hook sees them
+                self.params = params
+                self.grads = [p.grad for p in params]
                 if split is not None:
                     tg = model._tg
                     # graph B runs the fused table Adam (which keeps the norm)
@@ -1435,6 +1446,8 @@ class _CapturedStep:
         if self.split is not None:
             if m._tg is not None:
                 m._tg.pending = True  # the replayed backward left S / coef
+            for p, g in zip(self.params, self.grads):
+                p.grad = g
             hook()
             if m._tg is not None:
                 m._tg.pending = False

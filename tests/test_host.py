@@ -244,6 +244,161 @@ def test_data_parallel_equals_union_batch(golden, mode):
     assert np.max(np.abs(res[0] - ref)) / np.max(np.abs(ref)) < 2e-5
 
 
+class _AccumEngine(OracleEngine):
+    """OracleEngine that also sums the loss into the step's accumulator (as
+    the HIP engine's bpr does)."""
+
+    def bpr(self, out, emb, users, pos, neg, decay, loss_accum=None, grad_scale=1.0):
+        loss = super().bpr(out, emb, users, pos, neg, decay, None, grad_scale)
+        if loss_accum is not None:
+            loss_accum += loss
+        return loss
+
+
+class _CpuLGCN(torch.nn.Module):
+    """The model surface DPTrainer uses (state_dict, optim) over the oracle."""
+
+    def __init__(self, o):
+        super().__init__()
+        self.o = o
+        self.emb = o.emb
+        self.optim = o.optim
+
+
+def _dp_sampler(ds_pos, n_users, m_items, rank, world):
+    """Rank-local triples from the rank's user shard, a rank-dependent count
+    (the capped sampler keeps a data-dependent number per rank)."""
+    def sample(epoch):
+        rng = np.random.default_rng(1000 * epoch + rank)
+        n = 40 + 7 * rank
+        us = rng.integers(0, (n_users - rank + world - 1) // world, n) * world + rank
+        u, p, ng = [], [], []
+        for x in us:
+            if len(ds_pos[x]) == 0:
+                continue
+            u.append(x)
+            p.append(sorted(ds_pos[x])[rng.integers(0, len(ds_pos[x]))])
+            while True:
+                j = int(rng.integers(0, m_items))
+                if j not in ds_pos[x]:
+                    break
+            ng.append(j)
+        return np.array(u), np.array(p), np.array(ng)
+    return sample
+
+
+def _dp_trainer_worker(rank, world, port, fpath, ckpt, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from furusato_recommend_amd.dist import DataParallel
+    from furusato_recommend_amd.train_dp import DPTrainer
+    f = dict(np.load(fpath))
+    nu, mi = int(f["n_users"]), int(f["m_items"])
+    tu, ti = f["train_user"], f["train_item"]
+    pos = [set(ti[tu == k].tolist()) for k in range(nu)]
+    test = {k: sorted(pos[k])[:1] for k in range(0, nu, 3) if pos[k]}
+
+    class DS:
+        n_users, m_items, trainDataSize, testDict = nu, mi, len(tu), test
+
+    def make(seed_shift):
+        o = O.OracleLightGCN(tu, ti, nu, mi, 64, 3, float(f["lr"]), float(f["decay"]),
+                             emb=torch.from_numpy(f["emb0"]) + seed_shift)
+        m = _CpuLGCN(o)
+        dp = DataParallel(_AccumEngine(o, 16), o.emb.data, o.optim, mode="sparse")
+        return o, m, dp
+
+    def evaluator(model):
+        with torch.no_grad():
+            out = model.o.propagated()
+        ue, ie = out[:nu], out[nu:]
+        allpos = [np.array(sorted(s)) for s in pos]
+        res = O.evaluate(ue, ie, test, allpos, topks=(10, 20))
+        users = sorted(test)
+        r = ue[torch.tensor(users)] @ ie.t()
+        for i, u in enumerate(users):
+            r[i, list(pos[u])] = -(1 << 10)
+        return res, torch.topk(r, 20).indices.numpy()
+
+    cfg = {"bpr_batch_size": 16, "decay": float(f["decay"]), "test_span": 1,
+           "checkpoint_path": ckpt, "topks": (10, 20)}
+    o, m, dp = make(0.5 if rank else 0.0)  # rank 1's init is overwritten by the broadcast
+    sampler = _dp_sampler(pos, nu, mi, rank, world)
+    seen = []
+
+    def logged(ep):
+        t = sampler(ep)
+        seen.append(t)
+        return t
+    tr = DPTrainer(cfg, DS, m, dp=dp, sampler=logged, evaluator=evaluator)
+    hist = tr.fit(2)
+    final = o.emb.detach().numpy().copy()
+    # resume: a fresh model (other init) from the checkpoint, then one more epoch
+    o2, m2, dp2 = make(0.25)
+    tr2 = DPTrainer(cfg, DS, m2, dp=dp2, sampler=sampler, evaluator=evaluator)
+    loaded = tr2.load_checkpoint()
+    resumed = (loaded, tr2.epoch, np.array_equal(o2.emb.detach().numpy(), final),
+               all(torch.equal(a, b) for a, b in zip(
+                   o2.optim.state[o2.emb].values(), o.optim.state[o.emb].values())))
+    h2 = tr2.fit(1)
+    q.put((rank, final, hist, seen, resumed, h2, o2.emb.detach().numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_dp_trainer_two_ranks_gloo(golden, tmp_path):
+    """train_dp.DPTrainer (the ddp_lgcn.py:625-746 epoch driver) over the real
+    DataParallel, 2 gloo ranks on CPU with the oracle-backed engine: two
+    epochs with a barrier each, rank-local samples equalised to the same
+    count, a checkpoint + evaluation (Recall / Precision / NDCG / HR /
+    Coverage @10, @20) every epoch; replicas identical and equal to ONE
+    oracle process stepping the union batches; the checkpoint reloads into
+    a fresh model (table, Adam state, next epoch) and training resumes."""
+    from tests.conftest import GOLDEN
+    fpath = os.path.join(GOLDEN, "lgcn_d64_L3.npz")
+    ckpt = str(tmp_path / "ckpt" / "ddp_lgn_all.pth")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_trainer_worker, args=(r, 2, port, fpath, ckpt, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, *rest = q.get(timeout=240)
+        res[r] = rest
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    f = golden("lgcn_d64_L3.npz")
+    (fin0, hist0, seen0, resumed0, h20, e20), (fin1, hist1, seen1, resumed1, h21, e21) = \
+        res[0], res[1]
+    assert np.array_equal(fin0, fin1) and np.array_equal(e20, e21)
+    assert [h["epoch"] for h in hist0] == [0, 1] and [h["epoch"] for h in h20] == [2]
+    for h in hist0:
+        assert h["triples_per_rank"] == min(len(seen0[h["epoch"]][0]), len(seen1[h["epoch"]][0]))
+        met = h["metrics"]
+        for k in ("recall", "precision", "ndcg", "hr", "coverage"):
+            assert len(met[k]) == 2 and all(np.isfinite(met[k]))
+        assert 0 < met["coverage"][0] <= met["coverage"][1] <= 1
+    assert hist1[0]["metrics"] is None  # rank 1 waits while rank 0 evaluates
+    assert resumed0 == (True, 2, True, True) and resumed1 == (True, 2, True, True)
+    assert hist0[0]["loss"] == hist1[0]["loss"]  # the union mean on every rank
+    # one process stepping the union batches (rank-major) == the replicas
+    nu, mi = int(f["n_users"]), int(f["m_items"])
+    o = O.OracleLightGCN(f["train_user"], f["train_item"], nu, mi, 64, 3, float(f["lr"]),
+                         float(f["decay"]), emb=torch.from_numpy(f["emb0"]))
+    for ep in range(2):
+        k = hist0[ep]["triples_per_rank"]
+        for i in range(0, k, 16):
+            j = min(i + 16, k)
+            tri = [np.concatenate([seen0[ep][c][i:j], seen1[ep][c][i:j]]) for c in range(3)]
+            o.stageOne(*tri)
+    ref = o.emb.detach().numpy()
+    assert np.max(np.abs(fin0 - ref)) / np.max(np.abs(ref)) < 2e-5
+    assert os.path.exists(ckpt) and os.path.exists(ckpt + ".train")
+
+
 def _calib_worker(rank, world, port, fpath, q, prefer):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -455,6 +610,35 @@ def test_bench_self_launch_two_ranks_gloo():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1
     assert json.loads(lines[0]) == {"n_gpus": 2, "sum": 3.0}
+
+
+def test_bench_oracle_parity_leg():
+    """bench.py's parity leg: the oracle takes the snapshot's step from the
+    snapshot's table, Adam moments and step count.  A snapshot whose "GPU"
+    half is another oracle taking the same step from the same state passes
+    with zero error; a perturbed table or loss fails the 1e-4 bar."""
+    import bench
+    from oracle.lightgcn_oracle import OracleLightGCN
+    rng = np.random.default_rng(3)
+    nu, mi, E, D = 60, 40, 500, 16
+    tu, ti = rng.integers(0, nu, E), rng.integers(0, mi, E)
+    trip = (rng.integers(0, nu, 32), rng.integers(0, mi, 32), rng.integers(0, mi, 32))
+    a = OracleLightGCN(tu, ti, nu, mi, D, 3, 1e-3, 1e-4, seed=1)
+    for _ in range(3):  # non-trivial Adam state
+        a.stageOne(*trip)
+    st = a.optim.state[a.emb]
+    snap = {"emb0": a.emb.detach().clone(), "exp_avg": st["exp_avg"].clone(),
+            "exp_avg_sq": st["exp_avg_sq"].clone(), "n_steps": int(st["step"]),
+            "lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8, "out_gpu": a.propagated(),
+            "users": trip[0], "pos": trip[1], "neg": trip[2], "step_index": 3}
+    snap["loss_gpu"] = a.stageOne(*trip)
+    snap["emb1_gpu"] = a.emb.detach().clone()
+    fresh = OracleLightGCN(tu, ti, nu, mi, D, 3, 1e-3, 1e-4, seed=9)  # other init: overwritten
+    r = bench.oracle_parity(fresh, snap)
+    assert r["ok"] and r["rel_out"] == 0.0 and r["rel_emb_step"] == 0.0 and r["rel_loss"] == 0.0
+    snap["emb1_gpu"] = snap["emb1_gpu"] + 1e-3 * snap["emb1_gpu"].abs().max()
+    r = bench.oracle_parity(OracleLightGCN(tu, ti, nu, mi, D, 3, 1e-3, 1e-4), snap)
+    assert not r["ok"] and r["rel_emb_step"] > 1e-4 and r["rel_out"] == 0.0
 
 
 def test_host_threads_bounded():
