@@ -217,6 +217,25 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
   }
 }
 
+// Score tiles on the bf16 MFMA pipe (MIREC_TOPK_X6, default on, D <= 128):
+// the exact three-term split of gemm.hip (f32-class error per product; the
+// top-k is checked against float64 scores by the near-tie criterion of
+// test_evaluate_matches_oracle).  The user rows are split once into
+// registers (the B operand: D/16 Split3 = 3 D/4 VGPRs), every item tile once
+// at staging into three bf16 planes [3][32][D + 8] whose 16-deep k blocks are
+// permuted so a lane half's 8 values (x6_k order) are one 16-byte read
+// (plane_pos, as gemm.hip's [row][k] planes; row stride 2 D + 16 B: the 16
+// lanes of a read phase hit distinct 4-bank groups).  Per 32 x 32 tile and
+// 16 dims: 6 v_mfma_f32_32x32x16_bf16 (192 cycles) instead of 8
+// v_mfma_f32_32x32x2_f32 (512).
+#ifndef MIREC_TOPK_X6
+#define MIREC_TOPK_X6 1
+#endif
+
+__device__ __forceinline__ int st_plane_pos(int c4) {
+  return (c4 >> 2) * 16 + 8 * (c4 & 1) + 4 * ((c4 >> 1) & 1);
+}
+
 template <int D>
 __global__ __launch_bounds__(128) void score_topk_kernel(
     const float *__restrict__ U, int64_t n_eval, const float *__restrict__ I, int64_t m_items,
@@ -232,8 +251,11 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   // workgroup per CU).  k-step s of lane half h covers dim 2 s + h (D <= 128)
   // or dim h·D/2 + s (D > 128); A and B use the same map.
   constexpr bool UL = D > 128;
+  constexpr bool X6 = MIREC_TOPK_X6 && !UL;
   constexpr int NB = UL ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) float sI[NB][kStTile * LD];
+  constexpr int LP = D + 8;  // bf16 plane row stride (X6)
+  constexpr int kSI = X6 ? (3 * kStTile * LP + 1) / 2 : kStTile * LD;  // floats per buffer
+  __shared__ __attribute__((aligned(16))) float sI[NB][kSI];
   __shared__ __attribute__((aligned(16))) float sU[UL ? kStUsers * LD : 4];
   __shared__ float cv[kStUsers][kStCap];
   __shared__ int ci[kStUsers][kStCap];
@@ -251,8 +273,20 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   const int64_t it0 = (int64_t)blockIdx.y * chunk;
   const int64_t it1 = min(m_items, it0 + chunk);
   // the user's embedding as the B operand: ue[s] = U[ub][2 s + h]
-  float ue[UL ? 1 : KS];
-  if constexpr (!UL) {
+  float ue[(UL || X6) ? 1 : KS];
+  // X6: the user's row split once, block s16 = dims 16 s16 + x6_k(h, e)
+  Split3 us[X6 ? D / 16 : 1];
+  if constexpr (X6) {
+#pragma unroll
+    for (int s16 = 0; s16 < D / 16; ++s16) {
+      float x[8];
+      const float4 lo = uok ? ld4(U + ub * D + 16 * s16 + 4 * h) : f4_zero();
+      const float4 hi = uok ? ld4(U + ub * D + 16 * s16 + 8 + 4 * h) : f4_zero();
+      x[0] = lo.x, x[1] = lo.y, x[2] = lo.z, x[3] = lo.w;
+      x[4] = hi.x, x[5] = hi.y, x[6] = hi.z, x[7] = hi.w;
+      us[s16] = split3(x);
+    }
+  } else if constexpr (!UL) {
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
   } else {
@@ -295,7 +329,28 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
       const int e = t + 128 * q, row = e / (D / 4), c4 = e % (D / 4);
-      if (e < kStTile * D / 4) st4(sI[buf] + row * LD + 4 * c4, r[q]);
+      if (e >= kStTile * D / 4) continue;
+      if constexpr (X6) {  // three bf16 planes, k-permuted per 16-deep block
+        const float x[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
+        uint32_t H[2], M[2], Lo[2];
+#pragma unroll
+        for (int p2 = 0; p2 < 2; ++p2) {
+          const float a = x[2 * p2], b = x[2 * p2 + 1];
+          const uint32_t ph = pk_bf16(a, b);
+          const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+          const uint32_t pm = pk_bf16(ra, rb);
+          const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
+          H[p2] = ph;
+          M[p2] = pm;
+          Lo[p2] = pk_bf16(sa, sb);
+        }
+        uint16_t *d = reinterpret_cast<uint16_t *>(sI[buf]) + row * LP + st_plane_pos(c4);
+        *reinterpret_cast<uint2 *>(d) = make_uint2(H[0], H[1]);
+        *reinterpret_cast<uint2 *>(d + kStTile * LP) = make_uint2(M[0], M[1]);
+        *reinterpret_cast<uint2 *>(d + 2 * kStTile * LP) = make_uint2(Lo[0], Lo[1]);
+      } else {
+        st4(sI[buf] + row * LD + 4 * c4, r[q]);
+      }
     }
   };
   // user slot u's buffer entry of this lane, with the train-positive mask
@@ -342,7 +397,17 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if constexpr (!UL) {
+    if constexpr (X6) {
+      const uint16_t *ap = reinterpret_cast<const uint16_t *>(sI[cur]) + i * LP + 8 * h;
+#pragma unroll
+      for (int s16 = 0; s16 < D / 16; ++s16) {
+        Split3 a;
+        a.h = *reinterpret_cast<const bf16x8 *>(ap + 16 * s16);
+        a.m = *reinterpret_cast<const bf16x8 *>(ap + kStTile * LP + 16 * s16);
+        a.l = *reinterpret_cast<const bf16x8 *>(ap + 2 * kStTile * LP + 16 * s16);
+        acc = mfma_x6(a, us[s16], acc);
+      }
+    } else if constexpr (!UL) {
       const float *arow = sI[cur] + i * LD + h;
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);

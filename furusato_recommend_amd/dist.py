@@ -421,6 +421,24 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, 
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
+def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0) -> torch.Tensor:
+    """Ascending distinct ids of the int32 device tensor ``ids`` in [0,
+    n_rows) outside [lo, hi) (mirec_distinct_rows: byte map, block counts,
+    ordered writes — no sort); one host sync for the count."""
+    from . import _lib
+    from ._lib import check, lib
+    ids = ids.to(torch.int32).contiguous()
+    dev = ids.device
+    nb = int(lib.mirec_distinct_rows_workspace(int(n_rows)))
+    ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
+    out = torch.empty(max(int(n_rows), 1), dtype=torch.int32, device=dev)
+    cnt = torch.empty(1, dtype=torch.int32, device=dev)
+    check(lib.mirec_distinct_rows(ids.data_ptr(), ids.numel(), int(n_rows), int(lo), int(hi),
+                                  out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                  _lib.stream_handle()), "distinct_rows")
+    return out[: int(cnt.item())]
+
+
 def route_ids(ids: torch.Tensor, n_rows: int, group=None):
     """Send every row id to the rank owning it (contiguous blocks of
     n_rows/W rows; ``ids`` ascending int32).  Returns (received ids in
@@ -705,8 +723,7 @@ class DenseGradDataParallel:
         n_own = N // self.world
         lo = self.rank * n_own
         ids = torch.cat([g for g, _ in tree.groups])
-        uniq = torch.unique(ids[ids >= 0])
-        need = uniq[(uniq < lo) | (uniq >= lo + n_own)].to(torch.int32).contiguous()
+        need = distinct_rows(ids, N, lo, lo + n_own)
         a = self._event()
         req, rc, sc = route_ids(need, N, self.group)
         rows = p.data.index_select(0, req.long())

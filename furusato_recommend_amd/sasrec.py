@@ -37,20 +37,30 @@ from .rows import gather_rows, gather_rows_norm
 
 
 # Optional per-launch timing (tools/bench_sasrec.py): a list receiving
-# (kind, start_event, end_event, (B, T, heads, head_dim), offsets or None);
-# packed launches have T = -1 and their int32 offsets.
+# (kind, start_event, end_event, (B, T, heads, head_dim), offsets or None,
+# launches between the events); packed launches have T = -1 and their int32
+# offsets.  ATTN_REPEAT = R > 1 times R back-to-back launches of the same
+# kernel on the same operands after one untimed launch, so the interval holds
+# kernel time only — in a host-bound eager step the GPU can idle between the
+# start event and the launch (timing only: a backward launched R times
+# leaves R times its accumulated input gradient).
 ATTN_EVENTS = None
+ATTN_REPEAT = 1
 
 
 def _timed(kind, shape, launch, offsets=None):
     ev = ATTN_EVENTS
     if ev is None:
         return launch()
+    reps = max(1, int(ATTN_REPEAT))
+    if reps > 1:
+        launch()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    r = launch()
+    for _ in range(reps):
+        r = launch()
     e.record()
-    ev.append((kind, s, e, shape, offsets))
+    ev.append((kind, s, e, shape, offsets, reps))
     return r
 
 

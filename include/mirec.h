@@ -255,6 +255,18 @@ int mirec_mask_compact(const mirec_csr_t *csr, const uint8_t *bm,
                        int32_t *wide_list, int32_t *wide_count,
                        mirec_stream_t stream);
 
+/* The ascending distinct ids of ids[0 .. n) that lie in [0, n_rows) and
+ * outside [lo, hi) -> out[0 .. *count) (capacity n_rows): the rows a
+ * data-parallel rank fetches from their owners before a GraphSAGE forward
+ * (the fetch exchange of dist.DenseGradDataParallel; replaces torch.unique
+ * of ddp-time bookkeeping, ddp_sage.py:754-878 has no exchange).  Byte map +
+ * per-block counts + scan + ordered writes: no sort.  Workspace (16-byte
+ * aligned): mirec_distinct_rows_workspace(n_rows) bytes. */
+int64_t mirec_distinct_rows_workspace(int64_t n_rows);
+int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows, int64_t lo,
+                        int64_t hi, int32_t *out, int32_t *count, void *workspace,
+                        size_t workspace_bytes, mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */
 /* ------------------------------------------------------------------------ */

@@ -16,6 +16,34 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+F32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense f32 MFMA
+
+
+@torch.no_grad()
+def near_tie(U, I, bu, graph, top, k):
+    """test_evaluate_matches_oracle's criterion on the device: every picked
+    item is in the exact top-k of the float64 scores (train positives
+    excluded) or within 1e-5 x max|score| of the exact k-th score."""
+    s = U[bu].double() @ I.double().t()
+    rp, col = graph.rowptr, graph.col
+    users = bu.long()
+    beg, end = rp[users], rp[users + 1]
+    cnt = end - beg
+    rows = torch.repeat_interleave(torch.arange(len(users), device=s.device), cnt)
+    off = torch.arange(int(cnt.sum()), device=s.device) - \
+        torch.repeat_interleave(torch.cumsum(cnt, 0) - cnt, cnt)
+    items = col[torch.repeat_interleave(beg, cnt) + off].long() - graph.n_users
+    s[rows, items] = -float("inf")
+    kth = torch.topk(s, k, dim=1).values[:, k - 1]
+    eps = 1e-5 * float(s[torch.isfinite(s)].abs().max())
+    picked = torch.gather(s, 1, top[:, :k].long())
+    exact = picked >= kth[:, None]
+    ok = bool((picked >= kth[:, None] - eps).all())
+    return {"check": "float64 near-tie (test_evaluate_matches_oracle)", "all_picks_ok": ok,
+            "near_tie_users": int((~exact.all(dim=1)).sum()), "users": int(len(users)),
+            "eps": eps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--users", type=int, default=1_000_000)
@@ -25,6 +53,9 @@ def main():
     ap.add_argument("--batch", type=int, default=10_000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--dense", type=int, default=1, help="also time the GEMM + top-k path")
+    ap.add_argument("--check64", type=int, default=1,
+                    help="check every streamed pick against float64 scores (near-tie test)")
     a = ap.parse_args()
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
     from furusato_recommend_amd.evaluate import score_topk, topk_masked
@@ -42,7 +73,8 @@ def main():
         return topk_masked((U[bu] @ I.t()).contiguous(), bu, m.graph, a.k)
 
     out = {}
-    for name, fn in (("stream", stream), ("dense", dense)):
+    paths = (("stream", stream), ("dense", dense)) if a.dense else (("stream", stream),)
+    for name, fn in paths:
         fn()
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,8 +89,14 @@ def main():
         print(json.dumps({"path": name, "batch_users": a.batch, "items": a.items, "dim": a.dim,
                           "k": a.k, "ms_per_batch": round(ms, 3),
                           "tflops_scores": round(flop / ms / 1e9, 1),
+                          "frac_f32_mfma_peak": round(flop / ms / 1e9 / F32_PEAK_TFLOPS, 4),
+                          "lib": os.path.basename(os.environ.get("MIREC_LIB", "libmirec.so")),
                           "rating_matrix_bytes": 0 if name == "stream" else 4 * a.batch * a.items}),
               flush=True)
+    if a.check64:
+        print(json.dumps(near_tie(U, I, bu, m.graph, out["stream"][1], a.k)), flush=True)
+    if not a.dense:
+        return
     si, di = out["stream"][1], out["dense"][1]
     same = torch.equal(si, di)
     rows_same = float((si == di).all(dim=1).float().mean())

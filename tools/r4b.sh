@@ -1,0 +1,27 @@
+# Round 4 (session 1b): split score tiles in the streamed top-k (tests,
+# x6 vs f32 at C2 with the float64 near-tie check, C5 line), tg_sum
+# counter bytes at C3, the C4 line with back-to-back attention timing.
+set -u
+mkdir -p gpurun_out/r4b
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "evaluate or score_topk or mf_c1 or topk or trajectory or distinct_rows or union_step or routed" > gpurun_out/r4b/pytest_eval.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/r4b/pytest_eval.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for v in libmirec var_topk_f32; do
+  MIREC_LIB=$PWD/furusato_recommend_amd/$v.so timeout -k 10 300 python -u tools/eval_bench.py --reps 10 > gpurun_out/r4b/eval_c2_$v.jsonl 2>&1
+  rc=$?; echo "eval $v rc=$rc"; cat gpurun_out/r4b/eval_c2_$v.jsonl
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+timeout -k 10 200 python -u tools/tg_sum_bytes.py > gpurun_out/r4b/tg_counts.json 2> gpurun_out/r4b/tg_counts.log
+rc=$?; echo "tg counts rc=$rc"; cat gpurun_out/r4b/tg_counts.json
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex tg_sum -d gpurun_out/r4b/tgf -o run --output-format csv -- python3 tools/bench_sage.py --steps 5 --warmup 2 --cpu-baseline 0 > gpurun_out/r4b/tgf.log 2>&1
+rc=$?; echo "pmc fetch rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex tg_sum -d gpurun_out/r4b/tgw -o run --output-format csv -- python3 tools/bench_sage.py --steps 5 --warmup 2 --cpu-baseline 0 > gpurun_out/r4b/tgw.log 2>&1
+rc=$?; echo "pmc write rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
+python tools/tg_sum_bytes.py --counts gpurun_out/r4b/tg_counts.json --fetch gpurun_out/r4b/tgf --write gpurun_out/r4b/tgw --out gpurun_out/r4b/pmc_tg_sum.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b/c3prof -o run -- python3 tools/bench_sage.py --steps 10 --warmup 3 --cpu-baseline 0 > gpurun_out/r4b/c3prof.log 2>&1
+rc=$?; echo "c3 prof rc=$rc"; tail -1 gpurun_out/r4b/c3prof.log; if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 400 python -u tools/bench_sasrec.py > gpurun_out/r4b/c4.json 2> gpurun_out/r4b/c4.log
+rc=$?; echo "c4 rc=$rc"; cat gpurun_out/r4b/c4.json
+exit $rc

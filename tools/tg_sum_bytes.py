@@ -1,0 +1,99 @@
+"""Algorithmic bytes of the C3 sorted table-gradient sum (tg_sum_kernel) per
+launch, from the row groups one real C3 step hands to TableGrad.accumulate,
+and — with a rocprofv3 FETCH_SIZE / WRITE_SIZE pass directory — the counter
+bytes of the same kernel beside them.
+
+    python tools/tg_sum_bytes.py                     # counts, one JSON line
+    python tools/tg_sum_bytes.py --fetch DIR --write DIR [--out FILE]
+
+Algorithmic (every operand once): the sort's keys and values read (8 B per
+entry), one weight per target (4 B), every gradient row read ONCE (inner
+entries' rows; a leaf group's g_out row per target), the summed rows written
+once per distinct row id (d x 4 B) and its stamp (4 B).  The pull form reads
+a target's g_out row once per child entry instead ("pull_read_bytes")."""
+import argparse
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def counts(B=2048, fan=(25, 10), dim=128):
+    import torch
+
+    from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
+    from furusato_recommend_amd import graphsage as G
+    ds = SyntheticBipartite(1_000_000, 100_000, 20_000_000, seed=0)
+    torch.manual_seed(2020)
+    m = GraphSAGE({"recdim": dim, "layer": len(fan), "fanouts": list(fan), "lr": 1e-3,
+                   "decay": 1e-7, "device": "cuda:0", "bpr_batch_size": B}, ds)
+    seen = []
+    orig = G.TableGrad.accumulate
+
+    def spy(self, groups):
+        seen.append([(ids.clone(), int(g.shape[0]), int(k)) for ids, g, k, *_ in groups])
+        return orig(self, groups)
+    G.TableGrad.accumulate = spy
+    u, p, n = m.sample(B, seed=7, offset=0)
+    m.stageOne(u, p, n)
+    torch.cuda.synchronize()
+    G.TableGrad.accumulate = orig
+    groups = seen[-1]
+    n_ent = sum(ids.numel() for ids, _, _ in groups)
+    valid = torch.cat([ids[ids >= 0] for ids, _, _ in groups])
+    n_tgt = sum(nt for _, nt, _ in groups)
+    rows_once = 0
+    for ids, nt, k in groups:
+        if k == 1:
+            rows_once += int((ids >= 0).sum())
+        else:  # targets with at least one valid child
+            rows_once += int(((ids.view(nt, k) >= 0).any(1)).sum())
+    distinct = int(torch.unique(valid).numel())
+    rb = dim * 4
+    alg = 8 * n_ent + 4 * n_tgt + rb * rows_once + (rb + 4) * distinct
+    return {"entries": n_ent, "valid_entries": int(valid.numel()), "targets": n_tgt,
+            "grad_rows_once": rows_once, "distinct_rows": distinct,
+            "groups": [(int(ids.numel()), nt, k) for ids, nt, k in groups],
+            "algorithmic_bytes": alg,
+            "pull_read_bytes": 8 * n_ent + 4 * n_tgt + rb * int(valid.numel()),
+            "write_bytes": (rb + 4) * distinct}
+
+
+def pmc(dirname, counter, kernel="tg_sum_kernel"):
+    vals = []
+    for f in glob.glob(os.path.join(dirname, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    vals.append(float(row["Counter_Value"]))
+    return vals
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--counts")
+    ap.add_argument("--out")
+    a = ap.parse_args()
+    if a.fetch:
+        c = json.load(open(a.counts))
+        fs, ws = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
+        rd = 2 * 1024 * sum(fs) / max(len(fs), 1)  # gfx950: 2 x FETCH_SIZE x 1 KiB
+        wr = 1024 * sum(ws) / max(len(ws), 1)
+        res = dict(c, kernel="tg_sum_kernel<32> (C3 sorted table-gradient sum, pass 1)",
+                   launches=[len(fs), len(ws)], read_bytes=rd, write_bytes_counter=wr,
+                   hbm_bytes_per_launch=rd + wr,
+                   counter_over_algorithmic=round((rd + wr) / c["algorithmic_bytes"], 3),
+                   correction="read = 2*FETCH_SIZE*1024 (gfx950), write = WRITE_SIZE*1024; "
+                              "FETCH_SIZE counts L2 misses, Infinity-Cache hits included")
+        s = json.dumps(res, indent=1)
+        if a.out:
+            open(a.out, "w").write(s + "\n")
+        print(s)
+    else:
+        print(json.dumps(counts()), flush=True)
