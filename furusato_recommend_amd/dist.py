@@ -514,8 +514,13 @@ class DenseGradDataParallel:
     BUCKET_MIN = 1 << 20  # elements: gradients this large are reduced in place
 
     def __init__(self, model, group=None, shard_optimizer: bool | None = None,
-                 table_exchange: str | None = None):
+                 table_exchange: str | None = None, microbatches: int | None = None):
         self.model = model
+        # fetch exchange: the step as this many micro-batches whose row
+        # fetches and routed gradient rows overlap the other micro-batches'
+        # compute (_pipelined_step); 1 = one tree per step
+        self.microbatches = max(1, int(os.environ.get("MIREC_DP_MICROBATCHES", "1")
+                                       if microbatches is None else microbatches))
         self.group = group
         self.distributed = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.distributed else 1
@@ -626,6 +631,23 @@ class DenseGradDataParallel:
         fused table Adam (G = W·c ⊙ table + S formed in the kernel) on the
         own rows only; with ``norms`` [2] the updated block's user / item slice
         norms are written there (the kernel's fixed-order partials)."""
+        self._owner_adam([(rid, rv, counts)], self._union_coef(self.model._tg.coef), norms)
+
+    def _union_coef(self, coef: torch.Tensor) -> torch.Tensor:
+        """The union's norm coefficient: the SUM of the ranks' (each scales
+        with its own 1/B, graphsage.py:333-336, so ranks with uneven batches —
+        a short last batch — differ); 2 floats."""
+        coef = coef.clone()
+        if self.distributed:
+            dist.all_reduce(coef, op=dist.ReduceOp.SUM, group=self.group)
+        return coef
+
+    @torch.no_grad()
+    def _owner_adam(self, blocks, coef: torch.Tensor, norms: torch.Tensor | None = None):
+        """S of the own row block from received (ids, rows, per-source
+        counts) blocks, added in list order and source-rank order within a
+        block (each source's rows distinct), then the fused table Adam with
+        the union coefficient ``coef`` on the own rows."""
         from . import _lib
         from ._lib import check, lib
         from .engine import _note_raw_write
@@ -635,19 +657,14 @@ class DenseGradDataParallel:
         n_own = N // self.world
         lo = self.rank * n_own
         s_own = torch.zeros(n_own, d, dtype=p.dtype, device=p.device)
-        off = 0
-        for c in counts:
-            if c:
-                s_own.index_add_(0, (rid[off:off + c] - lo).long(), rv[off:off + c])
-            off += c
+        for rid, rv, counts in blocks:
+            off = 0
+            for c in counts:
+                if c:
+                    s_own.index_add_(0, (rid[off:off + c] - lo).long(), rv[off:off + c])
+                off += c
         if self._ones is None or self._ones.numel() != n_own:
             self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
-        # the union's norm coefficient: the SUM of the ranks' (each scales with
-        # its own 1/B, graphsage.py:333-336, so ranks with uneven batches —
-        # a short last batch — differ); 2 floats
-        coef = tg.coef.clone()
-        if self.distributed:
-            dist.all_reduce(coef, op=dist.ReduceOp.SUM, group=self.group)
         n_user = min(max(tg.n_user - lo, 0), n_own)
         hp = st.next_hparams()
         pf = p.data.view(-1)
@@ -734,6 +751,132 @@ class DenseGradDataParallel:
         self.last_exchange_bytes += need.numel() * d * p.element_size() + \
             (sum(rc) - rc[self.rank]) * 4
 
+    # ---------------------------------------------- pipelined fetch exchange
+    # The step as C micro-batches (GraphSAGE.stageOne(chunks=C)): every
+    # micro-batch's tree is sampled first, so the ids of all C read sets are
+    # routed to their owners at once and the owners gather all requested rows
+    # from the current table up front (the table changes only in this step's
+    # Adam); micro-batch k + 1's rows then travel (async all-to-all) while
+    # micro-batch k computes, and micro-batch k's table-gradient rows leave
+    # for their owners (async) while k + 1 computes.  The owner adds the
+    # received blocks in (micro-batch, source rank) order and steps its row
+    # block once.  Rows fetched for micro-batch k are not fetched again for
+    # later ones (same table version).  Under gloo the transfers run
+    # synchronously (same arithmetic, no overlap).
+
+    def _a2a_async(self, out, inp, out_splits, in_splits):
+        if dist.get_backend(self.group) == "nccl":
+            return dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group,
+                                          async_op=True)
+        _a2a(out, inp, out_splits, in_splits, group=self.group)
+        return None
+
+    @torch.no_grad()
+    def _plan_fetch(self, trees, st):
+        m = self.model
+        if self._norms_next is not None:
+            m._norm_cache = (self._norms_next, m._norm_token())
+            self._norms_next = None
+        st["fetch"] = []
+        if not self.distributed or self.world == 1:
+            return
+        p = m._table_state.param
+        N, d = p.shape
+        n_own = N // self.world
+        lo = self.rank * n_own
+        have = torch.zeros(N, dtype=torch.bool, device=p.device)
+        a = self._event()
+        for tree in trees:
+            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, lo, lo + n_own)
+            if st["fetch"]:
+                need = need[~have[need.long()]]
+            have[need.long()] = True
+            req, rc, sc = route_ids(need, N, self.group)
+            rows = p.data.index_select(0, req.long())  # owner side: the current rows
+            st["fetch"].append({"need": need, "rows": rows, "rc": rc, "sc": sc})
+            self.last_exchange_bytes += need.numel() * d * p.element_size() + \
+                (sum(rc) - rc[self.rank]) * 4
+        self._note(a, self._event())
+        self._fetch_issue(0, st)
+
+    def _fetch_issue(self, k, st):
+        f = st["fetch"][k]
+        p = self.model._table_state.param
+        f["got"] = torch.empty(f["need"].numel(), p.shape[1], dtype=p.dtype, device=p.device)
+        f["work"] = self._a2a_async(f["got"], f["rows"], f["sc"], f["rc"])
+
+    @torch.no_grad()
+    def _fetch_wait(self, k, st):
+        if not st["fetch"]:
+            return
+        f = st["fetch"][k]
+        a = self._event()
+        if f["work"] is not None:
+            f["work"].wait()
+        self._note(a, self._event())
+        self.model._table_state.param.data.index_copy_(0, f["need"].long(), f["got"])
+        if k + 1 < len(st["fetch"]):
+            self._fetch_issue(k + 1, st)  # in flight while micro-batch k computes
+        st["fetch"][k] = None
+
+    @torch.no_grad()
+    def _route_chunk(self, k, st):
+        tg = self.model._tg
+        rows, vals = self.routed_export()
+        st["coef"] = tg.coef.clone() if st.get("coef") is None else st["coef"] + tg.coef
+        tg.pending = False
+        if not self.distributed:
+            st["route"].append((rows, vals, [rows.numel()], None, None))
+            return
+        p = self.model._table_state.param
+        N, d = p.shape
+        a = self._event()
+        rid, rc, sc = route_ids(rows, N, self.group)
+        self._note(a, self._event())
+        rv = torch.empty(rid.numel(), d, dtype=vals.dtype, device=vals.device)
+        work = self._a2a_async(rv, vals, rc, sc)  # in flight while k + 1 computes
+        st["route"].append((rid, rv, rc, work, vals))
+        self.last_exchange_bytes += (sum(rc) - rc[self.rank]) * (4 + d * p.element_size())
+
+    @torch.no_grad()
+    def _finish_routed(self, st):
+        W = self.world
+        a = self._event()
+        for *_, work, _ in st["route"]:
+            if work is not None:
+                work.wait()
+        self._note(a, self._event())
+        blocks = [(rid, rv, counts) for rid, rv, counts, _, _ in st["route"]]
+        own = torch.empty(2, device=self.model._table_state.param.device)
+        self._owner_adam(blocks, self._union_coef(st["coef"]), norms=own)
+        sq = own * own
+        allp = torch.empty(W, 2, device=own.device)
+        if self.distributed:
+            a = self._event()
+            dist.all_gather_into_tensor(allp.view(-1), sq, group=self.group)
+            self._note(a, self._event())
+        else:
+            allp.copy_(sq.view(1, 2))
+        tot = allp[0].clone()
+        for q in range(1, W):
+            tot += allp[q]
+        self._norms_next = tot.sqrt()
+        if self.distributed and W > 1:
+            self.model.table_stale = True
+
+    def _pipelined_step(self, users, pos, neg):
+        st = {"fetch": [], "route": [], "coef": None}
+
+        def chunk_hook(k, phase):
+            if phase == "pre":
+                self._fetch_wait(k, st)
+            else:
+                self._route_chunk(k, st)
+        return self.model.stageOne(users, pos, neg, grad_hook=lambda: self._allreduce(st),
+                                   loss_scale=1.0 / self.world,
+                                   tree_hook=lambda trees: self._plan_fetch(trees, st),
+                                   chunks=self.microbatches, chunk_hook=chunk_hook)
+
     @torch.no_grad()
     def sync_table(self):
         """``fetch``: all-gather the owners' row blocks, so every rank's table
@@ -764,11 +907,14 @@ class DenseGradDataParallel:
                                                 group=self.group)
                 st.stale_rows = False
 
-    def _allreduce(self):
+    def _allreduce(self, pipelined: dict | None = None):
+        if pipelined is not None:  # the micro-batches' routed rows: owner Adam
+            self._finish_routed(pipelined)
         if not self.distributed:
             return
         tg = getattr(self.model, "_tg", None)
-        if self.table_exchange != "dense" and tg is not None and tg.pending:
+        if (pipelined is None and self.table_exchange != "dense" and tg is not None
+                and tg.pending):
             self._routed_table_step()
         params = [p for p in self.model.parameters() if p.grad is not None]
         # large gradients (the id tables) are reduced in place or by row shard;
@@ -810,6 +956,8 @@ class DenseGradDataParallel:
 
     def step(self, users, pos, neg):
         self.last_exchange_bytes = 0
+        if self.table_exchange == "fetch" and self.microbatches > 1:
+            return self._pipelined_step(users, pos, neg)
         kw = {}
         if self.table_exchange == "fetch":
             kw["tree_hook"] = self.fetch_rows

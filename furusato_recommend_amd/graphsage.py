@@ -614,9 +614,11 @@ class GraphSAGE(nn.Module):
             out += [w.weight, w.bias]
         return out
 
-    def loss(self, user_emb, pos_emb, neg_emb):
+    def loss(self, user_emb, pos_emb, neg_emb, decay_scale: float = 1.0):
         """graphsage.py:326-337, including its parameter-norm accumulation
-        (all_param += all_param + |p|, i.e. doubling) over the parameters."""
+        (all_param += all_param + |p|, i.e. doubling) over the parameters.
+        ``decay_scale`` scales the norm term (1/C for each of C micro-batches
+        of one batch, so their summed gradients are the batch's)."""
         pos_scores = torch.sum(user_emb * pos_emb, dim=1)
         neg_scores = torch.sum(user_emb * neg_emb, dim=1)
         all_param = 0
@@ -629,18 +631,18 @@ class GraphSAGE(nn.Module):
             all_param = all_param + all_param + nrm
         all_param = all_param / user_emb.size(0)
         loss = torch.mean(F.softplus(neg_scores - pos_scores))
-        return loss + all_param * self.config["decay"]
+        return loss + all_param * (self.config["decay"] * decay_scale)
 
-    def loss_fused(self, emb: torch.Tensor) -> torch.Tensor:
+    def loss_fused(self, emb: torch.Tensor, decay_scale: float = 1.0) -> torch.Tensor:
         """loss() on the forward's seed embeddings emb = [u ; p ; n] [3B, d]
         in two launches (_SageLoss); the same value up to fp32 order."""
         n2 = getattr(self, "_slice_norms2", None)
         if n2 is None or not emb.is_contiguous() or emb.shape[1] % 4:
             B = emb.shape[0] // 3
-            return self.loss(emb[:B], emb[B:2 * B], emb[2 * B:])
+            return self.loss(emb[:B], emb[B:2 * B], emb[2 * B:], decay_scale)
         self._slice_norms2 = None
         small = [q for w in self.w_linears for q in (w.weight, w.bias)]
-        return _SageLoss.apply(emb, n2, float(self.config["decay"]), *small)
+        return _SageLoss.apply(emb, n2, float(self.config["decay"]) * decay_scale, *small)
 
     def embed_triples(self, users, pos, neg, seed: int):
         """One tree over the 3B seeds (users, pos+n_user, neg+n_user)."""
@@ -652,16 +654,28 @@ class GraphSAGE(nn.Module):
 
     # ------------------------------------------------------------ training
     def stageOne(self, users, pos, neg, grad_hook=None, loss_scale: float = 1.0,
-                 tree: SampleTree | None = None, tree_hook=None):
+                 tree: SampleTree | None = None, tree_hook=None, chunks: int = 1,
+                 chunk_hook=None):
         """One BPR step (graphsage.py:366-397).  ``loss_scale`` scales the
         gradient (1/world_size under data parallelism); ``grad_hook`` runs
         between backward and Adam (the gradient all-reduce); ``tree_hook(tree)``
         runs between sampling and the forward (DenseGradDataParallel's row
-        fetch)."""
+        fetch).  ``chunks`` = C > 1 (with ``chunk_hook``, the pipelined fetch
+        exchange): the batch as C micro-batches of its triples, one tree each
+        (``chunk_seeds``), all sampled first (``tree_hook`` gets the list),
+        then per micro-batch ``chunk_hook(k, "pre")``, forward, loss x 1/C
+        (the norm term x 1/C too: the C gradients sum to the batch's),
+        backward, ``chunk_hook(k, "post")`` — the hook exports each
+        micro-batch's table-gradient rows before the next overwrites them."""
         seed = self._step_seed * 7919 + self._calls
         self._calls += 1
         for p in self.parameters():
             p.grad = None
+        if chunks > 1:
+            if chunk_hook is None or tree is not None:
+                raise ValueError("micro-batched steps need a chunk_hook (DP fetch exchange)")
+            return self._stage_chunks(users, pos, neg, seed, grad_hook, loss_scale, tree_hook,
+                                      int(chunks), chunk_hook)
         if tree is None:
             u32, p32, n32 = (torch.as_tensor(t).to(device=self.device, dtype=torch.int32)
                              .contiguous() for t in (users, pos, neg))
@@ -682,6 +696,52 @@ class GraphSAGE(nn.Module):
             grad_hook()
         self.optimizer_step()
         return loss.detach()
+
+    @staticmethod
+    def chunk_bounds(B: int, C: int):
+        return [(k * B) // C for k in range(C + 1)]
+
+    @staticmethod
+    def chunk_seed(seed: int, k: int) -> int:
+        """Tree / dropout seed of micro-batch k of the step with seed ``seed``."""
+        return seed * 1009 + k + 1
+
+    def _seed_nodes(self, users, pos, neg):
+        u32, p32, n32 = (torch.as_tensor(t).to(device=self.device, dtype=torch.int32)
+                         .contiguous() for t in (users, pos, neg))
+        seeds = torch.empty(3 * u32.numel(), dtype=torch.int32, device=u32.device)
+        check(lib.mirec_pack_seed_nodes(u32.data_ptr(), p32.data_ptr(), n32.data_ptr(),
+                                        u32.numel(), self.n_user, seeds.data_ptr(),
+                                        _lib.stream_handle()), "pack_seed_nodes")
+        return seeds
+
+    def _stage_chunks(self, users, pos, neg, seed, grad_hook, loss_scale, tree_hook, C,
+                      chunk_hook):
+        users, pos, neg = (torch.as_tensor(t).to(self.device) for t in (users, pos, neg))
+        bnd = self.chunk_bounds(int(users.numel()), C)
+        trees = []
+        for k in range(C):
+            a, b = bnd[k], bnd[k + 1]
+            trees.append(self.sample_tree(self._seed_nodes(users[a:b], pos[a:b], neg[a:b]),
+                                          self.chunk_seed(seed, k)))
+        if tree_hook is not None:
+            tree_hook(trees)
+        one = self.__dict__.get("_loss_seed")
+        if one is None or one.device != self.device:
+            one = self._loss_seed = torch.ones((), dtype=torch.float32, device=self.device)
+        total = torch.zeros((), device=self.device)
+        for k, tree in enumerate(trees):
+            chunk_hook(k, "pre")
+            sk = self.chunk_seed(seed, k)
+            emb = self.forward(tree, dropout_seed=sk if self.training else None)
+            loss = self.loss_fused(emb, decay_scale=1.0 / C)
+            loss.backward(one * (loss_scale / C))
+            total += loss.detach()
+            chunk_hook(k, "post")
+        if grad_hook is not None:
+            grad_hook()
+        self.optimizer_step()
+        return total / C
 
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])

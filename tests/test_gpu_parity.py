@@ -2683,7 +2683,8 @@ def test_dense_grad_data_parallel_two_ranks(kind):
         assert np.array_equal(rs[r][3][0], res[0][3][0])
 
 
-def _dp_rank_union(rank, world, port, kind, exchange, q, over=None, bucket_min=None, steps=3):
+def _dp_rank_union(rank, world, port, kind, exchange, q, over=None, bucket_min=None, steps=3,
+                   microbatches=1):
     """One rank of DenseGradDataParallel (GraphSAGE / SASRec) on cuda:0 with
     the table exchange ``exchange``; returns what the single-process
     reference step needs (the batches, the CPU generator states SASRec's
@@ -2703,7 +2704,7 @@ def _dp_rank_union(rank, world, port, kind, exchange, q, over=None, bucket_min=N
         m, ds = _union_model(kind, **(over or {}))
         if bucket_min is not None:
             DenseGradDataParallel.BUCKET_MIN = int(bucket_min)
-        dp = DenseGradDataParallel(m, table_exchange=exchange)
+        dp = DenseGradDataParallel(m, table_exchange=exchange, microbatches=microbatches)
         assert dp.table_exchange == exchange
         if bucket_min is not None and exchange == "dense":
             assert dp.table_stepped_by_hook()  # the row-sharded table Adam
@@ -2814,6 +2815,55 @@ def test_dense_grad_data_parallel_equals_union_step(kind, exchange):
     mom = m._table_state.exp_avg.cpu()
     assert rel(torch.from_numpy(res[0][3]), mom) <= (1e-6 if exchange != "dense" else 0.0)
     assert res[0][4] > 0  # bytes received in the last step's exchange
+
+
+def _dp_rank_union_chunks(rank, world, port, q):
+    _dp_rank_union(rank, world, port, "sage", "fetch", q, microbatches=3)
+
+
+@pytest.mark.timeout(900)
+def test_pipelined_fetch_equals_union_microbatches():
+    """The pipelined fetch exchange (DenseGradDataParallel(microbatches=3):
+    every micro-batch's read set routed up front, micro-batch k + 1's rows
+    and micro-batch k's table-gradient rows in flight while the other
+    computes), 2 ranks on one GPU, against ONE process that takes, at the
+    same parameters, each rank's micro-batch gradients (loss x 1/(2 x 3), the
+    norm term x 1/3 — GraphSAGE.stageOne(chunks=3)'s seeds), sums them and
+    steps the dense Adam: every parameter at 1e-6 on every element whose
+    exact gradient is non-zero, over 3 steps (the routed sums are added in
+    another order: fp32 rounding)."""
+    res = _run_ranks(_dp_rank_union_chunks, ())
+    for a, b in zip(res[0][0], res[1][0]):
+        assert np.array_equal(a, b)
+    m, ds = _union_model("sage")
+    m._tg.dense = True
+    params = list(m.parameters())
+    C = 3
+    for i in range(3):
+        grads = []
+        for r in (0, 1):
+            u, p, n = (torch.from_numpy(x).cuda() for x in res[r][1][i])
+            for x in params:
+                x.grad = None
+            seed = m._step_seed * 7919 + i
+            bnd = m.chunk_bounds(u.numel(), C)
+            for k in range(C):
+                a, b = bnd[k], bnd[k + 1]
+                sk = m.chunk_seed(seed, k)
+                seeds = torch.cat([u[a:b].int(), p[a:b].int() + m.n_user, n[a:b].int() + m.n_user])
+                emb = m.forward(m.sample_tree(seeds, sk), dropout_seed=sk)
+                m.loss_fused(emb, decay_scale=1.0 / C).backward(
+                    torch.tensor(0.5 / C, device="cuda"))
+            grads.append([x.grad.clone() for x in params])
+        for x, g0, g1 in zip(params, *grads):
+            x.grad = g0 + g1
+        m.optimizer_step()
+    torch.cuda.synchronize()
+    for (nm, _), x, got in zip(m.named_parameters(), params, res[0][0]):
+        ref, got = x.detach().cpu(), torch.from_numpy(got)
+        assert float((got - ref).abs().max()) <= 3 * 1e-3 + 1e-7, nm
+        assert rel(got, ref) < 1e-5, (nm, rel(got, ref))
+    assert res[0][4] > 0
 
 
 def _dp_trainer_rank(rank, world, port, kind, ckpt, q):

@@ -57,6 +57,9 @@ def main():
                     help="sage: table exchanges to simulate")
     ap.add_argument("--rates", default="100,200,300,400",
                     help="sage: link rates (GB/s of received bytes per rank) to project at")
+    ap.add_argument("--microbatches", default="1",
+                    help="sage fetch: comma list of micro-batch counts C (the pipelined "
+                         "exchange; C = 1 is the unpipelined step)")
     args = ap.parse_args()
     if args.model == "sage":
         return sage_main(args)
@@ -154,6 +157,9 @@ def sage_main(args):
         for ex in args.exchanges.split(","):
             if N % W:
                 continue
+            if ex == "fetch" and W > 1:
+                for C in [int(c) for c in args.microbatches.split(",") if int(c) > 1]:
+                    sage_pipelined(args, m, W, C, base, rates)
             dp = DenseGradDataParallel(m, table_exchange=ex)  # world 1: no collectives
             dp.world, dp.rank = W, 0  # rank 0 of a world of W (local work only)
             m._tg.dense = ex == "dense"
@@ -251,6 +257,138 @@ def sage_main(args):
                               "projected": proj if W > 1 else None}), flush=True)
             if W == 1:
                 break  # one single-GPU baseline (both exchanges are the plain step)
+
+
+def sage_pipelined(args, m, W, C, base, rates):
+    """Rank 0 of a world of W under the pipelined fetch exchange with C
+    micro-batches (dist.DenseGradDataParallel._pipelined_step), simulated on
+    one GPU: its local work is run and timed — the read sets of all
+    micro-batches (distinct rows outside block 0, deduplicated across
+    micro-batches), the owner-side gathers of the requested rows, the
+    installs of the fetched rows, each micro-batch's forward / backward and
+    table-gradient export, the owner Adam over its block with the other
+    ranks' routed rows (produced up front by their own backward passes) —
+    and the transfers are projected from the bytes each phase moves: the
+    first micro-batch's rows are exposed, micro-batch k + 1's rows and
+    micro-batch k - 1's routed rows overlap micro-batch k's compute (HIP
+    events around it), the last micro-batch's routed rows are exposed."""
+    from furusato_recommend_amd.dist import DenseGradDataParallel, distinct_rows
+    dev = torch.device("cuda:0")
+    B = args.batch
+    N, d = m._table.shape
+    n_own = N // W
+    row_b = 4 + 4 * d
+    dp = DenseGradDataParallel(m, table_exchange="fetch")
+    dp.world, dp.rank = W, 0
+    m._tg.dense = False
+    m._tg_routed = True
+    others = []
+    for r in range(1, W):
+        u, p, n = m.sample(B, seed=11, offset=10**8 + r * B, shard=r, n_shards=W)
+
+        def capture():
+            rows, vals = dp.routed_export()
+            k = int((rows < n_own).sum())
+            others.append((rows[:k].clone(), vals[:k].clone()))
+            for q in m.parameters():
+                q.grad = None
+            m._tg.pending = False
+        m.stageOne(u, p, n, grad_hook=capture, loss_scale=1.0 / W)
+    route_other = sum(o[0].numel() for o in others) * row_b
+    rec = {}
+
+    def tree_hook(trees):
+        have = torch.zeros(N, dtype=torch.bool, device=dev)
+        rec["need"], rec["fetch_rows"] = [], []
+        for tree in trees:
+            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own)
+            if rec["need"]:
+                need = need[~have[need.long()]]
+            have[need.long()] = True
+            # the owners' gather of the requested rows (rank 0 serves a share of
+            # the same size) and the install after the transfer
+            rec["need"].append((need.long(), m._table.data.index_select(0, need.long())))
+            rec["fetch_rows"].append(need.numel())
+        rec["ev"] = []
+
+    def chunk_hook(k, phase):
+        if phase == "pre":
+            need, rows = rec["need"][k]
+            m._table.data.index_copy_(0, need, rows)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            rec["ev"].append([e])
+        else:
+            rows, vals = dp.routed_export()
+            rec.setdefault("own", []).append((rows[rows < n_own].clone(),
+                                              vals[: int((rows < n_own).sum())].clone()))
+            rec["coef"] = m._tg.coef.clone() + (rec["coef"] if "coef" in rec else 0.0)
+            m._tg.pending = False
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            rec["ev"][k].append(e)
+
+    def grad_hook():
+        blocks = []
+        for rows, vals in rec.pop("own"):
+            blocks.append((rows, vals, [rows.numel()]))
+        blocks.append((torch.cat([o[0] for o in others]), torch.cat([o[1] for o in others]),
+                       [o[0].numel() for o in others]))
+        dp._owner_adam(blocks, rec.pop("coef"), norms=torch.empty(2, device=dev))
+        small = [q.grad for q in m.parameters() if q.grad is not None]
+        if small:
+            flat = torch.cat([g.reshape(-1) for g in small])
+            off = 0
+            for g in small:
+                g.copy_(flat[off: off + g.numel()].view_as(g))
+                off += g.numel()
+
+    step_no = [0]
+
+    def step():
+        u, p, n = m.sample(B, seed=7, offset=step_no[0] * B, shard=0, n_shards=W)
+        step_no[0] += 1
+        m.stageOne(u, p, n, grad_hook=grad_hook, loss_scale=1.0 / W, tree_hook=tree_hook,
+                   chunks=C, chunk_hook=chunk_hook)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    chunk_ms = [0.0] * C
+    fetch_rows = [0] * C
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        torch.cuda.synchronize()
+        for k in range(C):
+            chunk_ms[k] += rec["ev"][k][0].elapsed_time(rec["ev"][k][1]) / args.steps
+            fetch_rows[k] += rec["fetch_rows"][k] / args.steps
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    small_b = sum(q.numel() for q in m.parameters() if q is not m._table) * 4
+    fetch_b = [f * row_b for f in fetch_rows]
+    route_b = route_other / C  # the other ranks' routed rows, per micro-batch
+    recv = sum(fetch_b) + route_other + 2 * (W - 1) * small_b // W
+    proj = {}
+    for r in rates:
+        rate = r * 1e6  # bytes per ms
+        exposed = fetch_b[0] / rate + route_b / rate + 2 * (W - 1) * small_b / W / rate
+        for k in range(C):
+            hidden = ((fetch_b[k + 1] if k + 1 < C else 0.0) + (route_b if k > 0 else 0.0)) / rate
+            exposed += max(0.0, hidden - chunk_ms[k])
+        proj[f"{int(r)}GBps"] = {"ms": round(ms + exposed, 3), "exposed_comm_ms": round(exposed, 3),
+                                  "efficiency": round(base / (ms + exposed), 3) if base else None}
+    print(json.dumps({"model": "sage C3", "world": W, "table_exchange": "fetch",
+                      "microbatches": C, "pipelined": True,
+                      "ms_per_step_rank_compute": round(ms, 4),
+                      "chunk_compute_ms": [round(x, 4) for x in chunk_ms],
+                      "fetched_rows_per_chunk": [int(x) for x in fetch_rows],
+                      "routed_rows_from_others": int(route_other // row_b),
+                      "recv_bytes_per_rank": int(recv),
+                      "projection": "compute (measured, no transfers) + the first "
+                                    "micro-batch's rows + the last's routed rows + the "
+                                    "small bucket + whatever of micro-batch k+1's rows and "
+                                    "k-1's routed rows exceeds micro-batch k's compute",
+                      "projected": proj}), flush=True)
 
 
 if __name__ == "__main__":
