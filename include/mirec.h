@@ -738,6 +738,17 @@ int mirec_zero_tail_rows(float *buf, const int32_t *offsets, int64_t B, int64_t 
 /* f32 MFMA GEMMs of the Linear layers on token rows (model/sasrec.py:385-421,
  * model/graphsage.py:311-324).  Row-major, device pointers, 16-byte aligned.
  *
+ * Arithmetic (default build, MIREC_GEMM_X6): every f32 operand is split
+ * exactly into three bf16 terms and each product is formed from the six
+ * largest term products on bf16 MFMA with f32 accumulation — the error of
+ * one f32 rounding per product.  Edge semantics differ from
+ * an fp32 FMA chain: an infinite or NaN operand gives NaN (inf - inf in the
+ * split), so an overflowed input yields NaN where fp32 would give +-inf; and
+ * operands below ~2^-110 lose low-order bits (the third term underflows
+ * bf16's range) — far below anything a finite, non-overflowing training step
+ * feeds these GEMMs.  Building with -DMIREC_GEMM_X6=0 selects exact f32
+ * v_mfma_f32_32x32x2_f32 products.
+ *
  * C[n, No] = A[n, Kr] · B[No, Kr]ᵀ (+ bias[No] if bias != NULL): the forward
  * y = x Wᵀ + b, and the input gradient dX = dY W with B = Wᵀ (a [K, N] copy
  * of the weight).  Kr % 32 == 0, No % 128 == 0. */

@@ -18,7 +18,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c3 -o run --output-form
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c4 -o run --output-format csv -- python3 tools/bench_sasrec.py --steps 10 --warmup 3 --cpu-baseline 0 > $E/c4.log 2>&1 || { echo "c4 trace rc=$?"; exit 1; }
 
 # skewed C2 graph (Zipf item popularity): bench line and kernel stats
-timeout -k 10 300 python bench.py --kind zipf --steps 20 --warmup 3 --cpu-baseline off --quality-steps 0 > $E/bench_c2_zipf.log 2>&1 || { echo "zipf rc=$?"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 > $E/zipf.log 2>&1 || { echo "zipf trace rc=$?"; exit 1; }
+timeout -k 10 300 python bench.py --kind zipf --steps 20 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0 > $E/bench_c2_zipf.log 2>&1 || { echo "zipf rc=$?"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0 > $E/zipf.log 2>&1 || { echo "zipf trace rc=$?"; exit 1; }
 echo "zipf ok"
 echo "evidence ok"

@@ -8,7 +8,7 @@ set -u
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 export TMPDIR=/tmp
-BARGS=${BENCH_ARGS:-"--steps 10 --warmup 3 --cpu-baseline off --quality-steps 0"}
+BARGS=${BENCH_ARGS:-"--steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0"}
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 bench.py $BARGS > $OUT/trace.log 2>&1 || { echo "trace pass rc=$?"; exit 1; }
 echo "trace ok"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex prop_kernel -d $OUT/fetch -o run --output-format csv -- python3 bench.py $BARGS > $OUT/fetch.log 2>&1 || { echo "fetch pass rc=$?"; exit 1; }

@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out/r4b
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "evaluate or score_topk or mf_c1 or topk or trajectory or distinct_rows or union_step or routed" > gpurun_out/r4b/pytest_eval.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "evaluate or score_topk or mf_c1 or topk or trajectory or distinct_rows or union_step or routed or repeatable or pipelined" > gpurun_out/r4b/pytest_eval.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/r4b/pytest_eval.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for v in libmirec var_topk_f32; do
