@@ -604,14 +604,30 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
 #pragma unroll
   for (int q = 0; q < RPG; ++q) {
 #if MIREC_RNBWD_MASKED
+    // (diagnostic builds, tools/build_r4_variants.sh: 1 = every row load
+    // exec-masked, 2 = the same + s_waitcnt 0 after the loads, 3 = only the
+    // statistics masked, 4 = only the out / g_out rows masked)
     const int64_t r = m0 + g + 8 * q;
+    const int64_t rc = min(r, n - 1);
     ov[q] = gv[q] = f4_zero();
     mv[q] = sv[q] = 0.f;
+    if (MIREC_RNBWD_MASKED == 3) {
+      ov[q] = ld4(a.out + rc * kTile + c);
+      gv[q] = a.g_out ? ld4(a.g_out + rc * kTile + c) : f4_zero();
+    }
+    if (MIREC_RNBWD_MASKED == 4) {
+      mv[q] = a.mean[rc];
+      sv[q] = a.rstd[rc];
+    }
     if (r < n) {
-      ov[q] = ld4(a.out + r * kTile + c);
-      gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
-      mv[q] = a.mean[r];
-      sv[q] = a.rstd[r];
+      if (MIREC_RNBWD_MASKED != 3) {
+        ov[q] = ld4(a.out + r * kTile + c);
+        gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
+      }
+      if (MIREC_RNBWD_MASKED != 4) {
+        mv[q] = a.mean[r];
+        sv[q] = a.rstd[r];
+      }
     }
 #else
     const int64_t r = min(m0 + g + 8 * q, n - 1);
@@ -621,6 +637,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
     sv[q] = a.rstd[r];
 #endif
   }
+#if MIREC_RNBWD_MASKED == 2
+  __builtin_amdgcn_s_waitcnt(0);  // every counter drained before the k loop
+#endif
   const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
   f32x16 acc[TM][2];
   nt_mainloop<BM, 1, true>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);

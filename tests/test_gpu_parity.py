@@ -2069,13 +2069,26 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
     assert rel(users, user_ref) < TOL
     assert abs(loss - loss_ref) <= TOL * abs(loss_ref)
     assert set(got) == set(names)
+    errs, bad = {}, []
     for n_ in names:
         a, b = got[n_].double().cpu(), g_ref[n_]
         if n_ == "item_last_proj.bias":
             scale = float(g_ref["item_last_proj.weight"].abs().max())
-            assert float((a - b).abs().max()) <= TOL * scale, n_
-            continue
-        assert rel(a, b) < TOL, (n_, rel(a, b))
+            errs[n_] = float((a - b).abs().max()) / scale
+        else:
+            errs[n_] = rel(a, b)
+        if errs[n_] >= TOL:
+            bad.append(n_)
+    diag = None
+    if "item_id_embedding.weight" in bad:  # where the table's rows differ
+        a, b = got["item_id_embedding.weight"].double().cpu(), g_ref["item_id_embedding.weight"]
+        e = (a - b).abs().max(1).values
+        top = torch.topk(e, 5).indices.tolist()
+        seq_ids = m.seq.items[u].cpu()
+        seq_ids = seq_ids[torch.arange(seq_ids.shape[1])[None, :] < m.seq.length[u].cpu()[:, None]]
+        diag = [(r, float(e[r]), float(b[r].abs().max()), int((seq_ids == r).sum()),
+                 int((pos.cpu() == r).sum()), int((neg.cpu() == r).sum())) for r in top]
+    assert not bad, (bad, errs, diag)
 
 
 @pytest.mark.parametrize("n,kr,no", [(1, 32, 128), (100, 128, 128), (4096, 128, 384),
@@ -2899,11 +2912,12 @@ def _dp_trainer_rank(rank, world, port, kind, ckpt, q):
         m2 = make(7)
         tr2 = DPTrainer(cfg, ds, m2)
         loaded = tr2.load_checkpoint()
+        resumed_at = tr2.epoch
         same = all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(m.parameters(), m2.parameters()))
         same_opt = all(torch.equal(a.exp_avg.cpu(), b.exp_avg.cpu())
                        for a, b in zip(optimizer_states(m), optimizer_states(m2)))
         h2 = tr2.fit(1)
-        q.put((rank, params, hist, (loaded, tr2.epoch, same, same_opt), h2))
+        q.put((rank, params, hist, (loaded, resumed_at, same, same_opt), h2))
     finally:
         dist.destroy_process_group()
 
@@ -3382,3 +3396,26 @@ def test_distinct_rows_matches_unique(n_rows, n, lo, hi):
     u = torch.unique(ids[ids >= 0].long())
     ref = u[(u < lo) | (u >= hi)].int()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n,k,no", [(56_321, 384, 128), (56_321, 128, 128), (56_321, 128, 384)])
+def test_plain_gemms_bitwise_repeatable(n, k, no):
+    """gemm_nt / gemm_nn / gemm_tn on the split-bf16 loop at a ragged row
+    count: 16 launches each give bit-identical results (their A loads are
+    exec-masked by row, the form under which the fused row-tail kernel once
+    returned wrong rows), and every launch agrees with float64 at 1e-6."""
+    from furusato_recommend_amd.linear import gemm_nn, gemm_nt, gemm_tn
+    torch.manual_seed(n + k + no)
+    a = torch.randn(n, k, device="cuda")
+    w_nt = torch.randn(no, k, device="cuda") * k ** -0.5
+    w_nn = torch.randn(k, no, device="cuda") * k ** -0.5
+    b = torch.randn(n, no, device="cuda")
+    refs = {"nt": a.double() @ w_nt.double().t(), "nn": a.double() @ w_nn.double(),
+            "tn": a.double().t() @ b.double()}
+    runs = {"nt": lambda: gemm_nt(a, w_nt), "nn": lambda: gemm_nn(a, w_nn),
+            "tn": lambda: gemm_tn(a, b, False)[0]}
+    for name, fn in runs.items():
+        first = fn().clone()
+        assert rel(first, refs[name]) < 1e-6, name
+        for _ in range(15):
+            assert torch.equal(fn(), first), name

@@ -2,6 +2,9 @@
 # Round-4 A/B libraries (furusato_recommend_amd/var_*.so, selected with
 # MIREC_LIB): every object of the current tree except the one varied.
 #   var_cur_masked     gemm.hip with exec-masked row-tail loads (MIREC_RNBWD_MASKED=1)
+#   var_cur_masked_wz  the same built with -amdgpu-waitcnt-forcezero
+#   var_cur_masked_w0  masked + s_waitcnt 0 after the row loads (=2)
+#   var_cur_masked_stats / _rows  only the statistics / only the rows masked (=3 / =4)
 #   var_old_masked     gemm.hip of commit cee0a0b (round 3, wave-side split loop)
 #                      with its original exec-masked loads — the failing form
 #   var_old_masked_wz  the same built with -amdgpu-waitcnt-forcezero
@@ -33,6 +36,10 @@ assert s.count(old) == 1
 open(sys.argv[2], "w").write(s.replace(old, new))
 EOF
 $H -DMIREC_RNBWD_MASKED=1 -c furusato_recommend_amd/csrc/gemm.hip -o build/var/cur_masked.o &
+$H -DMIREC_RNBWD_MASKED=1 -mllvm -amdgpu-waitcnt-forcezero -c furusato_recommend_amd/csrc/gemm.hip -o build/var/cur_masked_wz.o &
+$H -DMIREC_RNBWD_MASKED=2 -c furusato_recommend_amd/csrc/gemm.hip -o build/var/cur_masked_w0.o &
+$H -DMIREC_RNBWD_MASKED=3 -c furusato_recommend_amd/csrc/gemm.hip -o build/var/cur_masked_stats.o &
+$H -DMIREC_RNBWD_MASKED=4 -c furusato_recommend_amd/csrc/gemm.hip -o build/var/cur_masked_rows.o &
 $H -c $T/gemm_masked.hip -o build/var/old_masked.o &
 $H -mllvm -amdgpu-waitcnt-forcezero -c $T/gemm_masked.hip -o build/var/old_masked_wz.o &
 $H -c $T/gemm.hip -o build/var/old_clamped.o &
@@ -43,6 +50,10 @@ link() {  # name, replaced object, variant object
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 $objs $3 -lpthread -o furusato_recommend_amd/$1.so
 }
 link var_cur_masked gemm build/var/cur_masked.o
+link var_cur_masked_wz gemm build/var/cur_masked_wz.o
+link var_cur_masked_w0 gemm build/var/cur_masked_w0.o
+link var_cur_masked_stats gemm build/var/cur_masked_stats.o
+link var_cur_masked_rows gemm build/var/cur_masked_rows.o
 link var_old_masked gemm build/var/old_masked.o
 link var_old_masked_wz gemm build/var/old_masked_wz.o
 link var_old_clamped gemm build/var/old_clamped.o
