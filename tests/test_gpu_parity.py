@@ -1979,19 +1979,20 @@ def test_sasrec_graph_step_equals_eager():
     assert np.mean(losses[-5:]) < np.mean(losses[:5])
 
 
-def _sasrec_oracle_step(m, u, pos, neg, heads):
-    """The reference's SASRec step (model/sasrec.py:385-435, 437-469) in
-    float64 on the host (oracle.sasrec_forward_user) from m's parameters:
-    (pooled user rows [B, d], loss, {parameter name: gradient})."""
+def _sasrec_oracle_step(m, u, pos, neg, heads, dtype=torch.float64):
+    """The reference's SASRec step (model/sasrec.py:385-435, 437-469) on the
+    host (oracle.sasrec_forward_user) from m's parameters, in float64 (the
+    exact step) or float32 (the reference's own arithmetic): (pooled user
+    rows [B, d], loss, {parameter name: gradient})."""
     from oracle import lightgcn_oracle as O
     F = torch.nn.functional
-    P = {n: p.detach().double().cpu().requires_grad_(True) for n, p in m.named_parameters()}
+    P = {n: p.detach().to(dtype).cpu().requires_grad_(True) for n, p in m.named_parameters()}
     W = P["item_id_embedding.weight"]
     L = m.num_layers
     items = m.seq.items[u].long().cpu()
     length = m.seq.length[u].cpu()
     T = int(length.max())
-    mask = (torch.arange(T)[None, :] < length[:, None]).double()
+    mask = (torch.arange(T)[None, :] < length[:, None]).to(dtype)
     x = W[items[:, :T].clamp(min=0)] * mask[..., None]  # pad_sequence(padding_value=0)
     p = {}
     for i in range(L):
@@ -2017,7 +2018,7 @@ def _sasrec_oracle_step(m, u, pos, neg, heads):
     loss = torch.mean(F.softplus((user * ne).sum(1) - (user * pe).sum(1))) \
         + all_param / user.shape[0] * m.config["decay"]
     loss.backward()
-    return user.detach(), float(loss), {n_: v.grad for n_, v in P.items()}
+    return user.detach().double(), float(loss), {n_: v.grad.double() for n_, v in P.items()}
 
 
 @pytest.mark.timeout(600)
@@ -2030,7 +2031,14 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
     every pooled user row (the longest, the length-5 ones and every pack
     boundary among them), the loss, and the gradient of every parameter
     (the item table's formed from its sorted form, as the fused Adam forms
-    it) at 1e-4 relative.  The item tower's last bias has an exactly zero
+    it).  Rows and loss at 1e-4 relative.  Each gradient at 1e-4 relative,
+    or — where the reference's own float32 arithmetic (the same step on the
+    host in float32) is itself farther than that from the exact step — within
+    4x of that float32 error: the blocks' ReLU((x + attn)) puts ~10^7
+    elements through a kink, and the ones within rounding of zero flip their
+    mask between any two float32 orders, so a gradient that sums them (the
+    block weights', the sequence items' table rows) is only as determined as
+    float32 makes it.  The item tower's last bias has an exactly zero
     gradient (it adds <u, b> to both scores); its rounding noise is bounded
     against its weight's gradient instead."""
     from furusato_recommend_amd import SASRec
@@ -2052,6 +2060,7 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
     pn = m.sample_pairs(u, seed=3)
     pos, neg = pn[0], pn[1]
     user_ref, loss_ref, g_ref = _sasrec_oracle_step(m, u, pos, neg, heads=2)
+    _, _, g32 = _sasrec_oracle_step(m, u, pos, neg, heads=2, dtype=torch.float32)
     names = [n for n, _ in m.named_parameters()]
     got = {}
 
@@ -2071,14 +2080,16 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
     assert set(got) == set(names)
     errs, bad = {}, []
     for n_ in names:
-        a, b = got[n_].double().cpu(), g_ref[n_]
+        b = g_ref[n_]
         if n_ == "item_last_proj.bias":
             scale = float(g_ref["item_last_proj.weight"].abs().max())
-            errs[n_] = float((a - b).abs().max()) / scale
+            err = lambda a: float((a - b).abs().max()) / scale  # noqa: E731
         else:
-            errs[n_] = rel(a, b)
-        if errs[n_] >= TOL:
+            err = lambda a: rel(a, b)  # noqa: E731
+        errs[n_] = (err(got[n_].double().cpu()), err(g32[n_]))
+        if errs[n_][0] >= max(TOL, 4 * errs[n_][1]):
             bad.append(n_)
+    print("gradient rel err (hip, host fp32) vs float64:", errs)
     diag = None
     if "item_id_embedding.weight" in bad:  # where the table's rows differ
         a, b = got["item_id_embedding.weight"].double().cpu(), g_ref["item_id_embedding.weight"]
