@@ -140,12 +140,16 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   // decode entry beg + sub: row id, grad row address, hash base of its
   // dropout quads (key + first quad), threshold, weight (x dropout scale)
   const int64_t pe = beg + sub;
-  const int32_t km = (sub < kCh && pe < end) ? keys[pe] : kEnd;
+  const bool in_chunk = sub < kCh && pe < end;
+  const int32_t km = in_chunk ? keys[pe] : kEnd;
+  // the entry's index loads beside its key (not behind it): one round trip
+  // less before the row gathers
+  const int32_t vm = in_chunk ? vals[pe] : 0;
   uint64_t am = 0, hm = 0;
   uint32_t thm = 0;
   float wm = 0.f;
   if (km < n_rows) {
-    const int32_t v = vals[pe];
+    const int32_t v = vm;
     const int g = group_of(ga.ent_off, ga.n_groups, v);
     const int32_t e = v - (int32_t)pick(ga.ent_off, g);
     const int32_t t = e / pick(ga.k, g);

@@ -217,7 +217,7 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
   }
 }
 
-// Score tiles on the bf16 MFMA pipe (MIREC_TOPK_X6, default on, D <= 128):
+// Score tiles on the bf16 MFMA pipe (MIREC_TOPK_X6, default off, D <= 128):
 // the exact three-term split of gemm.hip (f32-class error per product; the
 // top-k is checked against float64 scores by the near-tie criterion of
 // test_evaluate_matches_oracle).  The user rows are split once into
@@ -227,9 +227,14 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
 // (plane_pos, as gemm.hip's [row][k] planes; row stride 2 D + 16 B: the 16
 // lanes of a read phase hit distinct 4-bank groups).  Per 32 x 32 tile and
 // 16 dims: 6 v_mfma_f32_32x32x16_bf16 (192 cycles) instead of 8
-// v_mfma_f32_32x32x2_f32 (512).
+// v_mfma_f32_32x32x2_f32 (512).  Measured at C2 (profiles/round4_eval_c2.jsonl):
+// both forms pass the float64 near-tie check on all 10 K users, but the split
+// form is slower (6.73 vs 5.69 ms per batch): its planes take 62.7 KB of LDS
+// per workgroup (two per CU, against three at 51 KB), and the tile loop is
+// bound by the candidate insertion / compaction and barriers around the
+// products, not by the MFMA issue it saves.
 #ifndef MIREC_TOPK_X6
-#define MIREC_TOPK_X6 1
+#define MIREC_TOPK_X6 0
 #endif
 
 __device__ __forceinline__ int st_plane_pos(int c4) {

@@ -1,9 +1,17 @@
 // Minimal probe for the fused dX + LayerNorm-backward finding (DESIGN.md
 // §9.1): a packed-f32 VALU op that reads the HIGH dword of a 64-bit VGPR
-// pair through op_sel (v_pk_add_f32 ... op_sel:[0,1]), the pair built by
-// v_mov_b64 before a bf16 MFMA loop and read right after it — the shape the
-// compiler gave the failing kernel.  Every lane checks that it got its own
-// high dword.  Not part of libmirec: built and run by tools/op_sel_repro.py.
+// pair through op_sel (v_pk_add_f32 ... op_sel:[0,1]), the pair built before
+// a bf16 MFMA loop and read after it — the shape the compiler gave the
+// failing kernel.  Every lane checks that it got its own high dword.  Not
+// part of libmirec: built and run by tools/op_sel_repro.py.
+//
+// Knobs: iters (MFMAs before the read), use_opsel (0: the same value built
+// without op_sel), mfma_odd_only (only odd workgroups run the MFMA loop —
+// waves of other workgroups share the SIMDs: does another wave's MFMA
+// matter?), nop_rounds
+// (s_nop 7 x rounds between the loop and the read), pair64 (the pair built
+// by v_mov_b64 or by two v_mov_b32).  bad[128]: wrong lanes by (workgroup
+// parity, lane); out keeps every lane's two results for the host to classify.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -14,11 +22,21 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 extern "C" __global__ __launch_bounds__(256) void op_sel_probe(const float *__restrict__ in,
                                                                float *__restrict__ out,
                                                                int32_t *__restrict__ bad,
-                                                               int iters, int use_opsel) {
+                                                               int iters, int use_opsel,
+                                                               int mfma_odd_only, int nop_rounds,
+                                                               int pair64) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int par = blockIdx.x & 1;
   const f32x2 src = {in[2 * t], in[2 * t + 1]};
   f32x2 pair;
-  asm volatile("v_mov_b64 %0, %1" : "=v"(pair) : "v"(src));
+  if (pair64) {
+    asm volatile("v_mov_b64 %0, %1" : "=v"(pair) : "v"(src));
+  } else {
+    float lo, hi;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(lo) : "v"(src.x));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(hi) : "v"(src.y));
+    pair = f32x2{lo, hi};
+  }
   // MFMA work between the pair's definition and its use (operands from the
   // thread index so the loop is not folded)
   f32x16 acc;
@@ -30,7 +48,9 @@ extern "C" __global__ __launch_bounds__(256) void op_sel_probe(const float *__re
     a[e] = (__bf16)(float)((t + e) & 7);
     b[e] = (__bf16)(float)((t * 3 + e) & 5);
   }
-  for (int i = 0; i < iters; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  const int my_iters = (mfma_odd_only && par == 0) ? 0 : iters;
+  for (int i = 0; i < my_iters; ++i) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  for (int i = 0; i < nop_rounds; ++i) asm volatile("s_nop 7");
   const f32x2 zero = {0.f, 0.f};
   f32x2 r;
   if (use_opsel) {
@@ -47,11 +67,12 @@ extern "C" __global__ __launch_bounds__(256) void op_sel_probe(const float *__re
   out[3 * t] = r.x;
   out[3 * t + 1] = r.y;
   out[3 * t + 2] = s;
-  if (r.x != src.y || r.y != src.y) atomicAdd(bad + (threadIdx.x & 63), 1);
+  if (r.x != src.y || r.y != src.y) atomicAdd(bad + 64 * par + (threadIdx.x & 63), 1);
 }
 
 extern "C" int op_sel_probe_launch(const float *in, float *out, int32_t *bad, int blocks, int iters,
-                                   int use_opsel) {
-  hipLaunchKernelGGL(op_sel_probe, dim3(blocks), dim3(256), 0, 0, in, out, bad, iters, use_opsel);
+                                   int use_opsel, int mfma_odd_only, int nop_rounds, int pair64) {
+  hipLaunchKernelGGL(op_sel_probe, dim3(blocks), dim3(256), 0, 0, in, out, bad, iters, use_opsel,
+                     mfma_odd_only, nop_rounds, pair64);
   return (int)hipGetLastError();
 }

@@ -24,6 +24,16 @@ for v in libmirec var_topk_f32; do
 done
 exit 0
 fi
+REPS=30 timeout -k 10 300 python -u tools/op_sel_repro.py > gpurun_out/r4b/opsel2.jsonl 2> gpurun_out/r4b/opsel2.log
+rc=$?; echo "opsel2 rc=$rc"; cat gpurun_out/r4b/opsel2.jsonl
+if [ $rc -ne 0 ]; then exit $rc; fi
+for v in libmirec var_tg_head var_tg_ch4; do
+  MIREC_LIB=$PWD/furusato_recommend_amd/$v.so timeout -k 10 200 python -u tools/tg_bench.py >> gpurun_out/r4b/tg_bench.jsonl 2> gpurun_out/r4b/tg_bench_$v.log
+  rc=$?; echo "tg_bench $v rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
+done
+cat gpurun_out/r4b/tg_bench.jsonl
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/r4b/tgprof -o run -- python3 tools/tg_bench.py --reps 20 > gpurun_out/r4b/tgprof.log 2>&1
+rc=$?; echo "tg prof rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 200 python -u tools/tg_sum_bytes.py > gpurun_out/r4b/tg_counts.json 2> gpurun_out/r4b/tg_counts.log
 rc=$?; echo "tg counts rc=$rc"; cat gpurun_out/r4b/tg_counts.json
 if [ $rc -ne 0 ]; then exit $rc; fi
