@@ -113,3 +113,17 @@ def test_csr_from_coo_and_long_rows():
         assert np.all(sr[lsp[k]:lsp[k + 1]] == r)
         assert segs[0] == rowptr[r] and np.all(np.diff(segs) == split)
         assert segs[-1] < rowptr[r + 1] <= segs[-1] + split
+
+
+def test_no_mfma_kernel_reads_high_dword_through_op_sel():
+    """The gfx950 code of every kernel that issues MFMAs is free of packed-f32
+    ops whose op_sel makes the low lane read a pair's high dword — the
+    instruction shape behind the fused dX + LayerNorm-backward kernel's wrong
+    upper-lane rows (tools/op_sel_repro.hip reproduces it).
+    Disassembles the built library with the ROCm llvm tools, no GPU."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import isa_scan
+    ks = isa_scan.kernels(LIB)
+    assert sum(1 for v in ks.values() if v["mfma"]) >= 20  # the scan sees the MFMA kernels
+    assert isa_scan.hazards(LIB) == []

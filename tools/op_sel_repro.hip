@@ -6,11 +6,12 @@
 // part of libmirec: built and run by tools/op_sel_repro.py.
 //
 // Knobs: iters (MFMAs before the read), use_opsel (0: the same value built
-// without op_sel), mfma_odd_only (only odd workgroups run the MFMA loop —
-// waves of other workgroups share the SIMDs: does another wave's MFMA
-// matter?), nop_rounds
+// without op_sel), mfma_odd_only (only the waves in an odd hardware wave
+// slot of their SIMD run the MFMA loop — HW_ID.WAVE_ID, read with s_getreg —
+// so waves that issue no MFMA share every SIMD with waves that do: does
+// another wave's MFMA matter?), nop_rounds
 // (s_nop 7 x rounds between the loop and the read), pair64 (the pair built
-// by v_mov_b64 or by two v_mov_b32).  bad[128]: wrong lanes by (workgroup
+// by v_mov_b64 or by two v_mov_b32).  bad[128]: wrong lanes by (wave slot
 // parity, lane); out keeps every lane's two results for the host to classify.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,7 +27,8 @@ extern "C" __global__ __launch_bounds__(256) void op_sel_probe(const float *__re
                                                                int mfma_odd_only, int nop_rounds,
                                                                int pair64) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  const int par = blockIdx.x & 1;
+  // HW_REG_HW_ID (hwreg 4) bits [3:0]: the wave's slot on its SIMD
+  const int par = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 4) & 1;
   const f32x2 src = {in[2 * t], in[2 * t + 1]};
   f32x2 pair;
   if (pair64) {
