@@ -1004,8 +1004,11 @@ static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
 
 // Column sums out[c] = Σ_r A[r, c] of a row-major [n, m] matrix in a fixed
 // order (the bias gradient db = Σ_rows dY of Linear layers whose widths the
-// GEMM tiles do not take; torch's reduction kernel gave replay-dependent
-// bias gradients inside the captured SASRec step).  Pass 1: workgroup
+// GEMM tiles do not take).  Slices of a fixed 64 rows while n <= 64 x 2048 /
+// ceil(m / 256): zero rows appended to A (the captured SASRec step's token
+// capacity padding) leave every partial and the result bitwise unchanged,
+// which torch's sum(0) — its reduction tree follows the row count — does not
+// (DESIGN.md §9.2).  Pass 1: workgroup
 // (slice s, column block) — one lane per column walks the slice's rows in
 // order with four row-interleaved partial sums added as ((p0 + p1) + (p2 +
 // p3)); pass 2: one lane per column adds the slices' partials in slice order.

@@ -685,8 +685,10 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
                        n_rows, part, bsum, acc, stamp, gen);                                 \
     MIREC_LAUNCH_CHECK();                                                                    \
     break;
-  switch (lpr) {
+  switch (lpr) {  // lpr >= kCh (lanes_per_row)
+#if MIREC_TG_CHUNK <= 8
     MIREC_TG_LAUNCH(8)
+#endif
     MIREC_TG_LAUNCH(16)
     MIREC_TG_LAUNCH(32)
     MIREC_TG_LAUNCH(64)

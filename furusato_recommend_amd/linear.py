@@ -83,14 +83,17 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, colsum: bool):
 
 
 # MIREC_TORCH_COLSUM=1: torch's sum(0) instead (the round-3 form of the
-# captured data-parallel step, for the investigation in DESIGN.md §9.2)
+# captured data-parallel step, kept to reproduce DESIGN.md §9.2)
 _TORCH_COLSUM = os.environ.get("MIREC_TORCH_COLSUM", "0") == "1"
 
 
 def col_sums(a: torch.Tensor) -> torch.Tensor:
     """Σ over the rows of a contiguous [n, m] float32 tensor, in a fixed order
-    (mirec_col_sums: deterministic and capturable — torch's reduction kernel
-    gave replay-dependent bias gradients inside the captured SASRec step).
+    (mirec_col_sums: deterministic, capturable, and — up to n = 64 x 2048 /
+    ceil(m / 256) rows — bitwise the same with zero rows appended, so the
+    captured SASRec step, which sums over its token capacity, gives the eager
+    step's bias gradients; torch's sum(0) picks its reduction tree from the
+    row count: DESIGN.md §9.2).
     Tensors off the HIP device or not float32 (the module used as a plain
     nn.Linear, e.g. float64 on the host) take torch's sum."""
     if not (a.is_cuda and a.dtype == torch.float32) or _TORCH_COLSUM:

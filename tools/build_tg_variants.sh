@@ -3,7 +3,7 @@
 # var_tg_*.so, selected with MIREC_LIB; timed by tools/tg_bench.py): every
 # object of the current tree except tablegrad.o.
 #   var_tg_head   tablegrad.hip as of the last commit
-#   var_tg_ch4    the current source with 4 entries per chunk
+#   var_tg_ch4 / var_tg_ch16   the current source with 4 / 16 entries per chunk
 set -e
 cd $(dirname $0)/..
 make -s -C furusato_recommend_amd/csrc
@@ -14,6 +14,7 @@ git show HEAD:furusato_recommend_amd/csrc/tablegrad.hip > $T/tablegrad_head.hip
 cp furusato_recommend_amd/csrc/common.h $T/
 $H -c $T/tablegrad_head.hip -o $T/head.o &
 $H -DMIREC_TG_CHUNK=4 -c furusato_recommend_amd/csrc/tablegrad.hip -o $T/ch4.o &
+$H -DMIREC_TG_CHUNK=16 -c furusato_recommend_amd/csrc/tablegrad.hip -o $T/ch16.o &
 wait
 link() {  # name, variant object
   objs=$(ls build/obj/*.o | grep -v "/tablegrad.o\$")
@@ -21,4 +22,5 @@ link() {  # name, variant object
 }
 link var_tg_head $T/head.o
 link var_tg_ch4 $T/ch4.o
+link var_tg_ch16 $T/ch16.o
 ls -la furusato_recommend_amd/var_tg_*.so
