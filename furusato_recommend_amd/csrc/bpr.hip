@@ -23,7 +23,7 @@ namespace mirec {
 constexpr int kWaves = 4;
 
 template <int D>
-__global__ __launch_bounds__(256) void bpr_forward_kernel(
+__global__ __launch_bounds__(256) MIREC_NO_PK_F32 void bpr_forward_kernel(
     const float *__restrict__ out, const float *__restrict__ emb, int64_t n_users,
     int64_t batch, const int32_t *__restrict__ users, const int32_t *__restrict__ pos,
     const int32_t *__restrict__ neg, float grad_scale, float *coef, float *softplus, float *reg,

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void zero_tail_rows_kernel(float *__restrict__
 // the B terms in a fixed order (deterministic).
 __device__ __forceinline__ float softplus20(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 
-__global__ __launch_bounds__(256) void bpr_rows_kernel(const float *__restrict__ u,
+__global__ __launch_bounds__(256) MIREC_NO_PK_F32 void bpr_rows_kernel(const float *__restrict__ u,
                                                        const float *__restrict__ p,
                                                        const float *__restrict__ n, int64_t B,
                                                        int32_t d, float *__restrict__ x_out,

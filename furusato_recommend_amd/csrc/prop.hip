@@ -429,7 +429,7 @@ void prop_kernel(PropK a) {
 // 50 loads deep per group instead of a serial walk of 800 dependent loads
 // (258 -> ~15 us per launch on the C2 Zipf graph).
 template <int D>
-__global__ __launch_bounds__(256) void prop_finalize(PropK a, const int32_t *long_rows,
+__global__ __launch_bounds__(256) MIREC_NO_PK_F32 void prop_finalize(PropK a, const int32_t *long_rows,
                                                      const int64_t *long_segptr, int64_t n_long) {
   constexpr int LPR = D / 4;
   constexpr int NG = 256 / LPR;
