@@ -17,14 +17,15 @@
 //       float atomics, bitwise repeatable.  The sums are STORED (not added)
 //       into acc[r] and stamp[r] = gen marks the row as touched this step,
 //       so neither buffer is ever cleared.  Pass 1: a group of LPR lanes
-//       owns a chunk of 64 sorted entries and sums every run segment in it,
-//       kBatch rows in flight; runs wholly inside the chunk are final, a
-//       segment continuing into / from a neighbouring chunk goes to that
-//       chunk's partial slot.  Pass 2: the chunk holding a crossing run's
-//       head adds the partials of the chunks the run covers, in chunk order,
-//       with every aligned block of 256 chunks inside the run pre-summed by
-//       its own group (pass 2a): a hub id in 1.5 M entries is ~730 block
-//       sums on the head's path, read LPR at a time, not 187 K partial rows.
+//       takes a chunk of kCh sorted entries, kCh rows in flight, and owns
+//       the runs that start in it; a run that leaves the chunk but ends
+//       within the next kCh entries (short: nearly every run) is summed whole
+//       by its owner, one more batch.  Only a long run (a hub id) is cut at
+//       chunk boundaries into partial slots.  Pass 2: the chunk holding a
+//       long run's head adds the partials of the chunks the run covers, in
+//       chunk order, with every aligned block of 256 chunks inside the run
+//       pre-summed by its own group (pass 2a): a hub id in 1.5 M entries is
+//       ~730 block sums on the head's path, read LPR at a time.
 //   mirec_adam_table   Adam over the whole table with G formed on the fly
 //       (W, m, v read once, written once; S read for stamped rows only) —
 //       the dense gradient is never written.  Optionally the sums of squares
@@ -111,14 +112,69 @@ __global__ __launch_bounds__(256) void tg_prep_kernel(GroupArgs ga, int64_t n_en
   }
 }
 
+// Entry v of the sorted order (its index in the groups' concatenation):
+// gradient row address, hash base of its dropout quads (key + first quad),
+// threshold, weight (x dropout scale).
+__device__ __forceinline__ void tg_decode(const GroupArgs &ga, const float *__restrict__ wt,
+                                          int32_t v, int32_t d, uint64_t &am, uint64_t &hm,
+                                          uint32_t &thm, float &wm) {
+  const int g = group_of(ga.ent_off, ga.n_groups, v);
+  const int32_t e = v - (int32_t)pick(ga.ent_off, g);
+  const int32_t t = e / pick(ga.k, g);
+  thm = pick(ga.thresh, g);
+  const float w = wt[pick(ga.tgt_off, g) + t];
+  wm = thm ? w * pick(ga.scale, g) : w;
+  am = (uint64_t)(pick(ga.grad, g) + (int64_t)t * d);
+  hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
+}
+
+// The kCh rows of one batch of entries (lane u of the group decoded entry u)
+// in flight at once, then weighted and masked (their inputs re-broadcast, so
+// only the rows stay live during the loads).  Only entries lo <= u < hi load
+// (the others were not decoded: their addresses are null).
+template <int LPR>
+__device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int hi, uint64_t am,
+                                        uint64_t hm, uint32_t thm, float wm,
+                                        float4 (&x)[kCh]) {
+  const uint32_t am_lo = (uint32_t)am, am_hi = (uint32_t)(am >> 32);
+  const uint32_t hm_lo = (uint32_t)hm, hm_hi = (uint32_t)(hm >> 32);
+#pragma unroll
+  for (int u = 0; u < kCh; ++u) {
+    const int src = base + u;
+    const uint64_t a = (uint64_t)(uint32_t)__shfl((int)am_lo, src) |
+                       ((uint64_t)(uint32_t)__shfl((int)am_hi, src) << 32);
+    x[u] = (act && u >= lo && u < hi) ? ld4(reinterpret_cast<const float *>(a) + col) : f4_zero();
+  }
+#pragma unroll
+  for (int u = 0; u < kCh; ++u) {
+    const int src = base + u;
+    const uint32_t th = (uint32_t)__shfl((int)thm, src);
+    const float w = __shfl(wm, src);
+    if (th != 0u) {
+      const uint64_t hq = ((uint64_t)(uint32_t)__shfl((int)hm_lo, src) |
+                           ((uint64_t)(uint32_t)__shfl((int)hm_hi, src) << 32)) +
+                          (uint64_t)(col >> 2);
+      x[u] = drop4_hq(x[u], hq, th, w);
+    } else {
+      x[u] = f4_scale(w, x[u]);
+    }
+  }
+}
+
 // Pass 1.  A group of LPR lanes (LPR >= kCh; d <= 4 LPR, or LPR = 64 with a
-// column loop) owns a chunk of kCh sorted entries.  Lane j < kCh loads and
-// decodes entry j (row id, grad row, weight, dropout element); the group then
-// fetches all kCh rows at once (ids broadcast by shuffle), weights and masks
-// them while they are in flight, and adds them in entry order.  Short chunks
-// keep many rows in flight chip-wide (the gathers are latency-bound: most
-// rows come from the L2 / Infinity Cache); runs that cross chunks go through
-// the partial slots and pass 2.
+// column loop) takes chunk c = sorted entries [c kCh, (c + 1) kCh) and owns
+// the RUNS (entries of one row id) that start in it.  Lane j < kCh loads and
+// decodes entry j; the group fetches all kCh rows at once (ids broadcast by
+// shuffle), weights and masks them while they are in flight, and adds them
+// in entry order.  A run that leaves the chunk is SHORT when it ends within
+// the next kCh entries (strictly before the next chunk's end, or the array
+// ends inside that window): the owner then sums it whole — one more batch
+// of at most kCh rows — and the next chunk skips those entries (the same
+// test from its side: the run entering it started in the previous chunk and
+// ends inside it).  Only LONG runs (hub rows) go through the partial slots
+// and pass 2: their head chunk's segment to slot 1, every later chunk's
+// first segment to slot 0.  Short runs — nearly all of them — are summed in
+// one place without partial rows.
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
                                                      const int32_t *__restrict__ vals,
@@ -135,94 +191,92 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   const int64_t beg = chunk * kCh;
   if (beg >= n) return;  // the whole group leaves together
   const int64_t end = beg + kCh < n ? beg + kCh : n;
+  const int64_t xend = end + kCh < n ? end + kCh : n;  // the window after the chunk
+  const int nin = (int)(end - beg);
   const int32_t kprev = beg > 0 ? keys[beg - 1] : -1;
-  const int32_t knext = end < n ? keys[end] : -1;
-  // decode entry beg + sub: row id, grad row address, hash base of its
-  // dropout quads (key + first quad), threshold, weight (x dropout scale)
-  const int64_t pe = beg + sub;
+  const int32_t kpp = beg > kCh ? keys[beg - kCh - 1] : -1;
+  const int64_t pe = beg + sub, px = end + sub;
   const bool in_chunk = sub < kCh && pe < end;
+  const bool in_win = sub < kCh && px < xend;
   const int32_t km = in_chunk ? keys[pe] : kEnd;
+  const int32_t kx = in_win ? keys[px] : kEnd;
   // the entry's index loads beside its key (not behind it): one round trip
   // less before the row gathers
   const int32_t vm = in_chunk ? vals[pe] : 0;
-  uint64_t am = 0, hm = 0;
-  uint32_t thm = 0;
-  float wm = 0.f;
-  if (km < n_rows) {
-    const int32_t v = vm;
-    const int g = group_of(ga.ent_off, ga.n_groups, v);
-    const int32_t e = v - (int32_t)pick(ga.ent_off, g);
-    const int32_t t = e / pick(ga.k, g);
-    thm = pick(ga.thresh, g);
-    const float w = wt[pick(ga.tgt_off, g) + t];
-    wm = thm ? w * pick(ga.scale, g) : w;
-    am = (uint64_t)(pick(ga.grad, g) + (int64_t)t * d);
-    hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
-  }
   const int32_t first = __shfl(km, base);
   if (first >= n_rows) return;  // only invalid entries from here on
-  const uint32_t am_lo = (uint32_t)am, am_hi = (uint32_t)(am >> 32);
-  const uint32_t hm_lo = (uint32_t)hm, hm_hi = (uint32_t)(hm >> 32);
+  const unsigned long long kmask = (1ull << kCh) - 1ull;
+  // the run entering the chunk: short (owned by the previous chunk's group)
+  // iff it started there and ends inside this chunk
+  const bool cont_in = beg > 0 && first == kprev;
+  const unsigned long long diff_in = (__ballot(in_chunk && km != kprev) >> base) & kmask;
+  const bool in_short =
+      cont_in && (beg <= kCh || kpp != kprev) && (diff_in != 0 || end < beg + kCh);
+  const int skip = in_short ? (diff_in != 0 ? (int)__builtin_ctzll(diff_in) : nin) : 0;
+  if (skip >= nin) return;
+  // the run leaving the chunk: short iff it started here and ends inside
+  // the window after the chunk
+  const int32_t klast = __shfl(km, base + nin - 1);
+  const int32_t knext = end < n ? __shfl(kx, base) : -1;
+  const bool cont_out = end < n && klast == knext && klast < n_rows;
+  const bool last_from_before = cont_in && klast == kprev;  // the run covers the chunk
+  const unsigned long long diff_out = (__ballot(in_win && kx != klast) >> base) & kmask;
+  const bool out_short = cont_out && !last_from_before && (diff_out != 0 || xend < end + kCh);
+  const int n_ext =
+      out_short ? (diff_out != 0 ? (int)__builtin_ctzll(diff_out) : (int)(xend - end)) : 0;
+  uint64_t am = 0, hm = 0, am2 = 0, hm2 = 0;
+  uint32_t thm = 0, thm2 = 0;
+  float wm = 0.f, wm2 = 0.f;
+  if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, wt, vm, d, am, hm, thm, wm);
+  if (sub < n_ext) tg_decode(ga, wt, vals[px], d, am2, hm2, thm2, wm2);
+  // valid entries of the chunk: up to the first invalid id (they sort last)
+  const unsigned long long bad = (__ballot(in_chunk && km >= n_rows) >> base) & kmask;
+  const int nval = bad != 0 ? (int)__builtin_ctzll(bad) : nin;
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
-    // all kCh rows in flight; weight and mask are applied after the loads
-    // (their inputs re-broadcast) so only the rows stay live meanwhile
     float4 x[kCh];
-    int32_t kk[kCh];
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      const int src = base + u;
-      kk[u] = __shfl(km, src);
-      const uint64_t a = (uint64_t)(uint32_t)__shfl((int)am_lo, src) |
-                         ((uint64_t)(uint32_t)__shfl((int)am_hi, src) << 32);
-      x[u] = (act && kk[u] < n_rows) ? ld4(reinterpret_cast<const float *>(a) + col)
-                                     : f4_zero();
-    }
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      const int src = base + u;
-      const uint32_t th = (uint32_t)__shfl((int)thm, src);
-      const float w = __shfl(wm, src);
-      if (th != 0u) {
-        const uint64_t hq = ((uint64_t)(uint32_t)__shfl((int)hm_lo, src) |
-                             ((uint64_t)(uint32_t)__shfl((int)hm_hi, src) << 32)) +
-                            (uint64_t)(col >> 2);
-        x[u] = drop4_hq(x[u], hq, th, w);
-      } else {
-        x[u] = f4_scale(w, x[u]);
-      }
-    }
-    int32_t cur = first;
-    int64_t seg_beg = beg;
+    tg_rows<LPR>(base, col, act, skip, nval, am, hm, thm, wm, x);
+    int32_t cur = -1;
+    int64_t seg_beg = 0;
     float4 acc = f4_zero();
-    bool done = false;
+    // segment [seg_beg, pos) of id cur ends: a final row sum, or (long runs
+    // only) a partial slot
+    auto close = [&](int64_t pos) {
+      const bool cont_prev = seg_beg == beg && cont_in && !in_short;
+      const bool cont_next = pos == end && cont_out && !out_short;
+      float *dst;
+      if (!cont_prev && !cont_next) {
+        dst = acc_out + (int64_t)cur * d;
+        if (sub == 0 && c0 == 0) stamp[cur] = gen;
+      } else {
+        dst = part + (2 * chunk + (cont_prev ? 0 : 1)) * (int64_t)d;
+      }
+      if (act) st4(dst + col, acc);
+    };
 #pragma unroll
-    for (int u = 0; u <= kCh; ++u) {
-      const int64_t pos = beg + u;
-      const int32_t ku = u < kCh ? kk[u] : kEnd;
-      if (!done && (pos >= end || ku != cur)) {
-        // segment [seg_beg, pos) of id cur ends
-        const bool cont_prev = seg_beg == beg && kprev == cur;
-        const bool cont_next = pos == end && knext == cur;
-        float *dst;
-        if (!cont_prev && !cont_next) {
-          dst = acc_out + (int64_t)cur * d;
-          if (sub == 0 && c0 == 0) stamp[cur] = gen;
-        } else {
-          dst = part + (2 * chunk + (cont_prev ? 0 : 1)) * (int64_t)d;
-        }
-        if (act) st4(dst + col, acc);
-        if (pos >= end || ku >= n_rows) {
-          done = true;
-        } else {
+    for (int u = 0; u < kCh; ++u) {
+      const int32_t ku = __shfl(km, base + u);
+      if (u >= skip && u < nval) {
+        if (cur < 0) {
           cur = ku;
-          seg_beg = pos;
+          seg_beg = beg + u;
+        } else if (ku != cur) {
+          close(beg + u);
+          cur = ku;
+          seg_beg = beg + u;
           acc = f4_zero();
         }
+        acc = f4_add(acc, x[u]);
       }
-      if (!done && u < kCh) acc = f4_add(acc, x[u]);
     }
+    if (n_ext > 0) {  // the rest of the last run (id klast == cur), in order
+      tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x);
+#pragma unroll
+      for (int u = 0; u < kCh; ++u)
+        if (u < n_ext) acc = f4_add(acc, x[u]);
+    }
+    if (cur >= 0) close(beg + nval);
   }
 }
 
@@ -269,7 +323,7 @@ __global__ __launch_bounds__(256) void tg_block_kernel(const int32_t *__restrict
   }
 }
 
-// Pass 2b: the group of the chunk holding a crossing run's head adds, in
+// Pass 2b: the group of the chunk holding a LONG run's head adds, in
 // chunk order, its tail slot and the head slots of the chunks the run
 // covers — a whole aligned block of G chunks inside the run as its block sum
 // — and stores the sum.  Lanes test LPR chunks (or blocks) per round.
@@ -294,6 +348,11 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
   const int32_t kp = beg > 0 ? keys[beg - 1] : -1;
   if (klast >= n_rows || kn != klast) return;  // last segment stays inside
   if (kp == klast) return;                      // the run's head is earlier
+  // a short run (it ends within the next kCh entries) was summed whole by
+  // its owner in pass 1: only long runs are left here
+  const int64_t xend = end + kCh < n ? end + kCh : n;
+  const bool differs = sub < kCh && end + sub < xend && keys[end + sub] != klast;
+  if (((__ballot(differs) >> base) & ((1ull << kCh) - 1ull)) != 0 || xend < end + kCh) return;
   const unsigned long long gmask = low_bits<LPR>() << base;
   const unsigned long long low = low_bits<LPR>();
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {

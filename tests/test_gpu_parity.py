@@ -3113,6 +3113,48 @@ def test_table_grad_hub_not_serial():
 
 
 @pytest.mark.parametrize("d", [16, 128, 256])
+def test_table_grad_runs_of_every_length_and_alignment(d):
+    """Pass 1 owns the runs that start in its chunk and sums a run that
+    leaves the chunk whole when it ends within the next chunk's span, else
+    (long runs) through the partial slots and pass 2: runs of every length
+    1..40 (then 100, 300, 1000) laid end to end, so every run length meets
+    every alignment to the chunk grid (8 entries), invalid entries mixed in
+    — each row against float64, only touched rows stamped, bitwise equal on
+    a rerun.  Inner (k = 1) rows and a dropout-mean leaf group (k = 10)."""
+    from furusato_recommend_amd.graphsage import TableGrad
+    n_rows = 6000
+    g = torch.Generator().manual_seed(d)
+    lens = torch.randint(1, 41, (1500,), generator=g)
+    lens = torch.cat([lens, torch.tensor([100, 300, 1000, 17, 9, 8, 7, 16, 15])])
+    ids = torch.repeat_interleave(torch.randperm(n_rows, generator=g)[:lens.numel()], lens)
+    ids = ids[torch.randperm(ids.numel(), generator=g)]  # the sort restores the runs
+    ids[::53] = -1
+    n_inner = (ids.numel() // 3) // 10 * 10
+    inner, leaf = ids[:n_inner], ids[n_inner:]
+    leaf = leaf[: leaf.numel() // 10 * 10]
+    groups = []
+    for q, k, mean, p, sd in ((inner, 1, 0, 0.0, 0), (leaf, 10, 1, 0.2, 21)):
+        gr = torch.randn(q.numel() // k, d, generator=g)
+        groups.append((q.int().cuda(), gr.cuda(), k, mean, p, sd))
+    tg = TableGrad(n_rows, 2000, d, "cuda")
+    tg.accumulate(groups)
+    a1, st = tg.acc.clone(), tg.stamp.clone()
+    tg.accumulate(groups)
+    assert torch.equal(tg.acc[st == 1], a1[st == 1])
+    ref = _tg_reference(groups, n_rows, d)
+    touched = torch.zeros(n_rows, dtype=torch.bool)
+    for q, *_ in groups:
+        qc = q.cpu().long()
+        touched[qc[qc >= 0]] = True
+    assert torch.equal(st.cpu() == 1, touched)
+    got = a1.cpu().double()
+    assert rel(got[touched], ref[touched]) < 1e-5
+    # per row (a lost or doubled contribution is an O(1) error on its row)
+    err = (got - ref).abs().max(1).values / ref.abs().max(1).values.clamp(min=1e-30)
+    assert float(err[touched].max()) < 1e-3
+
+
+@pytest.mark.parametrize("d", [16, 128, 256])
 @pytest.mark.parametrize("hub", [0, 200_000])
 def test_table_grad_sorted_matches_fp64_and_repeats(d, hub):
     """mirec_table_grad_sorted: per-row sums of inner rows and dropout-mean
