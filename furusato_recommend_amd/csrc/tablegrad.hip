@@ -537,6 +537,27 @@ __global__ __launch_bounds__(1024) void tg_norm_final_kernel(const float *__rest
 }
 
 // ------------------------------------------------------------ host side
+// The stable (key, value) radix sort of the entries.  MIREC_TG_SORT_BITS > 0
+// sorts that many bits per onesweep pass (rocprim's own choice for int pairs
+// on gfx950 is 8: three passes over the 21-bit row ids of C3; 11 covers them
+// in two); 0 keeps hipcub's default.
+#ifndef MIREC_TG_SORT_BITS
+#define MIREC_TG_SORT_BITS 0
+#endif
+static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *ko, const int32_t *vi,
+                          int32_t *vo, int n, int end_bit, hipStream_t st) {
+#if MIREC_TG_SORT_BITS > 0
+  using Onesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>,
+                                                       rocprim::kernel_config<1024, 8>,
+                                                       MIREC_TG_SORT_BITS,
+                                                       rocprim::block_radix_rank_algorithm::match>;
+  using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Onesweep>;
+  return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, ki, ko, vi, vo, (size_t)n, 0, end_bit, st);
+#else
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, n, 0, end_bit, st);
+#endif
+}
+
 static int lanes_per_row(int32_t d) {
   const int d4 = (d + 3) / 4;
   int l = kCh;  // pass 1: one entry per lane of a group
@@ -579,9 +600,8 @@ static int tg_layout(const mirec_row_grad_group_t *groups, int32_t n_groups, int
   while (bits < 31 && ((int64_t)1 << bits) <= n_rows) ++bits;
   L->end_bit = bits;
   size_t tb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (int32_t *)nullptr, (int32_t *)nullptr,
-                                           (int32_t *)nullptr, (int32_t *)nullptr,
-                                           (int)std::max<int64_t>(n_ent, 1), 0, bits);
+  (void)tg_sort(nullptr, tb, nullptr, nullptr, nullptr, nullptr, (int)std::max<int64_t>(n_ent, 1),
+                bits, nullptr);
   L->sort_bytes = tb;
   L->total = L->sort + up(tb);
   return MIREC_OK;
@@ -724,8 +744,9 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
                      L.n_ent, L.n_tgt, n_rows, keys_in, vals_in, wt);
   MIREC_LAUNCH_CHECK();
-  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws + L.sort, L.sort_bytes, keys_in, keys_out,
-                                               vals_in, vals_out, (int)L.n_ent, 0, L.end_bit, st));
+  size_t sort_bytes = L.sort_bytes;
+  MIREC_HIP(tg_sort(ws + L.sort, sort_bytes, keys_in, keys_out, vals_in, vals_out, (int)L.n_ent,
+                    L.end_bit, st));
   const int lpr = lanes_per_row(dim);
   const int64_t threads = L.n_chunks * lpr;
   const int64_t n_blocks = L.n_chunks / kBlockChunks;

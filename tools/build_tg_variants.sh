@@ -4,6 +4,7 @@
 # object of the current tree except tablegrad.o.
 #   var_tg_head   tablegrad.hip as of the last commit
 #   var_tg_ch4 / var_tg_ch16   the current source with 4 / 16 entries per chunk
+#   var_tg_sort11 the current source sorting 11 bits per onesweep pass (two passes at C3)
 set -e
 cd $(dirname $0)/..
 make -s -C furusato_recommend_amd/csrc
@@ -15,6 +16,7 @@ cp furusato_recommend_amd/csrc/common.h $T/
 $H -c $T/tablegrad_head.hip -o $T/head.o &
 $H -DMIREC_TG_CHUNK=4 -c furusato_recommend_amd/csrc/tablegrad.hip -o $T/ch4.o &
 $H -DMIREC_TG_CHUNK=16 -c furusato_recommend_amd/csrc/tablegrad.hip -o $T/ch16.o &
+$H -DMIREC_TG_SORT_BITS=11 -c furusato_recommend_amd/csrc/tablegrad.hip -o $T/sort11.o &
 wait
 link() {  # name, variant object
   objs=$(ls build/obj/*.o | grep -v "/tablegrad.o\$")
@@ -23,4 +25,5 @@ link() {  # name, variant object
 link var_tg_head $T/head.o
 link var_tg_ch4 $T/ch4.o
 link var_tg_ch16 $T/ch16.o
+link var_tg_sort11 $T/sort11.o
 ls -la furusato_recommend_amd/var_tg_*.so

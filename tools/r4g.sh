@@ -12,7 +12,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout
 rc=$?; echo "pytest tg rc=$rc"; grep -E "passed|failed|Error" $E/pytest_tg.log | tail -5
 if [ $rc -ne 0 ]; then exit $rc; fi
 grep "torch sum" $E/pytest_tg.log | head -4
-for v in libmirec var_tg_head var_tg_ch16 libmirec var_tg_head; do
+for v in libmirec var_tg_head var_tg_ch16 var_tg_sort11 libmirec var_tg_head var_tg_sort11; do
   MIREC_LIB=$PWD/furusato_recommend_amd/$v.so timeout -k 10 200 python -u tools/tg_bench.py >> $E/tg_bench.jsonl 2> $E/tg_bench_$v.log
   rc=$?; echo "tg_bench $v rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 done
