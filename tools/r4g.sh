@@ -21,6 +21,14 @@ timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $E/tgp
 rc=$?; echo "tg prof rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 find $E -type f ! -name "*.jsonl" ! -name "*.log" ! -name "*kernel_stats.csv" -delete
 find $E -name "*kernel_stats.csv" | while read f; do grep -E "tg_|onesweep" "$f" | cut -d, -f1-4 | sed 's/rocprim.*onesweep/onesweep/' | cut -c1-150; done
+# attention backward with phase A's P / dS kept in LDS (MIREC_ATTN_PDS=1)
+MIREC_LIB=$PWD/furusato_recommend_amd/var_attn_pds.so timeout -k 10 300 python -u -m pytest tests -m gpu -v -x --timeout 250 --timeout-method thread -k "attention or attn" > $E/pytest_attn_pds.log 2>&1
+rc=$?; echo "pytest attn pds rc=$rc"; grep -E "passed|failed" $E/pytest_attn_pds.log | tail -2
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for v in libmirec var_attn_pds; do
+  MIREC_LIB=$PWD/furusato_recommend_amd/$v.so timeout -k 10 200 python -u tools/attn_bench.py --mixes c4 --batches 2048 --reps 20 > $E/attn_$v.jsonl 2> $E/attn_$v.log
+  rc=$?; echo "attn bench $v rc=$rc"; grep -i "bwd\|packed" $E/attn_$v.jsonl | cut -c1-250; if [ $rc -ne 0 ]; then exit $rc; fi
+done
 REPS=30 timeout -k 10 300 python -u tools/op_sel_repro.py > $E/opsel.jsonl 2> $E/opsel.log
 rc=$?; echo "opsel rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 600 python bench.py > $E/bench_c2.log 2>&1
