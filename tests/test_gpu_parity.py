@@ -2849,7 +2849,13 @@ def test_dense_grad_data_parallel_equals_union_step(kind, exchange):
         # query) and the item tower's last bias (it adds <u, b> to the
         # positive and the negative score alike: the BPR difference cancels
         # it).  They are bounded by the step size; every other element is
-        # compared at 1e-6.
+        # compared at 1e-6 — 1e-5 for GraphSAGE, whose rank-split table
+        # gradient is summed in another association (each rank's row sums,
+        # then the owner's sum over ranks) than the union's one sequential
+        # sum per row, and whose last-layer bias gradient (a sum over the
+        # 3B seed rows with the pos / neg terms largely cancelling) carries
+        # that difference through three Adam steps.
+        tol = 1e-5 if kind == "sage" else 1e-6
         ok = torch.ones_like(got, dtype=torch.bool)
         if nm.endswith("in_proj_bias"):
             ok[got.numel() // 3: 2 * got.numel() // 3] = False
@@ -2857,7 +2863,7 @@ def test_dense_grad_data_parallel_equals_union_step(kind, exchange):
             ok[:] = False
         assert float((got - ref).abs().max()) <= 3 * 1e-3 + 1e-7, (nm, diffs)
         if bool(ok.any()):
-            assert rel(got[ok], ref[ok]) < 1e-6, (nm, diffs)
+            assert rel(got[ok], ref[ok]) < tol, (nm, diffs)
     mom = m._table_state.exp_avg.cpu()
     assert rel(torch.from_numpy(res[0][3]), mom) <= (1e-6 if exchange != "dense" else 0.0)
     assert res[0][4] > 0  # bytes received in the last step's exchange
