@@ -235,8 +235,11 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
-    float4 x[kCh];
+    // the chunk's rows and the owned run's rows past the chunk, all in
+    // flight together (one round trip, not two)
+    float4 x[kCh], x2[kCh];
     tg_rows<LPR>(base, col, act, skip, nval, am, hm, thm, wm, x);
+    tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x2);
     int32_t cur = -1;
     int64_t seg_beg = 0;
     float4 acc = f4_zero();
@@ -270,12 +273,10 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
         acc = f4_add(acc, x[u]);
       }
     }
-    if (n_ext > 0) {  // the rest of the last run (id klast == cur), in order
-      tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x);
+    // the rest of the last run (id klast == cur), in order
 #pragma unroll
-      for (int u = 0; u < kCh; ++u)
-        if (u < n_ext) acc = f4_add(acc, x[u]);
-    }
+    for (int u = 0; u < kCh; ++u)
+      if (u < n_ext) acc = f4_add(acc, x2[u]);
     if (cur >= 0) close(beg + nval);
   }
 }
@@ -540,9 +541,10 @@ __global__ __launch_bounds__(1024) void tg_norm_final_kernel(const float *__rest
 // The stable (key, value) radix sort of the entries.  MIREC_TG_SORT_BITS > 0
 // sorts that many bits per onesweep pass (rocprim's own choice for int pairs
 // on gfx950 is 8: three passes over the 21-bit row ids of C3; 11 covers them
-// in two); 0 keeps hipcub's default.
+// in two: the C3 accumulate 0.389 -> 0.367 ms, same order, bitwise equal
+// sums — profiles/round4_tg_bench.jsonl); 0 keeps hipcub's default.
 #ifndef MIREC_TG_SORT_BITS
-#define MIREC_TG_SORT_BITS 0
+#define MIREC_TG_SORT_BITS 11
 #endif
 static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *ko, const int32_t *vi,
                           int32_t *vo, int n, int end_bit, hipStream_t st) {
