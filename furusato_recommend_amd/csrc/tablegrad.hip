@@ -203,6 +203,7 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   // the entry's index loads beside its key (not behind it): one round trip
   // less before the row gathers
   const int32_t vm = in_chunk ? vals[pe] : 0;
+  const int32_t vx = in_win ? vals[px] : 0;  // the window's indices too (same round trip)
   const int32_t first = __shfl(km, base);
   if (first >= n_rows) return;  // only invalid entries from here on
   const unsigned long long kmask = (1ull << kCh) - 1ull;
@@ -228,7 +229,7 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   uint32_t thm = 0, thm2 = 0;
   float wm = 0.f, wm2 = 0.f;
   if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, wt, vm, d, am, hm, thm, wm);
-  if (sub < n_ext) tg_decode(ga, wt, vals[px], d, am2, hm2, thm2, wm2);
+  if (sub < n_ext) tg_decode(ga, wt, vx, d, am2, hm2, thm2, wm2);
   // valid entries of the chunk: up to the first invalid id (they sort last)
   const unsigned long long bad = (__ballot(in_chunk && km >= n_rows) >> base) & kmask;
   const int nval = bad != 0 ? (int)__builtin_ctzll(bad) : nin;
