@@ -236,11 +236,11 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
-    // the chunk's rows and the owned run's rows past the chunk, all in
-    // flight together (one round trip, not two)
-    float4 x[kCh], x2[kCh];
+    // (the owned run's rows past the chunk follow in a second batch: loading
+    // both at once measured slower — 127 VGPRs, four waves per SIMD instead
+    // of five: pass 1 263 vs 226 us at C3, profiles/round4_tg_bench.jsonl)
+    float4 x[kCh];
     tg_rows<LPR>(base, col, act, skip, nval, am, hm, thm, wm, x);
-    tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x2);
     int32_t cur = -1;
     int64_t seg_beg = 0;
     float4 acc = f4_zero();
@@ -274,10 +274,12 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
         acc = f4_add(acc, x[u]);
       }
     }
-    // the rest of the last run (id klast == cur), in order
+    if (n_ext > 0) {  // the rest of the last run (id klast == cur), in order
+      tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x);
 #pragma unroll
-    for (int u = 0; u < kCh; ++u)
-      if (u < n_ext) acc = f4_add(acc, x2[u]);
+      for (int u = 0; u < kCh; ++u)
+        if (u < n_ext) acc = f4_add(acc, x[u]);
+    }
     if (cur >= 0) close(beg + nval);
   }
 }

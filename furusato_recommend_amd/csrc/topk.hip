@@ -543,16 +543,62 @@ __global__ __launch_bounds__(64) void topk_merge_kernel(const float *__restrict_
   }
 }
 
-// chunk of items per stage-1 workgroup: enough workgroups for the chip
-// (>= 1024), at least 32 tiles each
-static void st_chunks(int64_t n_eval, int64_t m_items, int64_t *chunk, int64_t *n_chunks) {
+// Workgroups of score_topk_kernel<D> resident on the chip at once (CUs x
+// the occupancy its LDS / registers allow: 3 per CU at D <= 64, 2 at 128, 1
+// at 256), from the runtime, once per D.
+static int64_t st_slots(int D);
+
+// Items per stage-1 workgroup.  The grid is (user groups) x (item chunks) and
+// every workgroup of a chunk takes the same time, so the launch lasts
+// ceil(workgroups / slots) rounds of one chunk: pick the chunk count that
+// minimises rounds x (tiles per chunk + a chunk's fixed cost, ~24 tiles of
+// final sorts and partial writes), at least 32 tiles per chunk, fewest
+// chunks on a tie (less stage-2 merging).  (C2, 10 K users x 100 K items at
+// D = 64: 157 user groups, 768 slots -> 9 chunks in 2 full rounds instead of
+// the 7 = 1.43 rounds of a fixed >= 1024-workgroup rule.)
+static void st_chunks(int64_t n_eval, int64_t m_items, int D, int64_t *chunk, int64_t *n_chunks) {
   const int64_t ut = (n_eval + kStUsers - 1) / kStUsers;
-  int64_t want = std::max<int64_t>(1, (1024 + ut - 1) / ut);
-  int64_t c = (m_items + want - 1) / want;
-  c = std::max<int64_t>(c, 32 * kStTile);
-  c = (c + kStTile - 1) / kStTile * kStTile;
+  const int64_t slots = std::max<int64_t>(1, st_slots(D));
+  const int64_t tiles_all = (m_items + kStTile - 1) / kStTile;
+  const int64_t max_n = std::max<int64_t>(1, tiles_all / 32);
+  int64_t best_n = 1, best_cost = -1;
+  for (int64_t n = 1; n <= std::min<int64_t>(max_n, 256); ++n) {
+    const int64_t tiles = (tiles_all + n - 1) / n;
+    const int64_t rounds = (ut * n + slots - 1) / slots;
+    const int64_t cost = rounds * (tiles + 24);
+    if (best_cost < 0 || cost < best_cost) {
+      best_cost = cost;
+      best_n = n;
+    }
+  }
+  const int64_t c = (tiles_all + best_n - 1) / best_n * kStTile;
   *chunk = c;
   *n_chunks = (m_items + c - 1) / c;
+}
+
+template <int D>
+static int64_t st_slots_of() {
+  static int64_t slots = -1;
+  if (slots < 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_topk_kernel<D>, 128, 0) !=
+            hipSuccess)
+      return 1024;  // no device answer: the old fixed target
+    slots = (int64_t)cus * std::max(per, 1);
+  }
+  return slots;
+}
+
+static int64_t st_slots(int D) {
+  switch (D) {
+    case 16: return st_slots_of<16>();
+    case 32: return st_slots_of<32>();
+    case 64: return st_slots_of<64>();
+    case 128: return st_slots_of<128>();
+    default: return st_slots_of<256>();
+  }
 }
 
 }  // namespace mirec
@@ -579,9 +625,15 @@ extern "C" int mirec_topk_masked(float *scores, int64_t n_eval, int64_t m_items,
 extern "C" int64_t mirec_score_topk_workspace(int64_t n_eval, int64_t m_items, int32_t k) {
   using namespace mirec;
   if (n_eval < 0 || m_items <= 0 || k < 1 || k > 32) return -1;
-  int64_t chunk, n_chunks;
-  st_chunks(std::max<int64_t>(n_eval, 1), m_items, &chunk, &n_chunks);
-  return n_eval * n_chunks * k * (int64_t)(sizeof(float) + sizeof(int32_t));
+  // the largest partial-list count over the dims the kernel takes (the
+  // chunking follows the dim's occupancy; the workspace call has no dim)
+  int64_t most = 1;
+  for (int D : {16, 32, 64, 128, 256}) {
+    int64_t chunk, n_chunks;
+    st_chunks(std::max<int64_t>(n_eval, 1), m_items, D, &chunk, &n_chunks);
+    most = std::max(most, n_chunks);
+  }
+  return n_eval * most * k * (int64_t)(sizeof(float) + sizeof(int32_t));
 }
 
 extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const float *item_emb,
@@ -600,7 +652,7 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
   const int64_t need = mirec_score_topk_workspace(n_eval, m_items, k);
   if ((int64_t)workspace_bytes < need) return MIREC_ERR_WORKSPACE;
   int64_t chunk, n_chunks;
-  st_chunks(n_eval, m_items, &chunk, &n_chunks);
+  st_chunks(n_eval, m_items, dim, &chunk, &n_chunks);
   float *pv = static_cast<float *>(workspace);
   int32_t *pi = reinterpret_cast<int32_t *>(pv + n_eval * n_chunks * k);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
