@@ -175,35 +175,47 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
 // and pass 2: their head chunk's segment to slot 1, every later chunk's
 // first segment to slot 0.  Short runs — nearly all of them — are summed in
 // one place without partial rows.
-template <int LPR>
-__global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
-                                                     const int32_t *__restrict__ vals,
-                                                     const float *__restrict__ wt, int64_t n,
-                                                     int32_t d, int32_t n_rows,
-                                                     float *__restrict__ acc_out,
-                                                     int32_t *__restrict__ stamp, int32_t gen,
-                                                     float *__restrict__ part) {
-  static_assert(LPR >= kCh, "chunk layout: one entry per lane");
-  const int lane = threadIdx.x & 63;
-  const int sub = lane & (LPR - 1);
-  const int base = lane - sub;
-  const int64_t chunk = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+// The loads a chunk starts from (issued one chunk ahead by the persistent
+// loop below): the keys before and around it, its entries' keys and indices
+// and those of the window after it.
+struct TgRaw {
+  int32_t kprev, kpp, km, kx, vm, vx;
+};
+
+__device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
+                                            const int32_t *__restrict__ vals, int64_t n,
+                                            int64_t chunk, int sub, TgRaw &r) {
   const int64_t beg = chunk * kCh;
-  if (beg >= n) return;  // the whole group leaves together
   const int64_t end = beg + kCh < n ? beg + kCh : n;
-  const int64_t xend = end + kCh < n ? end + kCh : n;  // the window after the chunk
-  const int nin = (int)(end - beg);
-  const int32_t kprev = beg > 0 ? keys[beg - 1] : -1;
-  const int32_t kpp = beg > kCh ? keys[beg - kCh - 1] : -1;
+  const int64_t xend = end + kCh < n ? end + kCh : n;
   const int64_t pe = beg + sub, px = end + sub;
   const bool in_chunk = sub < kCh && pe < end;
   const bool in_win = sub < kCh && px < xend;
-  const int32_t km = in_chunk ? keys[pe] : kEnd;
-  const int32_t kx = in_win ? keys[px] : kEnd;
-  // the entry's index loads beside its key (not behind it): one round trip
-  // less before the row gathers
-  const int32_t vm = in_chunk ? vals[pe] : 0;
-  const int32_t vx = in_win ? vals[px] : 0;  // the window's indices too (same round trip)
+  r.kprev = beg > 0 ? keys[beg - 1] : -1;
+  r.kpp = beg > kCh ? keys[beg - kCh - 1] : -1;
+  r.km = in_chunk ? keys[pe] : kEnd;
+  r.kx = in_win ? keys[px] : kEnd;
+  // the entries' indices load beside their keys (not behind them)
+  r.vm = in_chunk ? vals[pe] : 0;
+  r.vx = in_win ? vals[px] : 0;
+}
+
+// One chunk of pass 1 from its loaded keys / indices (see below).
+template <int LPR>
+__device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__restrict__ wt,
+                                         int64_t n, int32_t d, int32_t n_rows,
+                                         float *__restrict__ acc_out,
+                                         int32_t *__restrict__ stamp, int32_t gen,
+                                         float *__restrict__ part, int64_t chunk, int sub,
+                                         int base, const TgRaw &r) {
+  const int64_t beg = chunk * kCh;
+  const int64_t end = beg + kCh < n ? beg + kCh : n;
+  const int64_t xend = end + kCh < n ? end + kCh : n;  // the window after the chunk
+  const int nin = (int)(end - beg);
+  const int64_t pe = beg + sub, px = end + sub;
+  const bool in_chunk = sub < kCh && pe < end;
+  const bool in_win = sub < kCh && px < xend;
+  const int32_t kprev = r.kprev, kpp = r.kpp, km = r.km, kx = r.kx;
   const int32_t first = __shfl(km, base);
   if (first >= n_rows) return;  // only invalid entries from here on
   const unsigned long long kmask = (1ull << kCh) - 1ull;
@@ -228,8 +240,8 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   uint64_t am = 0, hm = 0, am2 = 0, hm2 = 0;
   uint32_t thm = 0, thm2 = 0;
   float wm = 0.f, wm2 = 0.f;
-  if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, wt, vm, d, am, hm, thm, wm);
-  if (sub < n_ext) tg_decode(ga, wt, vx, d, am2, hm2, thm2, wm2);
+  if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, wt, r.vm, d, am, hm, thm, wm);
+  if (sub < n_ext) tg_decode(ga, wt, r.vx, d, am2, hm2, thm2, wm2);
   // valid entries of the chunk: up to the first invalid id (they sort last)
   const unsigned long long bad = (__ballot(in_chunk && km >= n_rows) >> base) & kmask;
   const int nval = bad != 0 ? (int)__builtin_ctzll(bad) : nin;
@@ -282,6 +294,49 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
     }
     if (cur >= 0) close(beg + nval);
   }
+}
+
+// Pass 1 driver.  MIREC_TG_PERSIST = 1: a fixed grid (the chip's resident
+// workgroups) whose lane groups walk chunks g, g + G, g + 2G, ..., loading
+// chunk i + 1's keys and indices while chunk i's weights and rows are in
+// flight, so a chunk pays one exposed round trip (its rows) instead of
+// three (keys, weights, rows).  0: one chunk per lane group.
+#ifndef MIREC_TG_PERSIST
+#define MIREC_TG_PERSIST 1
+#endif
+template <int LPR>
+__global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
+                                                     const int32_t *__restrict__ vals,
+                                                     const float *__restrict__ wt, int64_t n,
+                                                     int32_t d, int32_t n_rows,
+                                                     float *__restrict__ acc_out,
+                                                     int32_t *__restrict__ stamp, int32_t gen,
+                                                     float *__restrict__ part) {
+  static_assert(LPR >= kCh, "chunk layout: one entry per lane");
+  const int lane = threadIdx.x & 63;
+  const int sub = lane & (LPR - 1);
+  const int base = lane - sub;
+  const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+  const int64_t n_chunks = (n + kCh - 1) / kCh;
+#if MIREC_TG_PERSIST
+  const int64_t n_groups = (int64_t)gridDim.x * blockDim.x / LPR;
+  int64_t c = group;
+  TgRaw cur;
+  if (c < n_chunks) tg_load_raw(keys, vals, n, c, sub, cur);
+  while (c < n_chunks) {
+    const int64_t cn = c + n_groups;
+    TgRaw nxt;
+    if (cn < n_chunks) tg_load_raw(keys, vals, n, cn, sub, nxt);
+    tg_chunk<LPR>(ga, wt, n, d, n_rows, acc_out, stamp, gen, part, c, sub, base, cur);
+    cur = nxt;
+    c = cn;
+  }
+#else
+  if (group >= n_chunks) return;  // the whole group leaves together
+  TgRaw r;
+  tg_load_raw(keys, vals, n, group, sub, r);
+  tg_chunk<LPR>(ga, wt, n, d, n_rows, acc_out, stamp, gen, part, group, sub, base, r);
+#endif
 }
 
 // Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
@@ -703,6 +758,28 @@ extern "C" int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int
   return MIREC_OK;
 }
 
+// Pass 1's grid: one lane group per chunk, or (persistent form) at most the
+// workgroups the chip holds at once (CUs x the kernel's occupancy).
+template <int LP>
+static dim3 tg_sum_grid(dim3 full) {
+#if MIREC_TG_PERSIST
+  static unsigned resident = 0;
+  if (resident == 0) {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tg_sum_kernel<LP>, 256, 0) ==
+            hipSuccess && cus > 0 && per > 0)
+      resident = (unsigned)(cus * per);
+    else
+      resident = 2048;
+  }
+  return dim3(full.x < resident ? full.x : resident);
+#else
+  return full;
+#endif
+}
+
 extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
                                        int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
                                        int32_t gen, void *workspace, size_t workspace_bytes,
@@ -758,8 +835,8 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   const dim3 grid((unsigned)((threads + 255) / 256));
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
-    hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga, keys_out, vals_out, wt, \
-                       L.n_ent, dim, n_rows, acc, stamp, gen, part);                          \
+    hipLaunchKernelGGL(tg_sum_kernel<LP>, tg_sum_grid<LP>(grid), dim3(256), 0, st, ga,        \
+                       keys_out, vals_out, wt, L.n_ent, dim, n_rows, acc, stamp, gen, part);  \
     MIREC_LAUNCH_CHECK();                                                                    \
     if (n_blocks > 0) {                                                                      \
       hipLaunchKernelGGL(tg_block_kernel<LP>, dim3((unsigned)((n_blocks * LP + 255) / 256)),  \

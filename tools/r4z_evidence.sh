@@ -1,11 +1,13 @@
-# Round 4 final tree, part 2: smoke, the C2 bench line (oracle parity leg),
-# C2 rocprof passes, C3 / C4 lines, C3 / C4 kernel stats, FETCH / WRITE of
+# Round 4 final tree, part 2 (PART=1: smoke, the C2 bench line (oracle parity leg),
+# C2 rocprof passes, C3 / C4 lines; PART=2: C3 / C4 kernel stats, FETCH / WRITE of
 # the run-aligned table-gradient sum, the C3 world simulation.  rocprofv3
 # writes CSV; only the *_stats.csv and counter CSVs of the kept passes stay.
 set -u
 export TMPDIR=/tmp
 E=gpurun_out/r4z
 mkdir -p $E
+PART=${PART:-1}
+if [ "$PART" = 1 ]; then
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $E/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $E/smoke.log; exit 1; }
 tail -2 $E/smoke.log
 timeout -k 10 700 python bench.py > $E/bench_c2.log 2>&1 || { echo "bench rc=$?"; tail -5 $E/bench_c2.log; exit 1; }
@@ -16,6 +18,9 @@ timeout -k 10 400 python tools/bench_sage.py --steps 20 > $E/bench_c3.log 2>&1 |
 grep '^{' $E/bench_c3.log | cut -c1-300
 timeout -k 10 400 python tools/bench_sasrec.py --steps 100 > $E/bench_c4.log 2>&1 || { echo "c4 rc=$?"; exit 1; }
 grep '^{' $E/bench_c4.log | cut -c1-300
+echo "r4z part 1 ok"
+exit 0
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c3 -o run --output-format csv -- python3 tools/bench_sage.py --steps 10 --warmup 3 --cpu-baseline 0 > $E/c3prof.log 2>&1 || { echo "c3 trace rc=$?"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c4 -o run --output-format csv -- python3 tools/bench_sasrec.py --steps 10 --warmup 3 --cpu-baseline 0 > $E/c4prof.log 2>&1 || { echo "c4 trace rc=$?"; exit 1; }
 find $E/c3 $E/c4 -name "*kernel_trace.csv" -delete
