@@ -296,13 +296,16 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__res
   }
 }
 
-// Pass 1 driver.  MIREC_TG_PERSIST = 1: a fixed grid (the chip's resident
-// workgroups) whose lane groups walk chunks g, g + G, g + 2G, ..., loading
-// chunk i + 1's keys and indices while chunk i's weights and rows are in
-// flight, so a chunk pays one exposed round trip (its rows) instead of
-// three (keys, weights, rows).  0: one chunk per lane group.
+// Pass 1 driver: one chunk per lane group (default), or MIREC_TG_PERSIST = 1:
+// a fixed grid (the chip's resident workgroups) whose lane groups walk chunks
+// g, g + G, ..., loading chunk i + 1's keys and indices while chunk i's
+// weights and rows are in flight.  The persistent form measured slower at C3
+// (259 vs 231 us, profiles/round4_tg_bench.jsonl): the carried loads take
+// 109 VGPRs (four waves per SIMD instead of five) and the gathers, not the
+// key loads, are what each wave waits on — the bytes in flight per CU do not
+// grow.
 #ifndef MIREC_TG_PERSIST
-#define MIREC_TG_PERSIST 1
+#define MIREC_TG_PERSIST 0
 #endif
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
