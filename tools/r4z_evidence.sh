@@ -1,4 +1,4 @@
-# Round 4 final tree, part 2 (PART=1: smoke, the C2 bench line (oracle parity leg),
+# Round 4 final tree, part 2 (PART=1: the C2 bench line (oracle parity leg),
 # C2 rocprof passes, C3 / C4 lines; PART=2: C3 / C4 kernel stats, FETCH / WRITE of
 # the run-aligned table-gradient sum, the C3 world simulation.  rocprofv3
 # writes CSV; only the *_stats.csv and counter CSVs of the kept passes stay.
@@ -8,8 +8,6 @@ E=gpurun_out/r4z
 mkdir -p $E
 PART=${PART:-1}
 if [ "$PART" = 1 ]; then
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $E/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $E/smoke.log; exit 1; }
-tail -2 $E/smoke.log
 timeout -k 10 700 python bench.py > $E/bench_c2.log 2>&1 || { echo "bench rc=$?"; tail -5 $E/bench_c2.log; exit 1; }
 grep '^{' $E/bench_c2.log | cut -c1-400
 PROF_OUT=$E/prof bash tools/profile.sh || exit 1
