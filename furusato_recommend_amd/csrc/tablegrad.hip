@@ -514,6 +514,9 @@ __global__ __launch_bounds__(256) void tg_dense_kernel(const float *__restrict__
   }
 }
 
+#ifndef MIREC_TG_ADAM_UNROLL
+#define MIREC_TG_ADAM_UNROLL 2
+#endif
 __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
                                                       float *__restrict__ m, float *__restrict__ v,
                                                       const float *__restrict__ coef, int64_t n_user,
@@ -528,21 +531,39 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
   const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
   const int64_t n4 = n_rows * d4;
   float su = 0.f, si = 0.f;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t r = row_of(i, d4, shift);
-    float4 p = ld4(param + 4 * i), a = ld4(m + 4 * i), b = ld4(v + 4 * i);
-    const float4 g = table_grad4(p, acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci);
-    adam1(p.x, a.x, b.x, g.x, h);
-    adam1(p.y, a.y, b.y, g.y, h);
-    adam1(p.z, a.z, b.z, g.z, h);
-    adam1(p.w, a.w, b.w, g.w, h);
-    st4(param + 4 * i, p);
-    st4(m + 4 * i, a);
-    st4(v + 4 * i, b);
-    const float s = p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
-    if (r < n_user) su += s;
-    else si += s;
+  // MIREC_TG_ADAM_UNROLL float4 groups per thread and iteration, all loads
+  // issued before the first use (more bytes in flight per wave; the same
+  // adam1 arithmetic per element)
+  constexpr int U = MIREC_TG_ADAM_UNROLL;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
+    float4 p[U], a[U], b[U], g[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int64_t i = i0 + q * stride;
+      if (i < n4) {
+        p[q] = ld4(param + 4 * i);
+        a[q] = ld4(m + 4 * i);
+        b[q] = ld4(v + 4 * i);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int64_t i = i0 + q * stride;
+      if (i >= n4) break;
+      const int64_t r = row_of(i, d4, shift);
+      g[q] = table_grad4(p[q], acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci);
+      adam1(p[q].x, a[q].x, b[q].x, g[q].x, h);
+      adam1(p[q].y, a[q].y, b[q].y, g[q].y, h);
+      adam1(p[q].z, a[q].z, b[q].z, g[q].z, h);
+      adam1(p[q].w, a[q].w, b[q].w, g[q].w, h);
+      st4(param + 4 * i, p[q]);
+      st4(m + 4 * i, a[q]);
+      st4(v + 4 * i, b[q]);
+      const float s = p[q].x * p[q].x + p[q].y * p[q].y + p[q].z * p[q].z + p[q].w * p[q].w;
+      if (r < n_user) su += s;
+      else si += s;
+    }
   }
   if (sumsq == nullptr) return;
   red[0][threadIdx.x] = su;
