@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void tg_dense_kernel(const float *__restrict__
 }
 
 #ifndef MIREC_TG_ADAM_UNROLL
-#define MIREC_TG_ADAM_UNROLL 2
+#define MIREC_TG_ADAM_UNROLL 1
 #endif
 __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
                                                       float *__restrict__ m, float *__restrict__ v,
@@ -532,8 +532,10 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
   const int64_t n4 = n_rows * d4;
   float su = 0.f, si = 0.f;
   // MIREC_TG_ADAM_UNROLL float4 groups per thread and iteration, all loads
-  // issued before the first use (more bytes in flight per wave; the same
-  // adam1 arithmetic per element)
+  // issued before the first use (the same adam1 arithmetic per element).  1,
+  // 2 and 4 measured alike at C3 (0.67-0.70 ms, launch-to-launch noise: the
+  // kernel streams W, m, v in and out at ~5.3 TB/s with or without more
+  // loads in flight per thread; profiles/round4_adam_unroll.txt)
   constexpr int U = MIREC_TG_ADAM_UNROLL;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
