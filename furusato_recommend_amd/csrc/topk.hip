@@ -196,6 +196,41 @@ __device__ __forceinline__ unsigned bloom_h2(int64_t item) {
   return ((unsigned)item * 0x9E3779B1u) >> 24;
 }
 
+// x of lane (lane ^ stride), stride a power of two < 64, on the VALU instead
+// of the LDS crossbar (ds_bpermute: a round trip per exchange, 42 dependent
+// ones per sort): DPP quad_perm for 1 and 2; row_half_mirror then a
+// reversing quad_perm for 4 (i -> 7 - i within 8, then within 4: i ^ 4);
+// row_ror:8 for 8 (within 16: i + 8 = i ^ 8); v_permlane16_swap /
+// v_permlane32_swap (gfx950) for 16 / 32, each lane taking the half it
+// lacks.  MIREC_TOPK_DPP=0 keeps __shfl_xor.
+#ifndef MIREC_TOPK_DPP
+#define MIREC_TOPK_DPP 1
+#endif
+__device__ __forceinline__ int lane_xor(int x, int stride) {
+#if MIREC_TOPK_DPP
+  const int lane = threadIdx.x & 63;
+  switch (stride) {
+    case 1: return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    case 2: return __builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    case 4: {
+      const int h = __builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+      return __builtin_amdgcn_mov_dpp(h, 0x1B, 0xF, 0xF, false);          // quad_perm [3,2,1,0]
+    }
+    case 8: return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    case 16: {
+      const auto r = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)x, false, false);
+      return (int)((lane & 16) ? r[0] : r[1]);
+    }
+    default: {
+      const auto r = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)x, false, false);
+      return (int)((lane & 32) ? r[0] : r[1]);
+    }
+  }
+#else
+  return __shfl_xor(x, stride);
+#endif
+}
+
 // Bitonic sort of one (value, index) pair per lane over the wave, best first.
 __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
   const int lane = threadIdx.x & 63;
@@ -203,8 +238,8 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
   for (int size = 2; size <= 64; size <<= 1) {
 #pragma unroll
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const float ov = __shfl_xor(v, stride);
-      const int oi = __shfl_xor(ix, stride);
+      const float ov = __int_as_float(lane_xor(__float_as_int(v), stride));
+      const int oi = lane_xor(ix, stride);
       const bool up = ((lane & size) == 0);    // this lane's block sorts best-first
       const bool lower = (lane & stride) == 0;  // the lane keeps the better of the pair
       const bool mine_better = better(v, ix, ov, oi);
