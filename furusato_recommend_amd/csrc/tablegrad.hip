@@ -128,6 +128,26 @@ __device__ __forceinline__ void tg_decode(const GroupArgs &ga, const float *__re
   hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
 }
 
+// Lane base + u's x for every lane of a group of LPR lanes (u uniform, a
+// constant after unrolling).  Groups of 32 / 64 lanes read it with
+// v_readlane (one per group of the wave) instead of a ds_bpermute round trip
+// through the LDS crossbar; narrower groups keep __shfl.
+#ifndef MIREC_TG_READLANE
+#define MIREC_TG_READLANE 1
+#endif
+template <int LPR>
+__device__ __forceinline__ int grp_bcast(int x, int base, int u) {
+#if MIREC_TG_READLANE
+  if constexpr (LPR == 64) {
+    return __builtin_amdgcn_readlane(x, u);
+  } else if constexpr (LPR == 32) {
+    const int a = __builtin_amdgcn_readlane(x, u), b = __builtin_amdgcn_readlane(x, 32 + u);
+    return base ? b : a;
+  }
+#endif
+  return __shfl(x, base + u);
+}
+
 // The kCh rows of one batch of entries (lane u of the group decoded entry u)
 // in flight at once, then weighted and masked (their inputs re-broadcast, so
 // only the rows stay live during the loads).  Only entries lo <= u < hi load
@@ -140,19 +160,17 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
   const uint32_t hm_lo = (uint32_t)hm, hm_hi = (uint32_t)(hm >> 32);
 #pragma unroll
   for (int u = 0; u < kCh; ++u) {
-    const int src = base + u;
-    const uint64_t a = (uint64_t)(uint32_t)__shfl((int)am_lo, src) |
-                       ((uint64_t)(uint32_t)__shfl((int)am_hi, src) << 32);
+    const uint64_t a = (uint64_t)(uint32_t)grp_bcast<LPR>((int)am_lo, base, u) |
+                       ((uint64_t)(uint32_t)grp_bcast<LPR>((int)am_hi, base, u) << 32);
     x[u] = (act && u >= lo && u < hi) ? ld4(reinterpret_cast<const float *>(a) + col) : f4_zero();
   }
 #pragma unroll
   for (int u = 0; u < kCh; ++u) {
-    const int src = base + u;
-    const uint32_t th = (uint32_t)__shfl((int)thm, src);
-    const float w = __shfl(wm, src);
+    const uint32_t th = (uint32_t)grp_bcast<LPR>((int)thm, base, u);
+    const float w = __int_as_float(grp_bcast<LPR>(__float_as_int(wm), base, u));
     if (th != 0u) {
-      const uint64_t hq = ((uint64_t)(uint32_t)__shfl((int)hm_lo, src) |
-                           ((uint64_t)(uint32_t)__shfl((int)hm_hi, src) << 32)) +
+      const uint64_t hq = ((uint64_t)(uint32_t)grp_bcast<LPR>((int)hm_lo, base, u) |
+                           ((uint64_t)(uint32_t)grp_bcast<LPR>((int)hm_hi, base, u) << 32)) +
                           (uint64_t)(col >> 2);
       x[u] = drop4_hq(x[u], hq, th, w);
     } else {
@@ -272,7 +290,7 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__res
     };
 #pragma unroll
     for (int u = 0; u < kCh; ++u) {
-      const int32_t ku = __shfl(km, base + u);
+      const int32_t ku = grp_bcast<LPR>(km, base, u);
       if (u >= skip && u < nval) {
         if (cur < 0) {
           cur = ku;
