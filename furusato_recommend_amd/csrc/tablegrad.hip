@@ -129,11 +129,13 @@ __device__ __forceinline__ void tg_decode(const GroupArgs &ga, const float *__re
 }
 
 // Lane base + u's x for every lane of a group of LPR lanes (u uniform, a
-// constant after unrolling).  Groups of 32 / 64 lanes read it with
-// v_readlane (one per group of the wave) instead of a ds_bpermute round trip
-// through the LDS crossbar; narrower groups keep __shfl.
+// constant after unrolling): __shfl (ds_bpermute).  MIREC_TG_READLANE=1 reads
+// it with v_readlane for 32 / 64-lane groups (one per group of the wave):
+// 84 instead of 95 VGPRs, six waves per SIMD instead of five, but 208
+// readlanes whose SGPR results serialise the wave — measured slower at C3
+// (accumulate 0.379 vs 0.367 ms, profiles/round4_tg_bench.jsonl).
 #ifndef MIREC_TG_READLANE
-#define MIREC_TG_READLANE 1
+#define MIREC_TG_READLANE 0
 #endif
 template <int LPR>
 __device__ __forceinline__ int grp_bcast(int x, int base, int u) {
