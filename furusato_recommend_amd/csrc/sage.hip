@@ -160,16 +160,33 @@ __global__ __launch_bounds__(256) void fanout_mean_kernel(
   const int64_t d = (int64_t)d4 * 4;
   float4 acc = f4_zero();
   int cnt = 0;
-  for (int c = 0; c < k; ++c) {
-    const int64_t child = t * k + c;
-    if (valid != nullptr && valid[child] < 0) continue;
-    ++cnt;
-    const int64_t row = GATHER ? (int64_t)valid[child] : child;
-    float4 v = ld4(x + row * d + c4 * 4);
-    if (thresh != 0u) {
-      v = drop4(v, key, (uint64_t)(child * d + c4 * 4), thresh, scale);
+  // children in batches of kFmBatch: every id, then every row of the batch
+  // in flight at once (not one dependent id -> row round trip per child),
+  // then masked and added in child order (the same sum as one at a time)
+  constexpr int kFmBatch = 8;
+  for (int c0 = 0; c0 < k; c0 += kFmBatch) {
+    int32_t vid[kFmBatch];
+#pragma unroll
+    for (int u = 0; u < kFmBatch; ++u)
+      vid[u] = (c0 + u < k && valid != nullptr) ? valid[t * k + c0 + u] : 0;
+    float4 v[kFmBatch];
+#pragma unroll
+    for (int u = 0; u < kFmBatch; ++u) {
+      const int64_t child = t * k + c0 + u;
+      const bool ok = c0 + u < k && vid[u] >= 0;
+      const int64_t row = GATHER ? (int64_t)vid[u] : child;
+      v[u] = ok ? ld4(x + row * d + c4 * 4) : f4_zero();
     }
-    acc = f4_add(acc, v);
+#pragma unroll
+    for (int u = 0; u < kFmBatch; ++u) {
+      const int64_t child = t * k + c0 + u;
+      if (c0 + u < k && vid[u] >= 0) {
+        ++cnt;
+        float4 w = v[u];
+        if (thresh != 0u) w = drop4(w, key, (uint64_t)(child * d + c4 * 4), thresh, scale);
+        acc = f4_add(acc, w);
+      }
+    }
   }
   st4(out + i * 4, cnt > 0 ? f4_div(acc, (float)cnt) : f4_zero());
 }
