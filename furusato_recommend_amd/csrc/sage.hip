@@ -196,18 +196,32 @@ __global__ __launch_bounds__(256) void fanout_mean_bwd_kernel(
     int32_t k, int32_t d4, uint64_t key, uint32_t thresh, float scale,
     float *__restrict__ grad_x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // (child, float4)
-  if (i >= n_targets * k * d4) return;
+  if (i >= n_targets * k * d4) return;  // whole d4-lane groups leave together
   const int64_t child = i / d4;
   const int64_t c4 = i - child * d4;
   const int64_t t = child / k;
   const int64_t d = (int64_t)d4 * 4;
-  float4 g = f4_zero();
-  if (valid == nullptr || valid[child] >= 0) {
-    int cnt = k;
-    if (valid != nullptr) {
-      cnt = 0;
+  // valid children of target t: the d4 lanes of this child's group read the
+  // k flags d4 at a time and count them by ballot (d4 a power of two <= 64,
+  // so the groups are aligned inside the wave), instead of every lane
+  // loading all k flags
+  int cnt = k;
+  if (valid != nullptr) {
+    cnt = 0;
+    if (d4 <= 64 && (d4 & (d4 - 1)) == 0) {
+      const int lane = threadIdx.x & 63;
+      const int gbase = lane & ~(d4 - 1);
+      const unsigned long long gmask = (d4 == 64 ? ~0ull : ((1ull << d4) - 1ull)) << gbase;
+      for (int j0 = 0; j0 < k; j0 += d4) {
+        const int j = j0 + (int)c4;
+        cnt += __popcll(__ballot(j < k && valid[t * k + j] >= 0) & gmask);
+      }
+    } else {
       for (int c = 0; c < k; ++c) cnt += valid[t * k + c] >= 0 ? 1 : 0;
     }
+  }
+  float4 g = f4_zero();
+  if (valid == nullptr || valid[child] >= 0) {
     g = f4_div(ld4(grad_out + t * d + c4 * 4), (float)cnt);
     if (thresh != 0u) {
       g = drop4(g, key, (uint64_t)(child * d + c4 * 4), thresh, scale);
