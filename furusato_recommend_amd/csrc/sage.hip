@@ -122,30 +122,15 @@ __global__ __launch_bounds__(256) void sample_fanout_norep_reg_kernel(
     if (c < k) out[c] = sel[c];
 }
 
-// One thread per (group of kGrRows rows, float4 column): the group's ids,
-// then its rows, all in flight together (one id -> row round trip per
-// thread instead of one per row).
-constexpr int kGrRows = 4;
 __global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ table,
                                                           const int32_t *__restrict__ ids, int64_t n,
                                                           int32_t d4, float *__restrict__ out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t groups = (n + kGrRows - 1) / kGrRows;
-  if (i >= groups * d4) return;
-  const int64_t g = i / d4;
-  const int64_t c = i - g * d4;
-  int32_t id[kGrRows];
-#pragma unroll
-  for (int u = 0; u < kGrRows; ++u) id[u] = g * kGrRows + u < n ? ids[g * kGrRows + u] : -1;
-  float4 v[kGrRows];
-#pragma unroll
-  for (int u = 0; u < kGrRows; ++u)
-    v[u] = id[u] >= 0 ? ld4(table + ((int64_t)id[u] * d4 + c) * 4) : f4_zero();
-#pragma unroll
-  for (int u = 0; u < kGrRows; ++u) {
-    const int64_t r = g * kGrRows + u;
-    if (r < n) st4(out + (r * d4 + c) * 4, v[u]);
-  }
+  if (i >= n * d4) return;
+  const int64_t r = i / d4;
+  const int64_t c = i - r * d4;
+  const int32_t id = ids[r];
+  st4(out + 4 * i, id >= 0 ? ld4(table + ((int64_t)id * d4 + c) * 4) : f4_zero());
 }
 
 __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float *__restrict__ grad,
@@ -494,7 +479,7 @@ extern "C" int mirec_gather_rows(const float *table, const int32_t *ids, int64_t
   using namespace mirec;
   MIREC_CHECK_ARG(table && ids && out && n >= 0 && dim > 0 && dim % 4 == 0);
   if (n == 0) return MIREC_OK;
-  const int64_t tot = (n + kGrRows - 1) / kGrRows * (dim / 4);
+  const int64_t tot = n * (dim / 4);
   hipLaunchKernelGGL(gather_rows_kernel, dim3((tot + 255) / 256), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), table, ids, n, dim / 4, out);
   MIREC_LAUNCH_CHECK();
