@@ -1,6 +1,6 @@
-# Round 4 (session 2l): GraphSAGE fanout mean with each batch of children's
-# ids, then rows, in flight together — the GraphSAGE tests, then C3 per build
-# (line + kernel times).
+# Round 4 (session 2m): GraphSAGE table-row gather with 4 rows per thread in
+# flight — the GraphSAGE tests, then C3 per build (line + kernel times)
+# against the tree before it (var_sage_prev).
 set -u
 E=gpurun_out/r4q
 mkdir -p $E
