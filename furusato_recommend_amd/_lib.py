@@ -107,6 +107,10 @@ SIGNATURES = {
     "mirec_distinct_rows_workspace": (c_int64, [c_int64]),
     "mirec_distinct_rows": (c_int, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p,
                                     c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mirec_stamped_rows": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
+                                   c_void_p, c_size_t, c_void_p]),
+    "mirec_gather_rows_counted": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                          c_void_p, c_void_p]),
     "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -263,6 +263,59 @@ __global__ __launch_bounds__(256) void dr_write_kernel(const uint8_t *__restrict
     if ((set >> k) & 1u) out[o++] = (int32_t)(b0 + k);
 }
 
+// ------------------------------------------ the stamped rows of a table gradient
+// The rows a micro-batch's sorted table gradient wrote (stamp == gen,
+// graphsage.TableGrad) ascending, the count and the count per owner block,
+// all on the device: the pipelined fetch exchange exports micro-batch k's
+// rows with no host round trip and reads the counts one micro-batch later
+// (dist.DenseGradDataParallel._route_chunk).  The byte map is the stamp
+// comparison; count / scan / ordered writes are the distinct-rows kernels.
+__global__ __launch_bounds__(256) void sr_mark_kernel(const int32_t *__restrict__ stamp,
+                                                      int64_t n_rows, int32_t gen,
+                                                      uint8_t *__restrict__ bm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_rows) bm[i] = stamp[i] == gen ? 1 : 0;
+}
+
+// counts[1 + q] = rows in owner block q (q·per .. (q+1)·per, the last block
+// to n_rows): two lower bounds in the ascending rows[0 .. counts[0])
+__device__ __forceinline__ int32_t sr_lower_bound(const int32_t *__restrict__ rows, int32_t n,
+                                                  int64_t v) {
+  int32_t a = 0, b = n;
+  while (a < b) {
+    const int32_t m = (a + b) >> 1;
+    if ((int64_t)rows[m] < v) a = m + 1;
+    else b = m;
+  }
+  return a;
+}
+
+__global__ __launch_bounds__(256) void sr_parts_kernel(const int32_t *__restrict__ rows,
+                                                       int64_t n_rows, int32_t parts,
+                                                       int32_t *__restrict__ counts) {
+  const int n = counts[0];
+  const int64_t per = n_rows / parts;
+  for (int q = threadIdx.x; q < parts; q += blockDim.x) {
+    const int64_t lo = q * per, hi = q == parts - 1 ? n_rows : (q + 1) * per;
+    counts[1 + q] = sr_lower_bound(rows, n, hi) - sr_lower_bound(rows, n, lo);
+  }
+}
+
+// out[i, :] = src[rows[i], :] for i < *count (read on the device), float4
+// lanes, grid-stride over a grid sized for the capacity
+__global__ __launch_bounds__(256) void gather_counted_kernel(const float4 *__restrict__ src,
+                                                             const int32_t *__restrict__ rows,
+                                                             const int32_t *__restrict__ count,
+                                                             int64_t d4,
+                                                             float4 *__restrict__ out) {
+  const int64_t total = (int64_t)count[0] * d4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / d4, c = e - i * d4;
+    out[e] = src[(int64_t)rows[i] * d4 + c];
+  }
+}
+
 }  // namespace mirec
 
 extern "C" int64_t mirec_distinct_rows_workspace(int64_t n_rows) {
@@ -302,6 +355,55 @@ extern "C" int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows
   hipLaunchKernelGGL(dr_scan_kernel, dim3(1), dim3(256), 0, st, cnt, nb, count);
   MIREC_LAUNCH_CHECK();
   hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, out);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_stamped_rows(const int32_t *stamp, int64_t n_rows, int32_t gen,
+                                  int32_t parts, int32_t *rows, int32_t *counts, void *workspace,
+                                  size_t workspace_bytes, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(n_rows >= 0 && parts >= 1 && rows && counts && workspace);
+  MIREC_CHECK_ARG(n_rows == 0 || stamp);
+  MIREC_CHECK_ARG(((uintptr_t)workspace & 15u) == 0);
+  const int64_t need = mirec_distinct_rows_workspace(n_rows);
+  if ((int64_t)workspace_bytes < need) return MIREC_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nb = (n_rows + kDrBlock - 1) / kDrBlock;
+  if (nb == 0) {
+    MIREC_HIP(hipMemsetAsync(counts, 0, 4 * (size_t)(1 + parts), st));
+    return MIREC_OK;
+  }
+  uint8_t *bm = static_cast<uint8_t *>(workspace);
+  int32_t *cnt = reinterpret_cast<int32_t *>(bm + (n_rows + 15) / 16 * 16);
+  hipLaunchKernelGGL(sr_mark_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, st,
+                     stamp, n_rows, gen, bm);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dr_count_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dr_scan_kernel, dim3(1), dim3(256), 0, st, cnt, nb, counts);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, rows);
+  MIREC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sr_parts_kernel, dim3(1), dim3(256), 0, st, rows, n_rows, parts, counts);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_gather_rows_counted(const float *src, const int32_t *rows,
+                                         const int32_t *count, int64_t capacity, int32_t dim,
+                                         float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(capacity >= 0 && dim > 0 && dim % 4 == 0 && count);
+  MIREC_CHECK_ARG(capacity == 0 || (src && rows && out));
+  MIREC_CHECK_ARG(((uintptr_t)src & 15u) == 0 && ((uintptr_t)out & 15u) == 0);
+  if (capacity == 0) return MIREC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t d4 = dim / 4;
+  const int64_t blocks = std::min<int64_t>((capacity * d4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(gather_counted_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     reinterpret_cast<const float4 *>(src), rows, count, d4,
+                     reinterpret_cast<float4 *>(out));
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

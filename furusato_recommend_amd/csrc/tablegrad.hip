@@ -657,7 +657,12 @@ static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *
                                                        rocprim::kernel_config<1024, 8>,
                                                        MIREC_TG_SORT_BITS,
                                                        rocprim::block_radix_rank_algorithm::match>;
-  using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Onesweep>;
+  // onesweep from 128 K entries up: rocprim's default merge-sort limit (1 M)
+  // sent a micro-batch's ~0.9 M entries (the pipelined exchange, C = 2)
+  // through ~20 block-sort / merge launches, 150 us against the full
+  // batch's 85 us onesweep; both are stable, so the order is the same
+  using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Onesweep,
+                                         (size_t)1 << 17>;
   return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, ki, ko, vi, vo, (size_t)n, 0, end_bit, st);
 #else
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, n, 0, end_bit, st);

@@ -439,6 +439,32 @@ def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0) -> t
     return out[: int(cnt.item())]
 
 
+def export_stamped(tg, parts: int, ws: torch.Tensor | None = None):
+    """The rows the table gradient ``tg`` (graphsage.TableGrad) stamped in its
+    last accumulate, ascending, and their rows of S — with NO host sync: all
+    enqueued on the current stream (mirec_stamped_rows, then a gather that
+    reads the count on the device).  Returns (rows int32 [cap], vals [cap,
+    d], counts int32 [1 + parts] = total then per owner block, workspace);
+    the first counts[0] entries of rows / vals are valid, cap = the
+    accumulate's entry count (bounds the distinct rows)."""
+    from . import _lib
+    from ._lib import check, lib
+    N, d, dev = tg.n_rows, tg.dim, tg.acc.device
+    nb = max(int(lib.mirec_distinct_rows_workspace(N)), 16)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+    cap = max(min(N, int(tg.entries)), 1)
+    rows = torch.empty(max(N, 1), dtype=torch.int32, device=dev)
+    counts = torch.empty(1 + parts, dtype=torch.int32, device=dev)
+    s = _lib.stream_handle()
+    check(lib.mirec_stamped_rows(tg.stamp.data_ptr(), N, int(tg.gen), int(parts), rows.data_ptr(),
+                                 counts.data_ptr(), ws.data_ptr(), ws.numel(), s), "stamped_rows")
+    vals = torch.empty(cap, d, dtype=tg.acc.dtype, device=dev)
+    check(lib.mirec_gather_rows_counted(tg.acc.data_ptr(), rows.data_ptr(), counts.data_ptr(), cap,
+                                        d, vals.data_ptr(), s), "gather_rows_counted")
+    return rows, vals, counts, ws
+
+
 def route_ids(ids: torch.Tensor, n_rows: int, group=None):
     """Send every row id to the rank owning it (contiguous blocks of
     n_rows/W rows; ``ids`` ascending int32).  Returns (received ids in
@@ -557,6 +583,8 @@ class DenseGradDataParallel:
         self._ones = None      # the routed Adam's all-stamped shard
         self.comm_events = None  # (start, end) HIP events per collective (bench)
         self.last_exchange_bytes = 0
+        self._sr_ws = None        # pipelined fetch: export_stamped's workspace
+        self._side_stream = None  # pipelined fetch: the routed rows' stream
         if self.world > 1:
             for p in model.parameters():
                 dist.broadcast(p.data, src=0, group=group)
@@ -821,30 +849,71 @@ class DenseGradDataParallel:
 
     @torch.no_grad()
     def _route_chunk(self, k, st):
+        """After micro-batch k's backward: export its table-gradient rows on
+        the device (no host sync, export_stamped), then send micro-batch
+        k - 1's — whose counts are ready by now, while k computes — so the
+        host never waits for the micro-batch it has just issued."""
         tg = self.model._tg
-        rows, vals = self.routed_export()
+        rows, vals, counts, self._sr_ws = export_stamped(tg, self.world, self._sr_ws)
+        ev = torch.cuda.Event()
+        ev.record()
+        st["export"].append((rows, vals, counts, ev))
         st["coef"] = tg.coef.clone() if st.get("coef") is None else st["coef"] + tg.coef
         tg.pending = False
+        if k > 0:
+            self._route_issue(k - 1, st)
+
+    def _side(self):
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(device=self.model._table_state.param.device)
+        return self._side_stream
+
+    @torch.no_grad()
+    def _route_issue(self, j, st):
+        """Send micro-batch j's exported rows to their owners: on a side
+        stream that waits only for j's export, so the count exchange's host
+        read does not wait for the micro-batch computing meanwhile, and the
+        rows' all-to-all overlaps it."""
+        rows, vals, counts, ev = st["export"][j]
+        st["export"][j] = None
         if not self.distributed:
-            st["route"].append((rows, vals, [rows.numel()], None, None))
+            n = int(counts[0])
+            st["route"].append((rows[:n], vals[:n], [n], None, None))
             return
         p = self.model._table_state.param
-        N, d = p.shape
-        a = self._event()
-        rid, rc, sc = route_ids(rows, N, self.group)
-        self._note(a, self._event())
-        rv = torch.empty(rid.numel(), d, dtype=vals.dtype, device=vals.device)
-        work = self._a2a_async(rv, vals, rc, sc)  # in flight while k + 1 computes
-        st["route"].append((rid, rv, rc, work, vals))
+        d = p.shape[1]
+        side = self._side()
+        with torch.cuda.stream(side):
+            side.wait_event(ev)
+            a = self._event()
+            send = counts[1:].long()
+            recv = torch.empty_like(send)
+            _a2a(recv, send, group=self.group)
+            sc, rc = send.tolist(), recv.tolist()
+            n = sum(sc)
+            rid = torch.empty(int(sum(rc)), dtype=torch.int32, device=p.device)
+            _a2a(rid, rows[:n], rc, sc, group=self.group)
+            self._note(a, self._event())
+            rv = torch.empty(rid.numel(), d, dtype=vals.dtype, device=p.device)
+            work = self._a2a_async(rv, vals[:n], rc, sc)  # in flight while j + 1 computes
+        st["route"].append((rid, rv, rc, work, (rows, vals)))
         self.last_exchange_bytes += (sum(rc) - rc[self.rank]) * (4 + d * p.element_size())
 
     @torch.no_grad()
     def _finish_routed(self, st):
         W = self.world
+        if st["export"] and st["export"][-1] is not None:
+            self._route_issue(len(st["export"]) - 1, st)
         a = self._event()
-        for *_, work, _ in st["route"]:
+        cur = torch.cuda.current_stream()
+        for rid, rv, _, work, _ in st["route"]:
             if work is not None:
                 work.wait()
+            if self.distributed:  # allocated on the side stream, read here
+                rid.record_stream(cur)
+                rv.record_stream(cur)
+        if self.distributed and self._side_stream is not None:
+            cur.wait_stream(self._side_stream)
         self._note(a, self._event())
         blocks = [(rid, rv, counts) for rid, rv, counts, _, _ in st["route"]]
         own = torch.empty(2, device=self.model._table_state.param.device)
@@ -865,7 +934,7 @@ class DenseGradDataParallel:
             self.model.table_stale = True
 
     def _pipelined_step(self, users, pos, neg):
-        st = {"fetch": [], "route": [], "coef": None}
+        st = {"fetch": [], "export": [], "route": [], "coef": None}
 
         def chunk_hook(k, phase):
             if phase == "pre":

@@ -75,12 +75,14 @@ class TableGrad:
         # repeated id's sum not fixed) instead of the sorted segmented sums
         self.atomic = False
         self._ws = None
+        self.entries = 0  # row contributions of the last accumulate
 
     def accumulate(self, groups):
         """groups: [(ids int32, grad_out [n_t, d], k, mean, dropout p, seed)]."""
         n = len(groups)
         if not 1 <= n <= _lib.TABLE_GRAD_MAX_GROUPS:
             raise ValueError("table gradient: 1..8 row groups")
+        self.entries = sum(int(g[0].numel()) for g in groups)  # bounds the rows stamped
         arr = (_lib.RowGradGroup * n)()
         keep = []
         for a, (ids, g, k, mean, p, seed) in zip(arr, groups):
@@ -118,6 +120,7 @@ class TableGrad:
     def skip(self):
         """A backward with no row gradient: S = 0 (a fresh generation)."""
         self._next_gen()
+        self.entries = 0
         self.pending = True
 
     def materialize(self, table: torch.Tensor) -> torch.Tensor:

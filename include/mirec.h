@@ -267,6 +267,23 @@ int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows, int64_t l
                         int64_t hi, int32_t *out, int32_t *count, void *workspace,
                         size_t workspace_bytes, mirec_stream_t stream);
 
+/* The rows r in [0, n_rows) with stamp[r] == gen (the rows a table gradient
+ * of the sorted form wrote) ascending -> rows[0 .. counts[0]) (capacity
+ * n_rows), and counts[1 + q] = those in owner block q of `parts` contiguous
+ * blocks of n_rows / parts rows (the last to n_rows) — all on the device, no
+ * host round trip: the pipelined fetch exchange's export of a micro-batch's
+ * table-gradient rows (dist.DenseGradDataParallel; replaces torch.nonzero +
+ * bincount).  Workspace: mirec_distinct_rows_workspace(n_rows) bytes. */
+int mirec_stamped_rows(const int32_t *stamp, int64_t n_rows, int32_t gen, int32_t parts,
+                       int32_t *rows, int32_t *counts, void *workspace,
+                       size_t workspace_bytes, mirec_stream_t stream);
+
+/* out[i, :] = src[rows[i], :] for i < *count, the count read on the device
+ * (capacity rows of out); dim % 4 == 0, src and out 16-byte aligned. */
+int mirec_gather_rows_counted(const float *src, const int32_t *rows, const int32_t *count,
+                              int64_t capacity, int32_t dim, float *out,
+                              mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */
 /* ------------------------------------------------------------------------ */

@@ -3479,6 +3479,35 @@ def test_distinct_rows_matches_unique(n_rows, n, lo, hi):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("n_rows,n,parts", [(1_100_000, 880_000, 8), (4097, 10_000, 2),
+                                            (8, 3, 8), (70_001, 0, 1), (5000, 5000, 3)])
+def test_export_stamped_matches_nonzero(n_rows, n, parts):
+    """export_stamped (the pipelined exchange's device-side export: mirec_
+    stamped_rows + the counted gather) == torch.nonzero of stamp == gen, the
+    gathered rows of S and the per-owner bincount of route_ids — with stale
+    stamps of earlier generations in the map, ragged block tails and an
+    empty generation."""
+    from types import SimpleNamespace
+
+    from furusato_recommend_amd.dist import export_stamped
+    d = 8
+    g = torch.Generator(device="cuda").manual_seed(n_rows + n + parts)
+    stamp = torch.randint(0, 3, (n_rows,), device="cuda", generator=g, dtype=torch.int32)
+    ids = torch.randint(0, n_rows, (n,), device="cuda", generator=g, dtype=torch.int32)
+    stamp[ids.long()] = 5
+    acc = torch.randn(n_rows, d, device="cuda", generator=g)
+    tg = SimpleNamespace(n_rows=n_rows, dim=d, acc=acc, stamp=stamp, gen=5, entries=n)
+    rows, vals, counts, _ = export_stamped(tg, parts)
+    torch.cuda.synchronize()
+    ref = torch.nonzero(stamp == 5).view(-1)
+    c = counts.tolist()
+    assert c[0] == ref.numel()
+    assert torch.equal(rows[: c[0]].long(), ref)
+    assert torch.equal(vals[: c[0]], acc[ref])
+    owner = torch.div(ref, n_rows // parts, rounding_mode="floor").clamp_(max=parts - 1)
+    assert c[1:] == torch.bincount(owner, minlength=parts).tolist()
+
+
 @pytest.mark.parametrize("n,k,no", [(56_321, 384, 128), (56_321, 128, 128), (56_321, 128, 384)])
 def test_plain_gemms_bitwise_repeatable(n, k, no):
     """gemm_nt / gemm_nn / gemm_tn on the split-bf16 loop at a ragged row

@@ -166,6 +166,7 @@ def sage_main(args):
             m._tg_routed = ex != "dense"
             n_own = N // W
             fetched = [0]
+            last = {}
             others = []  # what ranks 1..W-1 send to owner 0: (ids, rows)
             for r in range(1, W):
                 u, p, n = m.sample(B, seed=11, offset=10**8 + r * B, shard=r, n_shards=W)
@@ -184,7 +185,10 @@ def sage_main(args):
             def tree_hook(tree):
                 # fetch's local work at rank 0: the tree's distinct rows outside
                 # block 0, their gather (at the owners: the same count) and the
-                # write into the local table
+                # write into the local table; the slice norms of the last
+                # update handed to the forward (dist.fetch_rows)
+                if "norms" in last:
+                    m._norm_cache = (last.pop("norms"), m._norm_token())
                 ids = torch.cat([g for g, _ in tree.groups])
                 uniq = torch.unique(ids[ids >= 0])
                 need = uniq[uniq >= n_own].long()
@@ -198,6 +202,8 @@ def sage_main(args):
                     rid = torch.cat([rows[:k]] + [o[0] for o in others])
                     rv = torch.cat([vals[:k]] + [o[1] for o in others])
                     norms = torch.empty(2, device=dev) if ex == "fetch" else None
+                    if norms is not None:
+                        last["norms"] = norms
                     dp.routed_adam(rid, rv, [k] + [o[0].numel() for o in others], norms=norms)
                 else:  # materialised G; the reduce-scatter's output stands in as a slice
                     g = m._table.grad
@@ -272,8 +278,9 @@ def sage_pipelined(args, m, W, C, base, rates):
     first micro-batch's rows are exposed, micro-batch k + 1's rows and
     micro-batch k - 1's routed rows overlap micro-batch k's compute (HIP
     events around it), the last micro-batch's routed rows are exposed."""
-    from furusato_recommend_amd.dist import DenseGradDataParallel, distinct_rows
+    from furusato_recommend_amd.dist import DenseGradDataParallel, distinct_rows, export_stamped
     dev = torch.device("cuda:0")
+    side = torch.cuda.Stream(device=dev)
     B = args.batch
     N, d = m._table.shape
     n_own = N // W
@@ -298,6 +305,8 @@ def sage_pipelined(args, m, W, C, base, rates):
     rec = {}
 
     def tree_hook(trees):
+        if "norms" in rec:  # as dist._plan_fetch: the last update's slice norms
+            m._norm_cache = (rec.pop("norms"), m._norm_token())
         have = torch.zeros(N, dtype=torch.bool, device=dev)
         rec["need"], rec["fetch_rows"] = [], []
         for tree in trees:
@@ -319,22 +328,37 @@ def sage_pipelined(args, m, W, C, base, rates):
             e.record()
             rec["ev"].append([e])
         else:
-            rows, vals = dp.routed_export()
-            rec.setdefault("own", []).append((rows[rows < n_own].clone(),
-                                              vals[: int((rows < n_own).sum())].clone()))
+            # as dist._route_chunk: the device-side export (no host sync), and
+            # micro-batch k - 1's counts read on a side stream behind its
+            # export only, so the host does not wait for micro-batch k
+            rows, vals, counts, rec["ws"] = export_stamped(m._tg, W, rec.get("ws"))
             rec["coef"] = m._tg.coef.clone() + (rec["coef"] if "coef" in rec else 0.0)
             m._tg.pending = False
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             rec["ev"][k].append(e)
+            rec.setdefault("exp", []).append((rows, vals, counts, e))
+            if k > 0:
+                take(k - 1)
+
+    def take(j):
+        rows, vals, counts, e = rec["exp"][j]
+        rec["exp"][j] = None
+        with torch.cuda.stream(side):
+            side.wait_event(e)
+            c = counts[1:2].tolist()[0]  # owner 0's rows: the first c (ascending)
+        rec.setdefault("own", []).append((rows[:c], vals[:c]))
 
     def grad_hook():
+        take(C - 1)
+        rec.pop("exp")
         blocks = []
         for rows, vals in rec.pop("own"):
             blocks.append((rows, vals, [rows.numel()]))
         blocks.append((torch.cat([o[0] for o in others]), torch.cat([o[1] for o in others]),
                        [o[0].numel() for o in others]))
-        dp._owner_adam(blocks, rec.pop("coef"), norms=torch.empty(2, device=dev))
+        rec["norms"] = torch.empty(2, device=dev)
+        dp._owner_adam(blocks, rec.pop("coef"), norms=rec["norms"])
         small = [q.grad for q in m.parameters() if q.grad is not None]
         if small:
             flat = torch.cat([g.reshape(-1) for g in small])
