@@ -177,11 +177,13 @@ constexpr int kDrBlock = 4096;  // rows per workgroup (256 threads x 16 bytes)
 
 __global__ __launch_bounds__(256) void dr_mark_kernel(const int32_t *__restrict__ ids, int64_t n,
                                                       int64_t n_rows, int64_t lo, int64_t hi,
+                                                      const uint8_t *__restrict__ have,
                                                       uint8_t *__restrict__ bm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t id = ids[i];
-  if (id >= 0 && id < n_rows && (id < lo || id >= hi)) bm[id] = 1;
+  if (id >= 0 && id < n_rows && (id < lo || id >= hi) && (have == nullptr || !have[id]))
+    bm[id] = 1;
 }
 
 // set-byte bit mask of the 16 map bytes of thread t of block b
@@ -253,14 +255,18 @@ __global__ __launch_bounds__(256) void dr_scan_kernel(int32_t *__restrict__ cnt,
 __global__ __launch_bounds__(256) void dr_write_kernel(const uint8_t *__restrict__ bm,
                                                        int64_t n_rows,
                                                        const int32_t *__restrict__ off,
-                                                       int32_t *__restrict__ out) {
+                                                       int32_t *__restrict__ out,
+                                                       uint8_t *__restrict__ have) {
   const int64_t b0 = (int64_t)blockIdx.x * kDrBlock + 16 * threadIdx.x;
   const uint32_t set = b0 < n_rows ? dr_bits(bm, n_rows, b0) : 0u;
   int tot;
   int o = off[blockIdx.x] + dr_block_scan(__popc(set), &tot);
 #pragma unroll
   for (int k = 0; k < 16; ++k)
-    if ((set >> k) & 1u) out[o++] = (int32_t)(b0 + k);
+    if ((set >> k) & 1u) {
+      out[o++] = (int32_t)(b0 + k);
+      if (have != nullptr) have[b0 + k] = 1;
+    }
 }
 
 // ------------------------------------------ the stamped rows of a table gradient
@@ -329,6 +335,14 @@ extern "C" int64_t mirec_distinct_rows_workspace(int64_t n_rows) {
 extern "C" int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows, int64_t lo,
                                    int64_t hi, int32_t *out, int32_t *count, void *workspace,
                                    size_t workspace_bytes, mirec_stream_t stream) {
+  return mirec_distinct_rows_unseen(ids, n, n_rows, lo, hi, nullptr, out, count, workspace,
+                                 workspace_bytes, stream);
+}
+
+extern "C" int mirec_distinct_rows_unseen(const int32_t *ids, int64_t n, int64_t n_rows, int64_t lo,
+                                       int64_t hi, uint8_t *have, int32_t *out, int32_t *count,
+                                       void *workspace, size_t workspace_bytes,
+                                       mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(n >= 0 && n_rows >= 0 && out && count && workspace);
   MIREC_CHECK_ARG(n == 0 || ids);
@@ -347,14 +361,15 @@ extern "C" int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows
   MIREC_HIP(hipMemsetAsync(bm, 0, (size_t)map, st));
   if (n > 0) {
     hipLaunchKernelGGL(dr_mark_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ids, n,
-                       n_rows, lo, hi, bm);
+                       n_rows, lo, hi, have, bm);
     MIREC_LAUNCH_CHECK();
   }
   hipLaunchKernelGGL(dr_count_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt);
   MIREC_LAUNCH_CHECK();
   hipLaunchKernelGGL(dr_scan_kernel, dim3(1), dim3(256), 0, st, cnt, nb, count);
   MIREC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, out);
+  hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, out,
+                     have);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -383,7 +398,8 @@ extern "C" int mirec_stamped_rows(const int32_t *stamp, int64_t n_rows, int32_t 
   MIREC_LAUNCH_CHECK();
   hipLaunchKernelGGL(dr_scan_kernel, dim3(1), dim3(256), 0, st, cnt, nb, counts);
   MIREC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, rows);
+  hipLaunchKernelGGL(dr_write_kernel, dim3((unsigned)nb), dim3(256), 0, st, bm, n_rows, cnt, rows,
+                     nullptr);
   MIREC_LAUNCH_CHECK();
   hipLaunchKernelGGL(sr_parts_kernel, dim3(1), dim3(256), 0, st, rows, n_rows, parts, counts);
   MIREC_LAUNCH_CHECK();

@@ -421,10 +421,13 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, 
     dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
 
 
-def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0) -> torch.Tensor:
+def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0,
+                  have: torch.Tensor | None = None) -> torch.Tensor:
     """Ascending distinct ids of the int32 device tensor ``ids`` in [0,
     n_rows) outside [lo, hi) (mirec_distinct_rows: byte map, block counts,
-    ordered writes — no sort); one host sync for the count."""
+    ordered writes — no sort); one host sync for the count.  ``have`` (bool
+    / uint8 [n_rows]): ids marked there are skipped, and the ids returned are
+    marked (mirec_distinct_rows_unseen)."""
     from . import _lib
     from ._lib import check, lib
     ids = ids.to(torch.int32).contiguous()
@@ -433,9 +436,17 @@ def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0) -> t
     ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=dev)
     out = torch.empty(max(int(n_rows), 1), dtype=torch.int32, device=dev)
     cnt = torch.empty(1, dtype=torch.int32, device=dev)
-    check(lib.mirec_distinct_rows(ids.data_ptr(), ids.numel(), int(n_rows), int(lo), int(hi),
-                                  out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
-                                  _lib.stream_handle()), "distinct_rows")
+    if have is None:
+        check(lib.mirec_distinct_rows(ids.data_ptr(), ids.numel(), int(n_rows), int(lo), int(hi),
+                                      out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      _lib.stream_handle()), "distinct_rows")
+    else:
+        if have.numel() < n_rows or have.element_size() != 1 or not have.is_contiguous():
+            raise ValueError("have: a contiguous 1-byte map of n_rows entries")
+        check(lib.mirec_distinct_rows_unseen(ids.data_ptr(), ids.numel(), int(n_rows), int(lo),
+                                             int(hi), have.data_ptr(), out.data_ptr(),
+                                             cnt.data_ptr(), ws.data_ptr(), ws.numel(),
+                                             _lib.stream_handle()), "distinct_rows_unseen")
     return out[: int(cnt.item())]
 
 
@@ -815,10 +826,9 @@ class DenseGradDataParallel:
         have = torch.zeros(N, dtype=torch.bool, device=p.device)
         a = self._event()
         for tree in trees:
-            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, lo, lo + n_own)
-            if st["fetch"]:
-                need = need[~have[need.long()]]
-            have[need.long()] = True
+            # rows fetched for an earlier micro-batch are skipped (and marked)
+            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, lo, lo + n_own,
+                                 have=have if len(trees) > 1 else None)
             req, rc, sc = route_ids(need, N, self.group)
             rows = p.data.index_select(0, req.long())  # owner side: the current rows
             st["fetch"].append({"need": need, "rows": rows, "rc": rc, "sc": sc})

@@ -266,6 +266,13 @@ int64_t mirec_distinct_rows_workspace(int64_t n_rows);
 int mirec_distinct_rows(const int32_t *ids, int64_t n, int64_t n_rows, int64_t lo,
                         int64_t hi, int32_t *out, int32_t *count, void *workspace,
                         size_t workspace_bytes, mirec_stream_t stream);
+/* The same, skipping the ids whose byte in have[0 .. n_rows) is set, and
+ * setting it for every id written: the pipelined exchange's read set of
+ * micro-batch k without the rows fetched for micro-batches 0 .. k-1 (one
+ * launch chain instead of a mask, a gather and a boolean compaction). */
+int mirec_distinct_rows_unseen(const int32_t *ids, int64_t n, int64_t n_rows, int64_t lo,
+                            int64_t hi, uint8_t *have, int32_t *out, int32_t *count,
+                            void *workspace, size_t workspace_bytes, mirec_stream_t stream);
 
 /* The rows r in [0, n_rows) with stamp[r] == gen (the rows a table gradient
  * of the sorted form wrote) ascending -> rows[0 .. counts[0]) (capacity

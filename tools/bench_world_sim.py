@@ -310,10 +310,7 @@ def sage_pipelined(args, m, W, C, base, rates):
         have = torch.zeros(N, dtype=torch.bool, device=dev)
         rec["need"], rec["fetch_rows"] = [], []
         for tree in trees:
-            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own)
-            if rec["need"]:
-                need = need[~have[need.long()]]
-            have[need.long()] = True
+            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own, have=have)
             # the owners' gather of the requested rows (rank 0 serves a share of
             # the same size) and the install after the transfer
             rec["need"].append((need.long(), m._table.data.index_select(0, need.long())))
