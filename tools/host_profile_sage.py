@@ -20,7 +20,11 @@ def main():
     ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--top", type=int, default=35)
+    ap.add_argument("--bwd-main-thread", type=int, default=0,
+                    help="1: the autograd backward on the calling thread (visible to cProfile)")
     args = ap.parse_args()
+    if args.bwd_main_thread:
+        torch.autograd.set_multithreading_enabled(False)
     from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
     dev = torch.device("cuda:0")
     ds = SyntheticBipartite(1_000_000, 100_000, 20_000_000, seed=0)
@@ -59,6 +63,7 @@ def main():
     torch.cuda.synchronize()
     print(f"chunks={C} wall {wall:.3f} ms/step; host issue under cProfile {host:.3f} ms/step")
     pstats.Stats(pr).sort_stats("tottime").print_stats(args.top)
+    pstats.Stats(pr).sort_stats("cumulative").print_stats(args.top)
 
 
 if __name__ == "__main__":
