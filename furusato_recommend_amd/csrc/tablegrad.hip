@@ -537,6 +537,31 @@ __global__ __launch_bounds__(256) void tg_dense_kernel(const float *__restrict__
 #ifndef MIREC_TG_ADAM_UNROLL
 #define MIREC_TG_ADAM_UNROLL 1
 #endif
+// MIREC_TG_ADAM_NT: bit 0 = the W / m / v loads, bit 1 = their stores as
+// non-temporal accesses (each byte is touched once per step: nothing to
+// keep).  Loads only is the default: the C3 launch 0.692 / 0.703 -> 0.667 /
+// 0.675 ms; non-temporal stores measured no gain (0.691 / 0.686), both 0.676
+// / 0.675 (profiles/round4_adam_nt.txt)
+#ifndef MIREC_TG_ADAM_NT
+#define MIREC_TG_ADAM_NT 1
+#endif
+typedef float adam_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 adam_ld4(const float *p) {
+#if MIREC_TG_ADAM_NT & 1
+  const adam_f4 x = __builtin_nontemporal_load(reinterpret_cast<const adam_f4 *>(p));
+  return make_float4(x.x, x.y, x.z, x.w);
+#else
+  return ld4(p);
+#endif
+}
+__device__ __forceinline__ void adam_st4(float *p, float4 v) {
+#if MIREC_TG_ADAM_NT & 2
+  const adam_f4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<adam_f4 *>(p));
+#else
+  st4(p, v);
+#endif
+}
 __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
                                                       float *__restrict__ m, float *__restrict__ v,
                                                       const float *__restrict__ coef, int64_t n_user,
@@ -564,9 +589,9 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
     for (int q = 0; q < U; ++q) {
       const int64_t i = i0 + q * stride;
       if (i < n4) {
-        p[q] = ld4(param + 4 * i);
-        a[q] = ld4(m + 4 * i);
-        b[q] = ld4(v + 4 * i);
+        p[q] = adam_ld4(param + 4 * i);
+        a[q] = adam_ld4(m + 4 * i);
+        b[q] = adam_ld4(v + 4 * i);
       }
     }
 #pragma unroll
@@ -579,9 +604,9 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
       adam1(p[q].y, a[q].y, b[q].y, g[q].y, h);
       adam1(p[q].z, a[q].z, b[q].z, g[q].z, h);
       adam1(p[q].w, a[q].w, b[q].w, g[q].w, h);
-      st4(param + 4 * i, p[q]);
-      st4(m + 4 * i, a[q]);
-      st4(v + 4 * i, b[q]);
+      adam_st4(param + 4 * i, p[q]);
+      adam_st4(m + 4 * i, a[q]);
+      adam_st4(v + 4 * i, b[q]);
       const float s = p[q].x * p[q].x + p[q].y * p[q].y + p[q].z * p[q].z + p[q].w * p[q].w;
       if (r < n_user) su += s;
       else si += s;
