@@ -233,6 +233,23 @@ __device__ __forceinline__ float4 combine_groups(float4 s) {
   return s;
 }
 
+// MIREC_PROP_ADAM_NT: the fused Adam's W / m / v loads non-temporal (each
+// read once per step).  Off: C2 4.844 / 4.844 ms per step with ordinary
+// loads, 4.868 / 4.854 with these (profiles/round4_prop_adam_nt.txt) — unlike
+// the table Adam's pure stream, here the loads follow the row's gather
+#ifndef MIREC_PROP_ADAM_NT
+#define MIREC_PROP_ADAM_NT 0
+#endif
+typedef float prop_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 adam_ld4(const float *p) {
+#if MIREC_PROP_ADAM_NT
+  const prop_f4 x = __builtin_nontemporal_load(reinterpret_cast<const prop_f4 *>(p));
+  return make_float4(x.x, x.y, x.z, x.w);
+#else
+  return ld4(p);
+#endif
+}
+
 template <int D>
 __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4 s, int sub) {
   const float di = a.dinv[row];
@@ -249,7 +266,7 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
   if (a.divisor != 1.f) o = f4_div(o, a.divisor);
   if (a.seed2 != nullptr && sl >= 0) o = f4_add(o, ld4(a.seed2 + (int64_t)sl * D + sub * 4));
   if (a.param != nullptr) {
-    float4 p = ld4(a.param + off), m = ld4(a.m + off), v = ld4(a.v + off);
+    float4 p = adam_ld4(a.param + off), m = adam_ld4(a.m + off), v = adam_ld4(a.v + off);
     adam_elem(p.x, m.x, v.x, o.x, a.adam);
     adam_elem(p.y, m.y, v.y, o.y, a.adam);
     adam_elem(p.z, m.z, v.z, o.z, a.adam);
