@@ -75,6 +75,11 @@ class RowGradGroup(Structure):
 
 TABLE_GRAD_MAX_GROUPS = 8
 
+
+class RowBlock(Structure):
+    """mirec_row_block_t (one source block of mirec_owner_sum)."""
+    _fields_ = [("ids", c_void_p), ("rows", c_void_p), ("n", c_int64)]
+
 # name -> (restype, argtypes); the single source of truth for the exports
 # test (tests/test_abi.py checks these against include/mirec.h).
 SIGNATURES = {
@@ -111,6 +116,10 @@ SIGNATURES = {
                                         c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_stamped_rows": (c_int, [c_void_p, c_int64, c_int32, c_int32, c_void_p, c_void_p,
                                    c_void_p, c_size_t, c_void_p]),
+    "mirec_scatter_rows": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    "mirec_owner_sum_workspace": (c_int64, [c_int32, c_int64]),
+    "mirec_owner_sum": (c_int, [POINTER(RowBlock), c_int32, c_int64, c_int64, c_int32, c_void_p,
+                                c_size_t, c_void_p, c_void_p]),
     "mirec_gather_rows_counted": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                           c_void_p, c_void_p]),
     "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,

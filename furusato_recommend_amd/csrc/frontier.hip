@@ -322,6 +322,60 @@ __global__ __launch_bounds__(256) void gather_counted_kernel(const float4 *__res
   }
 }
 
+// dst[ids[i], :] = src[i, :] (ids distinct, < 0 skipped): the install of
+// fetched rows into the local table; float4 lanes
+__global__ __launch_bounds__(256) void scatter_rows_kernel(const float4 *__restrict__ src,
+                                                           const int32_t *__restrict__ ids,
+                                                           int64_t n, int64_t d4,
+                                                           float4 *__restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * d4) return;
+  const int64_t i = e / d4, c = e - i * d4;
+  const int64_t id = ids[i];
+  if (id >= 0) dst[id * d4 + c] = src[e];
+}
+
+// ------------------------------------- the owner's ordered sum of row blocks
+// S of the own row block [lo, lo + n_own) from source blocks (ids, rows),
+// added in block order — each block's ids distinct — exactly as a sequence
+// of index_add_ launches would (0 + a, then + b, ...), in one pass: every
+// block's ids are first inverted into a position map pos[q][r] (-1: absent),
+// then one thread per (own row, float4 column) adds the blocks' rows in
+// order, writing each output row once.  Up to kOsMax blocks per pass; more
+// run as further passes that start from the output.
+constexpr int kOsMax = 64;
+struct OsBlocks {
+  const int32_t *ids[kOsMax];
+  const float4 *rows[kOsMax];
+  int64_t off[kOsMax + 1];  // prefix of the block sizes
+  int32_t n;
+};
+
+__global__ __launch_bounds__(256) void os_mark_kernel(OsBlocks b, int64_t lo, int64_t n_own,
+                                                      int32_t *__restrict__ pos) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= b.off[b.n]) return;
+  int q = 0;
+  while (q + 1 < b.n && b.off[q + 1] <= e) ++q;
+  const int64_t i = e - b.off[q];
+  const int64_t r = (int64_t)b.ids[q][i] - lo;
+  if (r >= 0 && r < n_own) pos[q * n_own + r] = (int32_t)i;
+}
+
+__global__ __launch_bounds__(256) void os_sum_kernel(OsBlocks b, const int32_t *__restrict__ pos,
+                                                     int64_t n_own, int64_t d4, int accumulate,
+                                                     float4 *__restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n_own * d4) return;
+  const int64_t r = t / d4, c = t - r * d4;
+  float4 acc = accumulate ? out[t] : f4_zero();
+  for (int q = 0; q < b.n; ++q) {
+    const int32_t i = pos[q * n_own + r];
+    if (i >= 0) acc = f4_add(acc, b.rows[q][(int64_t)i * d4 + c]);
+  }
+  out[t] = acc;
+}
+
 }  // namespace mirec
 
 extern "C" int64_t mirec_distinct_rows_workspace(int64_t n_rows) {
@@ -488,6 +542,69 @@ extern "C" int mirec_mask_compact(const mirec_csr_t *c, const uint8_t *bm, int32
   if (threads > 0) {
     hipLaunchKernelGGL(mask_compact_kernel, dim3((threads + 255) / 256), dim3(256), 0, st, bm,
                        c->rowptr, c->n_rows, narrow_max, list, count, wide_list, wide_count);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
+
+extern "C" int mirec_scatter_rows(const float *src, const int32_t *ids, int64_t n, int32_t dim,
+                                  float *dst, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(n >= 0 && dim > 0 && dim % 4 == 0);
+  if (n == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(src && ids && dst);
+  MIREC_CHECK_ARG(((uintptr_t)src & 15u) == 0 && ((uintptr_t)dst & 15u) == 0);
+  const int64_t d4 = dim / 4;
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)((n * d4 + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4 *>(src),
+                     ids, n, d4, reinterpret_cast<float4 *>(dst));
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int64_t mirec_owner_sum_workspace(int32_t n_blocks, int64_t n_own) {
+  if (n_blocks < 0 || n_own < 0) return -1;
+  return 4 * (int64_t)std::min<int32_t>(std::max<int32_t>(n_blocks, 1), mirec::kOsMax) * n_own;
+}
+
+extern "C" int mirec_owner_sum(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
+                               int64_t n_own, int32_t dim, void *workspace,
+                               size_t workspace_bytes, float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(n_blocks >= 0 && n_own >= 0 && dim > 0 && dim % 4 == 0);
+  MIREC_CHECK_ARG(n_blocks == 0 || blocks);
+  if (n_own == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(out && ((uintptr_t)out & 15u) == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t d4 = dim / 4;
+  if (n_blocks == 0) {
+    MIREC_HIP(hipMemsetAsync(out, 0, (size_t)(n_own * dim) * 4, st));
+    return MIREC_OK;
+  }
+  MIREC_CHECK_ARG(workspace);
+  if ((int64_t)workspace_bytes < mirec_owner_sum_workspace(n_blocks, n_own))
+    return MIREC_ERR_WORKSPACE;
+  int32_t *pos = static_cast<int32_t *>(workspace);
+  for (int32_t q0 = 0; q0 < n_blocks; q0 += kOsMax) {
+    OsBlocks b{};
+    b.n = std::min<int32_t>(kOsMax, n_blocks - q0);
+    b.off[0] = 0;
+    for (int q = 0; q < b.n; ++q) {
+      const mirec_row_block_t &x = blocks[q0 + q];
+      MIREC_CHECK_ARG(x.n >= 0 && (x.n == 0 || (x.ids && x.rows)));
+      MIREC_CHECK_ARG(((uintptr_t)x.rows & 15u) == 0);
+      b.ids[q] = x.ids;
+      b.rows[q] = reinterpret_cast<const float4 *>(x.rows);
+      b.off[q + 1] = b.off[q] + x.n;
+    }
+    MIREC_HIP(hipMemsetAsync(pos, 0xff, (size_t)(4 * b.n * n_own), st));
+    if (b.off[b.n] > 0) {
+      hipLaunchKernelGGL(os_mark_kernel, dim3((unsigned)((b.off[b.n] + 255) / 256)), dim3(256), 0,
+                         st, b, lo, n_own, pos);
+      MIREC_LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(os_sum_kernel, dim3((unsigned)((n_own * d4 + 255) / 256)), dim3(256), 0,
+                       st, b, pos, n_own, d4, q0 > 0 ? 1 : 0, reinterpret_cast<float4 *>(out));
     MIREC_LAUNCH_CHECK();
   }
   return MIREC_OK;

@@ -476,6 +476,41 @@ def export_stamped(tg, parts: int, ws: torch.Tensor | None = None):
     return rows, vals, counts, ws
 
 
+def scatter_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) -> None:
+    """dst[ids[i]] = src[i] (ids distinct int32; mirec_scatter_rows): the
+    install of fetched rows (replaces index_copy_, ~2x its rate)."""
+    from . import _lib
+    from ._lib import check, lib
+    n, d = src.shape
+    if n == 0:
+        return
+    ids = ids.to(torch.int32).contiguous()
+    check(lib.mirec_scatter_rows(src.contiguous().data_ptr(), ids.data_ptr(), n, d,
+                                 dst.data_ptr(), _lib.stream_handle()), "scatter_rows")
+
+
+def owner_sum(sources, lo: int, n_own: int, d: int, device, ws: torch.Tensor | None = None):
+    """S of the own row block from (ids int32, rows [n, d]) source blocks
+    added in list order (each block's ids distinct) — bitwise the sequence of
+    index_add_ calls, in one pass (mirec_owner_sum).  Returns (S [n_own, d],
+    workspace)."""
+    from . import _lib
+    from ._lib import check, lib
+    out = torch.empty(n_own, d, dtype=torch.float32, device=device)
+    arr = (_lib.RowBlock * max(len(sources), 1))()
+    keep = []
+    for a, (ids, rows) in zip(arr, sources):
+        ids, rows = ids.to(torch.int32).contiguous(), rows.contiguous()
+        keep.append((ids, rows))
+        a.ids, a.rows, a.n = ids.data_ptr(), rows.data_ptr(), ids.numel()
+    nb = max(int(lib.mirec_owner_sum_workspace(len(sources), n_own)), 16)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    check(lib.mirec_owner_sum(arr, len(sources), int(lo), int(n_own), int(d), ws.data_ptr(),
+                              ws.numel(), out.data_ptr(), _lib.stream_handle()), "owner_sum")
+    return out, ws
+
+
 def route_ids(ids: torch.Tensor, n_rows: int, group=None):
     """Send every row id to the rank owning it (contiguous blocks of
     n_rows/W rows; ``ids`` ascending int32).  Returns (received ids in
@@ -595,6 +630,7 @@ class DenseGradDataParallel:
         self.comm_events = None  # (start, end) HIP events per collective (bench)
         self.last_exchange_bytes = 0
         self._sr_ws = None        # pipelined fetch: export_stamped's workspace
+        self._os_ws = None        # routed / fetch: owner_sum's position maps
         self._side_stream = None  # pipelined fetch: the routed rows' stream
         if self.world > 1:
             for p in model.parameters():
@@ -695,13 +731,14 @@ class DenseGradDataParallel:
         N, d = p.shape
         n_own = N // self.world
         lo = self.rank * n_own
-        s_own = torch.zeros(n_own, d, dtype=p.dtype, device=p.device)
+        sources = []
         for rid, rv, counts in blocks:
             off = 0
             for c in counts:
                 if c:
-                    s_own.index_add_(0, (rid[off:off + c] - lo).long(), rv[off:off + c])
+                    sources.append((rid[off:off + c], rv[off:off + c]))
                 off += c
+        s_own, self._os_ws = owner_sum(sources, lo, n_own, d, p.device, self._os_ws)
         if self._ones is None or self._ones.numel() != n_own:
             self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
         n_user = min(max(tg.n_user - lo, 0), n_own)
@@ -786,7 +823,7 @@ class DenseGradDataParallel:
         got = torch.empty(need.numel(), d, dtype=p.dtype, device=p.device)
         _a2a(got, rows, sc, rc, group=self.group)
         self._note(a, self._event())
-        p.data.index_copy_(0, need.long(), got)
+        scatter_rows(p.data, need, got)
         self.last_exchange_bytes += need.numel() * d * p.element_size() + \
             (sum(rc) - rc[self.rank]) * 4
 
@@ -852,7 +889,7 @@ class DenseGradDataParallel:
         if f["work"] is not None:
             f["work"].wait()
         self._note(a, self._event())
-        self.model._table_state.param.data.index_copy_(0, f["need"].long(), f["got"])
+        scatter_rows(self.model._table_state.param.data, f["need"], f["got"])
         if k + 1 < len(st["fetch"]):
             self._fetch_issue(k + 1, st)  # in flight while micro-batch k computes
         st["fetch"][k] = None

@@ -285,6 +285,32 @@ int mirec_stamped_rows(const int32_t *stamp, int64_t n_rows, int32_t gen, int32_
                        int32_t *rows, int32_t *counts, void *workspace,
                        size_t workspace_bytes, mirec_stream_t stream);
 
+/* dst[ids[i], :] = src[i, :] for i < n (ids distinct; ids < 0 skipped);
+ * dim % 4 == 0, src and dst 16-byte aligned: the install of the rows a rank
+ * fetched into its local table (replaces index_copy_). */
+int mirec_scatter_rows(const float *src, const int32_t *ids, int64_t n, int32_t dim,
+                       float *dst, mirec_stream_t stream);
+
+/* One source block of rows for mirec_owner_sum: ids[0 .. n) distinct,
+ * rows [n, dim]. */
+typedef struct mirec_row_block {
+  const int32_t *ids;
+  const float *rows;
+  int64_t n;
+} mirec_row_block_t;
+
+/* out[r - lo, :] = sum over the blocks, IN BLOCK ORDER, of rows[i, :] where
+ * ids[i] == r, for every r of the own block [lo, lo + n_own) (0 where no
+ * block has r; ids outside the block ignored) — bitwise the sequence of
+ * index_add_ launches it replaces (the owner side of the data-parallel
+ * table-gradient exchange, dist.DenseGradDataParallel._owner_adam), in one
+ * pass per 64 blocks.  Workspace: mirec_owner_sum_workspace(n_blocks, n_own)
+ * bytes. */
+int64_t mirec_owner_sum_workspace(int32_t n_blocks, int64_t n_own);
+int mirec_owner_sum(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
+                    int64_t n_own, int32_t dim, void *workspace, size_t workspace_bytes,
+                    float *out, mirec_stream_t stream);
+
 /* out[i, :] = src[rows[i], :] for i < *count, the count read on the device
  * (capacity rows of out); dim % 4 == 0, src and out 16-byte aligned. */
 int mirec_gather_rows_counted(const float *src, const int32_t *rows, const int32_t *count,

@@ -3479,6 +3479,42 @@ def test_distinct_rows_matches_unique(n_rows, n, lo, hi):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("n_own,n_blocks,per,d", [(137_500, 16, 60_000, 128), (5000, 70, 300, 8),
+                                                  (1, 3, 1, 4), (4096, 0, 0, 16),
+                                                  (10_000, 5, 0, 8)])
+def test_owner_sum_equals_index_add_sequence(n_own, n_blocks, per, d):
+    """owner_sum (mirec_owner_sum: position maps + one ordered pass per 64
+    blocks) == the index_add_ launches it replaces, bitwise: blocks of
+    distinct ids in and outside the own block, overlapping across blocks,
+    empty blocks, more than 64 blocks."""
+    from furusato_recommend_amd.dist import owner_sum
+    g = torch.Generator(device="cuda").manual_seed(n_own + n_blocks + per + d)
+    lo = 3 * n_own
+    ref = torch.zeros(n_own, d, device="cuda")
+    sources = []
+    for q in range(n_blocks):
+        k = 0 if q % 7 == 3 else min(per, n_own + 50)
+        ids = torch.randperm(n_own + 100, device="cuda", generator=g)[:k].int() + lo - 50
+        rows = torch.randn(k, d, device="cuda", generator=g)
+        sources.append((ids, rows))
+        inside = (ids >= lo) & (ids < lo + n_own)
+        ref.index_add_(0, (ids[inside] - lo).long(), rows[inside])
+    got, _ = owner_sum(sources, lo, n_own, d, torch.device("cuda"))
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("n_rows,n,d", [(1_100_000, 300_000, 128), (4097, 4097, 8), (10, 0, 4)])
+def test_scatter_rows_equals_index_copy(n_rows, n, d):
+    from furusato_recommend_amd.dist import scatter_rows
+    g = torch.Generator(device="cuda").manual_seed(n_rows + n + d)
+    dst = torch.randn(n_rows, d, device="cuda", generator=g)
+    ids = torch.randperm(n_rows, device="cuda", generator=g)[:n].int()
+    src = torch.randn(n, d, device="cuda", generator=g)
+    ref = dst.clone().index_copy_(0, ids.long(), src)
+    scatter_rows(dst, ids, src)
+    assert torch.equal(dst, ref)
+
+
 @pytest.mark.parametrize("n_rows,n", [(1_100_000, 880_000), (4097, 10_000), (1, 5), (70_001, 0)])
 def test_distinct_rows_unseen_excludes_earlier_sets(n_rows, n):
     """distinct_rows(..., have=map) over three id lists (the pipelined

@@ -142,7 +142,7 @@ def main():
 
 def sage_main(args):
     from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
-    from furusato_recommend_amd.dist import DenseGradDataParallel
+    from furusato_recommend_amd.dist import DenseGradDataParallel, scatter_rows
     dev = torch.device("cuda:0")
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0)
     torch.manual_seed(2020)
@@ -193,7 +193,7 @@ def sage_main(args):
                 uniq = torch.unique(ids[ids >= 0])
                 need = uniq[uniq >= n_own].long()
                 fetched[0] = need.numel()
-                m._table.data.index_copy_(0, need, m._table.data.index_select(0, need))
+                scatter_rows(m._table.data, need, m._table.data.index_select(0, need))
 
             def hook():
                 if ex != "dense":
@@ -278,7 +278,8 @@ def sage_pipelined(args, m, W, C, base, rates):
     first micro-batch's rows are exposed, micro-batch k + 1's rows and
     micro-batch k - 1's routed rows overlap micro-batch k's compute (HIP
     events around it), the last micro-batch's routed rows are exposed."""
-    from furusato_recommend_amd.dist import DenseGradDataParallel, distinct_rows, export_stamped
+    from furusato_recommend_amd.dist import (DenseGradDataParallel, distinct_rows, export_stamped,
+                                             scatter_rows)
     dev = torch.device("cuda:0")
     side = torch.cuda.Stream(device=dev)
     B = args.batch
@@ -320,7 +321,7 @@ def sage_pipelined(args, m, W, C, base, rates):
     def chunk_hook(k, phase):
         if phase == "pre":
             need, rows = rec["need"][k]
-            m._table.data.index_copy_(0, need, rows)
+            scatter_rows(m._table.data, need, rows)
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             rec["ev"].append([e])
