@@ -489,6 +489,20 @@ def scatter_rows(dst: torch.Tensor, ids: torch.Tensor, src: torch.Tensor) -> Non
                                  dst.data_ptr(), _lib.stream_handle()), "scatter_rows")
 
 
+def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
+    """table[ids] for int32 ids (mirec_gather_rows): the owner side's
+    gather of requested rows (replaces index_select)."""
+    from . import _lib
+    from ._lib import check, lib
+    ids = ids.to(torch.int32).contiguous()
+    n, d = ids.numel(), table.shape[1]
+    out = torch.empty(n, d, dtype=table.dtype, device=table.device)
+    if n:
+        check(lib.mirec_gather_rows(table.data_ptr(), ids.data_ptr(), n, d, out.data_ptr(),
+                                    _lib.stream_handle()), "gather_rows")
+    return out
+
+
 def owner_sum(sources, lo: int, n_own: int, d: int, device, ws: torch.Tensor | None = None):
     """S of the own row block from (ids int32, rows [n, d]) source blocks
     added in list order (each block's ids distinct) — bitwise the sequence of
@@ -819,7 +833,7 @@ class DenseGradDataParallel:
         need = distinct_rows(ids, N, lo, lo + n_own)
         a = self._event()
         req, rc, sc = route_ids(need, N, self.group)
-        rows = p.data.index_select(0, req.long())
+        rows = gather_rows(p.data, req)
         got = torch.empty(need.numel(), d, dtype=p.dtype, device=p.device)
         _a2a(got, rows, sc, rc, group=self.group)
         self._note(a, self._event())
@@ -867,7 +881,7 @@ class DenseGradDataParallel:
             need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, lo, lo + n_own,
                                  have=have if len(trees) > 1 else None)
             req, rc, sc = route_ids(need, N, self.group)
-            rows = p.data.index_select(0, req.long())  # owner side: the current rows
+            rows = gather_rows(p.data, req)  # owner side: the current rows
             st["fetch"].append({"need": need, "rows": rows, "rc": rc, "sc": sc})
             self.last_exchange_bytes += need.numel() * d * p.element_size() + \
                 (sum(rc) - rc[self.rank]) * 4

@@ -142,7 +142,7 @@ def main():
 
 def sage_main(args):
     from furusato_recommend_amd import GraphSAGE, SyntheticBipartite
-    from furusato_recommend_amd.dist import DenseGradDataParallel, scatter_rows
+    from furusato_recommend_amd.dist import DenseGradDataParallel, gather_rows, scatter_rows
     dev = torch.device("cuda:0")
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=0)
     torch.manual_seed(2020)
@@ -193,7 +193,7 @@ def sage_main(args):
                 uniq = torch.unique(ids[ids >= 0])
                 need = uniq[uniq >= n_own].long()
                 fetched[0] = need.numel()
-                scatter_rows(m._table.data, need, m._table.data.index_select(0, need))
+                scatter_rows(m._table.data, need, gather_rows(m._table.data, need))
 
             def hook():
                 if ex != "dense":
@@ -279,7 +279,7 @@ def sage_pipelined(args, m, W, C, base, rates):
     micro-batch k - 1's routed rows overlap micro-batch k's compute (HIP
     events around it), the last micro-batch's routed rows are exposed."""
     from furusato_recommend_amd.dist import (DenseGradDataParallel, distinct_rows, export_stamped,
-                                             scatter_rows)
+                                             gather_rows, scatter_rows)
     dev = torch.device("cuda:0")
     side = torch.cuda.Stream(device=dev)
     B = args.batch
@@ -314,7 +314,7 @@ def sage_pipelined(args, m, W, C, base, rates):
             need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own, have=have)
             # the owners' gather of the requested rows (rank 0 serves a share of
             # the same size) and the install after the transfer
-            rec["need"].append((need.long(), m._table.data.index_select(0, need.long())))
+            rec["need"].append((need.long(), gather_rows(m._table.data, need)))
             rec["fetch_rows"].append(need.numel())
         rec["ev"] = []
 
