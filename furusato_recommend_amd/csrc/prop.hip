@@ -233,23 +233,6 @@ __device__ __forceinline__ float4 combine_groups(float4 s) {
   return s;
 }
 
-// MIREC_PROP_ADAM_NT: the fused Adam's W / m / v loads non-temporal (each
-// read once per step).  Off: C2 4.844 / 4.844 ms per step with ordinary
-// loads, 4.868 / 4.854 with these (profiles/round4_prop_adam_nt.txt) — unlike
-// the table Adam's pure stream, here the loads follow the row's gather
-#ifndef MIREC_PROP_ADAM_NT
-#define MIREC_PROP_ADAM_NT 0
-#endif
-typedef float prop_f4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 adam_ld4(const float *p) {
-#if MIREC_PROP_ADAM_NT
-  const prop_f4 x = __builtin_nontemporal_load(reinterpret_cast<const prop_f4 *>(p));
-  return make_float4(x.x, x.y, x.z, x.w);
-#else
-  return ld4(p);
-#endif
-}
-
 template <int D>
 __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4 s, int sub) {
   const float di = a.dinv[row];
@@ -266,7 +249,7 @@ __device__ __forceinline__ void row_epilogue(const PropK &a, int64_t row, float4
   if (a.divisor != 1.f) o = f4_div(o, a.divisor);
   if (a.seed2 != nullptr && sl >= 0) o = f4_add(o, ld4(a.seed2 + (int64_t)sl * D + sub * 4));
   if (a.param != nullptr) {
-    float4 p = adam_ld4(a.param + off), m = adam_ld4(a.m + off), v = adam_ld4(a.v + off);
+    float4 p = ld4(a.param + off), m = ld4(a.m + off), v = ld4(a.v + off);
     adam_elem(p.x, m.x, v.x, o.x, a.adam);
     adam_elem(p.y, m.y, v.y, o.y, a.adam);
     adam_elem(p.z, m.z, v.z, o.z, a.adam);
@@ -396,7 +379,7 @@ constexpr int64_t kListBlocks = 4096;  // 2 x the waves resident at 8/SIMD
 // VGPRs so 7-8 waves per SIMD keep enough gathers in flight.
 template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIREC_PROP_MIN_WAVES, 8)))
-void prop_kernel(PropK a) {
+MIREC_NO_PK_F32 void prop_kernel(PropK a) {
   constexpr int G = 64 / (D / 4);
   // wave index made provably uniform (SGPR): loop control stays scalar
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -315,3 +315,186 @@ def _after_load(model, dp):
             s.stale_rows = False
     if dp is not None and hasattr(dp, "_norms_next"):
         dp._norms_next = None
+
+
+# ------------------------------------------------------------------ launcher
+# ``python -m furusato_recommend_amd.train_dp --model lgn --gpus 8 ...``
+# replaces ``if __name__ == '__main__': mp.spawn(demo, nprocs=world_size)``
+# (ddp_lgcn.py:760-768, ddp_sage.py:892-899).  With --gpus N > 1 and no
+# WORLD_SIZE in the environment the parent starts torch.distributed.run as
+# a child process (N ranks, one per GPU, 127.0.0.1 rendezvous) and exits
+# with its status; the parent never touches the GPU.  Each rank builds the
+# dataset and the model, wraps it and runs DPTrainer.fit.  Option names are
+# the reference's (parse.py:4-64; ddp_lgcn.py:636-656 for the DDP values).
+
+def parse_args(argv=None):
+    import argparse
+    ap = argparse.ArgumentParser(
+        prog="python -m furusato_recommend_amd.train_dp",
+        description="Data-parallel BPR training (ddp_lgcn.py / ddp_sage.py on MI355X)")
+    ap.add_argument("--model", default="lgn", help="registry name: lgn | sage | sasrec | mf")
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one process per GPU)")
+    ap.add_argument("--epochs", type=int, default=200, help="ddp_lgcn.py:667 range(200)")
+    ap.add_argument("--bpr_batch", type=int, default=20000, help="per-rank batch (ddp_lgcn.py:646)")
+    ap.add_argument("--recdim", type=int, default=32, help="ddp_lgcn.py:647")
+    ap.add_argument("--layer", type=int, default=2, help="ddp_lgcn.py:648")
+    ap.add_argument("--lr", type=float, default=1e-3, help="ddp_lgcn.py:653")
+    ap.add_argument("--decay", type=float, default=1e-4, help="ddp_lgcn.py:645")
+    ap.add_argument("--num_neighbors", type=int, default=5, help="GraphSAGE fanout per hop")
+    ap.add_argument("--testbatch", type=int, default=1000, help="test_u_batch_size")
+    ap.add_argument("--topks", default="[10,20]")
+    ap.add_argument("--test_span", type=int, default=TEST_SPAN)
+    ap.add_argument("--test_count", type=int, default=TEST_COUNT,
+                    help="test batches per evaluation (ddp_lgcn.py:710); -1 = all users")
+    ap.add_argument("--train_iterative", type=int, default=TRAIN_ITERATIVE)
+    ap.add_argument("--positive_num_limit", type=int, default=POSITIVE_NUM_LIMIT)
+    ap.add_argument("--seed", type=int, default=2020)
+    ap.add_argument("--path", default="./checkpoints",
+                    help="checkpoint directory: <path>/ddp_<model>_<suffix>.pth")
+    ap.add_argument("--suffix", default="all")
+    ap.add_argument("--data", default=None,
+                    help="directory holding <suffix>/train<suffix>.txt and test<suffix>.txt "
+                         "(dataloader.py format)")
+    ap.add_argument("--synthetic", default=None,
+                    help="n_users,m_items,n_edges[,kind] instead of --data "
+                         "(SyntheticBipartite; kind uniform | zipf | cluster)")
+    ap.add_argument("--dp_mode", default=None,
+                    help="gradient exchange (LightGCN: auto | sparse | dense | sharded; "
+                         "GraphSAGE / SASRec: the table exchange)")
+    ap.add_argument("--backend", default=None, choices=("nccl", "gloo"),
+                    help="default nccl (RCCL) on GPUs, gloo with --device cpu")
+    ap.add_argument("--device", default="cuda", choices=("cuda", "cpu"))
+    ap.add_argument("--rehearse", action="store_true",
+                    help="every rank on cuda:0 over gloo (the N-rank path on one GPU)")
+    ap.add_argument("--factory", default=None,
+                    help="module:callable(config, dataset, rank, world) -> model, or a dict "
+                         "with 'model' and optionally 'dp', 'sampler', 'evaluator' "
+                         "(a model plugin outside the registry)")
+    ap.add_argument("--log", default=None, help="rank 0 appends one JSON line per epoch here")
+    return ap.parse_args(argv)
+
+
+def needs_launch(args, env=os.environ) -> bool:
+    return args.gpus > 1 and "WORLD_SIZE" not in env
+
+
+def launch_command(args, argv: list, port: int) -> list:
+    import sys
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+            "--master-port", str(port), "-m", "furusato_recommend_amd.train_dp", *argv]
+
+
+def launch(args, argv: list, runner=None) -> int:
+    """Start the ranks as a child process tree (nothing here initialises
+    HIP) and return their exit status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = os.pathsep.join(p for p in (root, env.get("PYTHONPATH")) if p)
+    if "OMP_NUM_THREADS" not in env:
+        env["OMP_NUM_THREADS"] = str(max(1, min(os.cpu_count() or 1, 64) // args.gpus))
+    r = (runner or subprocess.run)(launch_command(args, argv, port), env=env)
+    return int(r.returncode)
+
+
+def build_config(args, device: str) -> dict:
+    import ast
+    return {
+        "device": device, "bpr_batch_size": args.bpr_batch, "recdim": args.recdim,
+        "latent_dim_rec": args.recdim, "layer": args.layer, "lr": args.lr,
+        "decay": args.decay, "num_neighbors": args.num_neighbors,
+        "test_u_batch_size": args.testbatch, "topks": tuple(ast.literal_eval(args.topks)),
+        "test_span": args.test_span,
+        "test_count": None if args.test_count < 0 else args.test_count,
+        "train_iterative": args.train_iterative,
+        "positive_num_limit": args.positive_num_limit, "seed": args.seed,
+        "suffix": args.suffix, "dp_mode": args.dp_mode,
+        "checkpoint_path": os.path.join(args.path, f"ddp_{args.model}_{args.suffix}.pth"),
+    }
+
+
+def build_dataset(args, config: dict):
+    from .dataloader import Loader, SyntheticBipartite
+    if (args.data is None) == (args.synthetic is None):
+        raise SystemExit("train_dp: give exactly one of --data DIR or --synthetic n,m,e[,kind]")
+    if args.data is not None:
+        return Loader({"suffix": args.suffix}, path=args.data)
+    f = args.synthetic.split(",")
+    kind = f[3] if len(f) > 3 else "uniform"
+    return SyntheticBipartite(int(f[0]), int(f[1]), int(f[2]), seed=0, kind=kind)
+
+
+def _resolve(spec: str):
+    import importlib
+    mod, _, fn = spec.partition(":")
+    return getattr(importlib.import_module(mod), fn)
+
+
+def run_rank(args) -> list:
+    """One rank: process group (when launched with WORLD_SIZE), dataset,
+    model, DPTrainer.fit; rank 0 prints one JSON line per epoch."""
+    import json
+    from .dist import init_distributed
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    on_cpu = args.device == "cpu"
+    backend = args.backend or ("gloo" if (on_cpu or args.rehearse) else "nccl")
+    if on_cpu:
+        device = "cpu"
+    else:
+        device = f"cuda:{0 if args.rehearse else local}"
+        torch.cuda.set_device(torch.device(device))
+    if world > 1:
+        init_distributed(backend, device=None if (on_cpu or backend == "gloo")
+                         else torch.device(device))
+    rank, _ = _rank_world()
+    try:
+        config = build_config(args, device)
+        ds = build_dataset(args, config)
+        torch.manual_seed(args.seed)
+        parts = {}
+        if args.factory:
+            made = _resolve(args.factory)(config, ds, rank, world)
+            parts = made if isinstance(made, dict) else {"model": made}
+        else:
+            from .register import MODELS
+            if args.model not in MODELS:
+                raise SystemExit(f"train_dp: unknown model {args.model!r} "
+                                 f"(known: {sorted(MODELS)})")
+            parts = {"model": MODELS[args.model](config, ds)}
+
+        def log(rec):
+            if rank != 0:
+                return
+            line = json.dumps({"model": args.model, "world": world, **rec})
+            print(line, flush=True)
+            if args.log:
+                with open(args.log, "a") as f:
+                    f.write(line + "\n")
+        tr = DPTrainer(config, ds, parts["model"], dp=parts.get("dp"), sampler=parts.get("sampler"),
+                       evaluator=parts.get("evaluator"), log=log)
+        return tr.fit(args.epochs)
+    finally:
+        if world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def main(argv=None) -> int:
+    import sys
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if needs_launch(args):
+        return launch(args, argv)
+    run_rank(args)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

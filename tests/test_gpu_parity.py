@@ -2031,16 +2031,16 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
     every pooled user row (the longest, the length-5 ones and every pack
     boundary among them), the loss, and the gradient of every parameter
     (the item table's formed from its sorted form, as the fused Adam forms
-    it).  Rows and loss at 1e-4 relative.  Each gradient at 1e-4 relative,
-    or — where the reference's own float32 arithmetic (the same step on the
-    host in float32) is itself farther than that from the exact step — within
-    4x of that float32 error: the blocks' ReLU((x + attn)) puts ~10^7
-    elements through a kink, and the ones within rounding of zero flip their
-    mask between any two float32 orders, so a gradient that sums them (the
-    block weights', the sequence items' table rows) is only as determined as
-    float32 makes it.  The item tower's last bias has an exactly zero
-    gradient (it adds <u, b> to both scores); its rounding noise is bounded
-    against its weight's gradient instead."""
+    it).  Rows and loss at 1e-4 relative to float64.  Every gradient at 1e-4
+    relative to the reference's own float32 step on the host (the north
+    star's criterion); the float64 errors of both are printed beside it.
+    They are not the gate: a handful of the ~1.4e7 ReLU((x + attn))
+    pre-activations lie within the float32 error of the attention output
+    (|pre| ~ 1e-7 on operands ~1e-2..0.3), and both float32 paths take the
+    other mask there than float64 does (DESIGN §9.5 names the elements).
+    The item tower's last bias has an exactly zero gradient (it adds
+    <u, b> to both scores); its rounding noise is bounded against its
+    weight's gradient instead."""
     from furusato_recommend_amd import SASRec
     from furusato_recommend_amd.sasrec import SequenceData
 
@@ -2083,17 +2083,20 @@ def test_sasrec_c4_batch_step_matches_float64_oracle():
         b = g_ref[n_]
         if n_ == "item_last_proj.bias":
             scale = float(g_ref["item_last_proj.weight"].abs().max())
-            err = lambda a: float((a - b).abs().max()) / scale  # noqa: E731
+            err = lambda a, b: float((a - b).abs().max()) / scale  # noqa: E731
         else:
-            err = lambda a: rel(a, b)  # noqa: E731
+            err = rel
         a = got[n_].double().cpu()
-        errs[n_] = (err(a), err(g32[n_]), rel(a, g32[n_]))
-        if errs[n_][0] >= max(TOL, 4 * errs[n_][1]):
+        # hip vs the reference's own float32 step on the host is the gate
+        # (north star: "match the reference CPU path within 1e-4 rel fp32");
+        # float64 is printed as the sanity check beside it.
+        errs[n_] = (err(a, b), err(g32[n_], b), err(a, g32[n_]))
+        if errs[n_][2] >= TOL:
             bad.append(n_)
     print("gradient rel err (hip vs float64, host fp32 vs float64, hip vs host fp32):", errs)
     diag = None
     if "item_id_embedding.weight" in bad:  # where the table's rows differ
-        a, b = got["item_id_embedding.weight"].double().cpu(), g_ref["item_id_embedding.weight"]
+        a, b = got["item_id_embedding.weight"].double().cpu(), g32["item_id_embedding.weight"]
         e = (a - b).abs().max(1).values
         top = torch.topk(e, 5).indices.tolist()
         seq_ids = m.seq.items[u].cpu()

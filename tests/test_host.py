@@ -399,6 +399,82 @@ def test_dp_trainer_two_ranks_gloo(golden, tmp_path):
     assert os.path.exists(ckpt) and os.path.exists(ckpt + ".train")
 
 
+def _write_split(golden, root):
+    """The lgcn_d64_L3 fixture's graph as the reference's text files
+    (dataloader.py:73-173: ``uid i1 i2 ...`` per line, suffix 'all')."""
+    f = golden("lgcn_d64_L3.npz")
+    tu, ti, nu = f["train_user"], f["train_item"], int(f["n_users"])
+    d = root / "all"
+    d.mkdir(parents=True)
+    with open(d / "trainall.txt", "w") as fh:
+        for u in range(nu):
+            fh.write(" ".join(str(x) for x in [u, *ti[tu == u].tolist()]) + "\n")
+    with open(d / "testall.txt", "w") as fh:
+        for u in range(0, nu, 3):
+            its = ti[tu == u]
+            if len(its):
+                fh.write(f"{u} {int(its[0])}\n")
+
+
+def test_train_dp_cli_two_ranks_gloo(golden, tmp_path):
+    """``python -m furusato_recommend_amd.train_dp --gpus 2`` (the mp.spawn
+    entry point of ddp_lgcn.py:760-768): the parent starts
+    torch.distributed.run as a child, the 2 ranks meet over gloo on CPU and
+    run DPTrainer over the real DataParallel (the model plugin is the
+    oracle-backed test model): an epoch, an evaluation, a checkpoint at
+    <path>/ddp_lgn_all.pth; a second invocation resumes from it."""
+    import json
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    _write_split(golden, tmp_path / "data")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    ck = tmp_path / "ck"
+    cmd = [sys.executable, "-m", "furusato_recommend_amd.train_dp", "--model", "lgn",
+           "--gpus", "2", "--device", "cpu", "--data", str(tmp_path / "data"),
+           "--recdim", "16", "--layer", "3", "--bpr_batch", "16", "--test_span", "1",
+           "--path", str(ck), "--factory", "tests.dp_cli_factory:make", "--epochs"]
+    runs = []
+    for epochs in ("1", "1"):
+        r = subprocess.run(cmd + [epochs], env=env, cwd=ROOT, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr[-3000:]
+        runs.append([json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")])
+    (a,), (b,) = runs  # rank 0 prints one line per epoch
+    assert a["epoch"] == 0 and b["epoch"] == 1 and a["world"] == 2
+    assert a["triples_per_rank"] > 0 and np.isfinite(a["loss"])
+    for rec in (a, b):
+        for k in ("recall", "precision", "ndcg", "hr", "coverage"):
+            assert len(rec["metrics"][k]) == 2 and all(np.isfinite(rec["metrics"][k]))
+    p = ck / "ddp_lgn_all.pth"
+    assert p.exists()
+    assert torch.load(str(p) + ".train", weights_only=True)["epoch"] == 1
+
+
+def test_train_dp_cli_launch_command():
+    """The launcher's child command and environment (no processes)."""
+    from furusato_recommend_amd import train_dp as T
+    a = T.parse_args(["--model", "sage", "--gpus", "8"])
+    assert T.needs_launch(a, env={}) and not T.needs_launch(a, env={"WORLD_SIZE": "8"})
+    assert not T.needs_launch(T.parse_args([]), env={})
+    seen = {}
+
+    class R:
+        returncode = 3
+    assert T.launch(a, ["--model", "sage", "--gpus", "8"],
+                    runner=lambda cmd, env: seen.update(cmd=cmd, env=env) or R()) == 3
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=8" in cmd
+    assert cmd[cmd.index("-m", 3):][:2] == ["-m", "furusato_recommend_amd.train_dp"]
+    assert cmd[-4:] == ["--model", "sage", "--gpus", "8"] and "127.0.0.1" in cmd
+    assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    cfg = T.build_config(T.parse_args(["--model", "sage", "--suffix", "x", "--path", "/c"]), "cuda:0")
+    assert cfg["checkpoint_path"] == "/c/ddp_sage_x.pth" and cfg["topks"] == (10, 20)
+    assert cfg["bpr_batch_size"] == 20000 and cfg["decay"] == 1e-4 and cfg["lr"] == 1e-3
+
+
 def _calib_worker(rank, world, port, fpath, q, prefer):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
