@@ -674,9 +674,9 @@ class GraphSAGE(nn.Module):
         fetch).  ``chunks`` = C > 1 (with ``chunk_hook``, the pipelined fetch
         exchange): the batch as C micro-batches of its triples, one tree each
         (``chunk_seeds``), all sampled first (``tree_hook`` gets the list),
-        then per micro-batch ``chunk_hook(k, "pre")``, forward, loss x 1/C
-        (the norm term x 1/C too: the C gradients sum to the batch's),
-        backward, ``chunk_hook(k, "post")`` — the hook exports each
+        then per micro-batch ``chunk_hook(k, "pre")``, forward, loss
+        weighted so the micro-batches' gradients sum to the batch's
+        (``_stage_chunks``), backward, ``chunk_hook(k, "post")`` — the hook exports each
         micro-batch's table-gradient rows before the next overwrites them."""
         seed = self._step_seed * 7919 + self._calls
         self._calls += 1
@@ -729,8 +729,21 @@ class GraphSAGE(nn.Module):
 
     def _stage_chunks(self, users, pos, neg, seed, grad_hook, loss_scale, tree_hook, C,
                       chunk_hook):
+        """The batch's B triples as C_eff = min(C, B) micro-batches of B_k
+        triples.  Micro-batch k's loss is mean_k softplus + decay·all_param /
+        B_k · s; its backward is seeded with loss_scale · B_k / B and s =
+        1 / C_eff, so the summed gradients are exactly the whole batch's
+        (Σ_k B_k/B · mean_k = mean over B; Σ_k B_k/B · s / B_k = 1/B) for any
+        B, divisible by C or not; the returned loss is the same weighted sum.
+        C_eff depends only on B, which every data-parallel rank shares (equal
+        batch sizes), so every rank runs the same number of chunk hooks
+        (collectives)."""
         users, pos, neg = (torch.as_tensor(t).to(self.device) for t in (users, pos, neg))
-        bnd = self.chunk_bounds(int(users.numel()), C)
+        B = int(users.numel())
+        if B == 0:
+            raise ValueError("empty batch")
+        C = min(int(C), B)
+        bnd = self.chunk_bounds(B, C)
         trees = []
         for k in range(C):
             a, b = bnd[k], bnd[k + 1]
@@ -745,16 +758,17 @@ class GraphSAGE(nn.Module):
         for k, tree in enumerate(trees):
             chunk_hook(k, "pre")
             sk = self.chunk_seed(seed, k)
+            w = (bnd[k + 1] - bnd[k]) / B
             emb = self.forward(tree, dropout_seed=sk if self.training else None)
             loss = self.loss_fused(emb, decay_scale=1.0 / C)
             with _BWD_ON_CALLER():
-                loss.backward(one * (loss_scale / C))
-            total += loss.detach()
+                loss.backward(one * (loss_scale * w))
+            total += loss.detach() * w
             chunk_hook(k, "post")
         if grad_hook is not None:
             grad_hook()
         self.optimizer_step()
-        return total / C
+        return total
 
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])

@@ -221,7 +221,8 @@ class DPTrainer:
         torch.save(sd, path + ".tmp")
         os.replace(path + ".tmp", path)
         opt = [_to_cpu(s.state_dict()) for s in optimizer_states(self.model)]
-        torch.save({"epoch": int(epoch), "optim": opt, "max_recall": float(self.max_recall)},
+        torch.save({"epoch": int(epoch), "optim": opt, "max_recall": float(self.max_recall),
+                    "counters": _step_counters(self.model)},
                    self._train_state_path() + ".tmp")
         os.replace(self._train_state_path() + ".tmp", self._train_state_path())
 
@@ -241,6 +242,8 @@ class DPTrainer:
                 s.load_state_dict(o)
             self.epoch = int(st["epoch"]) + 1
             self.max_recall = float(st.get("max_recall", 0.0))
+            for k, v in st.get("counters", {}).items():
+                setattr(self.model, k, int(v))
         _after_load(self.model, self.dp)
         return True
 
@@ -304,9 +307,23 @@ def _to_cpu(x):
     return x
 
 
+# Per-step counters that seed a model's step (GraphSAGE: every step's tree
+# and dropout seed is _step_seed * 7919 + _calls): kept in the .train file
+# so a resumed run draws what an uninterrupted one would have.
+STEP_COUNTERS = ("_calls", "_step_seed")
+
+
+def _step_counters(model) -> dict:
+    return {k: int(getattr(model, k)) for k in STEP_COUNTERS
+            if isinstance(getattr(model, k, None), int)}
+
+
 def _after_load(model, dp):
     """After a checkpoint load: a fused engine forgets its cached dinv ⊙ E;
-    the wrappers' row-sharded state is whole again on every rank."""
+    the wrappers' row-sharded state is whole again on every rank, and so is
+    a ``fetch``-exchange table (the loaded table is the full one)."""
+    if getattr(model, "table_stale", False):
+        model.table_stale = False
     eng = getattr(model, "engine", None)
     if eng is not None and hasattr(eng, "invalidate_prescaled"):
         eng.invalidate_prescaled()

@@ -2733,7 +2733,7 @@ def test_dense_grad_data_parallel_two_ranks(kind):
 
 
 def _dp_rank_union(rank, world, port, kind, exchange, q, over=None, bucket_min=None, steps=3,
-                   microbatches=1):
+                   microbatches=1, sizes=None):
     """One rank of DenseGradDataParallel (GraphSAGE / SASRec) on cuda:0 with
     the table exchange ``exchange``; returns what the single-process
     reference step needs (the batches, the CPU generator states SASRec's
@@ -2759,7 +2759,7 @@ def _dp_rank_union(rank, world, port, kind, exchange, q, over=None, bucket_min=N
             assert dp.table_stepped_by_hook()  # the row-sharded table Adam
         batches, states, losses = [], [], []
         for i in range(steps):
-            u, p, n = _union_batch(m, ds, kind, i, rank, world)
+            u, p, n = _union_batch(m, ds, kind, i, rank, world, sizes[i] if sizes else 256)
             batches.append([torch.as_tensor(x).cpu().numpy() for x in (u, p, n)])
             states.append(torch.get_rng_state().numpy().copy())
             losses.append(float(dp.step(u, p, n)))
@@ -2782,9 +2782,9 @@ def _union_model(kind, **over):
     return (GraphSAGE(cfg, ds) if kind == "sage" else SASRec(cfg, ds)), ds
 
 
-def _union_batch(m, ds, kind, i, rank, world):
+def _union_batch(m, ds, kind, i, rank, world, n=256):
     if kind == "sage":
-        return m.sample(256, seed=5, offset=i * 256, shard=rank, n_shards=world)
+        return m.sample(n, seed=5, offset=i * 256, shard=rank, n_shards=world)
     g = torch.Generator().manual_seed(1000 * i + rank)
     u = torch.randint(0, ds.n_users // world, (256,), generator=g) * world + rank
     return u, torch.randint(0, ds.m_items, (256,), generator=g), \
@@ -2872,8 +2872,62 @@ def test_dense_grad_data_parallel_equals_union_step(kind, exchange):
     assert res[0][4] > 0  # bytes received in the last step's exchange
 
 
+@pytest.mark.parametrize("B", [256, 100, 2])
+def test_sage_microbatch_gradient_equals_batch_gradient(B):
+    """GraphSAGE.stageOne(chunks=3) on one process (the pipelined exchange's
+    micro-batching, hooks doing nothing): the gradients summed over the
+    micro-batches equal the gradient of the UNCHUNKED batch loss
+    (model/graphsage.py:326-337: mean over all B triples of softplus, plus
+    decay x all_param / B once), written out here in plain torch over the
+    same micro-batch trees, for B divisible by 3, not divisible, and B < 3
+    (two micro-batches); the returned loss is that loss.  1e-5 relative
+    (fp32 summation order)."""
+    import torch.nn.functional as F
+    m, _ = _union_model("sage")
+    m._tg.dense = True  # the table gradient lands in .grad (sums over backwards)
+    params = list(m.parameters())
+    u, p, n = m.sample(B, seed=9, offset=0)
+    u, p, n = u.long(), p.long(), n.long()
+    seed = m._step_seed * 7919 + m._calls
+    C = min(3, B)
+    bnd = m.chunk_bounds(B, C)
+    for x in params:
+        x.grad = None
+    ref_loss = 0.0
+    for k in range(C):
+        a, b = bnd[k], bnd[k + 1]
+        sk = m.chunk_seed(seed, k)
+        seeds = torch.cat([u[a:b], p[a:b] + m.n_user, n[a:b] + m.n_user]).int()
+        emb = m.forward(m.sample_tree(seeds, sk), dropout_seed=sk)
+        m._slice_norms2 = None
+        bk = b - a
+        ue, pe, ne = emb[:bk], emb[bk:2 * bk], emb[2 * bk:]
+        part = F.softplus((ue * ne).sum(1) - (ue * pe).sum(1)).sum() / B
+        part.backward()
+        ref_loss += float(part)
+    all_param = 0
+    for prm in m.reg_parameters():  # graphsage.py:329-332 (doubling)
+        all_param = all_param + all_param + prm.norm(2)
+    norm_term = all_param / B * m.config["decay"]
+    norm_term.backward()
+    ref_loss += float(norm_term)
+    ref = [x.grad.detach().clone() for x in params]
+    got = {}
+
+    def grab():
+        got["g"] = [x.grad.detach().clone() for x in params]
+    loss = m.stageOne(u, p, n, chunks=3, chunk_hook=lambda k, phase: None, grad_hook=grab)
+    assert m._calls == 1
+    for (nm, _), a, b in zip(m.named_parameters(), got["g"], ref):
+        assert rel(a, b) < 1e-5, (nm, rel(a, b))
+    assert abs(float(loss) - ref_loss) <= 1e-5 * abs(ref_loss)
+
+
+CHUNK_SIZES = (256, 100, 2)  # 85/85/86, 33/33/34, and fewer triples than micro-batches
+
+
 def _dp_rank_union_chunks(rank, world, port, q):
-    _dp_rank_union(rank, world, port, "sage", "fetch", q, microbatches=3)
+    _dp_rank_union(rank, world, port, "sage", "fetch", q, microbatches=3, sizes=CHUNK_SIZES)
 
 
 @pytest.mark.timeout(900)
@@ -2882,33 +2936,38 @@ def test_pipelined_fetch_equals_union_microbatches():
     every micro-batch's read set routed up front, micro-batch k + 1's rows
     and micro-batch k's table-gradient rows in flight while the other
     computes), 2 ranks on one GPU, against ONE process that takes, at the
-    same parameters, each rank's micro-batch gradients (loss x 1/(2 x 3), the
-    norm term x 1/3 — GraphSAGE.stageOne(chunks=3)'s seeds), sums them and
-    steps the dense Adam: every parameter at 1e-6 on every element whose
-    exact gradient is non-zero, over 3 steps (the routed sums are added in
-    another order: fp32 rounding)."""
+    same parameters, each rank's micro-batch gradients (micro-batch k of B_k
+    of the B triples seeded with 1/2 x B_k/B, its norm term x 1/C_eff:
+    GraphSAGE.stageOne(chunks=3)'s weights), sums them and steps the dense
+    Adam, over 3 steps of 256, 100 and 2 triples per rank (B % 3 != 0, and
+    B < 3: two micro-batches, the same count on both ranks): every
+    parameter at 1e-5 relative (the routed sums are added in another order:
+    fp32 rounding).  test_sage_microbatch_gradient_equals_batch_gradient
+    checks those weights against the unchunked batch loss."""
     res = _run_ranks(_dp_rank_union_chunks, ())
     for a, b in zip(res[0][0], res[1][0]):
         assert np.array_equal(a, b)
     m, ds = _union_model("sage")
     m._tg.dense = True
     params = list(m.parameters())
-    C = 3
     for i in range(3):
         grads = []
         for r in (0, 1):
             u, p, n = (torch.from_numpy(x).cuda() for x in res[r][1][i])
+            assert u.numel() == CHUNK_SIZES[i]
             for x in params:
                 x.grad = None
             seed = m._step_seed * 7919 + i
-            bnd = m.chunk_bounds(u.numel(), C)
+            B = u.numel()
+            C = min(3, B)
+            bnd = m.chunk_bounds(B, C)
             for k in range(C):
                 a, b = bnd[k], bnd[k + 1]
                 sk = m.chunk_seed(seed, k)
                 seeds = torch.cat([u[a:b].int(), p[a:b].int() + m.n_user, n[a:b].int() + m.n_user])
                 emb = m.forward(m.sample_tree(seeds, sk), dropout_seed=sk)
                 m.loss_fused(emb, decay_scale=1.0 / C).backward(
-                    torch.tensor(0.5 / C, device="cuda"))
+                    torch.tensor(0.5 * (b - a) / B, device="cuda"))
             grads.append([x.grad.clone() for x in params])
         for x, g0, g1 in zip(params, *grads):
             x.grad = g0 + g1
@@ -2958,8 +3017,10 @@ def _dp_trainer_rank(rank, world, port, kind, ckpt, q):
         same = all(torch.equal(a.cpu(), b.cpu()) for a, b in zip(m.parameters(), m2.parameters()))
         same_opt = all(torch.equal(a.exp_avg.cpu(), b.exp_avg.cpu())
                        for a, b in zip(optimizer_states(m), optimizer_states(m2)))
+        # GraphSAGE's step counter (tree / dropout seeds) resumes too
+        same_calls = getattr(m, "_calls", 0) == getattr(m2, "_calls", 0)
         h2 = tr2.fit(1)
-        q.put((rank, params, hist, (loaded, resumed_at, same, same_opt), h2))
+        q.put((rank, params, hist, (loaded, resumed_at, same, same_opt, same_calls), h2))
     finally:
         dist.destroy_process_group()
 
@@ -2988,7 +3049,7 @@ def test_dp_trainer_two_ranks(kind, tmp_path):
         assert len(met[k]) == 2 and all(np.isfinite(met[k]))
     assert met["recall"][1] > 0.0 and 0 < met["coverage"][0] <= met["coverage"][1] <= 1
     assert h1[1]["metrics"] is None
-    assert r0 == (True, 2, True, True) and r1 == (True, 2, True, True)
+    assert r0 == (True, 2, True, True, True) and r1 == (True, 2, True, True, True)
 
 
 def _dp_rank_union_graph(rank, world, port, exchange, graph, bucket_min, q):

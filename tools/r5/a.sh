@@ -11,3 +11,6 @@ timeout -k 10 300 python bench.py > $E/bench_c2.log 2>&1 || { echo "bench rc=$?"
 grep '^{' $E/bench_c2.log | cut -c1-600
 timeout -k 10 300 python -m furusato_recommend_amd.train_dp --model lgn --gpus 1 --synthetic 20000,2000,200000,cluster --recdim 64 --layer 3 --bpr_batch 4096 --epochs 2 --test_span 1 --train_iterative 1 --path $E/ck > $E/cli.log 2>&1 || { echo "cli rc=$?"; tail -20 $E/cli.log; exit 1; }
 cat $E/cli.log | cut -c1-400
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 500 --timeout-method thread -k "microbatch or dp_trainer_two_ranks" > $E/pytest_mb.log 2>&1
+rc=$?; echo "pytest mb rc=$rc"; tail -12 $E/pytest_mb.log
+exit $rc
