@@ -61,22 +61,6 @@ struct AttnShape {
   static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 3 * TR);
 };
 
-// MIREC_ATTN_PDS: the packed backward keeps phase A's P and dS tiles of every
-// causal (query block, key block) pair of the pack in LDS, so phase B reads
-// them instead of recomputing S and dP (per pair 112 -> 80 MFMAs; LDS +25.6
-// KB: two workgroups per CU instead of four).  Tile: 16 query rows x 16 key
-// columns at row stride 20 (float4 writes in phase A, conflict-free
-// transposed reads in phase B).
-#ifndef MIREC_ATTN_PDS
-#define MIREC_ATTN_PDS 0
-#endif
-constexpr int kPdsLd = 20;
-constexpr int kPdsTile = 16 * kPdsLd;
-constexpr int kPdsSlot = 2 * kPdsTile;  // P then dS
-__device__ __forceinline__ int pds_slot(int qblock, int kblock) {
-  return qblock * (qblock + 1) / 2 + kblock;
-}
-
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -589,8 +573,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
   float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
   float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
-  float *sPD = sD + S::TR;  // MIREC_ATTN_PDS: 10 (P, dS) tile slots
-  (void)sPD;
   const int64_t pk = blockIdx.x / H;
   const int64_t busy = (int64_t)packs[0] * H;
   if ((int64_t)blockIdx.x >= busy) {
@@ -681,13 +663,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
 #pragma unroll
         for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = mfma16(krow[kB * cb], dp[kb][r], dq[cb]);
       }
-#if MIREC_ATTN_PDS
-      {  // lane (j, g) holds P[query j][key 4 g + r] of pair (w, lo + kb)
-        float *sl = sPD + pds_slot(w, lo + kb) * kPdsSlot + j * kPdsLd + 4 * g;
-        st4(sl, make_float4(p[kb][0], p[kb][1], p[kb][2], p[kb][3]));
-        st4(sl + kPdsTile, make_float4(dp[kb][0], dp[kb][1], dp[kb][2], dp[kb][3]));
-      }
-#endif
     }
     if (ql < T) {
       float *row = gbase + (int64_t)ql * rs;
@@ -695,7 +670,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       for (int cb = 0; cb < S::NCB; ++cb) store4(row, kB * cb + 4 * g, dh, dq[cb]);
     }
 #pragma unroll
-    for (int c = 0; c < (MIREC_ATTN_PDS ? 0 : S::Q4 / 4); ++c) {
+    for (int c = 0; c < S::Q4 / 4; ++c) {
       const float4 k4 = ld4(sK + qa * S::LDK + 16 * c + 4 * g);
       const float4 v4 = ld4(sV + qa * S::LDK + 16 * c + 4 * g);
       kr[4 * c] = k4.x;
@@ -735,18 +710,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     (void)sMl, (void)sLl, (void)sDl;
     for (int qb = lw; qb < nbs; ++qb) {
       float pr[4], dsr[4];
-#if MIREC_ATTN_PDS
-      {  // P[query 4 g + r][key j] of pair (lo + qb, w), written by phase A
-        const float *sl = sPD + pds_slot(lo + qb, w) * kPdsSlot + j;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qq = kB * qb + 4 * g + r;
-          const bool ok = key <= qq && qq < T;
-          pr[r] = ok ? sl[(4 * g + r) * kPdsLd] : 0.f;
-          dsr[r] = ok ? sl[kPdsTile + (4 * g + r) * kPdsLd] : 0.f;
-        }
-      }
-#else
       f32x4 sc = zero4(), dpc = zero4();
       const float *qrow = sQl + (kB * qb + j) * S::LDK + 4 * g;
       const float *orow = sDOl + (kB * qb + j) * S::LDK + 4 * g;
@@ -770,7 +733,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
         pr[r] = pv;
         dsr[r] = pv * (dpc[r] - sDl[qq]) * scale;
       }
-#endif
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qq = kB * qb + 4 * g + r;
@@ -798,7 +760,7 @@ template <int DPAD>
 static int launch_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
                              const int32_t *packs, int64_t batch, int heads, int dh, float *dqkv,
                              int64_t n_rows, hipStream_t st) {
-  constexpr int lds = AttnShape<DPAD, 4>::bwd_lds + (MIREC_ATTN_PDS ? 10 * kPdsSlot * 4 : 0);
+  constexpr int lds = AttnShape<DPAD, 4>::bwd_lds;
   static int rc = -1;
   if (rc < 0)
     rc = hipFuncSetAttribute((const void *)attn_bwd_packed_kernel<DPAD>,

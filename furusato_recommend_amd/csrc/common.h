@@ -157,7 +157,7 @@ __device__ __forceinline__ void adam1(float &p, float &m, float &v, float g,
 
 // ---- exact three-term bf16 split of f32 operands (gemm.hip, attention.hip)
 // x = x_h + x_m + x_l, each term rounded to nearest; the residuals are exact
-// in f32 (error analysis: gemm.hip, MIREC_GEMM_X6).
+// in f32 (error analysis: gemm.hip, "f32 products on bf16 MFMA").
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));

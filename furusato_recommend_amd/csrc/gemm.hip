@@ -13,19 +13,13 @@
 //             output tile, partial tiles in a workspace) and the slices are
 //             summed in a fixed order by a second kernel: deterministic.
 // The f32 products run on the bf16 MFMA pipe as an exact three-term split
-// (MIREC_GEMM_X6, below: six v_mfma_f32_32x32x16_bf16 per 16-deep block,
-// f32-class error), the operands staged once per element as bf16 planes in
-// LDS (MIREC_GEMM_PLANES); MIREC_GEMM_X6=0 builds the round-2 form on
-// v_mfma_f32_32x32x2_f32 (exact f32 fmaf chains, 64 FLOP/clk/SIMD).  A
+// (below: six v_mfma_f32_32x32x16_bf16 per 16-deep block, f32-class error),
+// the operands staged once per element as bf16 planes in LDS.  A
 // 256-thread workgroup owns a 128 x 128 output tile, each of its 4 waves a
 // 64 x 64 quarter (2 x 2 MFMA tiles, 64 accumulator registers); the k loop
 // runs in chunks of 32 staged through LDS with the next chunk's global loads
 // in flight (in registers) while the current chunk is multiplied.
 //
-// MFMA operand order (f32 form): step s (0..3) of an 8-wide k sub-chunk
-// takes, in lane half h = lane >> 5, the k index 4h + s — both operands use
-// the same bijection, so the sum is unchanged — which lets a lane fetch its
-// four steps' operands with one 16-byte LDS read in gemm_nt.
 #include <algorithm>
 
 #include "common.h"
@@ -33,12 +27,8 @@
 namespace mirec {
 
 
-__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
 // ---------------------------------------------- f32 products on bf16 MFMA
-// MIREC_GEMM_X6 (default): every f32 operand is split exactly into three
+// Every f32 operand is split exactly into three
 // bf16 terms, x = x_h + x_m + x_l (round-to-nearest at each stage; the
 // residuals x - x_h and (x - x_h) - x_m are exact in f32, |x_m| <= 2^-8 |x|,
 // |x_l| <= 2^-16 |x|, and x_l carries the rest to 2^-25 |x|), and a·b is
@@ -50,9 +40,6 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 // f32 GEMM's own accuracy (tests against float64 at 1e-6), at 6 x 32 = 192
 // MFMA cycles per 32x32x16 block instead of 8 x 64 = 512 with
 // v_mfma_f32_32x32x2_f32 (MI355X_MICROARCH.md cycle constants).
-#ifndef MIREC_GEMM_X6
-#define MIREC_GEMM_X6 1
-#endif
 // (bf16x8, Split3, pk_bf16, split3: common.h)
 
 // (mfma_x6, x6_k: common.h)
@@ -66,27 +53,18 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 constexpr int kTile = 128;   // output tile edge
-#ifndef MIREC_GEMM_KC
-#define MIREC_GEMM_KC 32
-#endif
-constexpr int kChunk = MIREC_GEMM_KC;  // k per LDS stage
+constexpr int kChunk = 32;          // k per LDS stage
 constexpr int kC4 = kChunk / 4;        // float4 per staged row (gemm_nt)
 constexpr int kLdNT = kChunk + 4;   // gemm_nt LDS row stride [row][k]: 16-B reads, 4-bank groups
 constexpr int kLdO = 40;            // epilogue slab stride [row][col]: lane halves (rows
                                     // r, r + 4) 32 banks apart, 16-B row reads
-constexpr int kLdTN = kTile + 8;    // gemm_tn LDS row stride [k][col]: the two lane halves
-                                    // (k and k + 4) land 32 banks apart
 
-// bf16 planes (MIREC_GEMM_PLANES, with MIREC_GEMM_X6; [row][k] operands of
-// gemm_nt only): the staging thread splits its float4s once and stores the
-// three terms as bf16 planes [3][rows][kLdP], each 16-deep k block permuted
-// so that a lane half's 8 values (x6_k order) are contiguous: one 16-byte
+// bf16 planes ([row][k] operands of gemm_nt): the staging thread splits
+// its float4s once and stores the three terms as bf16 planes
+// [3][rows][kLdP], each 16-deep k block permuted so that a lane half's 8 values (x6_k order) are contiguous: one 16-byte
 // read per plane and operand.  Row stride 80 B: the 16 lanes of a read phase
-// hit distinct 4-bank groups.  Halves the split VALU of the wave-side split
-// (every element was split by both waves that read it).
-#ifndef MIREC_GEMM_PLANES
-#define MIREC_GEMM_PLANES 1
-#endif
+// hit distinct 4-bank groups.  Halves the split VALU of a wave-side split
+// (every element would be split by both waves that read it).
 constexpr int kLdP = kChunk + 8;  // bf16 units
 constexpr int kLdK = kTile + 32;  // bf16 units (k-major planes, below)
 template <int BM>
@@ -94,8 +72,7 @@ constexpr int nt_lds_floats() {
   // [row][k] planes of A and B, or of A with the [k][n] planes of B
   constexpr int pl = 3 * BM * kLdP / 2 +
                      (3 * kTile * kLdP > 3 * kChunk * kLdK ? 3 * kTile * kLdP : 3 * kChunk * kLdK) / 2;
-  return (MIREC_GEMM_X6 && MIREC_GEMM_PLANES) && pl > (BM + kTile) * kLdNT ? pl
-                                                                           : (BM + kTile) * kLdNT;
+  return pl > (BM + kTile) * kLdNT ? pl : (BM + kTile) * kLdNT;
 }
 
 struct Split3x4 {
@@ -154,7 +131,8 @@ __device__ __forceinline__ Split3 tr_split3(const uint16_t *planes, int plane_st
 // ------------------------------------------------------------------ gemm_nt
 // Workgroup (tile_m, tile_n): rows [BM tile_m, +BM) of C, columns
 // [128 tile_n, +128); waves 2 x 2, each BM/2 x 64 (BM/64 x 2 MFMA tiles).
-// LDS: sA[BM][36], sB[128][36] (k-contiguous rows).  PF chunks of global
+// LDS: bf16 planes of A [3][BM][kLdP] and B [3][128][kLdP] (k-contiguous
+// rows) or [3][kChunk][kLdK] ([k][n] B).  PF chunks of global
 // loads are in flight ahead of the one being multiplied (register staging).
 //
 // Fused forms (the GraphSAGE hop, model/graphsage.py:314-315, without the
@@ -178,7 +156,7 @@ struct NtArgs {
 // The k loop of gemm_nt (shared by the plain and the LayerNorm epilogues):
 // acc[TM][2] of wave (wm, wn) over output rows [m0, +BM), columns [n0, +128);
 // smem holds (BM + 128) * kLdNT floats.
-template <int BM, int PF, bool BKN, bool X6 = MIREC_GEMM_X6>
+template <int BM, int PF, bool BKN>
 __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict__ A,
                                             const float *__restrict__ B, int64_t n, int Kr,
                                             int No, const NtArgs &fx, int64_t m0, int n0,
@@ -186,8 +164,6 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
   constexpr int TM = BM / 64;        // 32-row MFMA tiles per wave
   constexpr int QA = BM * kC4 / 256;     // float4 of A per thread per chunk
   constexpr int QB = kTile * kC4 / 256;  // float4 of B per thread per chunk
-  static_assert(kChunk * kLdTN <= kTile * kLdNT, "[k][n] B image fits the [n][k] region");
-  float *sA = smem, *sB = smem + BM * kLdNT;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
@@ -231,33 +207,12 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
       }
     }
   };
-  auto stage = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
-#pragma unroll
-    for (int q = 0; q < QA; ++q) {
-      const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-      st4(sA + r * kLdNT + 4 * c4, xa[q]);
-    }
-    if constexpr (BKN) {  // [k][n] as in memory (row stride kLdTN)
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-        st4(sB + kk * kLdTN + 4 * c4, xb[q]);
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < QB; ++q) {
-        const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-        st4(sB + r * kLdNT + 4 * c4, xb[q]);
-      }
-    }
-  };
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  constexpr bool PL = X6 && MIREC_GEMM_PLANES;
   uint16_t *pA = reinterpret_cast<uint16_t *>(smem);      // [3][BM][kLdP]
   uint16_t *pB = pA + 3 * BM * kLdP;  // [3][128][kLdP], or [3][kChunk][kLdK] ([k][n] B)
   constexpr int kPB = BKN ? kChunk * kLdK : kTile * kLdP;  // B plane stride
@@ -288,7 +243,6 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
     }
   };
   auto compute = [&]() {
-    if constexpr (PL) {
 #pragma unroll
       for (int s16 = 0; s16 < kChunk / 16; ++s16) {
         Split3 sa[TM], sb[2];
@@ -315,66 +269,6 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
 #pragma unroll
           for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
       }
-    } else if constexpr (X6) {
-#pragma unroll
-    for (int s16 = 0; s16 < kChunk / 16; ++s16) {
-      Split3 sa[TM], sb[2];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm) {
-        const float *ap = sA + (wm * (BM / 2) + tm * 32 + i) * kLdNT + s16 * 16 + 4 * h;
-        const float4 lo = ld4(ap), hi = ld4(ap + 8);
-        const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        sa[tm] = split3(x);
-      }
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        const int col = wn * 64 + tn * 32 + i;
-        float x[8];
-        if constexpr (BKN) {
-          const float *bp = sB + (s16 * 16 + 4 * h) * kLdTN + col;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] = bp[(x6_k(0, e)) * kLdTN];
-        } else {
-          const float *bp = sB + col * kLdNT + s16 * 16 + 4 * h;
-          const float4 lo = ld4(bp), hi = ld4(bp + 8);
-          x[0] = lo.x, x[1] = lo.y, x[2] = lo.z, x[3] = lo.w;
-          x[4] = hi.x, x[5] = hi.y, x[6] = hi.z, x[7] = hi.w;
-        }
-        sb[tn] = split3(x);
-      }
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
-    }
-    } else {
-#pragma unroll
-    for (int sub = 0; sub < kChunk / 8; ++sub) {
-      float4 fa[TM], fb[2];
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-        fa[tm] = ld4(sA + (wm * (BM / 2) + tm * 32 + i) * kLdNT + sub * 8 + 4 * h);
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        const int col = wn * 64 + tn * 32 + i;
-        if constexpr (BKN) {  // k rows 4 apart land 32 banks apart (kLdTN)
-          const float *bp = sB + (sub * 8 + 4 * h) * kLdTN + col;
-          fb[tn] = make_float4(bp[0], bp[kLdTN], bp[2 * kLdTN], bp[3 * kLdTN]);
-        } else {
-          fb[tn] = ld4(sB + col * kLdNT + sub * 8 + 4 * h);
-        }
-      }
-#pragma unroll
-      for (int tm = 0; tm < TM; ++tm)
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) {
-          acc[tm][tn] = mfma32(fa[tm].x, fb[tn].x, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].y, fb[tn].y, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].z, fb[tn].z, acc[tm][tn]);
-          acc[tm][tn] = mfma32(fa[tm].w, fb[tn].w, acc[tm][tn]);
-        }
-    }
-    }
   };
   const int nc = Kr / kChunk;
 #pragma unroll
@@ -386,8 +280,7 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
       const int c = c0 + p;
       if (c < nc) {
         __syncthreads();  // the previous chunk's LDS reads are done
-        if constexpr (PL) stage_planes(ra[p], rb[p]);
-        else stage(ra[p], rb[p]);
+        stage_planes(ra[p], rb[p]);
         __syncthreads();
         if (c + PF < nc) load(ra[p], rb[p], (c + PF) * kChunk);  // in flight during the products
         compute();
@@ -397,10 +290,7 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
 }
 
 template <int BM, int PF, bool BKN>
-#ifndef MIREC_NT_OCC
-#define MIREC_NT_OCC 2
-#endif
-__global__ __launch_bounds__(256, MIREC_NT_OCC) void gemm_nt_kernel(const float *__restrict__ A,
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         const float *__restrict__ bias,
                                                         float *__restrict__ C, int64_t n,
@@ -597,49 +487,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
   // row-tail statistics were wrong while its g_y was right (always a
   // second-pass row of an upper half-wave, local rows 9 / 11 / 13 / 15);
   // never with the f32 loop, never with these loads (0 in 120 launches over
-  // two builds) — tools/dbg_rnbwd.py, test_gemm_nn_resnorm_bwd_repeatable.
-#ifndef MIREC_RNBWD_MASKED
-#define MIREC_RNBWD_MASKED 0
-#endif
+  // two builds) — test_gemm_nn_resnorm_bwd_repeatable; the cause is the
+  // packed-f32 op_sel hazard of DESIGN.md §9.1 (tools/op_sel_repro.hip).
 #pragma unroll
   for (int q = 0; q < RPG; ++q) {
-#if MIREC_RNBWD_MASKED
-    // (diagnostic builds, tools/build_r4_variants.sh: 1 = every row load
-    // exec-masked, 2 = the same + s_waitcnt 0 after the loads, 3 = only the
-    // statistics masked, 4 = only the out / g_out rows masked)
-    const int64_t r = m0 + g + 8 * q;
-    const int64_t rc = min(r, n - 1);
-    ov[q] = gv[q] = f4_zero();
-    mv[q] = sv[q] = 0.f;
-    if (MIREC_RNBWD_MASKED == 3) {
-      ov[q] = ld4(a.out + rc * kTile + c);
-      gv[q] = a.g_out ? ld4(a.g_out + rc * kTile + c) : f4_zero();
-    }
-    if (MIREC_RNBWD_MASKED == 4) {
-      mv[q] = a.mean[rc];
-      sv[q] = a.rstd[rc];
-    }
-    if (r < n) {
-      if (MIREC_RNBWD_MASKED != 3) {
-        ov[q] = ld4(a.out + r * kTile + c);
-        gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
-      }
-      if (MIREC_RNBWD_MASKED != 4) {
-        mv[q] = a.mean[r];
-        sv[q] = a.rstd[r];
-      }
-    }
-#else
     const int64_t r = min(m0 + g + 8 * q, n - 1);
     ov[q] = ld4(a.out + r * kTile + c);
     gv[q] = a.g_out ? ld4(a.g_out + r * kTile + c) : f4_zero();
     mv[q] = a.mean[r];
     sv[q] = a.rstd[r];
-#endif
   }
-#if MIREC_RNBWD_MASKED == 2
-  __builtin_amdgcn_s_waitcnt(0);  // every counter drained before the k loop
-#endif
   const NtArgs fx{nullptr, nullptr, nullptr, 0, 0, 0, 1};
   f32x16 acc[TM][2];
   nt_mainloop<BM, 1, true>(smem, A, W, n, Kr, kTile, fx, m0, 0, acc);
@@ -703,7 +560,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nn_rnbwd_kernel(const float *__re
 // Workgroup (slice s, tile_m, tile_n): partial C tile over rows
 // [s * rows_per_slice, +rows_per_slice) -> work[s][M][No]; with colsum, the
 // tile_n == 0 workgroups also write the slice's column sums of A ->
-// work_cs[s][M].  LDS: sA[32][136], sB[32][136] (k-major, as in memory).
+// work_cs[s][M].  LDS: bf16 planes [3][kChunk][kLdK] of A and of B
+// (k-major, as in memory).
 // Fused forms: Amask zeroes A elements whose mask (same layout) is <= 0 (the
 // ReLU backward); B may be two blocks side by side, columns [0, Ns) from B
 // (row stride Ns) and [Ns, No) from B2 (row stride No - Ns), Ns % 128 == 0.
@@ -719,15 +577,13 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
                                                         float *__restrict__ work_cs,
                                                         int64_t n, int M, int No,
                                                         int64_t rows_per_slice, TnArgs fx) {
-  // TPL: both k-major operands as [k][col] bf16 planes read back with the
+  // both k-major operands as [k][col] bf16 planes read back with the
   // transposing LDS read (as gemm_nt's [k][n] B); the column sums of A are
-  // then taken from the staged f32 values
-  constexpr bool TPL = MIREC_GEMM_X6 && MIREC_GEMM_PLANES;
+  // taken from the staged f32 values
   constexpr int kPl = kChunk * kLdK;  // one plane (bf16 units)
-  constexpr int kTnLds = TPL ? 3 * kPl : 2 * kChunk * kLdTN;
+  constexpr int kTnLds = 3 * kPl;
   __shared__ __attribute__((aligned(16))) float smem[kTnLds];
   static_assert(4 * 32 * kLdO <= kTnLds && 8 * kTile <= kTnLds, "epilogue staging fits");
-  float *sA = smem, *sB = smem + kChunk * kLdTN;
   uint16_t *pA = reinterpret_cast<uint16_t *>(smem), *pB = pA + 3 * kPl;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
@@ -766,25 +622,20 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       }
     }
   };
-  float4 csv = f4_zero();  // TPL: this thread's column sums (columns 4 c4 ..)
+  float4 csv = f4_zero();  // this thread's column sums (columns 4 c4 ..)
   auto stage = [&]() {
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-      if constexpr (TPL) {
-        if (do_cs) csv = f4_add(csv, ra[q]);
-        const Split3x4 va = split3x4(ra[q]), vb = split3x4(rb[q]);
-        uint16_t *da = pA + kk * kLdK + 4 * c4, *db = pB + kk * kLdK + 4 * c4;
-        *reinterpret_cast<uint2 *>(da) = va.h;
-        *reinterpret_cast<uint2 *>(da + kPl) = va.m;
-        *reinterpret_cast<uint2 *>(da + 2 * kPl) = va.l;
-        *reinterpret_cast<uint2 *>(db) = vb.h;
-        *reinterpret_cast<uint2 *>(db + kPl) = vb.m;
-        *reinterpret_cast<uint2 *>(db + 2 * kPl) = vb.l;
-      } else {
-        st4(sA + kk * kLdTN + 4 * c4, ra[q]);
-        st4(sB + kk * kLdTN + 4 * c4, rb[q]);
-      }
+      if (do_cs) csv = f4_add(csv, ra[q]);
+      const Split3x4 va = split3x4(ra[q]), vb = split3x4(rb[q]);
+      uint16_t *da = pA + kk * kLdK + 4 * c4, *db = pB + kk * kLdK + 4 * c4;
+      *reinterpret_cast<uint2 *>(da) = va.h;
+      *reinterpret_cast<uint2 *>(da + kPl) = va.m;
+      *reinterpret_cast<uint2 *>(da + 2 * kPl) = va.l;
+      *reinterpret_cast<uint2 *>(db) = vb.h;
+      *reinterpret_cast<uint2 *>(db + kPl) = vb.m;
+      *reinterpret_cast<uint2 *>(db + 2 * kPl) = vb.l;
     }
   };
   f32x16 acc[2][2];
@@ -794,85 +645,25 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  // column sums of A from the MFMA operands themselves: lane (i, h) sees
-  // column wm 64 + tm 32 + i at the chunk rows 8 sub + 4 h + st; the two
-  // lane halves are added at the end (waves wn == 0 own the sums)
-  float cs[2] = {0.f, 0.f};
   if (r_beg < r_end) load(r_beg);
   for (int64_t r0 = r_beg; r0 < r_end; r0 += kChunk) {
     __syncthreads();
     stage();
     __syncthreads();
     if (r0 + kChunk < r_end) load(r0 + kChunk);
-#if MIREC_GEMM_X6
-    if constexpr (TPL) {
-#pragma unroll
-      for (int s16 = 0; s16 < kChunk / 16; ++s16) {
-        Split3 sa[2], sb[2];
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm) sa[tm] = tr_split3(pA, kPl, wm * 64 + tm * 32, s16, lane);
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) sb[tn] = tr_split3(pB, kPl, wn * 64 + tn * 32, s16, lane);
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
-      }
-      continue;
-    }
 #pragma unroll
     for (int s16 = 0; s16 < kChunk / 16; ++s16) {
       Split3 sa[2], sb[2];
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm) {
-        const float *ap = sA + (s16 * 16 + 4 * h) * kLdTN + wm * 64 + tm * 32 + i;
-        float x[8];
+      for (int tm = 0; tm < 2; ++tm) sa[tm] = tr_split3(pA, kPl, wm * 64 + tm * 32, s16, lane);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = ap[x6_k(0, e) * kLdTN];
-        if (do_cs) {
-          cs[tm] += (x[0] + x[1]) + (x[2] + x[3]);
-          cs[tm] += (x[4] + x[5]) + (x[6] + x[7]);
-        }
-        sa[tm] = split3(x);
-      }
-#pragma unroll
-      for (int tn = 0; tn < 2; ++tn) {
-        const float *bp = sB + (s16 * 16 + 4 * h) * kLdTN + wn * 64 + tn * 32 + i;
-        float x[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = bp[x6_k(0, e) * kLdTN];
-        sb[tn] = split3(x);
-      }
+      for (int tn = 0; tn < 2; ++tn) sb[tn] = tr_split3(pB, kPl, wn * 64 + tn * 32, s16, lane);
 #pragma unroll
       for (int tm = 0; tm < 2; ++tm)
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
     }
-#else
-#pragma unroll
-    for (int sub = 0; sub < kChunk / 8; ++sub) {
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int kk = sub * 8 + 4 * h + st;
-        float fa[2], fb[2];
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm) fa[tm] = sA[kk * kLdTN + wm * 64 + tm * 32 + i];
-#pragma unroll
-        for (int tn = 0; tn < 2; ++tn) fb[tn] = sB[kk * kLdTN + wn * 64 + tn * 32 + i];
-#pragma unroll
-        for (int tm = 0; tm < 2; ++tm)
-#pragma unroll
-          for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma32(fa[tm], fb[tn], acc[tm][tn]);
-        if (do_cs) {
-          cs[0] += fa[0];
-          cs[1] += fa[1];
-        }
-      }
-    }
-#endif
   }
-  cs[0] += __shfl_xor(cs[0], 32);
-  cs[1] += __shfl_xor(cs[1], 32);
   // partial tile out through a wave-private LDS slab as float4 rows (as in
   // gemm_nt_kernel)
   float *out = work + (int64_t)s * M * No;
@@ -893,20 +684,15 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
       }
       wave_sync();  // the slab is wave-private
     }
-  if constexpr (TPL) {
-    if (!do_cs) return;  // workgroup-uniform
-    __syncthreads();     // the slabs are no longer read
-    st4(smem + (t >> 5) * kTile + 4 * (t & 31), csv);
-    __syncthreads();
-    if (t < kTile) {  // the 8 row groups added in group order
-      float c = 0.f;
+  if (!do_cs) return;  // workgroup-uniform
+  __syncthreads();     // the slabs are no longer read
+  st4(smem + (t >> 5) * kTile + 4 * (t & 31), csv);
+  __syncthreads();
+  if (t < kTile) {  // the 8 row groups added in group order
+    float c = 0.f;
 #pragma unroll
-      for (int g8 = 0; g8 < 8; ++g8) c += smem[g8 * kTile + t];
-      work_cs[(int64_t)s * M + m0 + t] = c;
-    }
-  } else if (do_cs && wn == 0 && h == 0) {
-    work_cs[(int64_t)s * M + m0 + wm * 64 + i] = cs[0];
-    work_cs[(int64_t)s * M + m0 + wm * 64 + 32 + i] = cs[1];
+    for (int g8 = 0; g8 < 8; ++g8) c += smem[g8 * kTile + t];
+    work_cs[(int64_t)s * M + m0 + t] = c;
   }
 }
 
@@ -977,26 +763,19 @@ __global__ __launch_bounds__(1024) void gemm_tn_reduce_kernel(const float *__res
 // 256 -> 128 rows 1.45 -> 1.43 ms (two same-box A/B pairs), 128 -> 64 rows
 // another 1.2 % (three pairs); C3 unchanged (its large weight gradients
 // are not bound by the minimum).  tools/ab_tn.sh, tools/ab_libs.sh.)
-#ifndef MIREC_TN_MINROWS
-#define MIREC_TN_MINROWS 64
-#endif
+constexpr int64_t kTnMinRows = 64;
 // A single 128 x 128 output tile (the d = 128 projection / FFN weight
 // gradients of C4) takes 256 slices instead: half the partial tiles for the
 // reduce, and its load-latency-bound slices lose less than the reduce saves
 // (split bf16 loop: 30.4 -> 25.7 us, C4 1.259 -> 1.232 ms/step, same box;
 // 256 workgroups in total lose on 2- and 3-tile gradients: 125 -> 172 us,
 // 49.6 -> 52.9 us).
-#ifndef MIREC_TN_WANT
-#define MIREC_TN_WANT 512
-#endif
-#ifndef MIREC_TN_WANT1
-#define MIREC_TN_WANT1 256
-#endif
+constexpr int64_t kTnWant = 512, kTnWant1 = 256;  // workgroups (several tiles / one tile)
 static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
-  const int64_t total = tiles == 1 ? MIREC_TN_WANT1 : MIREC_TN_WANT;
+  const int64_t total = tiles == 1 ? kTnWant1 : kTnWant;
   const int64_t want = std::max<int64_t>(1, (total + tiles - 1) / tiles);
-  int64_t r = std::max<int64_t>(MIREC_TN_MINROWS, (n + want - 1) / want);
+  int64_t r = std::max<int64_t>(kTnMinRows, (n + want - 1) / want);
   r = (r + kChunk - 1) / kChunk * kChunk;
   *rows = r;
   *slices = (int)std::max<int64_t>(1, (n + r - 1) / r);
@@ -1112,11 +891,8 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   const int64_t t128 = (n + 127) / 128 * ncol, t64 = (n + 63) / 64 * ncol;
   const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
   const bool bm64 = r64 < r128 || (r64 == r128 && t128 > slots);
-#ifndef MIREC_NT_PF
-#define MIREC_NT_PF 1
-#endif
 #define MIREC_NT_LAUNCH(BM, BKN)                                                               \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, MIREC_NT_PF, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
                      dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx)
   if (bm64) {
     if (bkn) MIREC_NT_LAUNCH(64, true);

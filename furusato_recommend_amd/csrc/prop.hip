@@ -372,13 +372,10 @@ __device__ __forceinline__ void wave_row(const PropK &a, int32_t row) {
 
 constexpr int64_t kListBlocks = 4096;  // 2 x the waves resident at 8/SIMD
 
-#ifndef MIREC_PROP_MIN_WAVES
-#define MIREC_PROP_MIN_WAVES 7
-#endif
 // Occupancy floor (waves per SIMD): keeps the register allocator at <= 72
 // VGPRs so 7-8 waves per SIMD keep enough gathers in flight.
 template <int D, int UNROLL, int MODE, bool MASKED, bool ROWMASK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MIREC_PROP_MIN_WAVES, 8)))
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7, 8)))
 MIREC_NO_PK_F32 void prop_kernel(PropK a) {
   constexpr int G = 64 / (D / 4);
   // wave index made provably uniform (SGPR): loop control stays scalar

@@ -38,14 +38,10 @@
 
 #include "common.h"
 
-#ifndef MIREC_TG_CHUNK
-#define MIREC_TG_CHUNK 8
-#endif
-
 namespace mirec {
 
 constexpr int kMaxGroups = MIREC_TABLE_GRAD_MAX_GROUPS;
-constexpr int kCh = MIREC_TG_CHUNK;  // sorted entries per chunk (pass 1 loads them at once)
+constexpr int kCh = 8;       // sorted entries per chunk (pass 1 loads them at once)
 constexpr int kBatch = 8;            // partial rows in flight per lane in pass 2
 constexpr int32_t kEnd = 0x7fffffff;
 
@@ -129,24 +125,11 @@ __device__ __forceinline__ void tg_decode(const GroupArgs &ga, const float *__re
 }
 
 // Lane base + u's x for every lane of a group of LPR lanes (u uniform, a
-// constant after unrolling): __shfl (ds_bpermute).  MIREC_TG_READLANE=1 reads
-// it with v_readlane for 32 / 64-lane groups (one per group of the wave):
-// 84 instead of 95 VGPRs, six waves per SIMD instead of five, but 208
-// readlanes whose SGPR results serialise the wave — measured slower at C3
-// (accumulate 0.379 vs 0.367 ms, profiles/round4_tg_bench.jsonl).
-#ifndef MIREC_TG_READLANE
-#define MIREC_TG_READLANE 0
-#endif
+// constant after unrolling): __shfl (ds_bpermute).  (v_readlane for 32 /
+// 64-lane groups measured slower at C3: 208 readlanes whose SGPR results
+// serialise the wave, accumulate 0.379 vs 0.367 ms.)
 template <int LPR>
 __device__ __forceinline__ int grp_bcast(int x, int base, int u) {
-#if MIREC_TG_READLANE
-  if constexpr (LPR == 64) {
-    return __builtin_amdgcn_readlane(x, u);
-  } else if constexpr (LPR == 32) {
-    const int a = __builtin_amdgcn_readlane(x, u), b = __builtin_amdgcn_readlane(x, 32 + u);
-    return base ? b : a;
-  }
-#endif
   return __shfl(x, base + u);
 }
 
@@ -195,9 +178,8 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
 // and pass 2: their head chunk's segment to slot 1, every later chunk's
 // first segment to slot 0.  Short runs — nearly all of them — are summed in
 // one place without partial rows.
-// The loads a chunk starts from (issued one chunk ahead by the persistent
-// loop below): the keys before and around it, its entries' keys and indices
-// and those of the window after it.
+// The loads a chunk starts from: the keys before and around it, its
+// entries' keys and indices and those of the window after it.
 struct TgRaw {
   int32_t kprev, kpp, km, kx, vm, vx;
 };
@@ -316,17 +298,9 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__res
   }
 }
 
-// Pass 1 driver: one chunk per lane group (default), or MIREC_TG_PERSIST = 1:
-// a fixed grid (the chip's resident workgroups) whose lane groups walk chunks
-// g, g + G, ..., loading chunk i + 1's keys and indices while chunk i's
-// weights and rows are in flight.  The persistent form measured slower at C3
-// (259 vs 231 us, profiles/round4_tg_bench.jsonl): the carried loads take
-// 109 VGPRs (four waves per SIMD instead of five) and the gathers, not the
-// key loads, are what each wave waits on — the bytes in flight per CU do not
-// grow.
-#ifndef MIREC_TG_PERSIST
-#define MIREC_TG_PERSIST 0
-#endif
+// Pass 1 driver: one chunk per lane group.  (A persistent form whose groups
+// carry the next chunk's keys measured slower at C3, 259 vs 231 us: 109
+// VGPRs, and the gathers, not the key loads, are what each wave waits on.)
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
                                                      const int32_t *__restrict__ vals,
@@ -341,25 +315,10 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   const int base = lane - sub;
   const int64_t group = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
   const int64_t n_chunks = (n + kCh - 1) / kCh;
-#if MIREC_TG_PERSIST
-  const int64_t n_groups = (int64_t)gridDim.x * blockDim.x / LPR;
-  int64_t c = group;
-  TgRaw cur;
-  if (c < n_chunks) tg_load_raw(keys, vals, n, c, sub, cur);
-  while (c < n_chunks) {
-    const int64_t cn = c + n_groups;
-    TgRaw nxt;
-    if (cn < n_chunks) tg_load_raw(keys, vals, n, cn, sub, nxt);
-    tg_chunk<LPR>(ga, wt, n, d, n_rows, acc_out, stamp, gen, part, c, sub, base, cur);
-    cur = nxt;
-    c = cn;
-  }
-#else
   if (group >= n_chunks) return;  // the whole group leaves together
   TgRaw r;
   tg_load_raw(keys, vals, n, group, sub, r);
   tg_chunk<LPR>(ga, wt, n, d, n_rows, acc_out, stamp, gen, part, group, sub, base, r);
-#endif
 }
 
 // Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
@@ -534,33 +493,15 @@ __global__ __launch_bounds__(256) void tg_dense_kernel(const float *__restrict__
   }
 }
 
-#ifndef MIREC_TG_ADAM_UNROLL
-#define MIREC_TG_ADAM_UNROLL 1
-#endif
-// MIREC_TG_ADAM_NT: bit 0 = the W / m / v loads, bit 1 = their stores as
-// non-temporal accesses (each byte is touched once per step: nothing to
-// keep).  Loads only is the default: the C3 launch 0.692 / 0.703 -> 0.667 /
-// 0.675 ms; non-temporal stores measured no gain (0.691 / 0.686), both 0.676
-// / 0.675 (profiles/round4_adam_nt.txt)
-#ifndef MIREC_TG_ADAM_NT
-#define MIREC_TG_ADAM_NT 1
-#endif
+// The W / m / v loads are non-temporal (each byte is touched once per step:
+// nothing to keep): the C3 launch 0.692 / 0.703 -> 0.667 / 0.675 ms.
+// Non-temporal stores measured no gain (0.691 / 0.686 ms), nor more float4
+// groups per thread in flight (0.67-0.70 ms at 1, 2, 4: the kernel streams
+// at ~5.3 TB/s either way).
 typedef float adam_f4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 adam_ld4(const float *p) {
-#if MIREC_TG_ADAM_NT & 1
   const adam_f4 x = __builtin_nontemporal_load(reinterpret_cast<const adam_f4 *>(p));
   return make_float4(x.x, x.y, x.z, x.w);
-#else
-  return ld4(p);
-#endif
-}
-__device__ __forceinline__ void adam_st4(float *p, float4 v) {
-#if MIREC_TG_ADAM_NT & 2
-  const adam_f4 x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<adam_f4 *>(p));
-#else
-  st4(p, v);
-#endif
 }
 __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
                                                       float *__restrict__ m, float *__restrict__ v,
@@ -576,41 +517,21 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
   const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
   const int64_t n4 = n_rows * d4;
   float su = 0.f, si = 0.f;
-  // MIREC_TG_ADAM_UNROLL float4 groups per thread and iteration, all loads
-  // issued before the first use (the same adam1 arithmetic per element).  1,
-  // 2 and 4 measured alike at C3 (0.67-0.70 ms, launch-to-launch noise: the
-  // kernel streams W, m, v in and out at ~5.3 TB/s with or without more
-  // loads in flight per thread; profiles/round4_adam_unroll.txt)
-  constexpr int U = MIREC_TG_ADAM_UNROLL;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += U * stride) {
-    float4 p[U], a[U], b[U], g[U];
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const int64_t i = i0 + q * stride;
-      if (i < n4) {
-        p[q] = adam_ld4(param + 4 * i);
-        a[q] = adam_ld4(m + 4 * i);
-        b[q] = adam_ld4(v + 4 * i);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < U; ++q) {
-      const int64_t i = i0 + q * stride;
-      if (i >= n4) break;
-      const int64_t r = row_of(i, d4, shift);
-      g[q] = table_grad4(p[q], acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci);
-      adam1(p[q].x, a[q].x, b[q].x, g[q].x, h);
-      adam1(p[q].y, a[q].y, b[q].y, g[q].y, h);
-      adam1(p[q].z, a[q].z, b[q].z, g[q].z, h);
-      adam1(p[q].w, a[q].w, b[q].w, g[q].w, h);
-      adam_st4(param + 4 * i, p[q]);
-      adam_st4(m + 4 * i, a[q]);
-      adam_st4(v + 4 * i, b[q]);
-      const float s = p[q].x * p[q].x + p[q].y * p[q].y + p[q].z * p[q].z + p[q].w * p[q].w;
-      if (r < n_user) su += s;
-      else si += s;
-    }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p = adam_ld4(param + 4 * i), a = adam_ld4(m + 4 * i), b = adam_ld4(v + 4 * i);
+    const int64_t r = row_of(i, d4, shift);
+    const float4 g = table_grad4(p, acc, stamp, gen, r, 4 * i, r < n_user ? cu : ci);
+    adam1(p.x, a.x, b.x, g.x, h);
+    adam1(p.y, a.y, b.y, g.y, h);
+    adam1(p.z, a.z, b.z, g.z, h);
+    adam1(p.w, a.w, b.w, g.w, h);
+    st4(param + 4 * i, p);
+    st4(m + 4 * i, a);
+    st4(v + 4 * i, b);
+    const float s = p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
+    if (r < n_user) su += s;
+    else si += s;
   }
   if (sumsq == nullptr) return;
   red[0][threadIdx.x] = su;
@@ -667,20 +588,14 @@ __global__ __launch_bounds__(1024) void tg_norm_final_kernel(const float *__rest
 }
 
 // ------------------------------------------------------------ host side
-// The stable (key, value) radix sort of the entries.  MIREC_TG_SORT_BITS > 0
-// sorts that many bits per onesweep pass (rocprim's own choice for int pairs
-// on gfx950 is 8: three passes over the 21-bit row ids of C3; 11 covers them
-// in two: the C3 accumulate 0.389 -> 0.367 ms, same order, bitwise equal
-// sums — profiles/round4_tg_bench.jsonl); 0 keeps hipcub's default.
-#ifndef MIREC_TG_SORT_BITS
-#define MIREC_TG_SORT_BITS 11
-#endif
+// The stable (key, value) radix sort of the entries, 11 bits per onesweep
+// pass (rocprim's own choice for int pairs on gfx950 is 8: three passes over
+// the 21-bit row ids of C3; 11 covers them in two: the C3 accumulate 0.389
+// -> 0.367 ms, same order, bitwise equal sums).
 static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *ko, const int32_t *vi,
                           int32_t *vo, int n, int end_bit, hipStream_t st) {
-#if MIREC_TG_SORT_BITS > 0
   using Onesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>,
-                                                       rocprim::kernel_config<1024, 8>,
-                                                       MIREC_TG_SORT_BITS,
+                                                       rocprim::kernel_config<1024, 8>, 11,
                                                        rocprim::block_radix_rank_algorithm::match>;
   // onesweep from 128 K entries up: rocprim's default merge-sort limit (1 M)
   // sent a micro-batch's ~0.9 M entries (the pipelined exchange, C = 2)
@@ -689,9 +604,6 @@ static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *
   using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, Onesweep,
                                          (size_t)1 << 17>;
   return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, ki, ko, vi, vo, (size_t)n, 0, end_bit, st);
-#else
-  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, ki, ko, vi, vo, n, 0, end_bit, st);
-#endif
 }
 
 static int lanes_per_row(int32_t d) {
@@ -834,28 +746,6 @@ extern "C" int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int
   return MIREC_OK;
 }
 
-// Pass 1's grid: one lane group per chunk, or (persistent form) at most the
-// workgroups the chip holds at once (CUs x the kernel's occupancy).
-template <int LP>
-static dim3 tg_sum_grid(dim3 full) {
-#if MIREC_TG_PERSIST
-  static unsigned resident = 0;
-  if (resident == 0) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) == hipSuccess &&
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tg_sum_kernel<LP>, 256, 0) ==
-            hipSuccess && cus > 0 && per > 0)
-      resident = (unsigned)(cus * per);
-    else
-      resident = 2048;
-  }
-  return dim3(full.x < resident ? full.x : resident);
-#else
-  return full;
-#endif
-}
-
 extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
                                        int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
                                        int32_t gen, void *workspace, size_t workspace_bytes,
@@ -911,7 +801,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   const dim3 grid((unsigned)((threads + 255) / 256));
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
-    hipLaunchKernelGGL(tg_sum_kernel<LP>, tg_sum_grid<LP>(grid), dim3(256), 0, st, ga,        \
+    hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga,        \
                        keys_out, vals_out, wt, L.n_ent, dim, n_rows, acc, stamp, gen, part);  \
     MIREC_LAUNCH_CHECK();                                                                    \
     if (n_blocks > 0) {                                                                      \
@@ -924,9 +814,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
     MIREC_LAUNCH_CHECK();                                                                    \
     break;
   switch (lpr) {  // lpr >= kCh (lanes_per_row)
-#if MIREC_TG_CHUNK <= 8
     MIREC_TG_LAUNCH(8)
-#endif
     MIREC_TG_LAUNCH(16)
     MIREC_TG_LAUNCH(32)
     MIREC_TG_LAUNCH(64)
@@ -943,11 +831,8 @@ static int32_t pow2_shift(int32_t d4) {
   return -1;
 }
 
-#ifndef MIREC_TG_ADAM_BLOCKS
-#define MIREC_TG_ADAM_BLOCKS 65536
-#endif
 static unsigned tg_blocks(int64_t n4) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, MIREC_TG_ADAM_BLOCKS));
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 65536));
 }
 
 extern "C" int64_t mirec_adam_table_sumsq_floats(int64_t n_rows, int32_t dim) {

@@ -202,12 +202,8 @@ __device__ __forceinline__ unsigned bloom_h2(int64_t item) {
 // reversing quad_perm for 4 (i -> 7 - i within 8, then within 4: i ^ 4);
 // row_ror:8 for 8 (within 16: i + 8 = i ^ 8); v_permlane16_swap /
 // v_permlane32_swap (gfx950) for 16 / 32, each lane taking the half it
-// lacks.  MIREC_TOPK_DPP=0 keeps __shfl_xor.
-#ifndef MIREC_TOPK_DPP
-#define MIREC_TOPK_DPP 1
-#endif
+// lacks.
 __device__ __forceinline__ int lane_xor(int x, int stride) {
-#if MIREC_TOPK_DPP
   const int lane = threadIdx.x & 63;
   switch (stride) {
     case 1: return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
@@ -226,9 +222,6 @@ __device__ __forceinline__ int lane_xor(int x, int stride) {
       return (int)((lane & 32) ? r[0] : r[1]);
     }
   }
-#else
-  return __shfl_xor(x, stride);
-#endif
 }
 
 // Bitonic sort of one (value, index) pair per lane over the wave, best first.
@@ -252,29 +245,10 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
   }
 }
 
-// Score tiles on the bf16 MFMA pipe (MIREC_TOPK_X6, default off, D <= 128):
-// the exact three-term split of gemm.hip (f32-class error per product; the
-// top-k is checked against float64 scores by the near-tie criterion of
-// test_evaluate_matches_oracle).  The user rows are split once into
-// registers (the B operand: D/16 Split3 = 3 D/4 VGPRs), every item tile once
-// at staging into three bf16 planes [3][32][D + 8] whose 16-deep k blocks are
-// permuted so a lane half's 8 values (x6_k order) are one 16-byte read
-// (plane_pos, as gemm.hip's [row][k] planes; row stride 2 D + 16 B: the 16
-// lanes of a read phase hit distinct 4-bank groups).  Per 32 x 32 tile and
-// 16 dims: 6 v_mfma_f32_32x32x16_bf16 (192 cycles) instead of 8
-// v_mfma_f32_32x32x2_f32 (512).  Measured at C2 (profiles/round4_eval_c2.jsonl):
-// both forms pass the float64 near-tie check on all 10 K users, but the split
-// form is slower (6.73 vs 5.69 ms per batch): its planes take 62.7 KB of LDS
-// per workgroup (two per CU, against three at 51 KB), and the tile loop is
-// bound by the candidate insertion / compaction and barriers around the
-// products, not by the MFMA issue it saves.
-#ifndef MIREC_TOPK_X6
-#define MIREC_TOPK_X6 0
-#endif
-
-__device__ __forceinline__ int st_plane_pos(int c4) {
-  return (c4 >> 2) * 16 + 8 * (c4 & 1) + 4 * ((c4 >> 1) & 1);
-}
+// (Score tiles on the bf16 MFMA pipe through the exact three-term split of
+// gemm.hip passed the float64 near-tie check but measured slower at C2, 6.73
+// vs 5.69 ms per 10 K users: its bf16 planes take 62.7 KB of LDS per
+// workgroup, two per CU instead of three)
 
 template <int D>
 __global__ __launch_bounds__(128) void score_topk_kernel(
@@ -291,10 +265,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   // workgroup per CU).  k-step s of lane half h covers dim 2 s + h (D <= 128)
   // or dim h·D/2 + s (D > 128); A and B use the same map.
   constexpr bool UL = D > 128;
-  constexpr bool X6 = MIREC_TOPK_X6 && !UL;
   constexpr int NB = UL ? 1 : 2;
-  constexpr int LP = D + 8;  // bf16 plane row stride (X6)
-  constexpr int kSI = X6 ? (3 * kStTile * LP + 1) / 2 : kStTile * LD;  // floats per buffer
+  constexpr int kSI = kStTile * LD;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float sI[NB][kSI];
   __shared__ __attribute__((aligned(16))) float sU[UL ? kStUsers * LD : 4];
   __shared__ float cv[kStUsers][kStCap];
@@ -313,20 +285,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   const int64_t it0 = (int64_t)blockIdx.y * chunk;
   const int64_t it1 = min(m_items, it0 + chunk);
   // the user's embedding as the B operand: ue[s] = U[ub][2 s + h]
-  float ue[(UL || X6) ? 1 : KS];
-  // X6: the user's row split once, block s16 = dims 16 s16 + x6_k(h, e)
-  Split3 us[X6 ? D / 16 : 1];
-  if constexpr (X6) {
-#pragma unroll
-    for (int s16 = 0; s16 < D / 16; ++s16) {
-      float x[8];
-      const float4 lo = uok ? ld4(U + ub * D + 16 * s16 + 4 * h) : f4_zero();
-      const float4 hi = uok ? ld4(U + ub * D + 16 * s16 + 8 + 4 * h) : f4_zero();
-      x[0] = lo.x, x[1] = lo.y, x[2] = lo.z, x[3] = lo.w;
-      x[4] = hi.x, x[5] = hi.y, x[6] = hi.z, x[7] = hi.w;
-      us[s16] = split3(x);
-    }
-  } else if constexpr (!UL) {
+  float ue[UL ? 1 : KS];
+  if constexpr (!UL) {
 #pragma unroll
     for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
   } else {
@@ -370,27 +330,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     for (int q = 0; q < PER; ++q) {
       const int e = t + 128 * q, row = e / (D / 4), c4 = e % (D / 4);
       if (e >= kStTile * D / 4) continue;
-      if constexpr (X6) {  // three bf16 planes, k-permuted per 16-deep block
-        const float x[4] = {r[q].x, r[q].y, r[q].z, r[q].w};
-        uint32_t H[2], M[2], Lo[2];
-#pragma unroll
-        for (int p2 = 0; p2 < 2; ++p2) {
-          const float a = x[2 * p2], b = x[2 * p2 + 1];
-          const uint32_t ph = pk_bf16(a, b);
-          const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
-          const uint32_t pm = pk_bf16(ra, rb);
-          const float sa = ra - __uint_as_float(pm << 16), sb = rb - __uint_as_float(pm & 0xffff0000u);
-          H[p2] = ph;
-          M[p2] = pm;
-          Lo[p2] = pk_bf16(sa, sb);
-        }
-        uint16_t *d = reinterpret_cast<uint16_t *>(sI[buf]) + row * LP + st_plane_pos(c4);
-        *reinterpret_cast<uint2 *>(d) = make_uint2(H[0], H[1]);
-        *reinterpret_cast<uint2 *>(d + kStTile * LP) = make_uint2(M[0], M[1]);
-        *reinterpret_cast<uint2 *>(d + 2 * kStTile * LP) = make_uint2(Lo[0], Lo[1]);
-      } else {
-        st4(sI[buf] + row * LD + 4 * c4, r[q]);
-      }
+      st4(sI[buf] + row * LD + 4 * c4, r[q]);
     }
   };
   // user slot u's buffer entry of this lane, with the train-positive mask
@@ -437,17 +377,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if constexpr (X6) {
-      const uint16_t *ap = reinterpret_cast<const uint16_t *>(sI[cur]) + i * LP + 8 * h;
-#pragma unroll
-      for (int s16 = 0; s16 < D / 16; ++s16) {
-        Split3 a;
-        a.h = *reinterpret_cast<const bf16x8 *>(ap + 16 * s16);
-        a.m = *reinterpret_cast<const bf16x8 *>(ap + kStTile * LP + 16 * s16);
-        a.l = *reinterpret_cast<const bf16x8 *>(ap + 2 * kStTile * LP + 16 * s16);
-        acc = mfma_x6(a, us[s16], acc);
-      }
-    } else if constexpr (!UL) {
+    if constexpr (!UL) {
       const float *arow = sI[cur] + i * LD + h;
 #pragma unroll
       for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);

@@ -358,6 +358,8 @@ def parse_args(argv=None):
     ap.add_argument("--lr", type=float, default=1e-3, help="ddp_lgcn.py:653")
     ap.add_argument("--decay", type=float, default=1e-4, help="ddp_lgcn.py:645")
     ap.add_argument("--num_neighbors", type=int, default=5, help="GraphSAGE fanout per hop")
+    ap.add_argument("--fanouts", default=None,
+                    help="GraphSAGE fanout per hop as a list, e.g. [25,10] (C3)")
     ap.add_argument("--testbatch", type=int, default=1000, help="test_u_batch_size")
     ap.add_argument("--topks", default="[10,20]")
     ap.add_argument("--test_span", type=int, default=TEST_SPAN)
@@ -434,6 +436,7 @@ def build_config(args, device: str) -> dict:
         "positive_num_limit": args.positive_num_limit, "seed": args.seed,
         "suffix": args.suffix, "dp_mode": args.dp_mode,
         "checkpoint_path": os.path.join(args.path, f"ddp_{args.model}_{args.suffix}.pth"),
+        **({"fanouts": list(ast.literal_eval(args.fanouts))} if args.fanouts else {}),
     }
 
 

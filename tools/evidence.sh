@@ -1,24 +1,115 @@
 #!/bin/bash
-# Round-end evidence on one GPU box: C2 rocprofv3 passes (kernel stats +
-# FETCH_SIZE + WRITE_SIZE), the C2 bench line, C3 / C4 bench lines with their
-# CPU baselines and kernel stats.  Every GPU step has its own time limit and a
-# failure ends the script.
+# Measurement evidence on one GPU box, as named legs:
+#
+#   bash tools/evidence.sh [leg ...]        (default: tests c2 prof c3 c4 c3prof c4prof)
+#
+# Output under gpurun_out/${EV:-ev}/.  Every GPU step runs under its own time
+# limit and a failing step ends the script (nothing more touches the GPU).
+# rocprofv3 writes CSV; per-dispatch trace CSVs are deleted so only the
+# *_stats.csv (and counter CSVs of the PMC passes) stay.  The summaries that
+# profiles/ keeps come from these directories (profiles/README.md).
+#
+#   tests      the whole GPU suite in one process               -> pytest.log
+#   mark=EXPR  the GPU tests selected by -k EXPR, verbose        -> pytest_k.log
+#   smoke      __graft_entry__.smoke()                           -> smoke.log
+#   c2         the headline bench line (bench.py defaults: roofline, CPU
+#              baseline, oracle parity leg, Recall@20)           -> bench_c2.log
+#   prof       C2 rocprofv3 passes: kernel stats, FETCH_SIZE, WRITE_SIZE of
+#              prop_kernel (tools/profile.sh), summarised        -> prof/, summary.json
+#   c3 / c4    GraphSAGE C3 / SASRec C4 lines with CPU baselines -> bench_c3.log, bench_c4.log
+#   c3prof / c4prof   kernel stats of the C3 step / the captured C4 step
+#   zipf       the C2 Zipf-popularity graph: line + kernel stats
+#   c5         LightGCN-3 d=256 10 M x 1 M / 200 M on one GPU   -> bench_c5.log
+#   pmc_tg     FETCH / WRITE of the C3 table-gradient sum vs its algorithmic
+#              bytes (tools/tg_sum_bytes.py)                     -> pmc_tg_sum.json
+#   world_c3   the C3 world simulation (W = 1, 2, 8; 1 / 2 / 4 micro-batches)
+#   world_c2   rank 0's C2 step at W = 1..8 (sparse / sharded)
+#   eval       streamed evaluation at C2 with the float64 near-tie check
+#   attn       attention kernels at the C4 length mix
+#   gemm       the GEMM shapes of C3 / C4 and 4096^3
 set -u
 export TMPDIR=/tmp
-E=gpurun_out/ev
+E=gpurun_out/${EV:-ev}
 mkdir -p $E
-PROF_OUT=$E/prof2 bash tools/profile.sh || exit 1
-timeout -k 10 600 python bench.py > $E/bench_c2.log 2>&1 || { echo "bench rc=$?"; exit 1; }
-grep '^{' $E/bench_c2.log | cut -c1-200
-timeout -k 10 300 python tools/bench_sage.py --steps 20 > $E/bench_c3.log 2>&1 || { echo "c3 rc=$?"; exit 1; }
-grep '^{' $E/bench_c3.log | cut -c1-200
-timeout -k 10 300 python tools/bench_sasrec.py --steps 100 > $E/bench_c4.log 2>&1 || { echo "c4 rc=$?"; exit 1; }
-grep '^{' $E/bench_c4.log | cut -c1-200
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c3 -o run --output-format csv -- python3 tools/bench_sage.py --steps 10 --warmup 3 --cpu-baseline 0 > $E/c3.log 2>&1 || { echo "c3 trace rc=$?"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/c4 -o run --output-format csv -- python3 tools/bench_sasrec.py --steps 10 --warmup 3 --cpu-baseline 0 > $E/c4.log 2>&1 || { echo "c4 trace rc=$?"; exit 1; }
+LEGS=${*:-tests c2 prof c3 c4 c3prof c4prof}
 
-# skewed C2 graph (Zipf item popularity): bench line and kernel stats
-timeout -k 10 300 python bench.py --kind zipf --steps 20 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0 > $E/bench_c2_zipf.log 2>&1 || { echo "zipf rc=$?"; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0 > $E/zipf.log 2>&1 || { echo "zipf trace rc=$?"; exit 1; }
-echo "zipf ok"
-echo "evidence ok"
+run() {  # run LIMIT LOG CMD...: one GPU step, its own limit, stop on failure
+  local lim=$1 log=$2
+  shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ]; then
+    echo "FAILED rc=$rc: $*"
+    tail -20 "$log"
+    exit $rc
+  fi
+}
+
+lines() { grep '^{' "$1" | cut -c1-${2:-400} || true; }
+
+for leg in $LEGS; do
+  echo "== $leg"
+  case $leg in
+    tests)
+      run 1100 $E/pytest.log python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread
+      tail -3 $E/pytest.log ;;
+    mark=*)
+      run 900 $E/pytest_k.log python -u -m pytest tests -m gpu -x -v -s --timeout 500 --timeout-method thread -k "${leg#mark=}"
+      tail -5 $E/pytest_k.log ;;
+    smoke)
+      run 300 $E/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
+      tail -3 $E/smoke.log ;;
+    c2)
+      run 700 $E/bench_c2.log python bench.py
+      lines $E/bench_c2.log 600 ;;
+    prof)
+      PROF_OUT=$E/prof bash tools/profile.sh || exit 1
+      find $E/prof -name "*kernel_trace.csv" -delete
+      python tools/summarize_prof.py $E/prof ${TAG:-ev} > $E/summary.log 2>&1 || { echo "summarize failed"; tail $E/summary.log; } ;;
+    c3)
+      run 400 $E/bench_c3.log python tools/bench_sage.py --steps 20
+      lines $E/bench_c3.log ;;
+    c4)
+      run 400 $E/bench_c4.log python tools/bench_sasrec.py --steps 100
+      lines $E/bench_c4.log ;;
+    c3prof)
+      run 300 $E/c3prof.log rocprofv3 --kernel-trace --stats -d $E/c3 -o run --output-format csv -- python3 tools/bench_sage.py --steps 10 --warmup 3 --cpu-baseline 0
+      find $E/c3 -name "*kernel_trace.csv" -delete ;;
+    c4prof)
+      run 300 $E/c4prof.log rocprofv3 --kernel-trace --stats -d $E/c4 -o run --output-format csv -- python3 tools/bench_sasrec.py --steps 10 --warmup 3 --cpu-baseline 0
+      find $E/c4 -name "*kernel_trace.csv" -delete ;;
+    zipf)
+      run 300 $E/bench_c2_zipf.log python bench.py --kind zipf --steps 20 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0
+      lines $E/bench_c2_zipf.log
+      run 300 $E/zipf.log rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0
+      find $E/zipf -name "*kernel_trace.csv" -delete ;;
+    c5)
+      run 900 $E/bench_c5.log python bench.py --users 10000000 --items 1000000 --edges 200000000 --dim 256 --steps 5 --warmup 2 --cpu-baseline off --quality-steps 0 --parity 0
+      lines $E/bench_c5.log ;;
+    pmc_tg)
+      timeout -k 10 200 python -u tools/tg_sum_bytes.py > $E/tg_counts.json 2> $E/tg_counts.log || { echo "tg counts rc=$?"; exit 1; }
+      timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex tg_sum -d $E/tgf -o run --output-format csv -- python3 tools/bench_sage.py --steps 5 --warmup 2 --cpu-baseline 0 > $E/tgf.log 2>&1 || { echo "pmc fetch rc=$?"; exit 1; }
+      timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex tg_sum -d $E/tgw -o run --output-format csv -- python3 tools/bench_sage.py --steps 5 --warmup 2 --cpu-baseline 0 > $E/tgw.log 2>&1 || { echo "pmc write rc=$?"; exit 1; }
+      python tools/tg_sum_bytes.py --counts $E/tg_counts.json --fetch $E/tgf --write $E/tgw --out $E/pmc_tg_sum.json
+      find $E/tgf $E/tgw -name "*kernel_trace.csv" -delete ;;
+    world_c3)
+      timeout -k 10 900 python -u tools/bench_world_sim.py --model sage --worlds 1,2,8 --exchanges fetch --microbatches 1,2,4 --steps 10 > $E/world_sim_c3.jsonl 2> $E/world_sim_c3.log || { echo "world sim rc=$?"; tail $E/world_sim_c3.log; exit 1; }
+      lines $E/world_sim_c3.jsonl 300 ;;
+    world_c2)
+      timeout -k 10 900 python -u tools/bench_world_sim.py --modes sparse,sharded > $E/world_sim_c2.jsonl 2> $E/world_sim_c2.log || { echo "world sim rc=$?"; tail $E/world_sim_c2.log; exit 1; }
+      lines $E/world_sim_c2.jsonl 300 ;;
+    eval)
+      run 600 $E/eval_c2.log python -u tools/eval_bench.py --reps 10
+      lines $E/eval_c2.log 300 ;;
+    attn)
+      run 400 $E/attn.log python -u tools/attn_bench.py --mixes c4 --batches 2048
+      lines $E/attn.log 300 ;;
+    gemm)
+      run 400 $E/gemm.log python -u tools/gemm_bench.py
+      lines $E/gemm.log 300 ;;
+    *)
+      echo "unknown leg $leg"; exit 2 ;;
+  esac
+done
+du -sh $E
+echo "evidence ok: $LEGS"
