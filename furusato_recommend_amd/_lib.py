@@ -286,6 +286,14 @@ SIGNATURES = {
     "mirec_bpr_sample": (c_int, [POINTER(CSR), c_int64, c_int64, c_int64, c_uint64,
                                  c_uint64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                  c_void_p, c_void_p]),
+    "mirec_bpr_sample_ex": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int64, c_int64, c_uint64,
+                                    c_uint64, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p]),
+    "mirec_bpr_sample_capped_ex": (c_int, [POINTER(CSR), c_void_p, c_int64, c_int64, c_int64,
+                                           c_int32, c_uint64, c_uint64, c_int32, c_int32, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mirec_pos_cdf_build": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
 }
 
 

@@ -161,3 +161,39 @@ extern "C" int mirec_csr_sort_rows(const int64_t *rowptr, const int32_t *col, in
   for (auto &x : th) x.join();
   return MIREC_OK;
 }
+
+// Per-user positive CDF for the weighted samplers (the sample_pow option,
+// negative_sample.py:53-56): probs[e - rowptr[0]] = the probability of entry
+// e of its user row (rows 0 .. n_users - 1, the allPos order), each row's
+// probabilities non-negative with a positive sum; cdf[e - rowptr[0]] = the
+// inclusive cumulative sum in float64 divided by the row total (numpy's
+// choice normalises the same way), rounded to float, the row's last entry
+// exactly 1.  Empty rows are skipped.
+extern "C" int mirec_pos_cdf_build(const int64_t *rowptr, int64_t n_users, const double *probs,
+                                   float *cdf) {
+  if (rowptr == nullptr || n_users < 0) return MIREC_ERR_ARG;
+  const int64_t base = rowptr[0], total = rowptr[n_users] - base;
+  if (total > 0 && (probs == nullptr || cdf == nullptr)) return MIREC_ERR_ARG;
+  for (int64_t u = 0; u < n_users; ++u) {
+    const int64_t a = rowptr[u] - base, b = rowptr[u + 1] - base;
+    if (b < a) return MIREC_ERR_ARG;
+    if (a == b) continue;
+    double s = 0.0;
+    for (int64_t e = a; e < b; ++e) {
+      if (!(probs[e] >= 0.0) || !std::isfinite(probs[e])) return MIREC_ERR_ARG;
+      s += probs[e];
+    }
+    if (!(s > 0.0)) return MIREC_ERR_ARG;
+    double c = 0.0;
+    float prev = 0.f;
+    for (int64_t e = a; e < b; ++e) {
+      c += probs[e];
+      float v = (float)(c / s);
+      v = v < prev ? prev : (v > 1.f ? 1.f : v);
+      cdf[e] = v;
+      prev = v;
+    }
+    cdf[b - 1] = 1.f;
+  }
+  return MIREC_OK;
+}

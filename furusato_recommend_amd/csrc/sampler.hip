@@ -6,6 +6,10 @@
 //   u ~ U(users of this shard)       negative_sample.py:107  (redrawn if no positives,
 //                                    the reference skips them: :116-117)
 //   p = allPos[u][U(0, deg u)]       :119-120  (allPos order = CSR row order)
+//     or, with per-user positive probabilities (the sample_pow option,
+//     negative_sample.py:53-56: np.random.choice(len(allPos[u]), p=probs[u])),
+//     the inverse CDF of the user's row: the first entry whose cumulative
+//     probability exceeds a uniform draw (numpy's searchsorted 'right')
 //   n ~ U[0, m_items) until n not in allPos[u]   :121-126
 #include <hipcub/hipcub.hpp>
 
@@ -32,7 +36,30 @@ struct XorShift64Star {
   __device__ __forceinline__ int64_t below(int64_t n) {
     return (int64_t)__umul64hi(next(), (uint64_t)n);
   }
+  // Uniform float in [0, 1) on the 2^-24 grid (exactly representable).
+  __device__ __forceinline__ float unit() {
+    return (float)(uint32_t)(next() >> 40) * 0x1p-24f;
+  }
 };
+
+// The positive's entry offset in a user row [beg, beg + deg): uniform, or
+// (cdf given: cdf[e - base] is the inclusive cumulative probability of entry
+// e within its row, the row's last entry 1) the first entry whose cumulative
+// probability exceeds a uniform draw in [0, 1) — an entry of zero
+// probability is never chosen.
+__device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const float *__restrict__ cdf,
+                                                 int64_t base, int64_t beg, int64_t deg) {
+  if (cdf == nullptr) return rng.below(deg);
+  const float r = rng.unit();
+  const float *c = cdf + (beg - base);
+  int64_t lo = 0, hi = deg - 1;  // the last entry (cdf 1 > r) always qualifies
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (c[mid] > r) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
 
 // Is `node` among the entries [beg, beg + deg) of a user row?  Binary search
 // in the sorted copy of the row when the CSR carries one (csr.col_sorted),
@@ -60,7 +87,7 @@ constexpr int kMaxNegTries = 1 << 16;
 
 __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, int64_t n_users,
+    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
     int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
     int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg, int32_t *err) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -85,10 +112,10 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     neg[t] = 0;
     return;
   }
-  const int64_t p = (int64_t)col[beg + rng.below(deg)] - n_users;
+  const int64_t base = rowptr[0];
+  const int64_t p = (int64_t)col[beg + draw_positive(rng, pos_cdf, base, beg, deg)] - n_users;
   int64_t n = 0;
   bool ok = false;
-  const int64_t base = rowptr[0];
   for (int k = 0; k < kMaxNegTries && !ok; ++k) {
     n = rng.below(m_items);
     ok = !row_has(col, sorted, base, beg, deg, (int32_t)(n_users + n));
@@ -121,18 +148,21 @@ struct CandRng {
 
 // candidate t: user u (its shard), positive item p or -1 (no positives)
 __device__ __forceinline__ void draw_candidate(CandRng &c, const int64_t *__restrict__ rowptr,
-                                               const int32_t *__restrict__ col, int64_t n_users,
+                                               const int32_t *__restrict__ col,
+                                               const float *__restrict__ pos_cdf, int64_t n_users,
                                                int32_t shard, int32_t n_shards, int64_t &u,
                                                int64_t &p, int64_t &beg, int64_t &deg) {
   const int64_t n_local = (n_users - shard + n_shards - 1) / n_shards;
   u = shard + (int64_t)n_shards * c.rng.below(n_local);
   beg = rowptr[u];
   deg = rowptr[u + 1] - beg;
-  p = deg > 0 ? (int64_t)col[beg + c.rng.below(deg)] - n_users : -1;
+  p = deg > 0 ? (int64_t)col[beg + draw_positive(c.rng, pos_cdf, rowptr[0], beg, deg)] - n_users
+              : -1;
 }
 
 __global__ __launch_bounds__(256) void cand_kernel(const int64_t *__restrict__ rowptr,
                                                    const int32_t *__restrict__ col,
+                                                   const float *__restrict__ pos_cdf,
                                                    int64_t n_users, int64_t m_items, int64_t n,
                                                    uint64_t seed, uint64_t offset, int32_t shard,
                                                    int32_t n_shards, int32_t *__restrict__ keys,
@@ -143,7 +173,7 @@ __global__ __launch_bounds__(256) void cand_kernel(const int64_t *__restrict__ r
   if (t >= n) return;
   CandRng c(seed, offset, shard, t);
   int64_t u, p, beg, deg;
-  draw_candidate(c, rowptr, col, n_users, shard, n_shards, u, p, beg, deg);
+  draw_candidate(c, rowptr, col, pos_cdf, n_users, shard, n_shards, u, p, beg, deg);
   keys[t] = p >= 0 ? (int32_t)p : (int32_t)m_items;  // skipped users sort last
   vals[t] = (int32_t)t;
   if (cand_u) cand_u[t] = (int32_t)u;
@@ -170,8 +200,8 @@ __global__ __launch_bounds__(256) void cand_keep_kernel(const int32_t *__restric
 
 __global__ __launch_bounds__(256) void cand_emit_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, int64_t n_users, int64_t m_items, int64_t n,
-    uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
+    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    int64_t m_items, int64_t n, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
     const int32_t *__restrict__ flag, const int32_t *__restrict__ at, int32_t *__restrict__ users,
     int32_t *__restrict__ pos, int32_t *__restrict__ neg, int32_t *__restrict__ count,
     int32_t *__restrict__ err) {
@@ -181,7 +211,7 @@ __global__ __launch_bounds__(256) void cand_emit_kernel(
   if (!flag[t]) return;
   CandRng c(seed, offset, shard, t);  // the same stream: same u, p, then n
   int64_t u, p, beg, deg;
-  draw_candidate(c, rowptr, col, n_users, shard, n_shards, u, p, beg, deg);
+  draw_candidate(c, rowptr, col, pos_cdf, n_users, shard, n_shards, u, p, beg, deg);
   int64_t ng = 0;
   bool ok = false;
   const int64_t base = rowptr[0];
@@ -247,7 +277,8 @@ extern "C" int mirec_bpr_sample_capped_workspace(int64_t n_candidates, int64_t m
   return MIREC_OK;
 }
 
-extern "C" int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
+extern "C" int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const float *pos_cdf,
+                                          int64_t n_users, int64_t m_items,
                                        int64_t n_candidates, int32_t cap, uint64_t seed,
                                        uint64_t offset, int32_t shard, int32_t n_shards,
                                        int32_t *users, int32_t *pos, int32_t *neg,
@@ -282,7 +313,8 @@ extern "C" int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, 
   const int n = (int)n_candidates;
   const dim3 grid((unsigned)((n_candidates + 255) / 256));
   const int32_t *sorted = csr->n_sorted >= n_users ? csr->col_sorted : nullptr;
-  hipLaunchKernelGGL(cand_kernel, grid, dim3(256), 0, st, csr->rowptr, csr->col, n_users, m_items,
+  hipLaunchKernelGGL(cand_kernel, grid, dim3(256), 0, st, csr->rowptr, csr->col, pos_cdf, n_users,
+                     m_items,
                      n_candidates, seed, offset, shard, n_shards, keys_in, vals_in, cand_u,
                      cand_p);
   MIREC_LAUNCH_CHECK();
@@ -298,16 +330,28 @@ extern "C" int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, 
   tb = L.tmp_bytes;
   MIREC_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, at, n, st));
   hipLaunchKernelGGL(cand_emit_kernel, grid, dim3(256), 0, st, csr->rowptr, csr->col, sorted,
-                     n_users, m_items, n_candidates, seed, offset, shard, n_shards, flag, at,
+                     pos_cdf, n_users, m_items, n_candidates, seed, offset, shard, n_shards, flag, at,
                      users, pos, neg, count, err);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
 
-extern "C" int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
-                                int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
-                                int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg,
-                                int32_t *err, mirec_stream_t stream) {
+extern "C" int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
+                                       int64_t n_candidates, int32_t cap, uint64_t seed,
+                                       uint64_t offset, int32_t shard, int32_t n_shards,
+                                       int32_t *users, int32_t *pos, int32_t *neg,
+                                       int32_t *count, int32_t *err, int32_t *cand_u,
+                                       int32_t *cand_p, void *workspace, size_t workspace_bytes,
+                                       mirec_stream_t stream) {
+  return mirec_bpr_sample_capped_ex(csr, nullptr, n_users, m_items, n_candidates, cap, seed,
+                                    offset, shard, n_shards, users, pos, neg, count, err, cand_u,
+                                    cand_p, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mirec_bpr_sample_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+                                   int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset,
+                                   int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
+                                   int32_t *neg, int32_t *err, mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(csr && csr->rowptr && csr->col && users && pos && neg && err);
   MIREC_CHECK_ARG(n_users > 0 && m_items > 0 && batch >= 0);
@@ -316,8 +360,16 @@ extern "C" int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t
   if (batch == 0) return MIREC_OK;
   hipLaunchKernelGGL(bpr_sample_kernel, dim3((batch + 255) / 256), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), csr->rowptr, csr->col,
-                     csr->n_sorted >= n_users ? csr->col_sorted : nullptr, n_users, m_items,
-                     batch, seed, offset, shard, n_shards, users, pos, neg, err);
+                     csr->n_sorted >= n_users ? csr->col_sorted : nullptr, pos_cdf, n_users,
+                     m_items, batch, seed, offset, shard, n_shards, users, pos, neg, err);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
+}
+
+extern "C" int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
+                                int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
+                                int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg,
+                                int32_t *err, mirec_stream_t stream) {
+  return mirec_bpr_sample_ex(csr, nullptr, n_users, m_items, batch, seed, offset, shard, n_shards,
+                             users, pos, neg, err, stream);
 }

@@ -727,12 +727,15 @@ def propagate(graph: Graph, x: torch.Tensor, out: torch.Tensor):
 
 def sample_triples(graph: Graph, batch: int, seed: int, offset: int, users, pos, neg, err,
                    shard: int = 0, n_shards: int = 1):
-    """On-device UniformSample (negative_sample.py:98-134) into int32 buffers."""
-    check(lib.mirec_bpr_sample(graph.csr_ptr(), graph.n_users, graph.m_items, int(batch),
-                               ctypes.c_uint64(seed & (2**64 - 1)),
-                               ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
-                               int(n_shards), users.data_ptr(), pos.data_ptr(),
-                               neg.data_ptr(), err.data_ptr(), _lib.stream_handle()),
+    """On-device UniformSample (negative_sample.py:98-134) into int32 buffers
+    (the positive weighted by the graph's per-user probabilities when
+    ``graph.set_positive_probs`` gave some: negative_sample.py:53-56)."""
+    check(lib.mirec_bpr_sample_ex(graph.csr_ptr(), ptr(getattr(graph, "pos_cdf", None)),
+                                  graph.n_users, graph.m_items, int(batch),
+                                  ctypes.c_uint64(seed & (2**64 - 1)),
+                                  ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
+                                  int(n_shards), users.data_ptr(), pos.data_ptr(),
+                                  neg.data_ptr(), err.data_ptr(), _lib.stream_handle()),
           "bpr_sample")
 
 
@@ -756,12 +759,14 @@ def sample_epoch_capped(graph: Graph, n_candidates: int, cap: int, seed: int, of
     check(lib.mirec_bpr_sample_capped_workspace(n, graph.m_items, ctypes.byref(nb)),
           "bpr_sample_capped_workspace")
     ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=dev)
-    check(lib.mirec_bpr_sample_capped(graph.csr_ptr(), graph.n_users, graph.m_items, n, int(cap),
-                                      ctypes.c_uint64(seed & (2**64 - 1)),
-                                      ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
-                                      int(n_shards), users.data_ptr(), pos.data_ptr(),
-                                      neg.data_ptr(), count.data_ptr(), err.data_ptr(), ptr(cu),
-                                      ptr(cp), ws.data_ptr(), nb.value, _lib.stream_handle()),
+    check(lib.mirec_bpr_sample_capped_ex(graph.csr_ptr(), ptr(getattr(graph, "pos_cdf", None)),
+                                         graph.n_users, graph.m_items, n, int(cap),
+                                         ctypes.c_uint64(seed & (2**64 - 1)),
+                                         ctypes.c_uint64(offset & (2**64 - 1)), int(shard),
+                                         int(n_shards), users.data_ptr(), pos.data_ptr(),
+                                         neg.data_ptr(), count.data_ptr(), err.data_ptr(),
+                                         ptr(cu), ptr(cp), ws.data_ptr(), nb.value,
+                                         _lib.stream_handle()),
           "bpr_sample_capped")
     k = int(count.item())
     if int(err.item()) != 0:

@@ -70,6 +70,7 @@ class Graph:
                        col_sorted=None, n_sorted=0)
         self.transpose = None  # set for non-symmetric graphs (from_edge_index)
         self.col_sorted = None
+        self.pos_cdf = None  # weighted positives (set_positive_probs)
         if self.n_users > 0 and self.m_items > 0:
             self._sort_user_rows()
 
@@ -135,6 +136,38 @@ class Graph:
             g.transpose = cls(rowptr_t, col_t, dinv, n_nodes, 0, device, split)
         return g
 
+    def set_positive_probs(self, probs) -> None:
+        """Per-user positive probabilities for the samplers (the sample_pow
+        option of negative_sample.py:22-56: ``probs[u]`` is the probability
+        vector over ``allPos[u]``, which is this CSR's user-row order).
+        ``probs``: a sequence of per-user arrays, or one flat float array of
+        the user rows' entries; ``None`` restores the uniform positive.  The
+        row CDFs are built on the host (mirec_pos_cdf_build) and kept in HBM;
+        every sampler call on this graph then draws its positive from them."""
+        if probs is None:
+            self.pos_cdf = None
+            return
+        nu = self.n_users
+        n = int(self.rowptr_host[nu] - self.rowptr_host[0])
+        if isinstance(probs, np.ndarray) and probs.ndim == 1:
+            flat = np.ascontiguousarray(probs, dtype=np.float64)
+        else:
+            if len(probs) != nu:
+                raise ValueError(f"probs: one array per user ({nu}), got {len(probs)}")
+            deg = np.diff(self.rowptr_host[: nu + 1])
+            parts = [np.asarray(p, dtype=np.float64).reshape(-1) for p in probs]
+            bad = [u for u, (p, d) in enumerate(zip(parts, deg)) if p.size != d]
+            if bad:
+                raise ValueError(f"probs[{bad[0]}] has {parts[bad[0]].size} entries, "
+                                 f"the user has {deg[bad[0]]} positives")
+            flat = np.concatenate(parts) if parts else np.zeros(0)
+        if flat.size != n:
+            raise ValueError(f"probs: {flat.size} entries for {n} user-row entries")
+        cdf = np.empty(max(n, 1), np.float32)
+        check(lib.mirec_pos_cdf_build(self.rowptr_host.ctypes.data, nu, flat.ctypes.data,
+                                      cdf.ctypes.data), "pos_cdf_build")
+        self.pos_cdf = torch.from_numpy(cdf).to(self.device)
+
     # ---------------------------------------------------------------- helpers
     def degree(self) -> np.ndarray:
         return np.diff(self.rowptr_host)
@@ -160,6 +193,19 @@ class Graph:
         if fused_acc:
             b += 2 * n * dim * 4
         return b
+
+
+def positive_probs(config: dict):
+    """The per-user positive probabilities a model config asks for: the
+    reference's ``sample_pow`` (parse.py:48; negative_sample.py:22-38 loads
+    ``data/sample_prob/sample_prob_<pow>.pkl``, a list of per-user arrays over
+    allPos[u]) comes here as ``config["sample_probs"]`` — the arrays
+    themselves (this package does not unpickle files).  None = uniform."""
+    probs = config.get("sample_probs")
+    if probs is None and float(config.get("sample_pow", 0) or 0) != 0:
+        raise ValueError("sample_pow != 0: pass the per-user probabilities as "
+                         "config['sample_probs'] (the arrays of sample_prob_*.pkl)")
+    return probs
 
 
 _ = _lib  # keep the module import explicit for readers

@@ -39,7 +39,7 @@ from . import _lib
 from . import engine as _engine
 from ._lib import CSR, IN_PRESCALED, Prop, check, lib
 from .engine import AdamGroup, AdamState, sample_triples
-from .graph import DEFAULT_SPLIT, Graph
+from .graph import DEFAULT_SPLIT, Graph, positive_probs
 from .linear import Linear, sage_linear
 from .rows import slice_norms2
 
@@ -466,6 +466,7 @@ class GraphSAGE(nn.Module):
         self.graph = Graph.from_interactions(dataset.trainUser, dataset.trainItem,
                                              self.n_user, self.m_item, self.device,
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
+        self.graph.set_positive_probs(positive_probs(config))
         deg = torch.from_numpy(self.graph.degree()).to(self.device).float()
         self._mean_dinv = torch.where(deg > 0, 1.0 / deg.clamp(min=1), torch.zeros_like(deg))
         # the table's Adam state is stepped by the fused kernel (TableGrad.adam)

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from .engine import AdamState, PropagationEngine, sample_triples
-from .graph import DEFAULT_SPLIT, Graph
+from .graph import DEFAULT_SPLIT, Graph, positive_probs
 
 
 class _Propagate(torch.autograd.Function):
@@ -70,6 +70,7 @@ class LightGCN(nn.Module):
         self.graph = Graph.from_interactions(dataset.trainUser, dataset.trainItem,
                                              self.num_users, self.num_items, self.device,
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
+        self.graph.set_positive_probs(positive_probs(config))
         self.__init_weight()
         self.optim = AdamState(self.all_embedding.weight, lr=config["lr"])
         self.engine = PropagationEngine(self.graph, self.latent_dim, self.num_layers,

@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 
 from .engine import AdamState, PropagationEngine
-from .graph import DEFAULT_SPLIT, Graph
+from .graph import DEFAULT_SPLIT, Graph, positive_probs
 
 
 class MF(nn.Module):
@@ -38,6 +38,7 @@ class MF(nn.Module):
         self.graph = Graph.from_interactions(dataset.trainUser, dataset.trainItem,
                                              self.num_users, self.num_items, self.device,
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
+        self.graph.set_positive_probs(positive_probs(config))
         self.optim = AdamState(self._table, lr=config["lr"])
         self.engine = PropagationEngine(self.graph, self.latent_dim, 0,
                                         int(config.get("bpr_batch_size", 2048)))

@@ -452,12 +452,38 @@ int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
  * candidate's user and positive (-1 = skipped).  Workspace:
  * mirec_bpr_sample_capped_workspace bytes. */
 int mirec_bpr_sample_capped_workspace(int64_t n_candidates, int64_t m_items, size_t *bytes);
+
+/* The same two samplers with per-user positive probabilities (the sample_pow
+ * option of UniformSampling.sample_parallel, negative_sample.py:53-56:
+ * np.random.choice(len(allPos[u]), p=probs[u])): pos_cdf[e - rowptr[0]]
+ * is the inclusive cumulative probability of entry e within its user row
+ * (rows 0 .. n_users - 1 of the CSR, i.e. the allPos order), non-decreasing
+ * in the row, its last entry exactly 1.0f (mirec_pos_cdf_build makes it on
+ * the host).  The positive is the first entry whose cumulative probability
+ * exceeds a uniform draw on the 2^-24 grid (numpy's searchsorted 'right');
+ * with pos_cdf = NULL they are the functions above (bit for bit). */
+/* Host: cdf from probs[e - rowptr[0]] (float64, per user-row entry, each
+ * non-empty row non-negative with a positive sum; normalised per row in
+ * float64 as numpy's choice does).  MIREC_ERR_ARG on a negative / NaN entry
+ * or a zero row. */
+int mirec_pos_cdf_build(const int64_t *rowptr, int64_t n_users, const double *probs,
+                        float *cdf);
+int mirec_bpr_sample_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+                        int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset,
+                        int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
+                        int32_t *neg, int32_t *err, mirec_stream_t stream);
 int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, int64_t m_items,
                             int64_t n_candidates, int32_t cap, uint64_t seed, uint64_t offset,
                             int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
                             int32_t *neg, int32_t *count, int32_t *err, int32_t *cand_u,
                             int32_t *cand_p, void *workspace, size_t workspace_bytes,
                             mirec_stream_t stream);
+int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+                               int64_t m_items, int64_t n_candidates, int32_t cap,
+                               uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
+                               int32_t *users, int32_t *pos, int32_t *neg, int32_t *count,
+                               int32_t *err, int32_t *cand_u, int32_t *cand_p, void *workspace,
+                               size_t workspace_bytes, mirec_stream_t stream);
 
 /* ------------------------------------------------------------------------ */
 /* GraphSAGE hop ops (model/graphsage.py:311-324, neighbor_sampling.py)      */

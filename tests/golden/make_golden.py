@@ -342,6 +342,46 @@ def make_sasrec_golden():
         print("sasrec", d, heads, float(out.abs().mean()))
 
 
+def weighted_probs(all_pos, seed=17):
+    """Per-user positive probabilities over allPos[u] (the format of the
+    reference's sample_prob_*.pkl, negative_sample.py:22-38): Dirichlet
+    weights, with the first entry of every third multi-positive user set to
+    zero (a positive that must never be drawn)."""
+    rng = np.random.default_rng(seed)
+    probs = []
+    for k, pu in enumerate(all_pos):
+        if len(pu) == 0:
+            probs.append(np.zeros(0))
+            continue
+        p = rng.dirichlet(np.ones(len(pu)))
+        if len(pu) > 1 and k % 3 == 0:
+            p[0] = 0.0
+            p /= p.sum()
+        probs.append(p)
+    return probs
+
+
+def make_weighted_sampler_golden(negative_sample, ds, u, i, n_users, m_items):
+    """UniformSampling.sample_parallel with sample_pow != 0 (negative_sample.py:
+    45-72), the reference's own method on an instance whose probabilities are
+    set directly (its __init__ would read proprietary pickles), one process
+    (process_num = 1), after sample()'s user draw (:74-76)."""
+    probs = weighted_probs(ds.allPos)
+    obj = object.__new__(negative_sample.UniformSampling)
+    obj.m_items, obj.n_users, obj.user_num = m_items, n_users, ds.trainDataSize
+    obj.allPos, obj.config, obj.probs = ds.allPos, {"sample_pow": 0.5}, probs
+    np.random.seed(2021)
+    sample_users = np.random.randint(0, obj.n_users, obj.user_num)
+    out = {}
+    obj.sample_parallel(0, 1, sample_users, ds.allPos, out)
+    S = out[0]
+    flat = np.concatenate([p for p in probs if len(p)])
+    np.savez_compressed(os.path.join(OUT, "sampler_weighted.npz"), seed=2021, S=S,
+                        train_user=u, train_item=i, n_users=n_users, m_items=m_items,
+                        probs_flat=flat)
+    print("sampler_weighted", S.shape)
+
+
 def main():
     # optional filter: fixture name prefixes to (re)write, e.g. lgcn_d256_L3 sage_d128
     only = sys.argv[1:]
@@ -426,6 +466,8 @@ def main():
         make_sasrec_golden()
     if want("lgconv"):
         make_graph_op_golden()
+    if want("sampler_weighted"):
+        make_weighted_sampler_golden(negative_sample, ds, u, i, n_users, m_items)
     if only and not any(want(k) for k in ("mf", "sampler", "metrics")):
         return
 

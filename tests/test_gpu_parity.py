@@ -301,6 +301,64 @@ def test_sampler_invariants():
     assert np.all(us.cpu().numpy() % 4 == 1)
 
 
+def test_weighted_positive_sampler(golden):
+    """sample_pow (negative_sample.py:53-56): the device sampler with the
+    per-user probabilities of the reference-generated fixture
+    (sampler_weighted.npz; the reference's own draws pin the oracle, test
+    _oracle.py).  The RNG streams differ from numpy's, so the check is
+    distributional: per (user, item) cell the positive counts against S x
+    P(user) x P(item | user) (chi-square, cells with expectation >= 5),
+    zero-probability positives never drawn; the users and negatives are the
+    uniform sampler's bit for bit (one draw per positive either way); the
+    capped epoch sampler draws its candidates' positives the same way."""
+    from furusato_recommend_amd import LightGCN
+    from furusato_recommend_amd.engine import sample_epoch_capped
+    f = golden("sampler_weighted.npz")
+    u, i, nu, mi = f["train_user"], f["train_item"], int(f["n_users"]), int(f["m_items"])
+    all_pos = [i[u == k] for k in range(nu)]
+    probs = np.split(np.asarray(f["probs_flat"], np.float64),
+                     np.cumsum([len(p) for p in all_pos])[:-1])
+
+    class DS:
+        n_users, m_items, trainUser, trainItem = nu, mi, u, i
+    cfg = {"recdim": 16, "layer": 1, "lr": 1e-3, "decay": 1e-4, "device": "cuda:0",
+           "bpr_batch_size": 64}
+    plain = LightGCN(cfg, DS)
+    m = LightGCN({**cfg, "sample_probs": probs}, DS)
+    S = 400_000
+    uw, pw, nw = (t.cpu().numpy() for t in m.sample(S, seed=5))
+    uu, pu, nn_ = (t.cpu().numpy() for t in plain.sample(S, seed=5))
+    assert int(m._sample_err.item()) == 0
+    assert np.array_equal(uw, uu) and np.array_equal(nw, nn_)
+    assert not np.array_equal(pw, pu)
+    # expected cell probabilities (multi-edges: an item's entries add up)
+    exp = np.zeros((nu, mi))
+    for k in range(nu):
+        for it, pr in zip(all_pos[k], probs[k]):
+            exp[k, it] += pr / nu
+    cnt = np.zeros((nu, mi))
+    np.add.at(cnt, (uw, pw), 1)
+    assert cnt[exp == 0].sum() == 0  # never a zero-probability positive
+    e = exp * S
+    big = e >= 5
+    chi2 = float(((cnt[big] - e[big]) ** 2 / e[big]).sum())
+    dof = int(big.sum()) - 1
+    assert chi2 < dof + 6 * np.sqrt(2 * dof), (chi2, dof)
+    assert all(nw[k] not in all_pos[uw[k]] for k in range(0, S, 101))
+    # the capped epoch sampler: candidate positives from the same CDFs
+    _, _, _, cu, cp = sample_epoch_capped(m.graph, 200_000, 10**6, seed=3, return_candidates=True)
+    cu, cp = cu.cpu().numpy(), cp.cpu().numpy()
+    ok = cp >= 0
+    c2 = np.zeros((nu, mi))
+    np.add.at(c2, (cu[ok], cp[ok]), 1)
+    assert c2[exp == 0].sum() == 0
+    e2 = exp / exp[np.unique(cu[ok])].sum() * ok.sum()
+    big2 = e2 >= 5
+    chi2b = float(((c2[big2] - e2[big2]) ** 2 / e2[big2]).sum())
+    dof2 = int(big2.sum()) - 1
+    assert chi2b < dof2 + 6 * np.sqrt(2 * dof2), (chi2b, dof2)
+
+
 @pytest.mark.parametrize("narrow_max", [0, 64])
 def test_full_size_properties(narrow_max):
     """BASELINE C2 size (1M users x 100K items, 20M edges): size-independent

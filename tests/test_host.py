@@ -453,6 +453,46 @@ def test_train_dp_cli_two_ranks_gloo(golden, tmp_path):
     assert torch.load(str(p) + ".train", weights_only=True)["epoch"] == 1
 
 
+def test_pos_cdf_build_matches_numpy_choice(golden):
+    """mirec_pos_cdf_build (host, libmirec) == numpy choice's normalised
+    cumulative probabilities per user row (oracle.pos_cdf), rounded to
+    float32, each row ending at exactly 1; bad rows rejected."""
+    import ctypes
+
+    from furusato_recommend_amd import Graph
+    from furusato_recommend_amd._lib import lib
+    f = golden("sampler_weighted.npz")
+    u, i, nu, mi = f["train_user"], f["train_item"], int(f["n_users"]), int(f["m_items"])
+    all_pos = [i[u == k] for k in range(nu)]
+    flat = np.ascontiguousarray(f["probs_flat"], np.float64)
+    probs = np.split(flat, np.cumsum([len(p) for p in all_pos])[:-1])
+    g = Graph.from_interactions(u, i, nu, mi, "cpu")
+    rp = g.rowptr_host
+    # the CSR's user rows are the allPos order
+    assert all(np.array_equal(g.col_host[rp[k]:rp[k + 1]] - nu, all_pos[k]) for k in range(nu))
+    cdf = np.empty(len(flat), np.float32)
+    assert lib.mirec_pos_cdf_build(rp.ctypes.data, nu, flat.ctypes.data, cdf.ctypes.data) == 0
+    ref = O.pos_cdf(all_pos, probs)
+    assert np.max(np.abs(cdf - ref)) <= 2 ** -24
+    ends = rp[1:nu + 1] - rp[0] - 1
+    assert np.all(cdf[ends[np.diff(rp[:nu + 1]) > 0]] == 1.0)
+    for k in range(nu):
+        seg = cdf[rp[k] - rp[0]:rp[k + 1] - rp[0]]
+        assert np.all(np.diff(seg) >= 0)
+    bad = flat.copy()
+    bad[0] = -0.1
+    assert lib.mirec_pos_cdf_build(rp.ctypes.data, nu, bad.ctypes.data, cdf.ctypes.data) != 0
+    bad = flat.copy()
+    bad[rp[0]:rp[1]] = 0.0  # a row of zeros
+    assert lib.mirec_pos_cdf_build(rp.ctypes.data, nu, bad.ctypes.data, cdf.ctypes.data) != 0
+    # the Python entry point: per-user arrays, sizes checked
+    g.set_positive_probs(probs)
+    assert np.array_equal(g.pos_cdf.numpy(), cdf)
+    with pytest.raises(ValueError):
+        g.set_positive_probs(probs[:-1])
+    _ = ctypes
+
+
 def test_train_dp_cli_launch_command():
     """The launcher's child command and environment (no processes)."""
     from furusato_recommend_amd import train_dp as T

@@ -78,6 +78,32 @@ def test_sampler_bit_exact(golden):
         assert p in all_pos[uu] and n not in all_pos[uu]
 
 
+def _weighted_probs(f):
+    u, i, n_users = f["train_user"], f["train_item"], int(f["n_users"])
+    all_pos = [i[u == k] for k in range(n_users)]
+    flat, probs, o = f["probs_flat"], [], 0
+    for pu in all_pos:
+        probs.append(flat[o:o + len(pu)])
+        o += len(pu)
+    assert o == len(flat)
+    return all_pos, probs
+
+
+def test_weighted_sampler_bit_exact(golden):
+    """oracle.weighted_sample == the reference's UniformSampling.sample_parallel
+    with per-user probabilities (negative_sample.py:45-72, sample_pow != 0),
+    draw for draw; zero-probability positives never drawn."""
+    f = golden("sampler_weighted.npz")
+    all_pos, probs = _weighted_probs(f)
+    np.random.seed(int(f["seed"]))
+    S = O.weighted_sample(int(f["n_users"]), int(f["m_items"]), all_pos, len(f["train_user"]),
+                          probs)
+    assert np.array_equal(S, f["S"])
+    for uu, p, n in S:
+        pu, pr = all_pos[uu], probs[uu]
+        assert pr[pu == p].sum() > 0 and n not in pu
+
+
 def test_metrics_match_reference(golden):
     f = golden("metrics.npz")
     gt = np.split(f["gt_flat"], np.cumsum(f["gt_len"])[:-1])
