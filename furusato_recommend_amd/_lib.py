@@ -294,6 +294,12 @@ SIGNATURES = {
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_pos_cdf_build": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
+    "mirec_cpu_bpr_sample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                     c_int64, c_uint64, c_uint64, c_int32, c_int32, c_void_p,
+                                     c_void_p, c_void_p, c_void_p, c_int32]),
+    "mirec_cpu_bpr_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
+                                   c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float,
+                                   c_void_p, c_void_p, c_int32]),
 }
 
 

@@ -11,13 +11,20 @@
 //     the inverse CDF of the user's row: the first entry whose cumulative
 //     probability exceeds a uniform draw (numpy's searchsorted 'right')
 //   n ~ U[0, m_items) until n not in allPos[u]   :121-126
+#include <algorithm>
+#include <thread>
+#include <vector>
+
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
 
 namespace mirec {
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+// (The RNG and the per-triple draw are __host__ __device__: the host sampler
+// mirec_cpu_bpr_sample runs the same streams on CPU threads and returns the
+// device sampler's triples bit for bit.)
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
@@ -26,18 +33,22 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 struct XorShift64Star {
   uint64_t s;
-  __device__ __forceinline__ uint64_t next() {
+  __host__ __device__ __forceinline__ uint64_t next() {
     s ^= s >> 12;
     s ^= s << 25;
     s ^= s >> 27;
     return s * 0x2545F4914F6CDD1Dull;
   }
   // Uniform integer in [0, n) by 64x64 -> high-64 multiply (Lemire).
-  __device__ __forceinline__ int64_t below(int64_t n) {
+  __host__ __device__ __forceinline__ int64_t below(int64_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
     return (int64_t)__umul64hi(next(), (uint64_t)n);
+#else
+    return (int64_t)(uint64_t)(((unsigned __int128)next() * (uint64_t)n) >> 64);
+#endif
   }
   // Uniform float in [0, 1) on the 2^-24 grid (exactly representable).
-  __device__ __forceinline__ float unit() {
+  __host__ __device__ __forceinline__ float unit() {
     return (float)(uint32_t)(next() >> 40) * 0x1p-24f;
   }
 };
@@ -47,7 +58,7 @@ struct XorShift64Star {
 // e within its row, the row's last entry 1) the first entry whose cumulative
 // probability exceeds a uniform draw in [0, 1) — an entry of zero
 // probability is never chosen.
-__device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const float *__restrict__ cdf,
+__host__ __device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const float *__restrict__ cdf,
                                                  int64_t base, int64_t beg, int64_t deg) {
   if (cdf == nullptr) return rng.below(deg);
   const float r = rng.unit();
@@ -64,7 +75,7 @@ __device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const floa
 // Is `node` among the entries [beg, beg + deg) of a user row?  Binary search
 // in the sorted copy of the row when the CSR carries one (csr.col_sorted),
 // else a scan of the row in edge order.
-__device__ __forceinline__ bool row_has(const int32_t *__restrict__ col,
+__host__ __device__ __forceinline__ bool row_has(const int32_t *__restrict__ col,
                                         const int32_t *__restrict__ sorted, int64_t base,
                                         int64_t beg, int64_t deg, int32_t node) {
   if (sorted != nullptr) {
@@ -85,13 +96,13 @@ __device__ __forceinline__ bool row_has(const int32_t *__restrict__ col,
 constexpr int kMaxUserTries = 1 << 12;
 constexpr int kMaxNegTries = 1 << 16;
 
-__global__ __launch_bounds__(256) void bpr_sample_kernel(
+// Triple t of a call (its own stream): writes users / pos / neg [t]; false
+// if a draw exhausted its retry budget.
+__host__ __device__ __forceinline__ bool bpr_sample_one(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
-    int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
-    int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg, int32_t *err) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= batch) return;
+    int64_t m_items, int64_t t, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
+    int32_t *users, int32_t *pos, int32_t *neg) {
   XorShift64Star rng;
   // Shards get independent streams: (seed, shard) -> key, then (key, offset + t).
   const uint64_t key = splitmix64(seed + 0xD1B54A32D192ED03ull * (uint64_t)shard);
@@ -106,11 +117,10 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     deg = rowptr[u + 1] - beg;
   } while (deg == 0 && ++tries < kMaxUserTries);
   if (deg == 0) {
-    err[0] = 1;
     users[t] = (int32_t)u;
     pos[t] = 0;
     neg[t] = 0;
-    return;
+    return false;
   }
   const int64_t base = rowptr[0];
   const int64_t p = (int64_t)col[beg + draw_positive(rng, pos_cdf, base, beg, deg)] - n_users;
@@ -120,10 +130,22 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
     n = rng.below(m_items);
     ok = !row_has(col, sorted, base, beg, deg, (int32_t)(n_users + n));
   }
-  if (!ok) err[0] = 1;
   users[t] = (int32_t)u;
   pos[t] = (int32_t)p;
   neg[t] = (int32_t)n;
+  return ok;
+}
+
+__global__ __launch_bounds__(256) void bpr_sample_kernel(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
+    int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg, int32_t *err) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= batch) return;
+  if (!bpr_sample_one(rowptr, col, sorted, pos_cdf, n_users, m_items, t, seed, offset, shard,
+                      n_shards, users, pos, neg))
+    err[0] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -372,4 +394,39 @@ extern "C" int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t
                                 int32_t *err, mirec_stream_t stream) {
   return mirec_bpr_sample_ex(csr, nullptr, n_users, m_items, batch, seed, offset, shard, n_shards,
                              users, pos, neg, err, stream);
+}
+
+// The same sampler on the host (configuration C1, "CPU single-process":
+// BASELINE configs[0]; model/MF.py on a CPU device): host arrays, the same
+// streams, so the triples equal mirec_bpr_sample's bit for bit.  Threads
+// take contiguous blocks of triples.
+extern "C" int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col,
+                                    const int32_t *col_sorted, const float *pos_cdf,
+                                    int64_t n_users, int64_t m_items, int64_t batch,
+                                    uint64_t seed, uint64_t offset, int32_t shard,
+                                    int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg,
+                                    int32_t *err, int32_t n_threads) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(rowptr && col && users && pos && neg && err);
+  MIREC_CHECK_ARG(n_users > 0 && m_items > 0 && batch >= 0);
+  MIREC_CHECK_ARG(n_shards >= 1 && shard >= 0 && shard < n_shards && shard < n_users);
+  if (batch == 0) return MIREC_OK;
+  const int nt = (int)std::max<int64_t>(
+      1, std::min<int64_t>(std::min<int64_t>(n_threads > 0 ? n_threads : 1, 64),
+                           (batch + 4095) / 4096));
+  std::vector<int> bad(nt, 0);
+  auto work = [&](int w) {
+    const int64_t a = batch * w / nt, b = batch * (w + 1) / nt;
+    for (int64_t t = a; t < b; ++t)
+      if (!bpr_sample_one(rowptr, col, col_sorted, pos_cdf, n_users, m_items, t, seed, offset,
+                          shard, n_shards, users, pos, neg))
+        bad[w] = 1;
+  };
+  std::vector<std::thread> th;
+  for (int w = 1; w < nt; ++w) th.emplace_back(work, w);
+  work(0);
+  for (auto &x : th) x.join();
+  for (int w = 0; w < nt; ++w)
+    if (bad[w]) err[0] = 1;
+  return MIREC_OK;
 }

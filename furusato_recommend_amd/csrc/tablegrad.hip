@@ -108,18 +108,33 @@ __global__ __launch_bounds__(256) void tg_prep_kernel(GroupArgs ga, int64_t n_en
   }
 }
 
-// Entry v of the sorted order (its index in the groups' concatenation):
-// gradient row address, hash base of its dropout quads (key + first quad),
-// threshold, weight (x dropout scale).
-__device__ __forceinline__ void tg_decode(const GroupArgs &ga, const float *__restrict__ wt,
-                                          int32_t v, int32_t d, uint64_t &am, uint64_t &hm,
-                                          uint32_t &thm, float &wm) {
+// The plan of sorted entry i (tg_plan_kernel, after the sort): its index v
+// in the groups' concatenation and its weight (1/cnt of its target for a
+// mean group, else 1; x the dropout scale when its group drops out) — the
+// one lookup of an entry that depends on another load, taken here in bulk
+// so that pass 1's first round of loads carries everything but the rows.
+__global__ __launch_bounds__(256) void tg_plan_kernel(GroupArgs ga, const int32_t *__restrict__ vals,
+                                                      const float *__restrict__ wt, int64_t n,
+                                                      int2 *__restrict__ plan) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t v = vals[i];
+  const int g = group_of(ga.ent_off, ga.n_groups, v);
+  const int32_t t = (v - (int32_t)pick(ga.ent_off, g)) / pick(ga.k, g);
+  const float w = wt[pick(ga.tgt_off, g) + t];
+  plan[i] = make_int2(v, __float_as_int(pick(ga.thresh, g) ? w * pick(ga.scale, g) : w));
+}
+
+// Plan entry (v, w) of the sorted order: gradient row address, hash base of
+// its dropout quads (key + first quad), threshold, weight.
+__device__ __forceinline__ void tg_decode(const GroupArgs &ga, int2 pl, int32_t d, uint64_t &am,
+                                          uint64_t &hm, uint32_t &thm, float &wm) {
+  const int32_t v = pl.x;
   const int g = group_of(ga.ent_off, ga.n_groups, v);
   const int32_t e = v - (int32_t)pick(ga.ent_off, g);
   const int32_t t = e / pick(ga.k, g);
   thm = pick(ga.thresh, g);
-  const float w = wt[pick(ga.tgt_off, g) + t];
-  wm = thm ? w * pick(ga.scale, g) : w;
+  wm = __int_as_float(pl.y);
   am = (uint64_t)(pick(ga.grad, g) + (int64_t)t * d);
   hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
 }
@@ -181,11 +196,12 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
 // The loads a chunk starts from: the keys before and around it, its
 // entries' keys and indices and those of the window after it.
 struct TgRaw {
-  int32_t kprev, kpp, km, kx, vm, vx;
+  int32_t kprev, kpp, km, kx;
+  int2 pm, px;
 };
 
 __device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
-                                            const int32_t *__restrict__ vals, int64_t n,
+                                            const int2 *__restrict__ plan, int64_t n,
                                             int64_t chunk, int sub, TgRaw &r) {
   const int64_t beg = chunk * kCh;
   const int64_t end = beg + kCh < n ? beg + kCh : n;
@@ -197,15 +213,14 @@ __device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
   r.kpp = beg > kCh ? keys[beg - kCh - 1] : -1;
   r.km = in_chunk ? keys[pe] : kEnd;
   r.kx = in_win ? keys[px] : kEnd;
-  // the entries' indices load beside their keys (not behind them)
-  r.vm = in_chunk ? vals[pe] : 0;
-  r.vx = in_win ? vals[px] : 0;
+  // the entries' plans load beside their keys (not behind them)
+  r.pm = in_chunk ? plan[pe] : make_int2(0, 0);
+  r.px = in_win ? plan[px] : make_int2(0, 0);
 }
 
 // One chunk of pass 1 from its loaded keys / indices (see below).
 template <int LPR>
-__device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__restrict__ wt,
-                                         int64_t n, int32_t d, int32_t n_rows,
+__device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t d, int32_t n_rows,
                                          float *__restrict__ acc_out,
                                          int32_t *__restrict__ stamp, int32_t gen,
                                          float *__restrict__ part, int64_t chunk, int sub,
@@ -242,8 +257,8 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__res
   uint64_t am = 0, hm = 0, am2 = 0, hm2 = 0;
   uint32_t thm = 0, thm2 = 0;
   float wm = 0.f, wm2 = 0.f;
-  if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, wt, r.vm, d, am, hm, thm, wm);
-  if (sub < n_ext) tg_decode(ga, wt, r.vx, d, am2, hm2, thm2, wm2);
+  if (in_chunk && sub >= skip && km < n_rows) tg_decode(ga, r.pm, d, am, hm, thm, wm);
+  if (sub < n_ext) tg_decode(ga, r.px, d, am2, hm2, thm2, wm2);
   // valid entries of the chunk: up to the first invalid id (they sort last)
   const unsigned long long bad = (__ballot(in_chunk && km >= n_rows) >> base) & kmask;
   const int nval = bad != 0 ? (int)__builtin_ctzll(bad) : nin;
@@ -303,8 +318,7 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, const float *__res
 // VGPRs, and the gathers, not the key loads, are what each wave waits on.)
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
-                                                     const int32_t *__restrict__ vals,
-                                                     const float *__restrict__ wt, int64_t n,
+                                                     const int2 *__restrict__ plan, int64_t n,
                                                      int32_t d, int32_t n_rows,
                                                      float *__restrict__ acc_out,
                                                      int32_t *__restrict__ stamp, int32_t gen,
@@ -317,8 +331,8 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   const int64_t n_chunks = (n + kCh - 1) / kCh;
   if (group >= n_chunks) return;  // the whole group leaves together
   TgRaw r;
-  tg_load_raw(keys, vals, n, group, sub, r);
-  tg_chunk<LPR>(ga, wt, n, d, n_rows, acc_out, stamp, gen, part, group, sub, base, r);
+  tg_load_raw(keys, plan, n, group, sub, r);
+  tg_chunk<LPR>(ga, n, d, n_rows, acc_out, stamp, gen, part, group, sub, base, r);
 }
 
 // Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
@@ -615,7 +629,7 @@ static int lanes_per_row(int32_t d) {
 
 struct TgLayout {
   int64_t n_ent, n_tgt, n_chunks;
-  size_t keys_in, keys_out, vals_in, vals_out, wt, part, bsum, sort, sort_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, wt, plan, part, bsum, sort, sort_bytes, total;
   int end_bit;
 };
 
@@ -641,7 +655,8 @@ static int tg_layout(const mirec_row_grad_group_t *groups, int32_t n_groups, int
   L->vals_in = 2 * seg;
   L->vals_out = 3 * seg;
   L->wt = 4 * seg;
-  L->part = L->wt + up(sizeof(float) * std::max<int64_t>(n_tgt, 1));
+  L->plan = L->wt + up(sizeof(float) * std::max<int64_t>(n_tgt, 1));
+  L->part = L->plan + 2 * seg;
   L->bsum = L->part + up(sizeof(float) * 2 * std::max<int64_t>(L->n_chunks, 1) * dim);
   L->sort = L->bsum + up(sizeof(float) * std::max<int64_t>(L->n_chunks / kBlockChunks, 1) * dim);
   int bits = 1;
@@ -785,6 +800,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   int32_t *vals_in = reinterpret_cast<int32_t *>(ws + L.vals_in);
   int32_t *vals_out = reinterpret_cast<int32_t *>(ws + L.vals_out);
   float *wt = reinterpret_cast<float *>(ws + L.wt);
+  int2 *plan = reinterpret_cast<int2 *>(ws + L.plan);
   float *part = reinterpret_cast<float *>(ws + L.part);
   float *bsum = reinterpret_cast<float *>(ws + L.bsum);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -795,6 +811,9 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   size_t sort_bytes = L.sort_bytes;
   MIREC_HIP(tg_sort(ws + L.sort, sort_bytes, keys_in, keys_out, vals_in, vals_out, (int)L.n_ent,
                     L.end_bit, st));
+  hipLaunchKernelGGL(tg_plan_kernel, dim3((unsigned)((L.n_ent + 255) / 256)), dim3(256), 0, st,
+                     ga, vals_out, wt, L.n_ent, plan);
+  MIREC_LAUNCH_CHECK();
   const int lpr = lanes_per_row(dim);
   const int64_t threads = L.n_chunks * lpr;
   const int64_t n_blocks = L.n_chunks / kBlockChunks;
@@ -802,7 +821,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
     hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga,        \
-                       keys_out, vals_out, wt, L.n_ent, dim, n_rows, acc, stamp, gen, part);  \
+                       keys_out, plan, L.n_ent, dim, n_rows, acc, stamp, gen, part);          \
     MIREC_LAUNCH_CHECK();                                                                    \
     if (n_blocks > 0) {                                                                      \
       hipLaunchKernelGGL(tg_block_kernel<LP>, dim3((unsigned)((n_blocks * LP + 255) / 256)),  \

@@ -70,6 +70,8 @@ def evaluate(model, test_dict: dict, topks=(10, 20), batch: int = 10000,
     if users.size == 0:
         return res
     kmax = max(topks)
+    if getattr(model, "device", None) is not None and torch.device(model.device).type == "cpu":
+        return _evaluate_host(model, test_dict, users, topks, batch, return_topk, res)
     emb = None
     if stream is not False and hasattr(model, "eval_embeddings") and kmax <= STREAM_MAX_K:
         emb = model.eval_embeddings()   # propagates once
@@ -92,6 +94,35 @@ def evaluate(model, test_dict: dict, topks=(10, 20), batch: int = 10000,
         r = test_one_batch(top, gt, topks)
         for m in res:
             res[m] += r[m]
+    for m in res:
+        res[m] /= float(len(users))
+    if return_topk:
+        return res, np.concatenate(tops)
+    return res
+
+
+@torch.no_grad()
+def _evaluate_host(model, test_dict, users, topks, batch, return_topk, res):
+    """A CPU model (configuration C1): the reference's own arithmetic on the
+    host — rating = model.eval_ratings() rows, the train positives set to
+    -1024, torch.topk (trainer.py:115-138) — and the same metric sums."""
+    kmax = max(topks)
+    ratings = model.eval_ratings()
+    g = model.graph
+    rp, col, nu = g.rowptr_host, g.col_host, g.n_users
+    tops = []
+    for i in range(0, len(users), batch):
+        bu = users[i:i + batch]
+        rating = ratings(torch.from_numpy(bu)).clone()
+        for r, u in enumerate(bu.tolist()):
+            items = col[rp[u]:rp[u + 1]].astype(np.int64) - nu
+            rating[r, torch.from_numpy(items[(items >= 0) & (items < rating.shape[1])])] = -1024.0
+        top = torch.topk(rating, kmax).indices.numpy()
+        if return_topk:
+            tops.append(top)
+        r_ = test_one_batch(top, [test_dict[int(u)] for u in bu], topks)
+        for m in res:
+            res[m] += r_[m]
     for m in res:
         res[m] /= float(len(users))
     if return_topk:

@@ -6,12 +6,23 @@ rows.  The two reference tables ``embedding_user`` / ``embedding_item`` are
 views into one [n_users + m_items, d] device table so the fused BPR /
 seed / Adam kernels (one pass over the table) serve both; ``state_dict``
 keeps the reference keys ``embedding_user.weight`` / ``embedding_item.weight``.
+
+``device="cpu"`` is configuration C1 as BASELINE states it ("CPU
+single-process, no GPU"): the same model on host arrays, stepped by the
+library's host code — mirec_cpu_bpr_sample (the device sampler's streams on
+CPU threads: the same triples) and mirec_cpu_bpr_step (BPR loss, backward,
+dense Adam) — and evaluated with the reference's own rating / mask / topk
+arithmetic on the CPU (trainer.py:115-138).
 """
 from __future__ import annotations
+
+import ctypes
+import os
 
 import torch
 import torch.nn as nn
 
+from ._lib import check, lib, ptr
 from .engine import AdamState, PropagationEngine
 from .graph import DEFAULT_SPLIT, Graph, positive_probs
 
@@ -24,8 +35,9 @@ class MF(nn.Module):
         self.num_items = int(dataset.m_items)
         self.latent_dim = int(config.get("latent_dim_rec", config.get("recdim", 32)))
         self.device = torch.device(config.get("device", "cuda:0"))
-        if self.device.type != "cuda":
-            raise RuntimeError("MF (furusato_recommend_amd) runs on a HIP device only")
+        if self.device.type not in ("cuda", "cpu"):
+            raise RuntimeError(f"MF (furusato_recommend_amd): no {self.device.type} path")
+        self.on_host = self.device.type == "cpu"
         # model/MF.py:47-54: default nn.Embedding init, N(0, 1)
         table = torch.randn(self.num_users + self.num_items, self.latent_dim,
                             device=self.device)
@@ -40,9 +52,14 @@ class MF(nn.Module):
                                              split=int(config.get("csr_split", DEFAULT_SPLIT)))
         self.graph.set_positive_probs(positive_probs(config))
         self.optim = AdamState(self._table, lr=config["lr"])
-        self.engine = PropagationEngine(self.graph, self.latent_dim, 0,
-                                        int(config.get("bpr_batch_size", 2048)))
         self._loss_accum = torch.zeros(1, dtype=torch.float32, device=self.device)
+        if self.on_host:
+            self.engine = None
+            self._grad_ws = torch.empty_like(self._table)
+            self.n_threads = int(config.get("n_threads", os.cpu_count() or 1))
+        else:
+            self.engine = PropagationEngine(self.graph, self.latent_dim, 0,
+                                            int(config.get("bpr_batch_size", 2048)))
 
     def load_table(self, user_w: torch.Tensor, item_w: torch.Tensor):
         with torch.no_grad():
@@ -75,12 +92,23 @@ class MF(nn.Module):
 
     def sample(self, n_triples: int, seed: int, offset: int = 0, shard: int = 0,
                n_shards: int = 1):
-        """On-device UniformSample: int32 (users, pos, neg) device tensors."""
+        """UniformSample (negative_sample.py:98-134) on the model's device:
+        int32 (users, pos, neg) tensors (on the host: the device sampler's
+        streams, the same triples)."""
         from .engine import sample_triples
         u = torch.empty(n_triples, dtype=torch.int32, device=self.device)
         p, n = torch.empty_like(u), torch.empty_like(u)
         err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        sample_triples(self.graph, n_triples, seed, offset, u, p, n, err, shard, n_shards)
+        if self.on_host:
+            g = self.graph
+            check(lib.mirec_cpu_bpr_sample(
+                g.rowptr_host.ctypes.data, g.col_host.ctypes.data, ptr(g.col_sorted),
+                ptr(getattr(g, "pos_cdf", None)), g.n_users, g.m_items, int(n_triples),
+                ctypes.c_uint64(seed & (2**64 - 1)), ctypes.c_uint64(offset & (2**64 - 1)),
+                int(shard), int(n_shards), u.data_ptr(), p.data_ptr(), n.data_ptr(),
+                err.data_ptr(), self.n_threads), "cpu_bpr_sample")
+        else:
+            sample_triples(self.graph, n_triples, seed, offset, u, p, n, err, shard, n_shards)
         self._sample_err = err
         return u, p, n
 
@@ -106,9 +134,28 @@ class MF(nn.Module):
 
     @torch.no_grad()
     def stageOne(self, user, pos, neg, loss_accum=None):
+        if self.on_host:
+            return self._host_step(self._as_i32(user), self._as_i32(pos), self._as_i32(neg),
+                                   loss_accum)
         return self.engine.train_step(self._table, self.optim, self._as_i32(user),
                                       self._as_i32(pos), self._as_i32(neg),
                                       float(self.config["decay"]), loss_accum).clone()
+
+    def _host_step(self, u, p, n, loss_accum=None):
+        """model/MF.py:88-94 on the host (mirec_cpu_bpr_step)."""
+        hp = self.optim.next_hparams()
+        out = ctypes.c_float(0.0)
+        st = self.optim
+        check(lib.mirec_cpu_bpr_step(self._table.data_ptr(), st.exp_avg.data_ptr(),
+                                     st.exp_avg_sq.data_ptr(), self._grad_ws.data_ptr(),
+                                     self._table.shape[0], self.latent_dim, self.num_users,
+                                     u.data_ptr(), p.data_ptr(), n.data_ptr(), u.numel(),
+                                     float(self.config["decay"]), ctypes.byref(hp),
+                                     ctypes.byref(out), self.n_threads), "cpu_bpr_step")
+        loss = torch.tensor(out.value, dtype=torch.float32)
+        if loss_accum is not None:
+            loss_accum += loss
+        return loss
 
     @torch.no_grad()
     def OneEpoch(self, user, pos, neg):
@@ -117,6 +164,9 @@ class MF(nn.Module):
         user, pos, neg = self._as_i32(user), self._as_i32(pos), self._as_i32(neg)
         self._loss_accum.zero_()
         for i in range(0, n, B):
+            if self.on_host:
+                self._host_step(user[i:i + B], pos[i:i + B], neg[i:i + B], self._loss_accum)
+                continue
             self.engine.train_step(self._table, self.optim, user[i:i + B], pos[i:i + B],
                                    neg[i:i + B], float(self.config["decay"]),
                                    self._loss_accum)

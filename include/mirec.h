@@ -967,6 +967,31 @@ int mirec_score_topk(const float *user_emb, int64_t n_eval, const float *item_em
                      int64_t n_users, int32_t k, int32_t *topk_idx, float *topk_val,
                      void *workspace, size_t workspace_bytes, mirec_stream_t stream);
 
+/* ------------------------------------------------------------------------ */
+/* Host (CPU) path of configuration C1 (model/MF.py BPR, "CPU single-process", */
+/* BASELINE configs[0]): host pointers, no stream, n_threads worker threads.  */
+/* ------------------------------------------------------------------------ */
+
+/* mirec_bpr_sample on the host: the same counter streams, so the triples are
+ * the device sampler's bit for bit (col_sorted / pos_cdf optional, as in
+ * mirec_csr_t / mirec_bpr_sample_ex).  Replaces UniformSample,
+ * negative_sample.py:98-134, for a CPU model. */
+int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col, const int32_t *col_sorted,
+                         const float *pos_cdf, int64_t n_users, int64_t m_items, int64_t batch,
+                         uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
+                         int32_t *users, int32_t *pos, int32_t *neg, int32_t *err,
+                         int32_t n_threads);
+
+/* One MF stageOne (model/MF.py:62-94: BPR loss + decay x reg, backward,
+ * torch.optim.Adam over the whole table) on a [n_rows, dim] host table whose
+ * item rows start at item_offset (= n_users): grad is a [n_rows, dim]
+ * workspace; *loss_out = loss + decay reg (the value stageOne returns).
+ * MIREC_ERR_RANGE if an id is outside its table slice. */
+int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_sq, float *grad,
+                       int64_t n_rows, int32_t dim, int64_t item_offset, const int32_t *users,
+                       const int32_t *pos, const int32_t *neg, int64_t batch, float decay,
+                       const mirec_adam_hparams_t *h, float *loss_out, int32_t n_threads);
+
 #ifdef __cplusplus
 }
 #endif

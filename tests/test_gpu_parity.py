@@ -3375,6 +3375,41 @@ def test_capped_epoch_sampler_matches_sequential_rule():
         assert pp[k] in row and nn[k] not in row
 
 
+def test_host_sampler_equals_device_sampler(golden):
+    """mirec_cpu_bpr_sample (C1's host path) draws the device sampler's
+    triples bit for bit: the same counter streams, uniform and weighted
+    positives, sharded."""
+    import ctypes
+
+    from furusato_recommend_amd import SyntheticBipartite, _lib
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(5000, 300, 200_000, seed=6, kind="zipf", test_frac=0)
+    gd = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    gh = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cpu")
+    rng = np.random.default_rng(1)
+    probs = [rng.random(int(d)) + 0.01 for d in np.diff(gh.rowptr_host[: ds.n_users + 1])]
+    for weighted in (False, True):
+        for g in (gd, gh):
+            g.set_positive_probs(probs if weighted else None)
+        for shard, n_shards in ((0, 1), (2, 3)):
+            dev = [torch.empty(20_000, dtype=torch.int32, device="cuda") for _ in range(3)]
+            host = [torch.empty(20_000, dtype=torch.int32) for _ in range(3)]
+            err = torch.zeros(1, dtype=torch.int32, device="cuda")
+            herr = torch.zeros(1, dtype=torch.int32)
+            _lib.check(_lib.lib.mirec_bpr_sample_ex(
+                gd.csr_ptr(), _lib.ptr(gd.pos_cdf), gd.n_users, gd.m_items, 20_000,
+                ctypes.c_uint64(9), ctypes.c_uint64(77), shard, n_shards, dev[0].data_ptr(),
+                dev[1].data_ptr(), dev[2].data_ptr(), err.data_ptr(), _lib.stream_handle()), "d")
+            _lib.check(_lib.lib.mirec_cpu_bpr_sample(
+                gh.rowptr_host.ctypes.data, gh.col_host.ctypes.data, _lib.ptr(gh.col_sorted),
+                _lib.ptr(gh.pos_cdf), gh.n_users, gh.m_items, 20_000, ctypes.c_uint64(9),
+                ctypes.c_uint64(77), shard, n_shards, host[0].data_ptr(), host[1].data_ptr(),
+                host[2].data_ptr(), herr.data_ptr(), 8), "h")
+            assert int(err.item()) == 0 and int(herr.item()) == 0
+            for a, b in zip(dev, host):
+                assert torch.equal(a.cpu(), b), (weighted, shard)
+
+
 def test_sampler_binary_search_equals_scan():
     """With the sorted user rows (csr.col_sorted) the negative rejection is a
     binary search; the triples equal the row-scan ones draw for draw."""

@@ -944,3 +944,74 @@ def test_bf16_three_term_split_error_bound():
     exact = x.astype(np.float64) * y.astype(np.float64)
     rel = np.abs(six - exact) / np.abs(exact)
     assert rel.max() <= 2.0 ** -22, rel.max()
+
+
+# ---------------------------------------------- configuration C1 on the host
+class _DS:
+    def __init__(self, u, i, nu, mi):
+        self.trainUser, self.trainItem = np.asarray(u), np.asarray(i)
+        self.n_users, self.m_items = int(nu), int(mi)
+        self.trainDataSize = len(u)
+
+
+def test_mf_cpu_step_matches_reference_fixture(golden):
+    """C1's host path (mirec_cpu_bpr_step: model/MF.py:62-94 + torch Adam)
+    against the reference MF's own step (mf_d32.npz, make_golden.py): the
+    returned loss, both tables after the step, getUsersRating after it."""
+    from furusato_recommend_amd import MF
+    f = golden("mf_d32.npz")
+    m = MF({"latent_dim_rec": 32, "lr": float(f["lr"]), "decay": float(f["decay"]),
+            "device": "cpu", "bpr_batch_size": 64},
+           _DS(f["train_user"], f["train_item"], f["n_users"], f["m_items"]))
+    m.load_table(torch.from_numpy(f["user_w0"]), torch.from_numpy(f["item_w0"]))
+    t = torch.from_numpy(f["triples"])
+    loss, reg = m.bpr_loss(t[:, 0], t[:, 1], t[:, 2])
+    assert abs(float(loss) - float(f["loss"])) < 1e-5 * abs(float(f["loss"]))
+    sl = float(m.stageOne(t[:, 0], t[:, 1], t[:, 2]))
+    assert abs(sl - float(f["step_loss"])) < 1e-5 * abs(float(f["step_loss"]))
+
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        return float(np.abs(a - b).max() / np.abs(b).max())
+    assert rel(m.embedding_user.weight.detach(), f["user_w1"]) < 1e-6
+    assert rel(m.embedding_item.weight.detach(), f["item_w1"]) < 1e-6
+    assert rel(m.getUsersRating(torch.arange(5)), f["rating5"]) < 1e-6
+
+
+def test_mf_cpu_c1_epochs_and_evaluation_vs_oracle():
+    """BASELINE C1 as stated (10 000 users x 1 000 items, 5-core, d = 32,
+    CPU single-process): the model's own host sampler (triples the device
+    sampler draws too) and two OneEpochs against OracleMF stepping the same
+    triples (loss, tables at 1e-5), then evaluate() on the host == the
+    oracle's Trainer.test arithmetic (trainer.py:115-170) on the same tables."""
+    from furusato_recommend_amd import MF, FiveCore
+    from furusato_recommend_amd.evaluate import evaluate
+    ds = FiveCore(10_000, 1_000, 5, seed=0)
+    torch.manual_seed(2020)
+    m = MF({"latent_dim_rec": 32, "lr": 1e-3, "decay": 1e-4, "device": "cpu",
+            "bpr_batch_size": 2048, "n_threads": 4}, ds)
+    o = O.OracleMF(m.embedding_user.weight, m.embedding_item.weight, 1e-3, 1e-4)
+    for ep in range(2):
+        u, p, n = m.sample(ds.trainDataSize, seed=2020, offset=ep * ds.trainDataSize)
+        assert int(m._sample_err) == 0
+        uu, pp, nn_ = u.numpy(), p.numpy(), n.numpy()
+        for k in range(0, len(uu), 331):  # the sampler's invariants
+            assert pp[k] in ds.allPos[uu[k]] and nn_[k] not in ds.allPos[uu[k]]
+        lg = float(m.OneEpoch(u, p, n))
+        acc = 0.0
+        for i in range(0, len(uu), 2048):
+            acc += o.stageOne(uu[i:i + 2048], pp[i:i + 2048], nn_[i:i + 2048])
+        lo = acc / (len(uu) // 2048 + 1)
+        assert abs(lg - lo) < 1e-5 * abs(lo)
+        for a, b in ((m.embedding_user.weight, o.user), (m.embedding_item.weight, o.item)):
+            a, b = a.detach().double(), b.detach().double()
+            assert float((a - b).abs().max() / b.abs().max()) < 1e-5
+    # the host sampler is a pure function of (seed, offset): shape-independent
+    u2, _, _ = m.sample(1000, seed=2020, offset=500)
+    u1, _, _ = m.sample(2000, seed=2020, offset=0)
+    assert torch.equal(u2, u1[500:1500])
+    res, top = evaluate(m, ds.testDict, (10, 20), 4000, return_topk=True)
+    allpos = [np.asarray(a) for a in ds.allPos]
+    ref = O.evaluate(o.user.detach(), o.item.detach(), ds.testDict, allpos, topks=(10, 20))
+    for k in ("recall", "precision", "ndcg"):
+        assert np.allclose(res[k], ref[k], atol=2e-4), (k, res[k], ref[k])

@@ -15,3 +15,6 @@ timeout -k 10 300 python bench.py > $E/bench_c2.log 2>&1 || { echo "bench rc=$?"
 grep '^{' $E/bench_c2.log | cut -c1-700
 timeout -k 10 300 python -m furusato_recommend_amd.train_dp --model lgn --gpus 1 --synthetic 20000,2000,200000,cluster --recdim 64 --layer 3 --bpr_batch 4096 --epochs 2 --test_span 1 --train_iterative 1 --path $E/ck > $E/cli.log 2>&1 || { echo "cli rc=$?"; tail -20 $E/cli.log; exit 1; }
 cut -c1-400 $E/cli.log | tail -5
+for L in base tgA; do MIREC_LIB=var/libmirec_$L.so timeout -k 10 200 python tools/tg_bench.py --reps 50 >> $E/tg_ab.jsonl 2>> $E/tg_ab.log || { echo "tg_bench $L failed"; tail $E/tg_ab.log; exit 1; }; done
+for L in base tgA; do MIREC_LIB=var/libmirec_$L.so timeout -k 10 200 python tools/tg_bench.py --reps 50 >> $E/tg_ab.jsonl 2>> $E/tg_ab.log || { echo "tg_bench $L failed"; exit 1; }; done
+cat $E/tg_ab.jsonl
