@@ -191,9 +191,20 @@ __device__ __forceinline__ bool user_has(const int64_t *__restrict__ rowptr,
   return false;
 }
 
-__device__ __forceinline__ unsigned bloom_h1(int64_t item) { return (unsigned)item & 255u; }
-__device__ __forceinline__ unsigned bloom_h2(int64_t item) {
-  return ((unsigned)item * 0x9E3779B1u) >> 24;
+// Train positives of a user slot inside the workgroup's item chunk, kept in
+// LDS (at most kStPos; a user with more falls back to the binary search of
+// its CSR row in global memory): a candidate's mask test is then a scan of
+// a few LDS words instead of dependent global loads.  (Per C2 user ~20
+// positives over 100 K items, ~2 inside one chunk.)
+constexpr int kStPos = 8;
+
+// LDS visibility among the lanes of one wave (the candidate buffers are
+// wave-private): the wave's LDS operations complete in order, the fences
+// keep the compiler from moving accesses across.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // x of lane (lane ^ stride), stride a power of two < 64, on the VALU instead
@@ -272,11 +283,10 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   __shared__ float cv[kStUsers][kStCap];
   __shared__ int ci[kStUsers][kStCap];
   __shared__ int cnt[kStUsers];
-  // per user a 256-bit Bloom filter of its train items (2 hashes): a
-  // candidate whose bits are not both set is certainly not masked, so the
-  // binary search in global memory runs only for members (and ~2 % false
-  // hits at 20 items per user)
-  __shared__ unsigned bloom[kStUsers][8];
+  // per user its train positives inside the chunk (kStPos at most; npos >
+  // kStPos = overflow: the global binary search)
+  __shared__ int posl[kStUsers][kStPos];
+  __shared__ int npos[kStUsers];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int ul = 32 * w + i;  // user slot in the workgroup
@@ -297,7 +307,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     }
   }
   if (t < kStUsers) cnt[t] = 0;
-  for (int q = t; q < kStUsers * 8; q += 128) bloom[q / 8][q % 8] = 0u;
+  if (t < kStUsers) npos[t] = 0;
   __syncthreads();
   if (rowptr != nullptr && users != nullptr) {
     // two threads per user slot walk its row
@@ -307,9 +317,9 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       const int64_t us = users[b];
       for (int64_t e = rowptr[us] + (t & 1); e < rowptr[us + 1]; e += 2) {
         const int64_t item = (int64_t)col[e] - n_users;
-        const unsigned h1 = bloom_h1(item), h2 = bloom_h2(item);
-        atomicOr(&bloom[u][h1 >> 5], 1u << (h1 & 31));
-        atomicOr(&bloom[u][h2 >> 5], 1u << (h2 & 31));
+        if (item < it0 || item >= it1) continue;
+        const int q = atomicAdd(&npos[u], 1);
+        if (q < kStPos) posl[u][q] = (int)item;
       }
     }
   }
@@ -342,10 +352,15 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     ix = lane < n ? ci[u][lane] : INT_MAX;
     const int64_t b = (int64_t)blockIdx.x * kStUsers + u;
     if (lane < n && rowptr != nullptr && users != nullptr && b < n_eval && v != -1024.f) {
-      const unsigned h1 = bloom_h1(ix), h2 = bloom_h2(ix);
-      if (((bloom[u][h1 >> 5] >> (h1 & 31)) & (bloom[u][h2 >> 5] >> (h2 & 31)) & 1u) &&
-          user_has(rowptr, col, sorted, n_sorted, users[b], (int32_t)(n_users + ix)))
-        v = -1024.f;
+      const int np = npos[u];
+      bool hit = false;
+      if (np <= kStPos) {
+#pragma unroll
+        for (int q = 0; q < kStPos; ++q) hit |= q < np && posl[u][q] == ix;
+      } else {
+        hit = user_has(rowptr, col, sorted, n_sorted, users[b], (int32_t)(n_users + ix));
+      }
+      if (hit) v = -1024.f;
     }
   };
   // keep the best k of user slot `u` (one wave, lanes = entries)
@@ -393,35 +408,55 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
         acc = mfma32x2(a.w, bq.w, acc);
       }
     }
-    // candidates: acc[r] = score of item base + (r & 3) + 8 (r >> 2) + 4 h for user i
-    if (uok) {
+    // candidates: acc[r] = score of item base + (r & 3) + 8 (r >> 2) + 4 h
+    // for user i; the test against the user's k-th is conservative (a train
+    // positive would score -1024: the mask is applied when the buffer is
+    // compacted).  A user's buffer is compacted only when this tile's
+    // candidates would not fit (then they are tested again against the
+    // raised k-th): a full 64-entry buffer per compaction, not room kept for
+    // a whole tile — ~3x fewer compactions.  The buffers are the wave's own
+    // (its 32 users): wave-level LDS ordering, no workgroup barrier.
+    unsigned bits = 0u;
+    auto test_tile = [&]() {
+      bits = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t item = base + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (item >= it1) continue;
-        // (a train positive would score -1024: the test is conservative;
-        // the mask is applied when the buffer is compacted)
-        const float sc = acc[r];
-        if (!better(fmaxf(sc, -1024.f), (int)item, thr, thr_i)) continue;
+        const bool pass = uok && item < it1 &&
+                          better(fmaxf(acc[r], -1024.f), (int)item, thr, thr_i);
+        bits |= pass ? (1u << r) : 0u;
+      }
+    };
+    test_tile();
+    const int mine = __builtin_popcount(bits);
+    const int both = mine + __shfl_xor(mine, 32);  // the user's two lane halves
+    unsigned long long need = __ballot(h == 0 && cnt[ul] + both > kStCap);
+    if (need) {
+      while (need) {
+        const int j = __ffsll(need) - 1;
+        need &= need - 1;
+        const float2 th = compact(32 * w + j);
+        if (i == j) {
+          thr = th.x;
+          thr_i = __float_as_int(th.y);
+        }
+      }
+      wave_lds_sync();
+      test_tile();
+    }
+    if (bits != 0u) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (!((bits >> r) & 1u)) continue;
         const int slot = atomicAdd(&cnt[ul], 1);
-        cv[ul][slot] = sc;
-        ci[ul][slot] = (int)item;
+        cv[ul][slot] = acc[r];
+        ci[ul][slot] = (int)(base + (r & 3) + 8 * (r >> 2) + 4 * h);
       }
     }
-    __syncthreads();  // candidates of this tile in; sI[cur] reads done
-    // users whose buffer could overflow on the next tile (32 new at most)
-    unsigned long long need = __ballot(h == 0 && cnt[ul] > kStCap - kStTile);
-    while (need) {
-      const int j = __ffsll(need) - 1;
-      need &= need - 1;
-      const float2 th = compact(32 * w + j);
-      if (i == j) {
-        thr = th.x;
-        thr_i = __float_as_int(th.y);
-      }
-    }
+    wave_lds_sync();
+    if constexpr (UL) __syncthreads();  // the single buffer's reads done
     if (more) stage(UL ? 0 : cur ^ 1, rg);
-    __syncthreads();
+    __syncthreads();  // the next tile staged; (double buffer) this tile's reads done
     if constexpr (!UL) cur ^= 1;
   }
   // final: every user's best k of this chunk

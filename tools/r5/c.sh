@@ -1,0 +1,17 @@
+# Round 5 (c): streamed top-k, pipelined tile loop vs round 4 (A/B at C2),
+# then the evaluation tests on the product build.
+set -u
+export TMPDIR=/tmp
+E=gpurun_out/r5c
+mkdir -p $E
+for rep in 1 2; do
+  for L in tkold prod; do
+    if [ $L = prod ]; then unset MIREC_LIB; else export MIREC_LIB=var/libmirec_$L.so; fi
+    timeout -k 10 300 python -u tools/eval_bench.py --reps 10 --dense 0 --check64 $([ $rep = 1 ] && echo 1 || echo 0) >> $E/eval_ab.jsonl 2>> $E/eval_ab.log || { echo "eval_bench $L failed"; tail $E/eval_ab.log; exit 1; }
+  done
+done
+unset MIREC_LIB
+cat $E/eval_ab.jsonl
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 500 --timeout-method thread -k "evaluat or topk or recall" > $E/pytest_eval.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -12 $E/pytest_eval.log
+exit $rc
