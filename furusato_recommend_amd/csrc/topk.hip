@@ -273,8 +273,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   // D > 128: the users' rows live in LDS (their register image would take
   // D/2 VGPRs) and the B operand is read from there, four k-steps per
   // float4; the item tile is then single-buffered (LDS 132 KB: one
-  // workgroup per CU).  k-step s of lane half h covers dim 2 s + h (D <= 128)
-  // or dim h·D/2 + s (D > 128); A and B use the same map.
+  // workgroup per CU).  k-step s of lane half h covers dim h·D/2 + s; A and
+  // B use the same map.
   constexpr bool UL = D > 128;
   constexpr int NB = UL ? 1 : 2;
   constexpr int kSI = kStTile * LD;  // floats per buffer
@@ -294,11 +294,14 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   const bool uok = ub < n_eval;
   const int64_t it0 = (int64_t)blockIdx.y * chunk;
   const int64_t it1 = min(m_items, it0 + chunk);
-  // the user's embedding as the B operand: ue[s] = U[ub][2 s + h]
+  // the user's embedding as the B operand: ue[s] = U[ub][h D/2 + s]
   float ue[UL ? 1 : KS];
   if constexpr (!UL) {
 #pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) ue[s2] = uok ? U[ub * D + 2 * s2 + h] : 0.f;
+    for (int s4 = 0; s4 < KS / 4; ++s4) {
+      const float4 x = uok ? ld4(U + ub * D + h * KS + 4 * s4) : f4_zero();
+      ue[4 * s4] = x.x, ue[4 * s4 + 1] = x.y, ue[4 * s4 + 2] = x.z, ue[4 * s4 + 3] = x.w;
+    }
   } else {
     for (int e = t; e < kStUsers * D / 4; e += 128) {
       const int row = e / (D / 4), c4 = e % (D / 4);
@@ -393,9 +396,17 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     if constexpr (!UL) {
-      const float *arow = sI[cur] + i * LD + h;
+      // four k-steps per 16-byte LDS read (row stride D + 4: the 16 lanes of
+      // a read phase hit distinct 4-bank groups)
+      const float *arow = sI[cur] + i * LD + h * KS;
 #pragma unroll
-      for (int s2 = 0; s2 < KS; ++s2) acc = mfma32x2(arow[2 * s2], ue[s2], acc);
+      for (int s4 = 0; s4 < KS / 4; ++s4) {
+        const float4 a = ld4(arow + 4 * s4);
+        acc = mfma32x2(a.x, ue[4 * s4], acc);
+        acc = mfma32x2(a.y, ue[4 * s4 + 1], acc);
+        acc = mfma32x2(a.z, ue[4 * s4 + 2], acc);
+        acc = mfma32x2(a.w, ue[4 * s4 + 3], acc);
+      }
     } else {
       const float *arow = sI[cur] + i * LD + h * KS;
       const float *brow = sU + ul * LD + h * KS;
@@ -417,15 +428,22 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     // a whole tile — ~3x fewer compactions.  The buffers are the wave's own
     // (its 32 users): wave-level LDS ordering, no workgroup barrier.
     unsigned bits = 0u;
+    // 32-bit item ids (m_items < 2^31); the range test only on a ragged last
+    // tile (rows past the chunk were staged as zeros)
+    const int ib = (int)base + 4 * h;
+    const bool full = base + kStTile <= it1;
+    const int lim = (int)(it1 - base);
     auto test_tile = [&]() {
       bits = 0u;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int64_t item = base + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool pass = uok && item < it1 &&
-                          better(fmaxf(acc[r], -1024.f), (int)item, thr, thr_i);
+        const int off = (r & 3) + 8 * (r >> 2);
+        const float sc = fmaxf(acc[r], -1024.f);
+        const bool pass = (sc > thr || (sc == thr && ib + off < thr_i)) &&
+                          (full || off + 4 * h < lim);
         bits |= pass ? (1u << r) : 0u;
       }
+      if (!uok) bits = 0u;
     };
     test_tile();
     const int mine = __builtin_popcount(bits);
@@ -444,13 +462,19 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       wave_lds_sync();
       test_tile();
     }
-    if (bits != 0u) {
+    // insertion: every lane takes its lowest remaining candidate per round,
+    // so the wave runs max(candidates per lane) rounds (~1-3), not one per
+    // tile position some lane has
+    while (__ballot(bits != 0u)) {
+      if (bits != 0u) {
+        const int r = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        float sc = acc[0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (!((bits >> r) & 1u)) continue;
+        for (int q = 1; q < 16; ++q) sc = r == q ? acc[q] : sc;
         const int slot = atomicAdd(&cnt[ul], 1);
-        cv[ul][slot] = acc[r];
-        ci[ul][slot] = (int)(base + (r & 3) + 8 * (r >> 2) + 4 * h);
+        cv[ul][slot] = sc;
+        ci[ul][slot] = ib + (r & 3) + 8 * (r >> 2);
       }
     }
     wave_lds_sync();
