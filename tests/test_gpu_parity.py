@@ -473,6 +473,48 @@ def _nccl_world1():
                             world_size=1, device_id=torch.device("cuda:0"))
 
 
+def _pipelined_world1(backend):
+    """3 steps of DenseGradDataParallel(GraphSAGE, fetch, 3 micro-batches)
+    in a world of one process over ``backend``; the parameters after them."""
+    import socket
+
+    import torch.distributed as dist
+
+    from furusato_recommend_amd.dist import DenseGradDataParallel
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    kw = {"device_id": torch.device("cuda:0")} if backend == "nccl" else {}
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, **kw)
+    try:
+        m, ds = _union_model("sage")
+        dp = DenseGradDataParallel(m, table_exchange="fetch", microbatches=3)
+        assert dp.distributed and dp.world == 1
+        for i, n in enumerate((256, 100, 2)):
+            u, p, q = _union_batch(m, ds, "sage", i, 0, 1, n)
+            dp.step(u, p, q)
+        dp.gather_optimizer_state()
+        torch.cuda.synchronize()
+        return [x.detach().cpu().clone() for x in m.parameters()]
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipelined_exchange_rccl_world1_equals_gloo():
+    """The pipelined exchange's overlap machinery runs only under RCCL
+    (asynchronous all-to-all work handles, the route on a side stream that
+    waits for one micro-batch's export event, record_stream of the received
+    blocks, the main stream waiting for the side stream): at world size 1
+    through real RCCL it gives the gloo run's parameters bit for bit (the
+    same sums in the same order; gloo runs the transfers synchronously)."""
+    a = _pipelined_world1("nccl")
+    b = _pipelined_world1("gloo")
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
 def test_data_parallel_auto_calibration_rccl_world1(golden):
     """mode="auto" through real RCCL (world 1, calibration forced): both
     exchanges run — the sharded one with its row-block async all-gathers,
