@@ -326,8 +326,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       }
     }
   }
-  float thr = -INFINITY;  // the user's k-th best so far (after the last compaction)
-  int thr_i = INT_MAX;
+  float thr = -INFINITY;  // the user's k-th best score so far (after the last compaction)
   // item tile loader: 32 rows x D floats, float4 per thread (D % 4 == 0)
   constexpr int PER = (kStTile * D / 4 + 127) / 128;
   auto load = [&](int64_t base, float4 (&r)[PER]) {
@@ -377,10 +376,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       cv[u][lane] = v;
       ci[u][lane] = ix;
     }
-    const float kv = __shfl(v, k - 1);
-    const int ki = __shfl(ix, k - 1);
     if (lane == 0) cnt[u] = min(n, k);
-    return make_float2(kv, __int_as_float(n >= k ? ki : INT_MAX));
+    return __shfl(v, k - 1);  // (-inf while fewer than k)
   };
   float4 rg[PER];
   int cur = 0;
@@ -428,20 +425,25 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     // a whole tile — ~3x fewer compactions.  The buffers are the wave's own
     // (its 32 users): wave-level LDS ordering, no workgroup barrier.
     unsigned bits = 0u;
-    // 32-bit item ids (m_items < 2^31); the range test only on a ragged last
-    // tile (rows past the chunk were staged as zeros)
+    // 32-bit item ids (m_items < 2^31).  The test is `score >= k-th` (ties
+    // enter too; the compaction orders them exactly), and a masked train
+    // positive's -1024 is folded in per lane: any score passes once the k-th
+    // is <= -1024.  Bitwise, not short-circuit: no per-score exec-mask
+    // branches.  Rows past the chunk (staged as zeros) are cut only on a
+    // ragged last tile.
     const int ib = (int)base + 4 * h;
     const bool full = base + kStTile <= it1;
-    const int lim = (int)(it1 - base);
     auto test_tile = [&]() {
+      const unsigned low = thr <= -1024.f ? 0xFFFFu : 0u;
       bits = 0u;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int off = (r & 3) + 8 * (r >> 2);
-        const float sc = fmaxf(acc[r], -1024.f);
-        const bool pass = (sc > thr || (sc == thr && ib + off < thr_i)) &&
-                          (full || off + 4 * h < lim);
-        bits |= pass ? (1u << r) : 0u;
+      for (int r = 0; r < 16; ++r) bits |= (unsigned)(acc[r] >= thr) << r;
+      bits |= low;
+      if (!full) {
+        const int lim = (int)(it1 - base);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) + 4 * h >= lim) bits &= ~(1u << r);
       }
       if (!uok) bits = 0u;
     };
@@ -453,11 +455,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       while (need) {
         const int j = __ffsll(need) - 1;
         need &= need - 1;
-        const float2 th = compact(32 * w + j);
-        if (i == j) {
-          thr = th.x;
-          thr_i = __float_as_int(th.y);
-        }
+        const float th = compact(32 * w + j);
+        if (i == j) thr = th;
       }
       wave_lds_sync();
       test_tile();
