@@ -66,6 +66,23 @@ __device__ __forceinline__ float4 ld4(const float *p) {
 __device__ __forceinline__ void st4(float *p, float4 v) {
   *reinterpret_cast<float4 *>(p) = v;
 }
+// Row movers (gather / scatter / counted gather of [n, d] float rows): a
+// 256-thread block takes kRowRounds rounds of 256 >> lg rows, 1 << lg lanes
+// per row (lg = ceil log2 (d / 4); lanes past d / 4 idle), every thread
+// loading the ids of all its rows first, then all its rows — kRowRounds x 16
+// B in flight per lane instead of one dependent (id, row) pair — and no
+// 64-bit division in the index math.
+constexpr int kRowRounds = 4;
+inline int row_lg(int64_t d4) {
+  int lg = 0;
+  while ((int64_t(1) << lg) < d4) ++lg;
+  return lg;
+}
+inline int64_t row_blocks(int64_t n, int lg) {
+  const int64_t per = int64_t(256 >> lg) * kRowRounds;
+  return (n + per - 1) / per;
+}
+
 __device__ __forceinline__ float4 f4_shfl_xor(float4 v, int m) {
   return make_float4(__shfl_xor(v.x, m), __shfl_xor(v.y, m),
                      __shfl_xor(v.z, m), __shfl_xor(v.w, m));

@@ -307,32 +307,51 @@ __global__ __launch_bounds__(256) void sr_parts_kernel(const int32_t *__restrict
   }
 }
 
-// out[i, :] = src[rows[i], :] for i < *count (read on the device), float4
-// lanes, grid-stride over a grid sized for the capacity
+// out[i, :] = src[rows[i], :] for i < *count (read on the device); the
+// row-mover shape of common.h over a grid sized for the capacity
 __global__ __launch_bounds__(256) void gather_counted_kernel(const float4 *__restrict__ src,
                                                              const int32_t *__restrict__ rows,
                                                              const int32_t *__restrict__ count,
-                                                             int64_t d4,
+                                                             int32_t d4, int32_t lg,
                                                              float4 *__restrict__ out) {
-  const int64_t total = (int64_t)count[0] * d4;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
-       e += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t i = e / d4, c = e - i * d4;
-    out[e] = src[(int64_t)rows[i] * d4 + c];
-  }
+  const int64_t n = count[0];
+  const int per = 256 >> lg;
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r0 = (int64_t)blockIdx.x * per * kRowRounds + (threadIdx.x >> lg);
+  if (r0 >= n || c >= d4) return;
+  int32_t id[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k) id[k] = r0 + k * per < n ? rows[r0 + k * per] : -1;
+  float4 x[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    x[k] = id[k] >= 0 ? src[(int64_t)id[k] * d4 + c] : f4_zero();
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    if (r0 + k * per < n) out[(r0 + k * per) * d4 + c] = x[k];
 }
 
 // dst[ids[i], :] = src[i, :] (ids distinct, < 0 skipped): the install of
-// fetched rows into the local table; float4 lanes
+// fetched rows into the local table; the row-mover shape of common.h
 __global__ __launch_bounds__(256) void scatter_rows_kernel(const float4 *__restrict__ src,
                                                            const int32_t *__restrict__ ids,
-                                                           int64_t n, int64_t d4,
+                                                           int64_t n, int32_t d4, int32_t lg,
                                                            float4 *__restrict__ dst) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * d4) return;
-  const int64_t i = e / d4, c = e - i * d4;
-  const int64_t id = ids[i];
-  if (id >= 0) dst[id * d4 + c] = src[e];
+  const int per = 256 >> lg;
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r0 = (int64_t)blockIdx.x * per * kRowRounds + (threadIdx.x >> lg);
+  if (c >= d4) return;
+  int32_t id[kRowRounds];
+  float4 x[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k) {
+    const int64_t r = r0 + k * per;
+    id[k] = r < n ? ids[r] : -1;
+    x[k] = r < n ? src[r * d4 + c] : f4_zero();
+  }
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    if (id[k] >= 0) dst[(int64_t)id[k] * d4 + c] = x[k];
 }
 
 // ------------------------------------- the owner's ordered sum of row blocks
@@ -362,16 +381,28 @@ __global__ __launch_bounds__(256) void os_mark_kernel(OsBlocks b, int64_t lo, in
   if (r >= 0 && r < n_own) pos[q * n_own + r] = (int32_t)i;
 }
 
+// (1 << lg lanes per own row as the row movers; the blocks four at a time:
+// their positions, then their rows in flight together, then the adds in
+// block order)
 __global__ __launch_bounds__(256) void os_sum_kernel(OsBlocks b, const int32_t *__restrict__ pos,
-                                                     int64_t n_own, int64_t d4, int accumulate,
-                                                     float4 *__restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n_own * d4) return;
-  const int64_t r = t / d4, c = t - r * d4;
+                                                     int64_t n_own, int32_t d4, int32_t lg,
+                                                     int accumulate, float4 *__restrict__ out) {
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r = (int64_t)blockIdx.x * (256 >> lg) + (threadIdx.x >> lg);
+  if (r >= n_own || c >= d4) return;
+  const int64_t t = r * d4 + c;
   float4 acc = accumulate ? out[t] : f4_zero();
-  for (int q = 0; q < b.n; ++q) {
-    const int32_t i = pos[q * n_own + r];
-    if (i >= 0) acc = f4_add(acc, b.rows[q][(int64_t)i * d4 + c]);
+  for (int q0 = 0; q0 < b.n; q0 += 4) {
+    int32_t i[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) i[u] = q0 + u < b.n ? pos[(q0 + u) * n_own + r] : -1;
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = i[u] >= 0 ? b.rows[q0 + u][(int64_t)i[u] * d4 + c] : f4_zero();
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i[u] >= 0) acc = f4_add(acc, x[u]);
   }
   out[t] = acc;
 }
@@ -469,10 +500,10 @@ extern "C" int mirec_gather_rows_counted(const float *src, const int32_t *rows,
   MIREC_CHECK_ARG(((uintptr_t)src & 15u) == 0 && ((uintptr_t)out & 15u) == 0);
   if (capacity == 0) return MIREC_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t d4 = dim / 4;
-  const int64_t blocks = std::min<int64_t>((capacity * d4 + 255) / 256, 8192);
-  hipLaunchKernelGGL(gather_counted_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     reinterpret_cast<const float4 *>(src), rows, count, d4,
+  const int lg = row_lg(dim / 4);
+  MIREC_CHECK_ARG(lg <= 8);
+  hipLaunchKernelGGL(gather_counted_kernel, dim3((unsigned)row_blocks(capacity, lg)), dim3(256), 0,
+                     st, reinterpret_cast<const float4 *>(src), rows, count, dim / 4, lg,
                      reinterpret_cast<float4 *>(out));
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
@@ -554,10 +585,11 @@ extern "C" int mirec_scatter_rows(const float *src, const int32_t *ids, int64_t 
   if (n == 0) return MIREC_OK;
   MIREC_CHECK_ARG(src && ids && dst);
   MIREC_CHECK_ARG(((uintptr_t)src & 15u) == 0 && ((uintptr_t)dst & 15u) == 0);
-  const int64_t d4 = dim / 4;
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)((n * d4 + 255) / 256)), dim3(256), 0,
+  const int lg = row_lg(dim / 4);
+  MIREC_CHECK_ARG(lg <= 8);
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3((unsigned)row_blocks(n, lg)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4 *>(src),
-                     ids, n, d4, reinterpret_cast<float4 *>(dst));
+                     ids, n, dim / 4, lg, reinterpret_cast<float4 *>(dst));
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -603,8 +635,11 @@ extern "C" int mirec_owner_sum(const mirec_row_block_t *blocks, int32_t n_blocks
                          st, b, lo, n_own, pos);
       MIREC_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(os_sum_kernel, dim3((unsigned)((n_own * d4 + 255) / 256)), dim3(256), 0,
-                       st, b, pos, n_own, d4, q0 > 0 ? 1 : 0, reinterpret_cast<float4 *>(out));
+    const int lg = row_lg(d4);
+    MIREC_CHECK_ARG(lg <= 8);
+    hipLaunchKernelGGL(os_sum_kernel, dim3((unsigned)((n_own + (256 >> lg) - 1) / (256 >> lg))),
+                       dim3(256), 0, st, b, pos, n_own, (int32_t)d4, lg, q0 > 0 ? 1 : 0,
+                       reinterpret_cast<float4 *>(out));
     MIREC_LAUNCH_CHECK();
   }
   return MIREC_OK;

@@ -122,15 +122,26 @@ __global__ __launch_bounds__(256) void sample_fanout_norep_reg_kernel(
     if (c < k) out[c] = sel[c];
 }
 
-__global__ __launch_bounds__(256) void gather_rows_kernel(const float *__restrict__ table,
+// out[r, :] = table[ids[r], :] (zeros for an id < 0); the row-mover shape
+// of common.h
+__global__ __launch_bounds__(256) void gather_rows_kernel(const float4 *__restrict__ table,
                                                           const int32_t *__restrict__ ids, int64_t n,
-                                                          int32_t d4, float *__restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n * d4) return;
-  const int64_t r = i / d4;
-  const int64_t c = i - r * d4;
-  const int32_t id = ids[r];
-  st4(out + 4 * i, id >= 0 ? ld4(table + ((int64_t)id * d4 + c) * 4) : f4_zero());
+                                                          int32_t d4, int32_t lg,
+                                                          float4 *__restrict__ out) {
+  const int per = 256 >> lg;
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r0 = (int64_t)blockIdx.x * per * kRowRounds + (threadIdx.x >> lg);
+  const bool col = c < d4;
+  int32_t id[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k) id[k] = r0 + k * per < n ? ids[r0 + k * per] : -1;
+  float4 x[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    x[k] = (col && id[k] >= 0) ? table[(int64_t)id[k] * d4 + c] : f4_zero();
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    if (col && r0 + k * per < n) out[(r0 + k * per) * d4 + c] = x[k];
 }
 
 __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const float *__restrict__ grad,
@@ -479,9 +490,12 @@ extern "C" int mirec_gather_rows(const float *table, const int32_t *ids, int64_t
   using namespace mirec;
   MIREC_CHECK_ARG(table && ids && out && n >= 0 && dim > 0 && dim % 4 == 0);
   if (n == 0) return MIREC_OK;
-  const int64_t tot = n * (dim / 4);
-  hipLaunchKernelGGL(gather_rows_kernel, dim3((tot + 255) / 256), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), table, ids, n, dim / 4, out);
+  MIREC_CHECK_ARG(((uintptr_t)table & 15u) == 0 && ((uintptr_t)out & 15u) == 0);
+  const int lg = row_lg(dim / 4);
+  MIREC_CHECK_ARG(lg <= 8);
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)row_blocks(n, lg)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), reinterpret_cast<const float4 *>(table),
+                     ids, n, dim / 4, lg, reinterpret_cast<float4 *>(out));
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

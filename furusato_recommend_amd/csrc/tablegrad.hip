@@ -58,6 +58,21 @@ struct GroupArgs {
   int32_t n_groups;
 };
 
+// Where the summed rows go.  Dense (slot == nullptr): acc[r] and stamp[r] =
+// gen for row r.  Compact (slot != nullptr, mirec_table_grad_sorted_rows):
+// the row of the run whose head is sorted entry h goes to vals[slot[h]] and
+// its id to rows[slot[h]], slot = the exclusive prefix count of run heads —
+// the touched rows ascending, packed, with no dense array and no export
+// gather behind them.
+struct TgOut {
+  float *acc;
+  int32_t *stamp;
+  int32_t gen;
+  const int32_t *slot;
+  float *vals;
+  int32_t *rows;
+};
+
 // Group of a global entry / target index (unrolled selects: the argument
 // struct is never indexed dynamically, which would spill it to scratch).
 __device__ __forceinline__ int group_of(const int64_t (&off)[kMaxGroups + 1], int n_groups,
@@ -139,6 +154,17 @@ __device__ __forceinline__ void tg_decode(const GroupArgs &ga, int2 pl, int32_t 
   hm = pick(ga.key, g) + (uint64_t)((int64_t)e * (d / 4));
 }
 
+// A float4 through a pointer rebuilt from integers (e.g. broadcast by a lane
+// shuffle): named as global memory, so it compiles to global_load_dwordx4.
+// (A generic pointer makes it flat_load, which also counts on LGKM_CNT: every
+// later `s_waitcnt lgkmcnt(0)` of a shuffle then waits for the row too,
+// serialising the gathers.)
+__device__ __forceinline__ float4 ldg4(const float *p) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f v = *(const __attribute__((address_space(1))) v4f *)p;
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Lane base + u's x for every lane of a group of LPR lanes (u uniform, a
 // constant after unrolling): __shfl (ds_bpermute).  (v_readlane for 32 /
 // 64-lane groups measured slower at C3: 208 readlanes whose SGPR results
@@ -162,7 +188,7 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
   for (int u = 0; u < kCh; ++u) {
     const uint64_t a = (uint64_t)(uint32_t)grp_bcast<LPR>((int)am_lo, base, u) |
                        ((uint64_t)(uint32_t)grp_bcast<LPR>((int)am_hi, base, u) << 32);
-    x[u] = (act && u >= lo && u < hi) ? ld4(reinterpret_cast<const float *>(a) + col) : f4_zero();
+    x[u] = (act && u >= lo && u < hi) ? ldg4(reinterpret_cast<const float *>(a) + col) : f4_zero();
   }
 #pragma unroll
   for (int u = 0; u < kCh; ++u) {
@@ -196,12 +222,13 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int
 // The loads a chunk starts from: the keys before and around it, its
 // entries' keys and indices and those of the window after it.
 struct TgRaw {
-  int32_t kprev, kpp, km, kx;
+  int32_t kprev, kpp, km, kx, sl;
   int2 pm, px;
 };
 
 __device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
-                                            const int2 *__restrict__ plan, int64_t n,
+                                            const int2 *__restrict__ plan,
+                                            const int32_t *__restrict__ slot, int64_t n,
                                             int64_t chunk, int sub, TgRaw &r) {
   const int64_t beg = chunk * kCh;
   const int64_t end = beg + kCh < n ? beg + kCh : n;
@@ -216,14 +243,14 @@ __device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
   // the entries' plans load beside their keys (not behind them)
   r.pm = in_chunk ? plan[pe] : make_int2(0, 0);
   r.px = in_win ? plan[px] : make_int2(0, 0);
+  r.sl = (slot != nullptr && in_chunk) ? slot[pe] : 0;  // compact output: the entries' slots
 }
 
 // One chunk of pass 1 from its loaded keys / indices (see below).
 template <int LPR>
 __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t d, int32_t n_rows,
-                                         float *__restrict__ acc_out,
-                                         int32_t *__restrict__ stamp, int32_t gen,
-                                         float *__restrict__ part, int64_t chunk, int sub,
+                                         const TgOut &o, float *__restrict__ part,
+                                         int64_t chunk, int sub,
                                          int base, const TgRaw &r) {
   const int64_t beg = chunk * kCh;
   const int64_t end = beg + kCh < n ? beg + kCh : n;
@@ -280,8 +307,14 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
       const bool cont_next = pos == end && cont_out && !out_short;
       float *dst;
       if (!cont_prev && !cont_next) {
-        dst = acc_out + (int64_t)cur * d;
-        if (sub == 0 && c0 == 0) stamp[cur] = gen;
+        if (o.slot != nullptr) {  // a final row starts at its run's head: seg_beg
+          const int q = __shfl(r.sl, base + (int)(seg_beg - beg));
+          dst = o.vals + (int64_t)q * d;
+          if (sub == 0 && c0 == 0) o.rows[q] = cur;
+        } else {
+          dst = o.acc + (int64_t)cur * d;
+          if (sub == 0 && c0 == 0) o.stamp[cur] = o.gen;
+        }
       } else {
         dst = part + (2 * chunk + (cont_prev ? 0 : 1)) * (int64_t)d;
       }
@@ -319,9 +352,7 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
 template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
                                                      const int2 *__restrict__ plan, int64_t n,
-                                                     int32_t d, int32_t n_rows,
-                                                     float *__restrict__ acc_out,
-                                                     int32_t *__restrict__ stamp, int32_t gen,
+                                                     int32_t d, int32_t n_rows, TgOut o,
                                                      float *__restrict__ part) {
   static_assert(LPR >= kCh, "chunk layout: one entry per lane");
   const int lane = threadIdx.x & 63;
@@ -331,8 +362,8 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   const int64_t n_chunks = (n + kCh - 1) / kCh;
   if (group >= n_chunks) return;  // the whole group leaves together
   TgRaw r;
-  tg_load_raw(keys, plan, n, group, sub, r);
-  tg_chunk<LPR>(ga, n, d, n_rows, acc_out, stamp, gen, part, group, sub, base, r);
+  tg_load_raw(keys, plan, o.slot, n, group, sub, r);
+  tg_chunk<LPR>(ga, n, d, n_rows, o, part, group, sub, base, r);
 }
 
 // Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
@@ -386,9 +417,7 @@ template <int LPR>
 __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict__ keys, int64_t n,
                                                        int32_t d, int32_t n_rows,
                                                        const float *__restrict__ part,
-                                                       const float *__restrict__ bsum,
-                                                       float *__restrict__ acc_out,
-                                                       int32_t *__restrict__ stamp, int32_t gen) {
+                                                       const float *__restrict__ bsum, TgOut o) {
   const int lane = threadIdx.x & 63;
   const int sub = lane & (LPR - 1);
   const int base = lane - sub;
@@ -410,6 +439,14 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
   if (((__ballot(differs) >> base) & ((1ull << kCh) - 1ull)) != 0 || xend < end + kCh) return;
   const unsigned long long gmask = low_bits<LPR>() << base;
   const unsigned long long low = low_bits<LPR>();
+  // compact output: the run's head — its first entry in this chunk — and slot
+  int q = 0;
+  if (o.slot != nullptr) {
+    const bool hd = sub < kCh && keys[beg + sub] == klast;
+    const int h = (int)__builtin_ctzll((__ballot(hd) >> base) & ((1ull << kCh) - 1ull));
+    q = o.slot[beg + h];
+  }
+  float *dst = o.slot != nullptr ? o.vals + (int64_t)q * d : o.acc + (int64_t)klast * d;
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
@@ -469,9 +506,51 @@ __global__ __launch_bounds__(256) void tg_fixup_kernel(const int32_t *__restrict
       if (nfull < lim) break;
       cc += lim;
     }
-    if (act) st4(acc_out + (int64_t)klast * d + col, sum);
+    if (act) st4(dst + col, sum);
   }
-  if (sub == 0) stamp[klast] = gen;
+  if (sub == 0) {
+    if (o.slot != nullptr) o.rows[q] = klast;
+    else o.stamp[klast] = o.gen;
+  }
+}
+
+// Compact output: slot = exclusive prefix count of the run heads (sorted
+// entry i heads a run when its id is valid and differs from entry i - 1's).
+struct TgHeadFlag {
+  const int32_t *keys;
+  int32_t n_rows;
+  __host__ __device__ int operator()(int i) const {
+    return (keys[i] < n_rows && (i == 0 || keys[i] != keys[i - 1])) ? 1 : 0;
+  }
+};
+
+__device__ __forceinline__ int64_t tg_lower_bound(const int32_t *__restrict__ a, int64_t n,
+                                                  int64_t x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// counts[0] = the rows written, counts[1 + p] = those in owner block p (rows
+// [p N/P, (p + 1) N/P), the last block to N), from the packed ascending ids.
+__global__ __launch_bounds__(256) void tg_rows_count_kernel(const int32_t *__restrict__ keys,
+                                                            const int32_t *__restrict__ slot,
+                                                            int64_t n, int32_t n_rows,
+                                                            int32_t parts,
+                                                            const int32_t *__restrict__ rows,
+                                                            int32_t *__restrict__ counts) {
+  const TgHeadFlag f{keys, n_rows};
+  const int64_t tot = n > 0 ? (int64_t)slot[n - 1] + f((int)(n - 1)) : 0;
+  if (threadIdx.x == 0) counts[0] = (int32_t)tot;
+  const int64_t per = n_rows / parts;
+  for (int p = threadIdx.x; p < parts; p += blockDim.x) {
+    const int64_t lo = p * per, hi = p == parts - 1 ? n_rows : (p + 1) * per;
+    counts[1 + p] = (int32_t)(tg_lower_bound(rows, tot, hi) - tg_lower_bound(rows, tot, lo));
+  }
 }
 
 // ------------------------------------------------------------ consumers
@@ -629,7 +708,8 @@ static int lanes_per_row(int32_t d) {
 
 struct TgLayout {
   int64_t n_ent, n_tgt, n_chunks;
-  size_t keys_in, keys_out, vals_in, vals_out, wt, plan, part, bsum, sort, sort_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, wt, plan, part, bsum, slot, scan, scan_bytes, sort,
+      sort_bytes, total;
   int end_bit;
 };
 
@@ -658,7 +738,15 @@ static int tg_layout(const mirec_row_grad_group_t *groups, int32_t n_groups, int
   L->plan = L->wt + up(sizeof(float) * std::max<int64_t>(n_tgt, 1));
   L->part = L->plan + 2 * seg;
   L->bsum = L->part + up(sizeof(float) * 2 * std::max<int64_t>(L->n_chunks, 1) * dim);
-  L->sort = L->bsum + up(sizeof(float) * std::max<int64_t>(L->n_chunks / kBlockChunks, 1) * dim);
+  L->slot = L->bsum + up(sizeof(float) * std::max<int64_t>(L->n_chunks / kBlockChunks, 1) * dim);
+  L->scan = L->slot + seg;
+  size_t sb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(
+      nullptr, sb, hipcub::TransformInputIterator<int, TgHeadFlag, hipcub::CountingInputIterator<int>>(
+                       hipcub::CountingInputIterator<int>(0), TgHeadFlag{nullptr, 0}),
+      (int32_t *)nullptr, (int)std::max<int64_t>(n_ent, 1), (hipStream_t) nullptr);
+  L->scan_bytes = sb;
+  L->sort = L->scan + up(sb);
   int bits = 1;
   while (bits < 31 && ((int64_t)1 << bits) <= n_rows) ++bits;
   L->end_bit = bits;
@@ -761,15 +849,19 @@ extern "C" int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int
   return MIREC_OK;
 }
 
-extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
-                                       int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
-                                       int32_t gen, void *workspace, size_t workspace_bytes,
-                                       mirec_stream_t stream) {
+// The sorted accumulate into `o` (dense or compact; compact: also the
+// counts [1 + parts]).
+static int tg_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups, int32_t n_rows,
+                     int32_t dim, TgOut o, int32_t parts, int32_t *counts, void *workspace,
+                     size_t workspace_bytes, mirec_stream_t stream) {
   TgLayout L;
   const int rc = tg_layout(groups, n_groups, n_rows, dim, &L);
   if (rc != MIREC_OK) return rc;
-  MIREC_CHECK_ARG(acc && stamp);
-  if (L.n_ent == 0) return MIREC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (L.n_ent == 0) {
+    if (counts != nullptr) MIREC_HIP(hipMemsetAsync(counts, 0, 4 * (size_t)(1 + parts), st));
+    return MIREC_OK;
+  }
   MIREC_CHECK_ARG(workspace);
   if (workspace_bytes < L.total) return MIREC_ERR_WORKSPACE;
   GroupArgs ga = {};
@@ -803,7 +895,6 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   int2 *plan = reinterpret_cast<int2 *>(ws + L.plan);
   float *part = reinterpret_cast<float *>(ws + L.part);
   float *bsum = reinterpret_cast<float *>(ws + L.bsum);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int64_t nprep = std::max(L.n_ent, L.n_tgt);
   hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
                      L.n_ent, L.n_tgt, n_rows, keys_in, vals_in, wt);
@@ -814,6 +905,16 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   hipLaunchKernelGGL(tg_plan_kernel, dim3((unsigned)((L.n_ent + 255) / 256)), dim3(256), 0, st,
                      ga, vals_out, wt, L.n_ent, plan);
   MIREC_LAUNCH_CHECK();
+  int32_t *slot = reinterpret_cast<int32_t *>(ws + L.slot);
+  if (o.vals != nullptr) {  // compact: the run heads' slots
+    size_t sb = L.scan_bytes;
+    MIREC_HIP(hipcub::DeviceScan::ExclusiveSum(
+        ws + L.scan, sb,
+        hipcub::TransformInputIterator<int, TgHeadFlag, hipcub::CountingInputIterator<int>>(
+            hipcub::CountingInputIterator<int>(0), TgHeadFlag{keys_out, n_rows}),
+        slot, (int)L.n_ent, st));
+    o.slot = slot;
+  }
   const int lpr = lanes_per_row(dim);
   const int64_t threads = L.n_chunks * lpr;
   const int64_t n_blocks = L.n_chunks / kBlockChunks;
@@ -821,7 +922,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
     hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga,        \
-                       keys_out, plan, L.n_ent, dim, n_rows, acc, stamp, gen, part);          \
+                       keys_out, plan, L.n_ent, dim, n_rows, o, part);                        \
     MIREC_LAUNCH_CHECK();                                                                    \
     if (n_blocks > 0) {                                                                      \
       hipLaunchKernelGGL(tg_block_kernel<LP>, dim3((unsigned)((n_blocks * LP + 255) / 256)),  \
@@ -829,7 +930,7 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
       MIREC_LAUNCH_CHECK();                                                                  \
     }                                                                                        \
     hipLaunchKernelGGL(tg_fixup_kernel<LP>, grid, dim3(256), 0, st, keys_out, L.n_ent, dim,   \
-                       n_rows, part, bsum, acc, stamp, gen);                                 \
+                       n_rows, part, bsum, o);                                               \
     MIREC_LAUNCH_CHECK();                                                                    \
     break;
   switch (lpr) {  // lpr >= kCh (lanes_per_row)
@@ -841,7 +942,32 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
       return MIREC_ERR_ARG;
   }
 #undef MIREC_TG_LAUNCH
+  if (o.slot != nullptr) {
+    hipLaunchKernelGGL(tg_rows_count_kernel, dim3(1), dim3(256), 0, st, keys_out, slot, L.n_ent,
+                       n_rows, parts, o.rows, counts);
+    MIREC_LAUNCH_CHECK();
+  }
   return MIREC_OK;
+}
+
+extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                                       int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
+                                       int32_t gen, void *workspace, size_t workspace_bytes,
+                                       mirec_stream_t stream) {
+  MIREC_CHECK_ARG(acc && stamp);
+  return tg_sorted(groups, n_groups, n_rows, dim, TgOut{acc, stamp, gen, nullptr, nullptr, nullptr},
+                   1, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mirec_table_grad_sorted_rows(const mirec_row_grad_group_t *groups,
+                                            int32_t n_groups, int32_t n_rows, int32_t dim,
+                                            int32_t parts, int32_t *rows, float *vals,
+                                            int32_t *counts, void *workspace,
+                                            size_t workspace_bytes, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(rows && vals && counts && parts >= 1 && parts <= n_rows &&
+                  (uintptr_t)vals % 16 == 0);
+  return tg_sorted(groups, n_groups, n_rows, dim, TgOut{nullptr, nullptr, 0, nullptr, vals, rows},
+                   parts, counts, workspace, workspace_bytes, stream);
 }
 
 static int32_t pow2_shift(int32_t d4) {

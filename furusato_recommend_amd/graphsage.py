@@ -84,6 +84,13 @@ class TableGrad:
         self.atomic = False
         self._ws = None
         self.entries = 0  # row contributions of the last accumulate
+        # packed export (the pipelined data-parallel exchange): with rows_parts
+        # = P the accumulate writes S packed — (rows ascending, vals, counts
+        # [1 + P] per owner block), mirec_table_grad_sorted_rows — into
+        # ``export`` instead of acc / stamp (nothing stamped: a dense consumer
+        # sees S = 0, never stale rows)
+        self.rows_parts = None
+        self.export = None
 
     def accumulate(self, groups):
         """groups: [(ids int32, grad_out [n_t, d], k, mean, dropout p, seed)]."""
@@ -112,6 +119,20 @@ class TableGrad:
         if self._ws is None or self._ws.numel() < nb.value:
             self._ws = torch.empty(nb.value, dtype=torch.uint8, device=self.acc.device)
         self._next_gen()
+        if self.rows_parts:
+            dev = self.acc.device
+            cap = max(min(self.n_rows, self.entries), 1)
+            rows = torch.empty(cap, dtype=torch.int32, device=dev)
+            vals = torch.empty(cap, self.dim, device=dev)
+            counts = torch.empty(1 + int(self.rows_parts), dtype=torch.int32, device=dev)
+            check(lib.mirec_table_grad_sorted_rows(arr, n, self.n_rows, self.dim,
+                                                   int(self.rows_parts), rows.data_ptr(),
+                                                   vals.data_ptr(), counts.data_ptr(),
+                                                   self._ws.data_ptr(), self._ws.numel(),
+                                                   _lib.stream_handle()), "table_grad_sorted_rows")
+            self.export = (rows, vals, counts)
+            self.pending = True
+            return
         check(lib.mirec_table_grad_sorted(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
                                           self.stamp.data_ptr(), self.gen, self._ws.data_ptr(),
                                           self._ws.numel(), _lib.stream_handle()),
@@ -129,6 +150,7 @@ class TableGrad:
         """A backward with no row gradient: S = 0 (a fresh generation)."""
         self._next_gen()
         self.entries = 0
+        self.export = None
         self.pending = True
 
     def materialize(self, table: torch.Tensor) -> torch.Tensor:
@@ -434,6 +456,27 @@ class SampleTree:
         return t
 
 
+class _ChunkTrees:
+    """The C micro-batch trees of a step as a sequence whose tree k is
+    sampled when first accessed (trees before it first)."""
+
+    def __init__(self, sample, C: int):
+        self._sample = sample
+        self._trees = [None] * C
+
+    def __len__(self):
+        return len(self._trees)
+
+    def __getitem__(self, k: int):
+        for j in range(k + 1):
+            if self._trees[j] is None:
+                self._trees[j] = self._sample(j)
+        return self._trees[k]
+
+    def __iter__(self):
+        return (self[k] for k in range(len(self)))
+
+
 class GraphSAGE(nn.Module):
     def __init__(self, config: dict, dataset):
         super().__init__()
@@ -674,8 +717,8 @@ class GraphSAGE(nn.Module):
         runs between sampling and the forward (DenseGradDataParallel's row
         fetch).  ``chunks`` = C > 1 (with ``chunk_hook``, the pipelined fetch
         exchange): the batch as C micro-batches of its triples, one tree each
-        (``chunk_seeds``), all sampled first (``tree_hook`` gets the list),
-        then per micro-batch ``chunk_hook(k, "pre")``, forward, loss
+        (``chunk_seeds``; ``tree_hook`` gets them as a sequence whose tree k
+        is sampled when the hook first reaches it), then per micro-batch ``chunk_hook(k, "pre")``, forward, loss
         weighted so the micro-batches' gradients sum to the batch's
         (``_stage_chunks``), backward, ``chunk_hook(k, "post")`` — the hook exports each
         micro-batch's table-gradient rows before the next overwrites them."""
@@ -745,11 +788,16 @@ class GraphSAGE(nn.Module):
             raise ValueError("empty batch")
         C = min(int(C), B)
         bnd = self.chunk_bounds(B, C)
-        trees = []
-        for k in range(C):
+
+        def sample(k):
             a, b = bnd[k], bnd[k + 1]
-            trees.append(self.sample_tree(self._seed_nodes(users[a:b], pos[a:b], neg[a:b]),
-                                          self.chunk_seed(seed, k)))
+            return self.sample_tree(self._seed_nodes(users[a:b], pos[a:b], neg[a:b]),
+                                    self.chunk_seed(seed, k))
+        # sampled on first access, in order: the hook acts on tree k (issues
+        # its row fetch) before tree k + 1 is sampled, so the fetch overlaps
+        # the later trees' sampling and planning (each tree has its own seed:
+        # the same trees as sampling them all first)
+        trees = _ChunkTrees(sample, C)
         if tree_hook is not None:
             tree_hook(trees)
         one = self.__dict__.get("_loss_seed")

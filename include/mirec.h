@@ -598,6 +598,20 @@ int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_grou
                             int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
                             void *workspace, size_t workspace_bytes, mirec_stream_t stream);
 
+/* The same S packed (the data-parallel exchanges' export): rows[j] = the
+ * j-th touched row id ascending and vals[j] its row of S, j < counts[0];
+ * counts[1 + p] = the touched rows in owner block p (rows [p N/P, (p + 1)
+ * N/P), the last block to N = n_rows, P = parts) — all on the device, no
+ * host sync.  The same sums bit for bit as mirec_table_grad_sorted; acc /
+ * stamp are not touched.  rows / vals hold at least min(entries, n_rows)
+ * rows; the workspace is mirec_table_grad_workspace's.  Replaces the
+ * stamped-row scan + gather of the dense form for a routed step
+ * (reference: the gradient all-reduce of ddp_sage.py:800-806). */
+int mirec_table_grad_sorted_rows(const mirec_row_grad_group_t *groups, int32_t n_groups,
+                                 int32_t n_rows, int32_t dim, int32_t parts, int32_t *rows,
+                                 float *vals, int32_t *counts, void *workspace,
+                                 size_t workspace_bytes, mirec_stream_t stream);
+
 /* The same S in the atomic form, for plain groups only (k = 1, mean = 0,
  * dropout_p = 0): touched rows stamped and zeroed, then every gradient row
  * added with float atomics — two launches, no workspace; the summation

@@ -3322,6 +3322,15 @@ def test_table_grad_runs_of_every_length_and_alignment(d):
     # per row (a lost or doubled contribution is an O(1) error on its row)
     err = (got - ref).abs().max(1).values / ref.abs().max(1).values.clamp(min=1e-30)
     assert float(err[touched].max()) < 1e-3
+    # the packed form (mirec_table_grad_sorted_rows) over the same runs
+    from furusato_recommend_amd.dist import export_stamped
+    tg.rows_parts = 4
+    tg.accumulate(groups)
+    rows, vals, counts, _ = export_stamped(tg, 4)
+    ref_rows = torch.nonzero(st == 1).view(-1).int()
+    assert int(counts[0]) == ref_rows.numel() and int(counts[1:].sum()) == ref_rows.numel()
+    assert torch.equal(rows[:ref_rows.numel()], ref_rows)
+    assert torch.equal(vals[:ref_rows.numel()], a1[ref_rows.long()])
 
 
 @pytest.mark.parametrize("d", [16, 128, 256])
@@ -3351,6 +3360,40 @@ def test_table_grad_sorted_matches_fp64_and_repeats(d, hub):
     if hub:
         assert float((got[torch.nonzero(touched).squeeze(1) == 7] - ref[7]).abs().max()) \
             < 1e-5 * float(ref[7].abs().max())
+
+
+@pytest.mark.parametrize("d", [16, 128, 256])
+@pytest.mark.parametrize("hub", [0, 200_000])
+@pytest.mark.parametrize("parts", [1, 3, 8])
+def test_table_grad_packed_rows_equal_dense_form(d, hub, parts):
+    """mirec_table_grad_sorted_rows (the pipelined exchange's export): the
+    touched rows ascending with their rows of S bitwise equal to the dense
+    form's acc rows, counts[0] = the touched rows and counts[1 + p] = those
+    of owner block p (ragged last block), acc / stamp untouched; also
+    through runs of every length and a hub (chunk partials, fixup)."""
+    from furusato_recommend_amd.dist import export_stamped
+    from furusato_recommend_amd.graphsage import TableGrad
+    n_rows = 5000
+    groups = _tg_groups(n_rows, d, seed=d + hub + 1, hub_count=hub)
+    tg = TableGrad(n_rows, 2000, d, "cuda")
+    tg.accumulate(groups)
+    rows_ref = torch.nonzero(tg.stamp == tg.gen).view(-1).int()
+    vals_ref = tg.acc[rows_ref.long()].clone()
+    acc0, st0 = tg.acc.clone(), tg.stamp.clone()
+    tg.rows_parts = parts
+    tg.accumulate(groups)
+    assert torch.equal(tg.acc, acc0) and torch.equal(tg.stamp, st0)
+    rows, vals, counts, _ = export_stamped(tg, parts)
+    assert tg.export is None
+    n = int(counts[0])
+    assert n == rows_ref.numel()
+    assert torch.equal(rows[:n], rows_ref)
+    assert torch.equal(vals[:n], vals_ref)
+    per = n_rows // parts
+    lo = torch.arange(parts, device="cuda") * per
+    hi = torch.cat([lo[1:], torch.tensor([n_rows], device="cuda")])
+    ref_counts = ((rows_ref[None, :] >= lo[:, None]) & (rows_ref[None, :] < hi[:, None])).sum(1)
+    assert torch.equal(counts[1:].long(), ref_counts)
 
 
 def test_fused_table_adam_equals_dense_adam():
@@ -3680,7 +3723,8 @@ def test_distinct_rows_matches_unique(n_rows, n, lo, hi):
 
 @pytest.mark.parametrize("n_own,n_blocks,per,d", [(137_500, 16, 60_000, 128), (5000, 70, 300, 8),
                                                   (1, 3, 1, 4), (4096, 0, 0, 16),
-                                                  (10_000, 5, 0, 8)])
+                                                  (10_000, 5, 0, 8), (3001, 6, 2000, 12),
+                                                  (500, 5, 400, 520)])
 def test_owner_sum_equals_index_add_sequence(n_own, n_blocks, per, d):
     """owner_sum (mirec_owner_sum: position maps + one ordered pass per 64
     blocks) == the index_add_ launches it replaces, bitwise: blocks of
@@ -3702,7 +3746,8 @@ def test_owner_sum_equals_index_add_sequence(n_own, n_blocks, per, d):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("n_rows,n,d", [(1_100_000, 300_000, 128), (4097, 4097, 8), (10, 0, 4)])
+@pytest.mark.parametrize("n_rows,n,d", [(1_100_000, 300_000, 128), (4097, 4097, 8), (10, 0, 4),
+                                        (3000, 1001, 12), (100, 37, 520)])
 def test_scatter_rows_equals_index_copy(n_rows, n, d):
     from furusato_recommend_amd.dist import scatter_rows
     g = torch.Generator(device="cuda").manual_seed(n_rows + n + d)
@@ -3712,6 +3757,32 @@ def test_scatter_rows_equals_index_copy(n_rows, n, d):
     ref = dst.clone().index_copy_(0, ids.long(), src)
     scatter_rows(dst, ids, src)
     assert torch.equal(dst, ref)
+
+
+@pytest.mark.parametrize("n_rows,n,d", [(1_100_000, 300_000, 128), (5000, 4097, 12), (300, 7, 4),
+                                        (1000, 513, 256), (64, 33, 520), (10, 0, 8)])
+def test_row_movers_equal_indexing(n_rows, n, d):
+    """The row movers (common.h shape: 1 << lg lanes per row, lanes past
+    d / 4 idle, four rows per lane): mirec_gather_rows == table[ids] with
+    zero rows for ids < 0, and mirec_gather_rows_counted == src[rows[:count]]
+    with the rows past the device-side count untouched — ragged last block,
+    d / 4 not a power of two (3, 130), d / 4 = 64, an empty list."""
+    from furusato_recommend_amd._lib import check, lib
+    from furusato_recommend_amd.dist import gather_rows
+    g = torch.Generator(device="cuda").manual_seed(n_rows + n + d)
+    table = torch.randn(n_rows, d, device="cuda", generator=g)
+    ids = torch.randint(-1, n_rows, (n,), device="cuda", generator=g, dtype=torch.int32)
+    ref = table[ids.clamp(min=0).long()] * (ids >= 0).float()[:, None]
+    assert torch.equal(gather_rows(table, ids), ref)
+    rows = torch.randint(0, n_rows, (n,), device="cuda", generator=g, dtype=torch.int32)
+    cnt = torch.tensor([n // 2 + (n & 1)], dtype=torch.int32, device="cuda")
+    out = torch.full((n, d), 7.0, device="cuda")
+    check(lib.mirec_gather_rows_counted(table.data_ptr(), rows.data_ptr(), cnt.data_ptr(), n, d,
+                                        out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+          "gather_rows_counted")
+    k = int(cnt)
+    assert torch.equal(out[:k], table[rows[:k].long()])
+    assert bool((out[k:] == 7.0).all())
 
 
 @pytest.mark.parametrize("n_rows,n", [(1_100_000, 880_000), (4097, 10_000), (1, 5), (70_001, 0)])

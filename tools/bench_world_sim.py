@@ -303,19 +303,27 @@ def sage_pipelined(args, m, W, C, base, rates):
             m._tg.pending = False
         m.stageOne(u, p, n, grad_hook=capture, loss_scale=1.0 / W)
     route_other = sum(o[0].numel() for o in others) * row_b
+    # the other ranks' rows as they arrive: one receive buffer (concatenated
+    # once here, not inside the timed step)
+    others_block = (torch.cat([o[0] for o in others]), torch.cat([o[1] for o in others]),
+                    [o[0].numel() for o in others])
     rec = {}
 
     def tree_hook(trees):
         if "norms" in rec:  # as dist._plan_fetch: the last update's slice norms
             m._norm_cache = (rec.pop("norms"), m._norm_token())
-        have = torch.zeros(N, dtype=torch.bool, device=dev)
-        rec["need"], rec["fetch_rows"] = [], []
+        have = rec.setdefault("have", torch.empty(N, dtype=torch.uint8, device=dev))
+        have.zero_()  # (as dist._plan_fetch: a kept map)
+        rec["need"], rec["fetch_rows"], rec["plan_ev"] = [], [], []
         for tree in trees:
             need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own, have=have)
             # the owners' gather of the requested rows (rank 0 serves a share of
             # the same size) and the install after the transfer
             rec["need"].append((need.long(), gather_rows(m._table.data, need)))
             rec["fetch_rows"].append(need.numel())
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            rec["plan_ev"].append(e)  # micro-batch 0's fetch leaves at the first
         rec["ev"] = []
 
     def chunk_hook(k, phase):
@@ -353,8 +361,7 @@ def sage_pipelined(args, m, W, C, base, rates):
         blocks = []
         for rows, vals in rec.pop("own"):
             blocks.append((rows, vals, [rows.numel()]))
-        blocks.append((torch.cat([o[0] for o in others]), torch.cat([o[1] for o in others]),
-                       [o[0].numel() for o in others]))
+        blocks.append(others_block)
         rec["norms"] = torch.empty(2, device=dev)
         dp._owner_adam(blocks, rec.pop("coef"), norms=rec["norms"])
         small = [q.grad for q in m.parameters() if q.grad is not None]
@@ -370,14 +377,17 @@ def sage_pipelined(args, m, W, C, base, rates):
     def step():
         u, p, n = m.sample(B, seed=7, offset=step_no[0] * B, shard=0, n_shards=W)
         step_no[0] += 1
+        m._tg.rows_parts = W  # as dist._pipelined_step: S packed per owner
         m.stageOne(u, p, n, grad_hook=grad_hook, loss_scale=1.0 / W, tree_hook=tree_hook,
                    chunks=C, chunk_hook=chunk_hook)
+        m._tg.rows_parts = None
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     chunk_ms = [0.0] * C
     fetch_rows = [0] * C
+    plan_rest_ms = 0.0  # planning of micro-batches 1.. (device), after micro-batch 0's fetch left
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -385,6 +395,8 @@ def sage_pipelined(args, m, W, C, base, rates):
         for k in range(C):
             chunk_ms[k] += rec["ev"][k][0].elapsed_time(rec["ev"][k][1]) / args.steps
             fetch_rows[k] += rec["fetch_rows"][k] / args.steps
+        pe = rec["plan_ev"]
+        plan_rest_ms += pe[0].elapsed_time(pe[-1]) / args.steps
     ms = (time.perf_counter() - t0) / args.steps * 1e3
     small_b = sum(q.numel() for q in m.parameters() if q is not m._table) * 4
     fetch_b = [f * row_b for f in fetch_rows]
@@ -393,7 +405,10 @@ def sage_pipelined(args, m, W, C, base, rates):
     proj = {}
     for r in rates:
         rate = r * 1e6  # bytes per ms
-        exposed = fetch_b[0] / rate + route_b / rate + 2 * (W - 1) * small_b / W / rate
+        # micro-batch 0's rows (own communicator, dist._plan_fetch) travel
+        # while the later micro-batches' read sets are planned
+        exposed = max(0.0, fetch_b[0] / rate - plan_rest_ms) + route_b / rate + \
+            2 * (W - 1) * small_b / W / rate
         for k in range(C):
             hidden = ((fetch_b[k + 1] if k + 1 < C else 0.0) + (route_b if k > 0 else 0.0)) / rate
             exposed += max(0.0, hidden - chunk_ms[k])
@@ -403,11 +418,13 @@ def sage_pipelined(args, m, W, C, base, rates):
                       "microbatches": C, "pipelined": True,
                       "ms_per_step_rank_compute": round(ms, 4),
                       "chunk_compute_ms": [round(x, 4) for x in chunk_ms],
+                      "plan_after_first_fetch_ms": round(plan_rest_ms, 4),
                       "fetched_rows_per_chunk": [int(x) for x in fetch_rows],
                       "routed_rows_from_others": int(route_other // row_b),
                       "recv_bytes_per_rank": int(recv),
-                      "projection": "compute (measured, no transfers) + the first "
-                                    "micro-batch's rows + the last's routed rows + the "
+                      "projection": "compute (measured, no transfers) + what of the first "
+                                    "micro-batch's rows exceeds the later micro-batches' "
+                                    "planning + the last's routed rows + the "
                                     "small bucket + whatever of micro-batch k+1's rows and "
                                     "k-1's routed rows exceeds micro-batch k's compute",
                       "projected": proj}), flush=True)
