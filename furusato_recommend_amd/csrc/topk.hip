@@ -160,7 +160,11 @@ __global__ __launch_bounds__(64) void topk_masked_kernel(
 // mirec_topk_masked's lane lists).  Order: score descending, ties to the
 // lower item id — deterministic, independent of insertion order.
 constexpr int kStUsers = 64;  // users per workgroup (2 waves of 32)
-constexpr int kStCap = 64;    // candidate slots per user
+// candidate slots per user: k + 32 at least (after a compaction the k best
+// stay and a tile brings up to 32 more); 52 for k <= 20 fits four
+// workgroups per CU at D <= 64 (39.9 KB of LDS), 64 otherwise (three)
+constexpr int kStCapSmall = 52, kStCapLarge = 64, kStCapSmallK = 20;
+constexpr int kStMaxChunk = 65536;  // items per chunk: slot ids are 16-bit offsets
 constexpr int kStTile = 32;   // items per MFMA tile
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -261,7 +265,7 @@ __device__ __forceinline__ void wave_sort_desc(float &v, int &ix) {
 // vs 5.69 ms per 10 K users: its bf16 planes take 62.7 KB of LDS per
 // workgroup, two per CU instead of three)
 
-template <int D>
+template <int D, int CAP>
 __global__ __launch_bounds__(128) void score_topk_kernel(
     const float *__restrict__ U, int64_t n_eval, const float *__restrict__ I, int64_t m_items,
     const int32_t *__restrict__ users, const int64_t *__restrict__ rowptr,
@@ -280,8 +284,8 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   constexpr int kSI = kStTile * LD;  // floats per buffer
   __shared__ __attribute__((aligned(16))) float sI[NB][kSI];
   __shared__ __attribute__((aligned(16))) float sU[UL ? kStUsers * LD : 4];
-  __shared__ float cv[kStUsers][kStCap];
-  __shared__ int ci[kStUsers][kStCap];
+  __shared__ float cv[kStUsers][CAP];
+  __shared__ uint16_t ci[kStUsers][CAP];  // item - it0 (chunk <= kStMaxChunk items)
   __shared__ int cnt[kStUsers];
   // per user its train positives inside the chunk (kStPos at most; npos >
   // kStPos = overflow: the global binary search)
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   auto entry = [&](int u, float &v, int &ix) {
     const int n = cnt[u];
     v = lane < n ? cv[u][lane] : -INFINITY;
-    ix = lane < n ? ci[u][lane] : INT_MAX;
+    ix = lane < n ? (int)it0 + ci[u][lane] : INT_MAX;
     const int64_t b = (int64_t)blockIdx.x * kStUsers + u;
     if (lane < n && rowptr != nullptr && users != nullptr && b < n_eval && v != -1024.f) {
       const int np = npos[u];
@@ -374,7 +378,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     wave_sort_desc(v, ix);
     if (lane < k) {
       cv[u][lane] = v;
-      ci[u][lane] = ix;
+      ci[u][lane] = (uint16_t)(ix - (int)it0);
     }
     if (lane == 0) cnt[u] = min(n, k);
     return __shfl(v, k - 1);  // (-inf while fewer than k)
@@ -450,7 +454,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     test_tile();
     const int mine = __builtin_popcount(bits);
     const int both = mine + __shfl_xor(mine, 32);  // the user's two lane halves
-    unsigned long long need = __ballot(h == 0 && cnt[ul] + both > kStCap);
+    unsigned long long need = __ballot(h == 0 && cnt[ul] + both > CAP);
     if (need) {
       while (need) {
         const int j = __ffsll(need) - 1;
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
         for (int q = 1; q < 16; ++q) sc = r == q ? acc[q] : sc;
         const int slot = atomicAdd(&cnt[ul], 1);
         cv[ul][slot] = sc;
-        ci[ul][slot] = ib + (r & 3) + 8 * (r >> 2);
+        ci[ul][slot] = (uint16_t)(ib - (int)it0 + (r & 3) + 8 * (r >> 2));
       }
     }
     wave_lds_sync();
@@ -566,10 +570,12 @@ __global__ __launch_bounds__(64) void topk_merge_kernel(const float *__restrict_
   }
 }
 
-// Workgroups of score_topk_kernel<D> resident on the chip at once (CUs x
-// the occupancy its LDS / registers allow: 3 per CU at D <= 64, 2 at 128, 1
-// at 256), from the runtime, once per D.
-static int64_t st_slots(int D);
+// Workgroups of score_topk_kernel<D, CAP> resident on the chip at once (CUs
+// x the occupancy its LDS / registers allow: 4 / 3 per CU at D <= 64 with
+// the small / large buffers, 2 at 128, 1 at 256), from the runtime, once per
+// instantiation.
+static int64_t st_slots(int D, int k);
+static int st_cap(int k) { return k <= kStCapSmallK ? kStCapSmall : kStCapLarge; }
 
 // Items per stage-1 workgroup.  The grid is (user groups) x (item chunks) and
 // every workgroup of a chunk takes the same time, so the launch lasts
@@ -579,13 +585,16 @@ static int64_t st_slots(int D);
 // chunks on a tie (less stage-2 merging).  (C2, 10 K users x 100 K items at
 // D = 64: 157 user groups, 768 slots -> 9 chunks in 2 full rounds instead of
 // the 7 = 1.43 rounds of a fixed >= 1024-workgroup rule.)
-static void st_chunks(int64_t n_eval, int64_t m_items, int D, int64_t *chunk, int64_t *n_chunks) {
+static void st_chunks(int64_t n_eval, int64_t m_items, int D, int k, int64_t *chunk,
+                      int64_t *n_chunks) {
   const int64_t ut = (n_eval + kStUsers - 1) / kStUsers;
-  const int64_t slots = std::max<int64_t>(1, st_slots(D));
+  const int64_t slots = std::max<int64_t>(1, st_slots(D, k));
   const int64_t tiles_all = (m_items + kStTile - 1) / kStTile;
   const int64_t max_n = std::max<int64_t>(1, tiles_all / 32);
-  int64_t best_n = 1, best_cost = -1;
-  for (int64_t n = 1; n <= std::min<int64_t>(max_n, 256); ++n) {
+  // at most kStMaxChunk items per chunk (16-bit candidate ids)
+  const int64_t min_n = (tiles_all + kStMaxChunk / kStTile - 1) / (kStMaxChunk / kStTile);
+  int64_t best_n = min_n, best_cost = -1;
+  for (int64_t n = min_n; n <= std::max<int64_t>(min_n, std::min<int64_t>(max_n, 256)); ++n) {
     const int64_t tiles = (tiles_all + n - 1) / n;
     const int64_t rounds = (ut * n + slots - 1) / slots;
     const int64_t cost = rounds * (tiles + 24);
@@ -599,14 +608,14 @@ static void st_chunks(int64_t n_eval, int64_t m_items, int D, int64_t *chunk, in
   *n_chunks = (m_items + c - 1) / c;
 }
 
-template <int D>
+template <int D, int CAP>
 static int64_t st_slots_of() {
   static int64_t slots = -1;
   if (slots < 0) {
     int dev = 0, cus = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_topk_kernel<D>, 128, 0) !=
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, score_topk_kernel<D, CAP>, 128, 0) !=
             hipSuccess)
       return 1024;  // no device answer: the old fixed target
     slots = (int64_t)cus * std::max(per, 1);
@@ -614,14 +623,19 @@ static int64_t st_slots_of() {
   return slots;
 }
 
-static int64_t st_slots(int D) {
+template <int CAP>
+static int64_t st_slots_cap(int D) {
   switch (D) {
-    case 16: return st_slots_of<16>();
-    case 32: return st_slots_of<32>();
-    case 64: return st_slots_of<64>();
-    case 128: return st_slots_of<128>();
-    default: return st_slots_of<256>();
+    case 16: return st_slots_of<16, CAP>();
+    case 32: return st_slots_of<32, CAP>();
+    case 64: return st_slots_of<64, CAP>();
+    case 128: return st_slots_of<128, CAP>();
+    default: return st_slots_of<256, CAP>();
   }
+}
+
+static int64_t st_slots(int D, int k) {
+  return st_cap(k) == kStCapSmall ? st_slots_cap<kStCapSmall>(D) : st_slots_cap<kStCapLarge>(D);
 }
 
 }  // namespace mirec
@@ -653,7 +667,7 @@ extern "C" int64_t mirec_score_topk_workspace(int64_t n_eval, int64_t m_items, i
   int64_t most = 1;
   for (int D : {16, 32, 64, 128, 256}) {
     int64_t chunk, n_chunks;
-    st_chunks(std::max<int64_t>(n_eval, 1), m_items, D, &chunk, &n_chunks);
+    st_chunks(std::max<int64_t>(n_eval, 1), m_items, D, k, &chunk, &n_chunks);
     most = std::max(most, n_chunks);
   }
   return n_eval * most * k * (int64_t)(sizeof(float) + sizeof(int32_t));
@@ -675,7 +689,7 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
   const int64_t need = mirec_score_topk_workspace(n_eval, m_items, k);
   if ((int64_t)workspace_bytes < need) return MIREC_ERR_WORKSPACE;
   int64_t chunk, n_chunks;
-  st_chunks(n_eval, m_items, dim, &chunk, &n_chunks);
+  st_chunks(n_eval, m_items, dim, k, &chunk, &n_chunks);
   float *pv = static_cast<float *>(workspace);
   int32_t *pi = reinterpret_cast<int32_t *>(pv + n_eval * n_chunks * k);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -684,11 +698,13 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
   const int32_t *so = csr ? csr->col_sorted : nullptr;
   const int64_t ns = csr ? csr->n_sorted : 0;
   const dim3 grid((unsigned)((n_eval + kStUsers - 1) / kStUsers), (unsigned)n_chunks);
-#define MIREC_ST_CASE(DD)                                                                    \
-  case DD:                                                                                   \
-    hipLaunchKernelGGL(score_topk_kernel<DD>, grid, dim3(128), 0, st, user_emb, n_eval,      \
-                       item_emb, m_items, users, rp, cl, so, ns, n_users, (int)k, chunk, pv, \
-                       pi);                                                                  \
+#define MIREC_ST_LAUNCH(DD, CC)                                                              \
+  hipLaunchKernelGGL((score_topk_kernel<DD, CC>), grid, dim3(128), 0, st, user_emb, n_eval,  \
+                     item_emb, m_items, users, rp, cl, so, ns, n_users, (int)k, chunk, pv, pi)
+#define MIREC_ST_CASE(DD)                                  \
+  case DD:                                                 \
+    if (st_cap(k) == kStCapSmall) MIREC_ST_LAUNCH(DD, kStCapSmall); \
+    else MIREC_ST_LAUNCH(DD, kStCapLarge);                 \
     break;
   switch (dim) {
     MIREC_ST_CASE(16)
@@ -698,6 +714,7 @@ extern "C" int mirec_score_topk(const float *user_emb, int64_t n_eval, const flo
     MIREC_ST_CASE(256)
   }
 #undef MIREC_ST_CASE
+#undef MIREC_ST_LAUNCH
   MIREC_LAUNCH_CHECK();
   hipLaunchKernelGGL((topk_merge_kernel<64>), dim3((unsigned)n_eval), dim3(64), 0, st, pv, pi,
                      n_eval, n_chunks * k, (int)k, topk_idx, topk_val);

@@ -693,10 +693,15 @@ def test_topk_masked_matches_torch():
     ds = SyntheticBipartite(3000, 1500, 40_000, seed=5, test_frac=0)
     g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
     users = torch.arange(0, 3000, 7, device="cuda")
-    rating = torch.randn(len(users), ds.m_items, device="cuda")
+    # seeded (an unseeded draw once held an exact tie in a top-64, which
+    # torch.topk may order either way)
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    rating = torch.randn(len(users), ds.m_items, device="cuda", generator=gen)
     ref = rating.clone()
     for r, u in enumerate(users.tolist()):
         ref[r, torch.from_numpy(ds.allPos[u]).cuda()] = -(1 << 10)
+    top = torch.topk(ref, k=65).values
+    assert bool((top[:, 1:] != top[:, :-1]).all())  # no ties: the order is unique
     for k in (1, 20, 50, 64):
         rv, ri = torch.topk(ref, k=k)
         val, idx = topk_masked(rating.clone(), users, g, k)
