@@ -22,10 +22,17 @@
 #   c5         LightGCN-3 d=256 10 M x 1 M / 200 M on one GPU   -> bench_c5.log
 #   pmc_tg     FETCH / WRITE of the C3 table-gradient sum vs its algorithmic
 #              bytes (tools/tg_sum_bytes.py)                     -> pmc_tg_sum.json
-#   world_c3   the C3 world simulation (W = 1, 2, 8; 1 / 2 / 4 micro-batches)
+#   world_c3   the C3 world simulation (W = 1 over 30 steps, W = 8 with 2 / 3
+#              micro-batches and the plain fetch exchange)
+#   trace_c3   device timeline of one simulated pipelined C3 step (W = 8, C = 2):
+#              rocprofv3 --kernel-trace + tools/trace_step.py  -> trace_c3_step.txt
 #   world_c2   rank 0's C2 step at W = 1..8 (sparse / sharded)
 #   eval       streamed evaluation at C2 with the float64 near-tie check
+#   eval_d256  the streamed evaluation at d = 256 (2 M x 1 M, the D > 128 path)
 #   attn       attention kernels at the C4 length mix
+#   attn_pmc   SQ counters of the packed attention backward (two passes)
+#   topk_pmc   SQ counters of the streamed top-k at C2 (two passes)
+#   tg         the C3 table-gradient accumulate alone (tools/tg_bench.py)
 #   gemm       the GEMM shapes of C3 / C4 and 4096^3
 set -u
 export TMPDIR=/tmp
@@ -93,17 +100,42 @@ for leg in $LEGS; do
       python tools/tg_sum_bytes.py --counts $E/tg_counts.json --fetch $E/tgf --write $E/tgw --out $E/pmc_tg_sum.json
       find $E/tgf $E/tgw -name "*kernel_trace.csv" -delete ;;
     world_c3)
-      timeout -k 10 900 python -u tools/bench_world_sim.py --model sage --worlds 1,2,8 --exchanges fetch --microbatches 1,2,4 --steps 10 > $E/world_sim_c3.jsonl 2> $E/world_sim_c3.log || { echo "world sim rc=$?"; tail $E/world_sim_c3.log; exit 1; }
+      timeout -k 10 900 python -u tools/bench_world_sim.py --model sage --worlds 1,8 --exchanges fetch --microbatches 2,3 --steps 30 > $E/world_sim_c3.jsonl 2> $E/world_sim_c3.log || { echo "world sim rc=$?"; tail $E/world_sim_c3.log; exit 1; }
       lines $E/world_sim_c3.jsonl 300 ;;
+    trace_c3)
+      run 300 $E/trace_c3.log rocprofv3 --kernel-trace --output-format csv -d $E/trc3 -o run -- python3 tools/bench_world_sim.py --model sage --worlds 8 --exchanges fetch --microbatches 2 --steps 3 --warmup 2
+      f=$(find $E/trc3 -name '*kernel_trace.csv' | head -1)
+      # the pipelined run's steps come first (7 + 5 bpr_sample markers); step 11 is its last
+      python3 tools/trace_step.py "$f" --nth 11 --width 90 > $E/trace_c3_step.txt
+      rm -rf $E/trc3
+      tail -1 $E/trace_c3_step.txt ;;
     world_c2)
       timeout -k 10 900 python -u tools/bench_world_sim.py --modes sparse,sharded > $E/world_sim_c2.jsonl 2> $E/world_sim_c2.log || { echo "world sim rc=$?"; tail $E/world_sim_c2.log; exit 1; }
       lines $E/world_sim_c2.jsonl 300 ;;
     eval)
       run 600 $E/eval_c2.log python -u tools/eval_bench.py --reps 10
       lines $E/eval_c2.log 300 ;;
+    eval_d256)
+      run 600 $E/eval_d256.log python -u tools/eval_bench.py --users 2000000 --items 1000000 --edges 40000000 --dim 256 --batch 2000 --reps 3 --dense 0
+      lines $E/eval_d256.log 300 ;;
     attn)
       run 400 $E/attn.log python -u tools/attn_bench.py --mixes c4 --batches 2048
       lines $E/attn.log 300 ;;
+    attn_pmc|topk_pmc)
+      if [ $leg = attn_pmc ]; then K=attn_bwd_packed; CMD="python3 tools/attn_bench.py --mixes c4 --batches 2048 --reps 3"
+      else K=score_topk; CMD="python3 tools/eval_bench.py --reps 2 --dense 0 --check64 0"; fi
+      P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
+      P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
+      n=0
+      for P in "$P1" "$P2"; do
+        n=$((n + 1))
+        timeout -s KILL 120 rocprofv3 --pmc $P --kernel-include-regex $K --output-format csv -d $E/${leg}$n -o run -- $CMD > $E/${leg}$n.log 2>&1 || { echo "$leg pass $n rc=$?"; tail -5 $E/${leg}$n.log; exit 1; }
+        cp $(find $E/${leg}$n -name '*counter_collection.csv' | head -1) $E/${leg}$n.csv
+        rm -rf $E/${leg}$n
+      done ;;
+    tg)
+      run 200 $E/tg.json python tools/tg_bench.py --reps 50
+      cat $E/tg.json ;;
     gemm)
       run 400 $E/gemm.log python -u tools/gemm_bench.py
       lines $E/gemm.log 300 ;;
