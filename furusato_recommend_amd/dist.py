@@ -608,7 +608,8 @@ class DenseGradDataParallel:
     BUCKET_MIN = 1 << 20  # elements: gradients this large are reduced in place
 
     def __init__(self, model, group=None, shard_optimizer: bool | None = None,
-                 table_exchange: str | None = None, microbatches: int | None = None):
+                 table_exchange: str | None = None, microbatches: int | None = None,
+                 fetch_group=None):
         self.model = model
         # fetch exchange: the step as this many micro-batches whose row
         # fetches and routed gradient rows overlap the other micro-batches'
@@ -657,12 +658,16 @@ class DenseGradDataParallel:
         # fetch exchange: the row fetches on a communicator of their own, so
         # micro-batch 0's rows travel while the later micro-batches' id
         # exchanges (on `group`) run — one communicator would queue them
-        # behind the fetch (created on every rank of `group`, collectively)
-        self._fetch_group = None
+        # behind the fetch.  With the default group it is created here
+        # (collectively: every rank constructs this object); with a caller's
+        # subgroup the caller passes ``fetch_group`` (a second group over the
+        # same ranks — dist.new_group must run on every process), else the
+        # fetches share ``group`` (same results, no overlap).
+        self._fetch_group = fetch_group
         self._have = None  # pipelined fetch: rows fetched for an earlier micro-batch
-        if self.distributed and self.world > 1 and table_exchange == "fetch":
-            ranks = None if group is None else dist.get_process_group_ranks(group)
-            self._fetch_group = dist.new_group(ranks=ranks)
+        if (fetch_group is None and group is None and self.distributed and self.world > 1
+                and table_exchange == "fetch"):
+            self._fetch_group = dist.new_group()
         if self.world > 1:
             for p in model.parameters():
                 dist.broadcast(p.data, src=0, group=group)

@@ -10,7 +10,7 @@
 # profiles/ keeps come from these directories (profiles/README.md).
 #
 #   tests      the whole GPU suite in one process               -> pytest.log
-#   mark=EXPR  the GPU tests selected by -k EXPR, verbose        -> pytest_k.log
+#   mark=EXPR  the GPU tests selected by -k EXPR ('+' for spaces: mark=a+or+b), verbose -> pytest_k.log
 #   smoke      __graft_entry__.smoke()                           -> smoke.log
 #   c2         the headline bench line (bench.py defaults: roofline, CPU
 #              baseline, oracle parity leg, Recall@20)           -> bench_c2.log
@@ -61,7 +61,7 @@ for leg in $LEGS; do
       run 1100 $E/pytest.log python -u -m pytest tests -m gpu -q -rf --timeout 500 --timeout-method thread
       tail -3 $E/pytest.log ;;
     mark=*)
-      run 900 $E/pytest_k.log python -u -m pytest tests -m gpu -x -v -s --timeout 500 --timeout-method thread -k "${leg#mark=}"
+      run 900 $E/pytest_k.log python -u -m pytest tests -m gpu -x -v -s --timeout 500 --timeout-method thread -k "$(echo "${leg#mark=}" | tr '+' ' ')"
       tail -5 $E/pytest_k.log ;;
     smoke)
       run 300 $E/smoke.log python -c "import __graft_entry__ as g; g.smoke()"
