@@ -739,6 +739,34 @@ def test_score_topk_streaming_matches_exact_topk(d):
             assert np.array_equal(val[r], ref[r, order].astype(np.float32)), (k, r)
 
 
+@pytest.mark.parametrize("d", [16, 64])
+def test_score_topk_streaming_exact_past_65536_items(d):
+    """mirec_score_topk past 65 536 items (several chunks of <= 65 536: the
+    candidates' 16-bit ids, both slot counts) == the exact masked top-k
+    (integer embeddings: exact scores, many ties, train positives at -1024)
+    for k = 1, 20, 32, with a ragged item count."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.evaluate import score_topk
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(1500, 70_003, 120_000, seed=9, test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    gen = torch.Generator().manual_seed(d + 1)
+    users = torch.arange(5, 1500, 13)
+    U = torch.randint(-2, 3, (len(users), d), generator=gen).float()
+    I = torch.randint(-2, 3, (ds.m_items, d), generator=gen).float()
+    ref = (U.double() @ I.double().t()).numpy()
+    for r, u in enumerate(users.tolist()):
+        ref[r, ds.allPos[u]] = -1024.0
+    items = np.arange(ds.m_items)
+    for k in (1, 20, 32):
+        val, idx = score_topk(U.cuda(), I.cuda(), users.cuda(), g, k)
+        val, idx = val.cpu().numpy(), idx.cpu().numpy()
+        for r in range(len(users)):
+            order = np.lexsort((items, -ref[r]))[:k]
+            assert np.array_equal(idx[r], order), (k, r)
+            assert np.array_equal(val[r], ref[r, order].astype(np.float32)), (k, r)
+
+
 def test_evaluate_matches_oracle():
     """Recall/Precision/NDCG/HR@{10,20} of evaluate() == the oracle's
     restatement of Trainer.test on the same propagated embeddings."""
