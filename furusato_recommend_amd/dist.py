@@ -462,7 +462,7 @@ def export_stamped(tg, parts: int, ws: torch.Tensor | None = None):
     it is: no scan, no gather."""
     from . import _lib
     from ._lib import check, lib
-    if tg.export is not None:
+    if getattr(tg, "export", None) is not None:
         rows, vals, counts = tg.export
         tg.export = None
         if counts.numel() != 1 + parts:
