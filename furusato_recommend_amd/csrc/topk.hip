@@ -286,7 +286,6 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   __shared__ __attribute__((aligned(16))) float sU[UL ? kStUsers * LD : 4];
   __shared__ float cv[kStUsers][CAP];
   __shared__ uint16_t ci[kStUsers][CAP];  // item - it0 (chunk <= kStMaxChunk items)
-  __shared__ int cnt[kStUsers];
   // per user its train positives inside the chunk (kStPos at most; npos >
   // kStPos = overflow: the global binary search)
   __shared__ int posl[kStUsers][kStPos];
@@ -313,7 +312,6 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       st4(sU + row * LD + 4 * c4, b < n_eval ? ld4(U + b * D + 4 * c4) : f4_zero());
     }
   }
-  if (t < kStUsers) cnt[t] = 0;
   if (t < kStUsers) npos[t] = 0;
   __syncthreads();
   if (rowptr != nullptr && users != nullptr) {
@@ -352,8 +350,11 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
   // user slot u's buffer entry of this lane, with the train-positive mask
   // applied now (entries go in with their raw scores; one parallel round of
   // membership tests per compaction instead of one per insertion)
-  auto entry = [&](int u, float &v, int &ix) {
-    const int n = cnt[u];
+  // cn = the entries in user i's buffer, kept in a register of both its
+  // lanes (only they insert for it; a compaction run by the whole wave hands
+  // the count back to them): no LDS counter, no atomics
+  int cn = 0;
+  auto entry = [&](int u, int n, float &v, int &ix) {
     v = lane < n ? cv[u][lane] : -INFINITY;
     ix = lane < n ? (int)it0 + ci[u][lane] : INT_MAX;
     const int64_t b = (int64_t)blockIdx.x * kStUsers + u;
@@ -370,17 +371,15 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     }
   };
   // keep the best k of user slot `u` (one wave, lanes = entries)
-  auto compact = [&](int u) {
-    const int n = cnt[u];
+  auto compact = [&](int u, int n) {
     float v;
     int ix;
-    entry(u, v, ix);
+    entry(u, n, v, ix);
     wave_sort_desc(v, ix);
     if (lane < k) {
       cv[u][lane] = v;
       ci[u][lane] = (uint16_t)(ix - (int)it0);
     }
-    if (lane == 0) cnt[u] = min(n, k);
     return __shfl(v, k - 1);  // (-inf while fewer than k)
   };
   float4 rg[PER];
@@ -454,13 +453,17 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     test_tile();
     const int mine = __builtin_popcount(bits);
     const int both = mine + __shfl_xor(mine, 32);  // the user's two lane halves
-    unsigned long long need = __ballot(h == 0 && cnt[ul] + both > CAP);
+    unsigned long long need = __ballot(h == 0 && cn + both > CAP);
     if (need) {
       while (need) {
         const int j = __ffsll(need) - 1;
         need &= need - 1;
-        const float th = compact(32 * w + j);
-        if (i == j) thr = th;
+        const int nj = __shfl(cn, j);
+        const float th = compact(32 * w + j, nj);
+        if (i == j) {
+          thr = th;
+          cn = min(nj, k);
+        }
       }
       wave_lds_sync();
       test_tile();
@@ -468,17 +471,22 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     // insertion: every lane takes its lowest remaining candidate per round,
     // so the wave runs max(candidates per lane) rounds (~1-3), not one per
     // tile position some lane has
+    // (the user's two lanes take slots cn and cn + 1 in a round where both
+    // insert: lane half 1 after half 0)
     while (__ballot(bits != 0u)) {
-      if (bits != 0u) {
+      const int take = bits != 0u ? 1 : 0;
+      const int other = __shfl_xor(take, 32);
+      if (take) {
         const int r = __builtin_ctz(bits);
         bits &= bits - 1u;
         float sc = acc[0];
 #pragma unroll
         for (int q = 1; q < 16; ++q) sc = r == q ? acc[q] : sc;
-        const int slot = atomicAdd(&cnt[ul], 1);
+        const int slot = cn + (h ? other : 0);
         cv[ul][slot] = sc;
         ci[ul][slot] = (uint16_t)(ib - (int)it0 + (r & 3) + 8 * (r >> 2));
       }
+      cn += take + other;
     }
     wave_lds_sync();
     if constexpr (UL) __syncthreads();  // the single buffer's reads done
@@ -494,7 +502,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     if (b >= n_eval) break;
     float v;
     int ix;
-    entry(u, v, ix);
+    entry(u, __shfl(cn, j), v, ix);
     wave_sort_desc(v, ix);
     if (lane < k) {
       part_val[(b * n_chunks + blockIdx.y) * k + lane] = v;
