@@ -380,7 +380,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
       cv[u][lane] = v;
       ci[u][lane] = (uint16_t)(ix - (int)it0);
     }
-    return __shfl(v, k - 1);  // (-inf while fewer than k)
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k - 1));  // (-inf while fewer than k)
   };
   float4 rg[PER];
   int cur = 0;
@@ -452,13 +452,13 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     };
     test_tile();
     const int mine = __builtin_popcount(bits);
-    const int both = mine + __shfl_xor(mine, 32);  // the user's two lane halves
+    const int both = mine + lane_xor(mine, 32);  // the user's two lane halves (permlane32)
     unsigned long long need = __ballot(h == 0 && cn + both > CAP);
     if (need) {
       while (need) {
         const int j = __ffsll(need) - 1;
         need &= need - 1;
-        const int nj = __shfl(cn, j);
+        const int nj = __builtin_amdgcn_readlane(cn, j);  // (j uniform)
         const float th = compact(32 * w + j, nj);
         if (i == j) {
           thr = th;
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     // insert: lane half 1 after half 0)
     while (__ballot(bits != 0u)) {
       const int take = bits != 0u ? 1 : 0;
-      const int other = __shfl_xor(take, 32);
+      const int other = lane_xor(take, 32);
       if (take) {
         const int r = __builtin_ctz(bits);
         bits &= bits - 1u;
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(128) void score_topk_kernel(
     if (b >= n_eval) break;
     float v;
     int ix;
-    entry(u, __shfl(cn, j), v, ix);
+    entry(u, __builtin_amdgcn_readlane(cn, j), v, ix);
     wave_sort_desc(v, ix);
     if (lane < k) {
       part_val[(b * n_chunks + blockIdx.y) * k + lane] = v;
