@@ -184,6 +184,9 @@ SIGNATURES = {
     "mirec_table_grad_dense": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32,
                                        c_int64, c_int32, c_void_p, c_void_p]),
     "mirec_adam_table_sumsq_floats": (c_int64, [c_int64, c_int32]),
+    "mirec_owner_adam": (c_int, [POINTER(RowBlock), c_int32, c_int64, c_int64, c_int32, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_int64, POINTER(AdamH), c_void_p,
+                                 c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_adam_table": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
                                  c_void_p, c_int32, c_int64, c_int32, POINTER(AdamH), c_void_p,
                                  c_void_p, c_void_p]),

@@ -354,59 +354,6 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const float4 *__restr
     if (id[k] >= 0) dst[(int64_t)id[k] * d4 + c] = x[k];
 }
 
-// ------------------------------------- the owner's ordered sum of row blocks
-// S of the own row block [lo, lo + n_own) from source blocks (ids, rows),
-// added in block order — each block's ids distinct — exactly as a sequence
-// of index_add_ launches would (0 + a, then + b, ...), in one pass: every
-// block's ids are first inverted into a position map pos[q][r] (-1: absent),
-// then one thread per (own row, float4 column) adds the blocks' rows in
-// order, writing each output row once.  Up to kOsMax blocks per pass; more
-// run as further passes that start from the output.
-constexpr int kOsMax = 64;
-struct OsBlocks {
-  const int32_t *ids[kOsMax];
-  const float4 *rows[kOsMax];
-  int64_t off[kOsMax + 1];  // prefix of the block sizes
-  int32_t n;
-};
-
-__global__ __launch_bounds__(256) void os_mark_kernel(OsBlocks b, int64_t lo, int64_t n_own,
-                                                      int32_t *__restrict__ pos) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= b.off[b.n]) return;
-  int q = 0;
-  while (q + 1 < b.n && b.off[q + 1] <= e) ++q;
-  const int64_t i = e - b.off[q];
-  const int64_t r = (int64_t)b.ids[q][i] - lo;
-  if (r >= 0 && r < n_own) pos[q * n_own + r] = (int32_t)i;
-}
-
-// (1 << lg lanes per own row as the row movers; the blocks four at a time:
-// their positions, then their rows in flight together, then the adds in
-// block order)
-__global__ __launch_bounds__(256) void os_sum_kernel(OsBlocks b, const int32_t *__restrict__ pos,
-                                                     int64_t n_own, int32_t d4, int32_t lg,
-                                                     int accumulate, float4 *__restrict__ out) {
-  const int c = threadIdx.x & ((1 << lg) - 1);
-  const int64_t r = (int64_t)blockIdx.x * (256 >> lg) + (threadIdx.x >> lg);
-  if (r >= n_own || c >= d4) return;
-  const int64_t t = r * d4 + c;
-  float4 acc = accumulate ? out[t] : f4_zero();
-  for (int q0 = 0; q0 < b.n; q0 += 4) {
-    int32_t i[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) i[u] = q0 + u < b.n ? pos[(q0 + u) * n_own + r] : -1;
-    float4 x[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      x[u] = i[u] >= 0 ? b.rows[q0 + u][(int64_t)i[u] * d4 + c] : f4_zero();
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i[u] >= 0) acc = f4_add(acc, x[u]);
-  }
-  out[t] = acc;
-}
-
 }  // namespace mirec
 
 extern "C" int64_t mirec_distinct_rows_workspace(int64_t n_rows) {
@@ -594,53 +541,3 @@ extern "C" int mirec_scatter_rows(const float *src, const int32_t *ids, int64_t 
   return MIREC_OK;
 }
 
-extern "C" int64_t mirec_owner_sum_workspace(int32_t n_blocks, int64_t n_own) {
-  if (n_blocks < 0 || n_own < 0) return -1;
-  return 4 * (int64_t)std::min<int32_t>(std::max<int32_t>(n_blocks, 1), mirec::kOsMax) * n_own;
-}
-
-extern "C" int mirec_owner_sum(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
-                               int64_t n_own, int32_t dim, void *workspace,
-                               size_t workspace_bytes, float *out, mirec_stream_t stream) {
-  using namespace mirec;
-  MIREC_CHECK_ARG(n_blocks >= 0 && n_own >= 0 && dim > 0 && dim % 4 == 0);
-  MIREC_CHECK_ARG(n_blocks == 0 || blocks);
-  if (n_own == 0) return MIREC_OK;
-  MIREC_CHECK_ARG(out && ((uintptr_t)out & 15u) == 0);
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int64_t d4 = dim / 4;
-  if (n_blocks == 0) {
-    MIREC_HIP(hipMemsetAsync(out, 0, (size_t)(n_own * dim) * 4, st));
-    return MIREC_OK;
-  }
-  MIREC_CHECK_ARG(workspace);
-  if ((int64_t)workspace_bytes < mirec_owner_sum_workspace(n_blocks, n_own))
-    return MIREC_ERR_WORKSPACE;
-  int32_t *pos = static_cast<int32_t *>(workspace);
-  for (int32_t q0 = 0; q0 < n_blocks; q0 += kOsMax) {
-    OsBlocks b{};
-    b.n = std::min<int32_t>(kOsMax, n_blocks - q0);
-    b.off[0] = 0;
-    for (int q = 0; q < b.n; ++q) {
-      const mirec_row_block_t &x = blocks[q0 + q];
-      MIREC_CHECK_ARG(x.n >= 0 && (x.n == 0 || (x.ids && x.rows)));
-      MIREC_CHECK_ARG(((uintptr_t)x.rows & 15u) == 0);
-      b.ids[q] = x.ids;
-      b.rows[q] = reinterpret_cast<const float4 *>(x.rows);
-      b.off[q + 1] = b.off[q] + x.n;
-    }
-    MIREC_HIP(hipMemsetAsync(pos, 0xff, (size_t)(4 * b.n * n_own), st));
-    if (b.off[b.n] > 0) {
-      hipLaunchKernelGGL(os_mark_kernel, dim3((unsigned)((b.off[b.n] + 255) / 256)), dim3(256), 0,
-                         st, b, lo, n_own, pos);
-      MIREC_LAUNCH_CHECK();
-    }
-    const int lg = row_lg(d4);
-    MIREC_CHECK_ARG(lg <= 8);
-    hipLaunchKernelGGL(os_sum_kernel, dim3((unsigned)((n_own + (256 >> lg) - 1) / (256 >> lg))),
-                       dim3(256), 0, st, b, pos, n_own, (int32_t)d4, lg, q0 > 0 ? 1 : 0,
-                       reinterpret_cast<float4 *>(out));
-    MIREC_LAUNCH_CHECK();
-  }
-  return MIREC_OK;
-}

@@ -680,6 +680,125 @@ __global__ __launch_bounds__(1024) void tg_norm_final_kernel(const float *__rest
   }
 }
 
+// ------------------------------------- the owner's ordered sum of row blocks
+// S of the own row block [lo, lo + n_own) from source blocks (ids, rows),
+// added in block order — each block's ids distinct — exactly as a sequence
+// of index_add_ launches would (0 + a, then + b, ...), in one pass: every
+// block's ids are first inverted into a position map pos[q][r] (-1: absent),
+// then one thread per (own row, float4 column) adds the blocks' rows in
+// order, writing each output row once.  Up to kOsMax blocks per pass; more
+// run as further passes that start from the output.
+constexpr int kOsMax = 64;
+struct OsBlocks {
+  const int32_t *ids[kOsMax];
+  const float4 *rows[kOsMax];
+  int64_t off[kOsMax + 1];  // prefix of the block sizes
+  int32_t n;
+};
+
+__global__ __launch_bounds__(256) void os_mark_kernel(OsBlocks b, int64_t lo, int64_t n_own,
+                                                      int32_t *__restrict__ pos) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= b.off[b.n]) return;
+  int q = 0;
+  while (q + 1 < b.n && b.off[q + 1] <= e) ++q;
+  const int64_t i = e - b.off[q];
+  const int64_t r = (int64_t)b.ids[q][i] - lo;
+  if (r >= 0 && r < n_own) pos[q * n_own + r] = (int32_t)i;
+}
+
+// (1 << lg lanes per own row as the row movers; the blocks four at a time:
+// their positions, then their rows in flight together, then the adds in
+// block order)
+__global__ __launch_bounds__(256) void os_sum_kernel(OsBlocks b, const int32_t *__restrict__ pos,
+                                                     int64_t n_own, int32_t d4, int32_t lg,
+                                                     int accumulate, float4 *__restrict__ out) {
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r = (int64_t)blockIdx.x * (256 >> lg) + (threadIdx.x >> lg);
+  if (r >= n_own || c >= d4) return;
+  const int64_t t = r * d4 + c;
+  float4 acc = accumulate ? out[t] : f4_zero();
+  for (int q0 = 0; q0 < b.n; q0 += 4) {
+    int32_t i[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) i[u] = q0 + u < b.n ? pos[(q0 + u) * n_own + r] : -1;
+    float4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      x[u] = i[u] >= 0 ? b.rows[q0 + u][(int64_t)i[u] * d4 + c] : f4_zero();
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i[u] >= 0) acc = f4_add(acc, x[u]);
+  }
+  out[t] = acc;
+}
+
+
+// The owner's fused step (data-parallel exchanges): S of the own row block
+// as os_sum forms it — the blocks' rows at pos[q][r] added in block order
+// from zero — and the table Adam of tg_adam_kernel on those rows, in one
+// pass: S is neither written nor read back.  The same element mapping and
+// block partials as tg_adam_kernel (norms bitwise equal).
+__global__ __launch_bounds__(256) void os_adam_kernel(OsBlocks b, const int32_t *__restrict__ pos,
+                                                      int64_t n_own, float *__restrict__ param,
+                                                      float *__restrict__ m, float *__restrict__ v,
+                                                      const float *__restrict__ coef,
+                                                      int64_t n_user, int32_t d4, int32_t shift,
+                                                      mirec_adam_hparams_t h,
+                                                      float *__restrict__ sumsq) {
+  __shared__ float red[2][256];
+  const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
+  const int64_t n4 = n_own * d4;
+  float su = 0.f, si = 0.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 p = adam_ld4(param + 4 * i), a = adam_ld4(m + 4 * i), bv = adam_ld4(v + 4 * i);
+    const int64_t r = row_of(i, d4, shift);
+    const int64_t c = i - r * d4;
+    float4 s = f4_zero();
+    for (int q0 = 0; q0 < b.n; q0 += 4) {
+      int32_t k[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) k[u] = q0 + u < b.n ? pos[(q0 + u) * n_own + r] : -1;
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        x[u] = k[u] >= 0 ? b.rows[q0 + u][(int64_t)k[u] * d4 + c] : f4_zero();
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k[u] >= 0) s = f4_add(s, x[u]);
+    }
+    const float cc = r < n_user ? cu : ci;
+    const float4 g = make_float4(fmaf(cc, p.x, s.x), fmaf(cc, p.y, s.y), fmaf(cc, p.z, s.z),
+                                 fmaf(cc, p.w, s.w));
+    adam1(p.x, a.x, bv.x, g.x, h);
+    adam1(p.y, a.y, bv.y, g.y, h);
+    adam1(p.z, a.z, bv.z, g.z, h);
+    adam1(p.w, a.w, bv.w, g.w, h);
+    st4(param + 4 * i, p);
+    st4(m + 4 * i, a);
+    st4(v + 4 * i, bv);
+    const float sq = p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
+    if (r < n_user) su += sq;
+    else si += sq;
+  }
+  if (sumsq == nullptr) return;
+  red[0][threadIdx.x] = su;
+  red[1][threadIdx.x] = si;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    sumsq[2 * blockIdx.x] = red[0][0];
+    sumsq[2 * blockIdx.x + 1] = red[1][0];
+  }
+}
+
 // ------------------------------------------------------------ host side
 // The stable (key, value) radix sort of the entries, 11 bits per onesweep
 // pass (rocprim's own choice for int pairs on gfx950 is 8: three passes over
@@ -1069,5 +1188,97 @@ extern "C" int mirec_norm_coef(const float *g, int32_t g_stride, const float *no
   hipLaunchKernelGGL(norm_coef_kernel, dim3(1), dim3(64 * ((n + 63) / 64)), 0,
                      (hipStream_t)stream, g, g_stride, norm, norm_stride, n, coef);
   MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+// The owner's pos maps of blocks [q0, q0 + b.n) into `pos` (cleared first).
+static int os_blocks(const mirec_row_block_t *blocks, int32_t q0, int32_t n_blocks, int64_t lo,
+                     int64_t n_own, int32_t *pos, hipStream_t st, OsBlocks &b) {
+  b = OsBlocks{};
+  b.n = std::min<int32_t>(kOsMax, n_blocks - q0);
+  b.off[0] = 0;
+  for (int q = 0; q < b.n; ++q) {
+    const mirec_row_block_t &x = blocks[q0 + q];
+    MIREC_CHECK_ARG(x.n >= 0 && (x.n == 0 || (x.ids && x.rows)));
+    MIREC_CHECK_ARG(((uintptr_t)x.rows & 15u) == 0);
+    b.ids[q] = x.ids;
+    b.rows[q] = reinterpret_cast<const float4 *>(x.rows);
+    b.off[q + 1] = b.off[q] + x.n;
+  }
+  MIREC_HIP(hipMemsetAsync(pos, 0xff, (size_t)(4 * b.n * n_own), st));
+  if (b.off[b.n] > 0) {
+    hipLaunchKernelGGL(os_mark_kernel, dim3((unsigned)((b.off[b.n] + 255) / 256)), dim3(256), 0,
+                       st, b, lo, n_own, pos);
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
+
+extern "C" int64_t mirec_owner_sum_workspace(int32_t n_blocks, int64_t n_own) {
+  if (n_blocks < 0 || n_own < 0) return -1;
+  return 4 * (int64_t)std::min<int32_t>(std::max<int32_t>(n_blocks, 1), mirec::kOsMax) * n_own;
+}
+
+extern "C" int mirec_owner_sum(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
+                               int64_t n_own, int32_t dim, void *workspace,
+                               size_t workspace_bytes, float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(n_blocks >= 0 && n_own >= 0 && dim > 0 && dim % 4 == 0);
+  MIREC_CHECK_ARG(n_blocks == 0 || blocks);
+  if (n_own == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(out && ((uintptr_t)out & 15u) == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t d4 = dim / 4;
+  if (n_blocks == 0) {
+    MIREC_HIP(hipMemsetAsync(out, 0, (size_t)(n_own * dim) * 4, st));
+    return MIREC_OK;
+  }
+  MIREC_CHECK_ARG(workspace);
+  if ((int64_t)workspace_bytes < mirec_owner_sum_workspace(n_blocks, n_own))
+    return MIREC_ERR_WORKSPACE;
+  int32_t *pos = static_cast<int32_t *>(workspace);
+  for (int32_t q0 = 0; q0 < n_blocks; q0 += kOsMax) {
+    OsBlocks b;
+    const int rc = os_blocks(blocks, q0, n_blocks, lo, n_own, pos, st, b);
+    if (rc != MIREC_OK) return rc;
+    const int lg = row_lg(d4);
+    MIREC_CHECK_ARG(lg <= 8);
+    hipLaunchKernelGGL(os_sum_kernel, dim3((unsigned)((n_own + (256 >> lg) - 1) / (256 >> lg))),
+                       dim3(256), 0, st, b, pos, n_own, (int32_t)d4, lg, q0 > 0 ? 1 : 0,
+                       reinterpret_cast<float4 *>(out));
+    MIREC_LAUNCH_CHECK();
+  }
+  return MIREC_OK;
+}
+
+extern "C" int mirec_owner_adam(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
+                                int64_t n_own, int32_t dim, float *param, float *exp_avg,
+                                float *exp_avg_sq, const float *coef, int64_t n_user,
+                                const mirec_adam_hparams_t *h, float *sumsq, float *norms,
+                                void *workspace, size_t workspace_bytes, mirec_stream_t stream) {
+  MIREC_CHECK_ARG(n_blocks >= 0 && n_blocks <= kOsMax && n_own >= 0 && dim > 0 &&
+                  dim % 4 == 0 && h);
+  MIREC_CHECK_ARG(n_blocks == 0 || blocks);
+  MIREC_CHECK_ARG((norms == nullptr) == (sumsq == nullptr));
+  if (n_own == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(param && exp_avg && exp_avg_sq && workspace);
+  MIREC_CHECK_ARG((((uintptr_t)param | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq) & 15u) == 0);
+  if ((int64_t)workspace_bytes < mirec_owner_sum_workspace(n_blocks, n_own))
+    return MIREC_ERR_WORKSPACE;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int32_t *pos = static_cast<int32_t *>(workspace);
+  OsBlocks b;
+  const int rc = os_blocks(blocks, 0, n_blocks, lo, n_own, pos, st, b);
+  if (rc != MIREC_OK) return rc;
+  const int64_t n4 = n_own * (dim / 4);
+  const unsigned nblk = tg_blocks(n4);
+  hipLaunchKernelGGL(os_adam_kernel, dim3(nblk), dim3(256), 0, st, b, pos, n_own, param, exp_avg,
+                     exp_avg_sq, coef, n_user, dim / 4, pow2_shift(dim / 4), *h, sumsq);
+  MIREC_LAUNCH_CHECK();
+  if (norms) {
+    hipLaunchKernelGGL(tg_norm_final_kernel, dim3(1), dim3(1024), 0, st, sumsq, (int64_t)nblk,
+                       norms);
+    MIREC_LAUNCH_CHECK();
+  }
   return MIREC_OK;
 }

@@ -511,6 +511,9 @@ def gather_rows(table: torch.Tensor, ids: torch.Tensor) -> torch.Tensor:
     return out
 
 
+OWNER_ADAM_MAX_SOURCES = 64  # mirec_owner_adam's limit; more: owner_sum passes + adam_table
+
+
 def owner_sum(sources, lo: int, n_own: int, d: int, device, ws: torch.Tensor | None = None):
     """S of the own row block from (ids int32, rows [n, d]) source blocks
     added in list order (each block's ids distinct) — bitwise the sequence of
@@ -531,6 +534,36 @@ def owner_sum(sources, lo: int, n_own: int, d: int, device, ws: torch.Tensor | N
     check(lib.mirec_owner_sum(arr, len(sources), int(lo), int(n_own), int(d), ws.data_ptr(),
                               ws.numel(), out.data_ptr(), _lib.stream_handle()), "owner_sum")
     return out, ws
+
+
+def owner_adam(sources, lo: int, n_own: int, d: int, param: torch.Tensor,
+               exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, coef: torch.Tensor,
+               n_user: int, hp, norms: torch.Tensor | None = None,
+               ws: torch.Tensor | None = None):
+    """owner_sum + the table Adam of the own block in one pass
+    (mirec_owner_adam: S is never stored; bitwise the two-step result).
+    ``param`` / ``exp_avg`` / ``exp_avg_sq``: flat views starting at row
+    ``lo``; at most 64 sources.  Returns the workspace."""
+    from . import _lib
+    from ._lib import check, lib
+    arr = (_lib.RowBlock * max(len(sources), 1))()
+    keep = []
+    for a, (ids, rows) in zip(arr, sources):
+        ids, rows = ids.to(torch.int32).contiguous(), rows.contiguous()
+        keep.append((ids, rows))
+        a.ids, a.rows, a.n = ids.data_ptr(), rows.data_ptr(), ids.numel()
+    nb = max(int(lib.mirec_owner_sum_workspace(len(sources), n_own)), 16)
+    if ws is None or ws.numel() < nb:
+        ws = torch.empty(nb, dtype=torch.uint8, device=param.device)
+    sumsq = None
+    if norms is not None:
+        sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(n_own, d)),
+                            device=param.device)
+    check(lib.mirec_owner_adam(arr, len(sources), int(lo), int(n_own), int(d), param.data_ptr(),
+                               exp_avg.data_ptr(), exp_avg_sq.data_ptr(), coef.data_ptr(),
+                               int(n_user), ctypes.byref(hp), _lib.ptr(sumsq), _lib.ptr(norms),
+                               ws.data_ptr(), ws.numel(), _lib.stream_handle()), "owner_adam")
+    return ws
 
 
 def route_ids(ids: torch.Tensor, n_rows: int, group=None):
@@ -774,13 +807,21 @@ class DenseGradDataParallel:
                 if c:
                     sources.append((rid[off:off + c], rv[off:off + c]))
                 off += c
-        s_own, self._os_ws = owner_sum(sources, lo, n_own, d, p.device, self._os_ws)
-        if self._ones is None or self._ones.numel() != n_own:
-            self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
         n_user = min(max(tg.n_user - lo, 0), n_own)
         hp = st.next_hparams()
         pf = p.data.view(-1)
         ea, es = st.exp_avg.view(-1), st.exp_avg_sq.view(-1)
+        if len(sources) <= OWNER_ADAM_MAX_SOURCES:  # fused: S never stored
+            self._os_ws = owner_adam(sources, lo, n_own, d, pf[lo * d:], ea[lo * d:],
+                                     es[lo * d:], coef, n_user, hp, norms, self._os_ws)
+            _note_raw_write()
+            tg.pending = False
+            self._sharded.add(id(p))
+            st.stale_rows = self.world > 1
+            return
+        s_own, self._os_ws = owner_sum(sources, lo, n_own, d, p.device, self._os_ws)
+        if self._ones is None or self._ones.numel() != n_own:
+            self._ones = torch.ones(n_own, dtype=torch.int32, device=p.device)
         sumsq = None
         if norms is not None:
             sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(n_own, d)),

@@ -635,6 +635,21 @@ int mirec_adam_table(float *param, float *exp_avg, float *exp_avg_sq, const floa
                      int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
                      int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h, float *sumsq,
                      float *norms, mirec_stream_t stream);
+/* The owner's step of the data-parallel exchanges in one pass: S of the own
+ * row block [lo, lo + n_own) from the source blocks exactly as
+ * mirec_owner_sum forms it (block order), then mirec_adam_table on those
+ * rows with every row stamped (param / exp_avg / exp_avg_sq point at row lo;
+ * n_user = the block's user rows; sumsq / norms as there, sumsq of
+ * mirec_adam_table_sumsq_floats(n_own, dim) floats) — S is never stored.
+ * Bitwise the same parameters, moments and norms as mirec_owner_sum +
+ * mirec_adam_table.  At most 64 blocks.  Workspace:
+ * mirec_owner_sum_workspace(n_blocks, n_own) bytes.  (Reference: the Adam
+ * step of the synchronised table gradient, ddp_sage.py:800-806.) */
+int mirec_owner_adam(const mirec_row_block_t *blocks, int32_t n_blocks, int64_t lo,
+                     int64_t n_own, int32_t dim, float *param, float *exp_avg,
+                     float *exp_avg_sq, const float *coef, int64_t n_user,
+                     const mirec_adam_hparams_t *h, float *sumsq, float *norms, void *workspace,
+                     size_t workspace_bytes, mirec_stream_t stream);
 /* mirec_adam_table with the hyper-parameters read from device memory when
  * the kernel runs (capturable in a HIP graph). */
 int mirec_adam_table_dev(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,

@@ -3779,6 +3779,53 @@ def test_owner_sum_equals_index_add_sequence(n_own, n_blocks, per, d):
     assert torch.equal(got, ref)
 
 
+@pytest.mark.parametrize("n_own,n_blocks,per,d,n_user", [(137_500, 9, 60_000, 128, 50_000),
+                                                         (5000, 64, 300, 8, 0),
+                                                         (3001, 6, 2000, 12, 3001),
+                                                         (1000, 0, 0, 16, 400)])
+def test_owner_adam_equals_owner_sum_then_adam_table(n_own, n_blocks, per, d, n_user):
+    """mirec_owner_adam (the owner sum folded into the table Adam, S never
+    stored) == mirec_owner_sum then mirec_adam_table with every row
+    stamped: parameters, moments and the updated slices' norms bitwise —
+    overlapping blocks, ids outside the own block, empty blocks, 64 blocks,
+    the user / item split inside the block, no blocks at all."""
+    import ctypes
+
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd._lib import check, lib
+    from furusato_recommend_amd.dist import owner_adam, owner_sum
+    from furusato_recommend_amd.engine import AdamState
+    g = torch.Generator(device="cuda").manual_seed(n_own + n_blocks + d)
+    lo = 2 * n_own
+    sources = []
+    for q in range(n_blocks):
+        k = 0 if q % 5 == 2 else min(per, n_own + 50)
+        ids = torch.randperm(n_own + 100, device="cuda", generator=g)[:k].int() + lo - 50
+        sources.append((ids, torch.randn(k, d, device="cuda", generator=g)))
+    w0 = torch.randn(n_own, d, device="cuda", generator=g)
+    coef = torch.tensor([1e-3, -2e-3], device="cuda")
+    sa, sb = AdamState(w0.clone(), 1e-3), AdamState(w0.clone(), 1e-3)
+    for st in (sa, sb):  # non-zero moments
+        st.exp_avg.copy_(torch.randn(n_own, d, device="cuda", generator=g) * 1e-3)
+        st.exp_avg_sq.copy_(torch.rand(n_own, d, device="cuda", generator=g) * 1e-6)
+    sb.exp_avg.copy_(sa.exp_avg)
+    sb.exp_avg_sq.copy_(sa.exp_avg_sq)
+    na, nb = torch.empty(2, device="cuda"), torch.empty(2, device="cuda")
+    owner_adam(sources, lo, n_own, d, sa.param.view(-1), sa.exp_avg.view(-1),
+               sa.exp_avg_sq.view(-1), coef, n_user, sa.next_hparams(), na)
+    s_own, _ = owner_sum(sources, lo, n_own, d, torch.device("cuda"))
+    ones = torch.ones(n_own, dtype=torch.int32, device="cuda")
+    sumsq = torch.empty(int(lib.mirec_adam_table_sumsq_floats(n_own, d)), device="cuda")
+    hp = sb.next_hparams()
+    check(lib.mirec_adam_table(sb.param.data_ptr(), sb.exp_avg.data_ptr(),
+                               sb.exp_avg_sq.data_ptr(), coef.data_ptr(), n_user,
+                               s_own.data_ptr(), ones.data_ptr(), 1, n_own, d, ctypes.byref(hp),
+                               sumsq.data_ptr(), nb.data_ptr(), _lib.stream_handle()), "adam")
+    assert torch.equal(sa.param, sb.param)
+    assert torch.equal(sa.exp_avg, sb.exp_avg) and torch.equal(sa.exp_avg_sq, sb.exp_avg_sq)
+    assert torch.equal(na, nb)
+
+
 @pytest.mark.parametrize("n_rows,n,d", [(1_100_000, 300_000, 128), (4097, 4097, 8), (10, 0, 4),
                                         (3000, 1001, 12), (100, 37, 520)])
 def test_scatter_rows_equals_index_copy(n_rows, n, d):
