@@ -18,7 +18,10 @@
 // 256-thread workgroup owns a 128 x 128 output tile, each of its 4 waves a
 // 64 x 64 quarter (2 x 2 MFMA tiles, 64 accumulator registers); the k loop
 // runs in chunks of 32 staged through LDS with the next chunk's global loads
-// in flight (in registers) while the current chunk is multiplied.
+// in flight (in registers) while the current chunk is multiplied.  At K =
+// 128 with enough rows (the QKV in-projection) gemm_nt runs a resident-B
+// form instead: each workgroup splits its 128-column slice of B once into
+// LDS and its waves stream 32-row units of A (gemm_nt_res_kernel, below).
 //
 #include <algorithm>
 
@@ -290,7 +293,7 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
 }
 
 template <int BM, int PF, bool BKN>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict__ A,
+__global__ __launch_bounds__(256, 2) MIREC_NO_PK_F32 void gemm_nt_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         const float *__restrict__ bias,
                                                         float *__restrict__ C, int64_t n,
@@ -349,6 +352,144 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(const float *__restrict
       }
       wave_sync();  // the slab is wave-private
     }
+  }
+}
+
+// ------------------------------------------ gemm_nt at K = 128, B resident
+// C[n, No] = A[n, 128] · B[No, 128]ᵀ (+ bias, ReLU, split output): the
+// QKV in-projection of the SASRec block.  A workgroup splits its 128-column
+// slice of B once into bf16 planes that stay in LDS (104 KB) while its eight
+// waves (two per SIMD) stream 32-row units of A through them: a wave loads
+// its unit's rows straight into the MFMA operand layout (two float4 per lane
+// and 16-deep block, the next unit's loads in flight during the current
+// unit's products) and splits them in registers — once per element, the
+// wave owns all 128 columns of the slice.  No barrier after the one that
+// publishes B; per unit the LDS carries B operand reads and the epilogue
+// slab only.  (gemm_nt_kernel re-stages and re-splits the B slice for every
+// 64-row tile and synchronises its waves twice per 32-deep chunk: at K = 128
+// its load / split / LDS phases took ~32 of the QKV forward's 49 µs.)  The
+// operand values, the k blocks, their order and the six products per block
+// are gemm_nt_kernel's: bitwise the same C.
+constexpr int kRK = 128;        // the k extent of this form
+constexpr int kLdR = kRK + 8;   // bf16 row stride of the B planes (68 dwords: a 16-lane
+                                // group's 16-byte reads hit 16 distinct 4-bank groups)
+constexpr int kRWaves = 8;      // waves per workgroup sharing one B image
+constexpr size_t kResLds = sizeof(uint16_t) * 3 * kTile * kLdR + sizeof(float) * kRWaves * 32 * kLdO;
+constexpr int kResMinUnitsPerCU = 16;  // below: the tiled kernel (gemm_nt)
+
+__global__ __launch_bounds__(64 * kRWaves, 1) void gemm_nt_res_kernel(
+    const float *__restrict__ A, const float *__restrict__ B, const float *__restrict__ bias,
+    float *__restrict__ C, int64_t n, int No, int groups, NtArgs fx) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  uint16_t *pB = reinterpret_cast<uint16_t *>(smem);  // [3][128][kLdR]
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform unit indices
+  const int i = lane & 31, h = lane >> 5;
+  const int ncol = No / kTile;
+  const int n0 = (int)(blockIdx.x % ncol) * kTile;
+  const int64_t grp = blockIdx.x / ncol;
+  // the B slice (rows n0 .. n0 + 127) -> planes, each float4 at its plane_pos
+#pragma unroll
+  for (int q = 0; q < kTile * kRK / 4 / (64 * kRWaves); ++q) {
+    const int e = t + 64 * kRWaves * q, r = e >> 5, c4 = e & 31;
+    const Split3x4 v = split3x4(ld4(B + (int64_t)(n0 + r) * kRK + 4 * c4));
+    uint16_t *d = pB + r * kLdR + plane_pos(c4);
+    *reinterpret_cast<uint2 *>(d) = v.h;
+    *reinterpret_cast<uint2 *>(d + kTile * kLdR) = v.m;
+    *reinterpret_cast<uint2 *>(d + 2 * kTile * kLdR) = v.l;
+  }
+  __syncthreads();
+  float *sO = smem + 3 * kTile * kLdR / 2 + w * 32 * kLdO;  // wave-private slab
+  const int64_t units = (n + 31) / 32, stride = (int64_t)groups * kRWaves;
+  int64_t u = grp * kRWaves + w;
+  if (u >= units) return;  // (no barrier follows)
+  float bv[4];  // loaded before the first unit: an epilogue load would wait behind the prefetch
+#pragma unroll
+  for (int tn = 0; tn < 4; ++tn) bv[tn] = bias ? bias[n0 + tn * 32 + i] : 0.f;
+  // unit u: rows [32 u, +32); lane (i, h) holds row 32 u + i, k = 16 s + 4 h
+  // + (0..3) and 16 s + 8 + 4 h + (0..3) of block s (the x6_k order).  Rows
+  // past n load row n - 1 (unconditional loads: counted waits) and are not
+  // stored.
+  auto rowp = [&](int64_t uu) {
+    return A + std::min<int64_t>(32 * uu + i, n - 1) * kRK + 4 * h;
+  };
+  float4 x[2 * kRK / 16];
+  {
+    const float *p = rowp(u);
+#pragma unroll
+    for (int s = 0; s < kRK / 16; ++s) {
+      x[2 * s] = ld4(p + 16 * s);
+      x[2 * s + 1] = ld4(p + 16 * s + 8);
+    }
+  }
+  for (;;) {
+    const int64_t un = u + stride;
+    const bool more = un < units;
+    // the next unit's rows (the last unit reloads its own: unconditional
+    // loads into the same registers keep every wait counted)
+    const float *pn = rowp(more ? un : u);
+    f32x16 acc[4];
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[tn][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < kRK / 16; ++s) {
+      const float v[8] = {x[2 * s].x,     x[2 * s].y,     x[2 * s].z,     x[2 * s].w,
+                          x[2 * s + 1].x, x[2 * s + 1].y, x[2 * s + 1].z, x[2 * s + 1].w};
+      const Split3 sa = split3(v);
+      x[2 * s] = ld4(pn + 16 * s);  // block s of the next unit into the registers just split
+      x[2 * s + 1] = ld4(pn + 16 * s + 8);
+      __builtin_amdgcn_sched_barrier(0);  // issued here, a unit ahead of their use
+      Split3 sb[4];
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) {
+        const uint16_t *bp = pB + (tn * 32 + i) * kLdR + s * 16 + 8 * h;
+        sb[tn] = Split3{*reinterpret_cast<const bf16x8 *>(bp),
+                        *reinterpret_cast<const bf16x8 *>(bp + kTile * kLdR),
+                        *reinterpret_cast<const bf16x8 *>(bp + 2 * kTile * kLdR)};
+      }
+#pragma unroll
+      for (int tn = 0; tn < 4; ++tn) acc[tn] = mfma_x6(sa, sb[tn], acc[tn]);
+    }
+    // epilogue as gemm_nt_kernel's: bias, ReLU, split output, float4 rows
+    // through the wave's slab
+    const int64_t rbase = 32 * u;
+#pragma unroll
+    for (int tn = 0; tn < 4; ++tn) {
+      const int cbase = n0 + tn * 32;
+      float *cb = C;
+      int ldc = No, cc = cbase;
+      if (fx.C2 != nullptr) {
+        if (cbase < fx.Ns) {
+          ldc = fx.Ns;
+        } else {
+          cb = fx.C2;
+          ldc = No - fx.Ns;
+          cc = cbase - fx.Ns;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float y = acc[tn][r] + bv[tn];
+        if (fx.relu) y = fmaxf(y, 0.f);
+        sO[((r & 3) + 8 * (r >> 2) + 4 * h) * kLdO + i] = y;
+      }
+      wave_sync();
+      float4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = ld4(sO + (lane >> 3) * kLdO + 8 * q * kLdO + 4 * (lane & 7));
+      // rows past n computed row n - 1's product from its operands (clamped
+      // loads): they store those same values there — no branch, and every
+      // wait stays counted
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(cb + std::min<int64_t>(rbase + (lane >> 3) + 8 * q, n - 1) * ldc + cc + 4 * (lane & 7),
+            v[q]);
+      wave_sync();
+    }
+    if (!more) break;
+    u = un;
   }
 }
 
@@ -890,6 +1031,29 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
   const int64_t slots = 2 * (int64_t)std::max(cus, 1);
   const int64_t t128 = (n + 127) / 128 * ncol, t64 = (n + 63) / 64 * ncol;
   const int64_t r128 = 2 * ((t128 + slots - 1) / slots), r64 = (t64 + slots - 1) / slots;
+  // the resident-B form when every wave of a full grid gets two units or
+  // more: below that the per-workgroup B split is not amortised (a 4 K-row
+  // call: 14 vs 8 µs)
+  const int64_t res_units = (n + 31) / 32 * (int64_t)ncol;
+  if (Kr == kRK && !bkn && A2 == nullptr && Amask == nullptr &&
+      res_units >= (int64_t)kResMinUnitsPerCU * std::max(cus, 1)) {
+    static int rc = -1;  // dynamic LDS above 64 KiB needs the opt-in (once)
+    if (rc < 0)
+      rc = hipFuncSetAttribute((const void *)gemm_nt_res_kernel,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)kResLds) ==
+                   hipSuccess
+               ? 0
+               : 1;
+    if (rc != 0) return MIREC_ERR_HIP;
+    // one workgroup per CU and column slice, each wave a unit or more
+    const int64_t units = (n + 31) / 32;
+    const int groups = (int)std::min<int64_t>(std::max<int>(cus / (int)ncol, 1),
+                                              (units + kRWaves - 1) / kRWaves);
+    hipLaunchKernelGGL(gemm_nt_res_kernel, dim3((unsigned)(groups * ncol)), dim3(64 * kRWaves),
+                       kResLds, st, A, B, bias, C, n, (int)No, groups, fx);
+    MIREC_LAUNCH_CHECK();
+    return MIREC_OK;
+  }
   const bool bm64 = r64 < r128 || (r64 == r128 && t128 > slots);
 #define MIREC_NT_LAUNCH(BM, BKN)                                                               \
   hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \

@@ -2258,6 +2258,48 @@ def test_gemm_nt_matches_fp64(n, kr, no):
     LN.FORCE_MIREC_GEMM = False
 
 
+@pytest.mark.parametrize("n,no", [(56_321, 384), (200_003, 128), (70_001, 256)])
+def test_gemm_nt_resident_b_equals_tiled(n, no):
+    """At Kr = 128 mirec_gemm_nt runs the resident-B form (gemm_nt_res_kernel:
+    B split once per workgroup, waves streaming 32-row units) when the call
+    has at least 16 units of 32 rows x 128 columns per CU — every case here
+    on MI355X's 256 CUs — and the tiled kernel below that (the row slices of
+    at most 4 000 rows).  Rows are independent, so C of the slices must equal
+    the same rows of the full product bit for bit: plain, with bias, and with
+    bias + ReLU and the output split at column 128 (the GraphSAGE hop's
+    epilogue forms)."""
+    from furusato_recommend_amd import _lib
+    torch.manual_seed(n + no)
+    a = torch.randn(n, 128, device="cuda")
+    b = torch.randn(no, 128, device="cuda")
+    bias = torch.randn(no, device="cuda")
+    st = _lib.stream_handle()
+
+    def run(x, bb, relu, split):
+        m = x.shape[0]
+        c = torch.full((m, no), float("nan"), device="cuda")
+        c1 = torch.full((m, 128), float("nan"), device="cuda")
+        c2 = torch.full((m, no - 128), float("nan"), device="cuda")
+        _lib.check(_lib.lib.mirec_gemm_nt_ex(
+            x.data_ptr(), None, 0, None, b.data_ptr(), _lib.ptr(bb),
+            c1.data_ptr() if split else c.data_ptr(), c2.data_ptr() if split else None,
+            128 if split else 0, 1 if relu else 0, m, 128, no, st), "gemm_nt_ex")
+        return torch.cat([c1, c2], 1) if split else c
+
+    forms = [(None, False, False), (bias, False, False)]
+    if no > 128:
+        forms.append((bias, True, True))
+    for bb, relu, split in forms:
+        full = run(a, bb, relu, split)
+        ref = a.double() @ b.double().t() + (0 if bb is None else bb.double())
+        if relu:
+            ref = ref.clamp_min(0)
+        assert rel(full, ref) < 1e-6
+        for lo, hi in ((0, 4000), (n // 2 - 1000, n // 2 + 777), (max(n - 3001, 0), n)):
+            part = run(a[lo:hi].contiguous(), bb, relu, split)
+            assert torch.equal(part, full[lo:hi]), (lo, hi, bb is None, relu, split)
+
+
 @pytest.mark.parametrize("n,kr,no", [(1, 32, 128), (100, 384, 128), (56_321, 384, 128),
                                      (3000, 128, 256), (777, 256, 384)])
 def test_gemm_nn_matches_fp64(n, kr, no):

@@ -32,6 +32,7 @@
 #   attn       attention kernels at the C4 length mix
 #   attn_pmc   SQ counters of the packed attention backward (two passes)
 #   topk_pmc   SQ counters of the streamed top-k at C2 (two passes)
+#   gemm_pmc   SQ counters of the resident-B GEMM (gemm_bench shapes, two passes)
 #   tg         the C3 table-gradient accumulate alone (tools/tg_bench.py)
 #   gemm       the GEMM shapes of C3 / C4 and 4096^3
 set -u
@@ -121,8 +122,9 @@ for leg in $LEGS; do
     attn)
       run 400 $E/attn.log python -u tools/attn_bench.py --mixes c4 --batches 2048
       lines $E/attn.log 300 ;;
-    attn_pmc|topk_pmc)
+    attn_pmc|topk_pmc|gemm_pmc)
       if [ $leg = attn_pmc ]; then K=attn_bwd_packed; CMD="python3 tools/attn_bench.py --mixes c4 --batches 2048 --reps 3"
+      elif [ $leg = gemm_pmc ]; then K=gemm_nt_res; CMD="python3 tools/gemm_bench.py --reps 3"
       else K=score_topk; CMD="python3 tools/eval_bench.py --reps 2 --dense 0 --check64 0"; fi
       P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT"
       P2="SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS"
