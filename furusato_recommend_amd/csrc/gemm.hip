@@ -712,6 +712,7 @@ struct TnArgs {
   int Ns;
 };
 
+template <bool MASK, int PF>
 __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         float *__restrict__ work,
@@ -734,42 +735,54 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
   const int64_t r_beg = (int64_t)s * rows_per_slice;
   const int64_t r_end = min(n, r_beg + rows_per_slice);
   const bool do_cs = work_cs != nullptr && blockIdx.z == 0;
-  // element e = t + 256 q: chunk row e >> 5, float4 column e & 31
+  // B columns [n0, +128): from B, or from B2 past the split (workgroup-uniform)
+  const float *Bc = B + n0;
+  int64_t ldb = No;
+  if (fx.B2 != nullptr) {
+    if (n0 < fx.Ns) {
+      ldb = fx.Ns;
+    } else {
+      Bc = fx.B2 + (n0 - fx.Ns);
+      ldb = No - fx.Ns;
+    }
+  }
+  // element e = t + 256 q: chunk row e >> 5, float4 column e & 31.  Rows
+  // past the slice load its last row (unconditional loads: counted waits)
+  // and are zeroed when staged; PF chunks of loads are in flight.
   constexpr int QT = kChunk * 32 / 256;
-  float4 ra[QT], rb[QT];
-  auto load = [&](int64_t r0) {
+  float4 ra[PF][QT], rb[PF][QT], rm[MASK ? PF : 1][QT];
+  auto load = [&](int p, int64_t r0) {
+    const int lim = (int)min<int64_t>(r_end - r0, kChunk);  // rows of this chunk in the slice
 #pragma unroll
     for (int q = 0; q < QT; ++q) {
       const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-      const int64_t r = r0 + kk;
-      const bool ok = r < r_end;
-      float4 a = ok ? ld4(A + r * M + m0 + 4 * c4) : f4_zero();
-      if (ok && fx.Amask != nullptr) {
-        const float4 mk = ld4(fx.Amask + r * M + m0 + 4 * c4);
+      const int64_t r = r0 + min(kk, lim - 1);
+      ra[p][q] = ld4(A + r * M + m0 + 4 * c4);
+      rb[p][q] = ld4(Bc + r * ldb + 4 * c4);
+      if constexpr (MASK) rm[p][q] = ld4(fx.Amask + r * M + m0 + 4 * c4);
+    }
+  };
+  float4 csv = f4_zero();  // this thread's column sums (columns 4 c4 ..)
+  auto stage = [&](int p, int64_t r0) {
+    const int lim = (int)min<int64_t>(r_end - r0, kChunk);
+#pragma unroll
+    for (int q = 0; q < QT; ++q) {
+      const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
+      const bool ok = lim == kChunk || kk < lim;  // (the slice's last chunk may be short)
+      float4 a = ra[p][q], b = rb[p][q];
+      if constexpr (MASK) {
+        const float4 mk = rm[p][q];
         a.x = mk.x > 0.f ? a.x : 0.f;
         a.y = mk.y > 0.f ? a.y : 0.f;
         a.z = mk.z > 0.f ? a.z : 0.f;
         a.w = mk.w > 0.f ? a.w : 0.f;
       }
-      ra[q] = a;
       if (!ok) {
-        rb[q] = f4_zero();
-      } else if (fx.B2 == nullptr) {
-        rb[q] = ld4(B + r * No + n0 + 4 * c4);
-      } else if (n0 < fx.Ns) {
-        rb[q] = ld4(B + r * fx.Ns + n0 + 4 * c4);
-      } else {
-        rb[q] = ld4(fx.B2 + r * (No - fx.Ns) + (n0 - fx.Ns) + 4 * c4);
+        a = f4_zero();
+        b = f4_zero();
       }
-    }
-  };
-  float4 csv = f4_zero();  // this thread's column sums (columns 4 c4 ..)
-  auto stage = [&]() {
-#pragma unroll
-    for (int q = 0; q < QT; ++q) {
-      const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-      if (do_cs) csv = f4_add(csv, ra[q]);
-      const Split3x4 va = split3x4(ra[q]), vb = split3x4(rb[q]);
+      if (do_cs) csv = f4_add(csv, a);
+      const Split3x4 va = split3x4(a), vb = split3x4(b);
       uint16_t *da = pA + kk * kLdK + 4 * c4, *db = pB + kk * kLdK + 4 * c4;
       *reinterpret_cast<uint2 *>(da) = va.h;
       *reinterpret_cast<uint2 *>(da + kPl) = va.m;
@@ -786,23 +799,32 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(const float *__restrict
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  if (r_beg < r_end) load(r_beg);
-  for (int64_t r0 = r_beg; r0 < r_end; r0 += kChunk) {
-    __syncthreads();
-    stage();
-    __syncthreads();
-    if (r0 + kChunk < r_end) load(r0 + kChunk);
+  const int64_t nc = (r_end - r_beg + kChunk - 1) / kChunk;
 #pragma unroll
-    for (int s16 = 0; s16 < kChunk / 16; ++s16) {
-      Split3 sa[2], sb[2];
+  for (int p = 0; p < PF; ++p)
+    if (p < nc) load(p, r_beg + p * kChunk);
+  for (int64_t c0 = 0; c0 < nc; c0 += PF) {
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm) sa[tm] = tr_split3(pA, kPl, wm * 64 + tm * 32, s16, lane);
+    for (int p = 0; p < PF; ++p) {  // chunk c0 + p lives in staging slot p
+      const int64_t c = c0 + p;
+      if (c < nc) {
+        __syncthreads();  // the previous chunk's LDS reads are done
+        stage(p, r_beg + c * kChunk);
+        __syncthreads();
+        if (c + PF < nc) load(p, r_beg + (c + PF) * kChunk);  // in flight during the products
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn) sb[tn] = tr_split3(pB, kPl, wn * 64 + tn * 32, s16, lane);
+        for (int s16 = 0; s16 < kChunk / 16; ++s16) {
+          Split3 sa[2], sb[2];
 #pragma unroll
-      for (int tm = 0; tm < 2; ++tm)
+          for (int tm = 0; tm < 2; ++tm) sa[tm] = tr_split3(pA, kPl, wm * 64 + tm * 32, s16, lane);
 #pragma unroll
-        for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+          for (int tn = 0; tn < 2; ++tn) sb[tn] = tr_split3(pB, kPl, wn * 64 + tn * 32, s16, lane);
+#pragma unroll
+          for (int tm = 0; tm < 2; ++tm)
+#pragma unroll
+            for (int tn = 0; tn < 2; ++tn) acc[tm][tn] = mfma_x6(sa[tm], sb[tn], acc[tm][tn]);
+        }
+      }
     }
   }
   // partial tile out through a wave-private LDS slab as float4 rows (as in
@@ -912,6 +934,9 @@ constexpr int64_t kTnMinRows = 64;
 // 256 workgroups in total lose on 2- and 3-tile gradients: 125 -> 172 us,
 // 49.6 -> 52.9 us).
 constexpr int64_t kTnWant = 512, kTnWant1 = 256;  // workgroups (several tiles / one tile)
+// chunks of gemm_tn loads in flight: two measured 1-3 % slower on the C3 / C4
+// weight gradients (profiles/round5_gemm_tn.txt)
+constexpr int kTnPF = 1;
 static void tn_slices(int64_t n, int M, int No, int *slices, int64_t *rows) {
   const int64_t tiles = (int64_t)(M / kTile) * (No / kTile);
   const int64_t total = tiles == 1 ? kTnWant1 : kTnWant;
@@ -1117,8 +1142,12 @@ static int gemm_tn(const float *A, const float *Amask, const float *B, const flo
   float *work_cs = work + (int64_t)slices * M * No;
   const dim3 grid((unsigned)slices, (unsigned)(M / kTile), (unsigned)(No / kTile));
   TnArgs fx{Amask, B2, Ns};
-  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, st, A, B, work,
-                     colsum ? work_cs : nullptr, n, (int)M, (int)No, rows, fx);
+  if (Amask != nullptr)
+    hipLaunchKernelGGL((gemm_tn_kernel<true, kTnPF>), grid, dim3(256), 0, st, A, B, work,
+                       colsum ? work_cs : nullptr, n, (int)M, (int)No, rows, fx);
+  else
+    hipLaunchKernelGGL((gemm_tn_kernel<false, kTnPF>), grid, dim3(256), 0, st, A, B, work,
+                       colsum ? work_cs : nullptr, n, (int)M, (int)No, rows, fx);
   MIREC_LAUNCH_CHECK();
   const int64_t n4 = (int64_t)M * No / 4;
   const int64_t blocks = (std::max<int64_t>(n4, M) + 63) / 64;
