@@ -159,7 +159,7 @@ struct NtArgs {
 // The k loop of gemm_nt (shared by the plain and the LayerNorm epilogues):
 // acc[TM][2] of wave (wm, wn) over output rows [m0, +BM), columns [n0, +128);
 // smem holds (BM + 128) * kLdNT floats.
-template <int BM, int PF, bool BKN>
+template <int BM, int PF, bool BKN, bool MASK = false>
 __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict__ A,
                                             const float *__restrict__ B, int64_t n, int Kr,
                                             int No, const NtArgs &fx, int64_t m0, int n0,
@@ -170,43 +170,42 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int wm = w >> 1, wn = w & 1;
-  // element e = t + 256 q: row e / kC4, float4 column e % kC4
-  float4 ra[PF][QA], rb[PF][QB];
-  auto load = [&](float4 (&xa)[QA], float4 (&xb)[QB], int k0) {
+  // element e = t + 256 q: row e / kC4, float4 column e % kC4.  Rows past n
+  // load row n - 1 (unconditional loads: counted waits); their products are
+  // never stored (or stored as row n - 1's own values, gemm_nt_kernel).  The
+  // ReLU mask is loaded beside A and applied when the chunk is staged.
+  float4 ra[PF][QA], rb[PF][QB], rm[MASK ? PF : 1][QA];
+  auto load = [&](int p, int k0) {
+    // A columns [k0, k0 + 32): from A, or from A2 past Ks (chunk-uniform)
+    const float *Ab = A;
+    int lda = Kr, kc = k0;
+    if (fx.A2 != nullptr) {
+      if (k0 < fx.Ks) {
+        lda = fx.Ks;
+      } else {
+        Ab = fx.A2;
+        lda = Kr - fx.Ks;
+        kc = k0 - fx.Ks;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-      const int64_t row = m0 + r;
-      float4 v = f4_zero();
-      if (row < n) {
-        if (fx.A2 == nullptr) {
-          v = ld4(A + row * Kr + k0 + 4 * c4);
-        } else if (k0 < fx.Ks) {
-          v = ld4(A + row * fx.Ks + k0 + 4 * c4);
-        } else {
-          v = ld4(fx.A2 + row * (Kr - fx.Ks) + (k0 - fx.Ks) + 4 * c4);
-        }
-        if (fx.Amask != nullptr) {
-          const float4 mk = ld4(fx.Amask + row * Kr + k0 + 4 * c4);
-          v.x = mk.x > 0.f ? v.x : 0.f;
-          v.y = mk.y > 0.f ? v.y : 0.f;
-          v.z = mk.z > 0.f ? v.z : 0.f;
-          v.w = mk.w > 0.f ? v.w : 0.f;
-        }
-      }
-      xa[q] = v;
+      const int64_t row = min(m0 + r, n - 1);
+      ra[p][q] = ld4(Ab + row * lda + kc + 4 * c4);
+      if constexpr (MASK) rm[p][q] = ld4(fx.Amask + row * Kr + k0 + 4 * c4);
     }
     if constexpr (BKN) {  // element e: k row e / 32, float4 column e % 32 of the 128 n
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
         const int e = t + 256 * q, kk = e >> 5, c4 = e & 31;
-        xb[q] = ld4(B + (int64_t)(k0 + kk) * No + n0 + 4 * c4);
+        rb[p][q] = ld4(B + (int64_t)(k0 + kk) * No + n0 + 4 * c4);
       }
     } else {
 #pragma unroll
       for (int q = 0; q < QB; ++q) {
         const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-        xb[q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
+        rb[p][q] = ld4(B + (int64_t)(n0 + r) * Kr + k0 + 4 * c4);
       }
     }
   };
@@ -219,11 +218,20 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
   uint16_t *pA = reinterpret_cast<uint16_t *>(smem);      // [3][BM][kLdP]
   uint16_t *pB = pA + 3 * BM * kLdP;  // [3][128][kLdP], or [3][kChunk][kLdK] ([k][n] B)
   constexpr int kPB = BKN ? kChunk * kLdK : kTile * kLdP;  // B plane stride
-  auto stage_planes = [&](const float4 (&xa)[QA], const float4 (&xb)[QB]) {
+  auto stage_planes = [&](int p) {
+    const float4(&xb)[QB] = rb[p];
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int e = t + 256 * q, r = e / kC4, c4 = e % kC4;
-      const Split3x4 v = split3x4(xa[q]);
+      float4 a = ra[p][q];
+      if constexpr (MASK) {
+        const float4 mk = rm[p][q];
+        a.x = mk.x > 0.f ? a.x : 0.f;
+        a.y = mk.y > 0.f ? a.y : 0.f;
+        a.z = mk.z > 0.f ? a.z : 0.f;
+        a.w = mk.w > 0.f ? a.w : 0.f;
+      }
+      const Split3x4 v = split3x4(a);
       uint16_t *d = pA + r * kLdP + plane_pos(c4);
       *reinterpret_cast<uint2 *>(d) = v.h;
       *reinterpret_cast<uint2 *>(d + BM * kLdP) = v.m;
@@ -276,23 +284,23 @@ __device__ __forceinline__ void nt_mainloop(float *smem, const float *__restrict
   const int nc = Kr / kChunk;
 #pragma unroll
   for (int p = 0; p < PF; ++p)
-    if (p < nc) load(ra[p], rb[p], p * kChunk);
+    if (p < nc) load(p, p * kChunk);
   for (int c0 = 0; c0 < nc; c0 += PF) {
 #pragma unroll
     for (int p = 0; p < PF; ++p) {  // chunk c0 + p lives in staging slot p
       const int c = c0 + p;
       if (c < nc) {
         __syncthreads();  // the previous chunk's LDS reads are done
-        stage_planes(ra[p], rb[p]);
+        stage_planes(p);
         __syncthreads();
-        if (c + PF < nc) load(ra[p], rb[p], (c + PF) * kChunk);  // in flight during the products
+        if (c + PF < nc) load(p, (c + PF) * kChunk);  // in flight during the products
         compute();
       }
     }
   }
 }
 
-template <int BM, int PF, bool BKN>
+template <int BM, int PF, bool BKN, bool MASK>
 __global__ __launch_bounds__(256, 2) MIREC_NO_PK_F32 void gemm_nt_kernel(const float *__restrict__ A,
                                                         const float *__restrict__ B,
                                                         const float *__restrict__ bias,
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(256, 2) MIREC_NO_PK_F32 void gemm_nt_kernel(const f
   const int64_t m0 = (int64_t)(blockIdx.x / ncol) * BM;
   const int n0 = (int)(blockIdx.x % ncol) * kTile;
   f32x16 acc[TM][2];
-  nt_mainloop<BM, PF, BKN>(smem, A, B, n, Kr, No, fx, m0, n0, acc);
+  nt_mainloop<BM, PF, BKN, MASK>(smem, A, B, n, Kr, No, fx, m0, n0, acc);
   // C layout of 32x32: lane holds column i, rows (r & 3) + 8 (r >> 2) + 4 h.
   // Stored through LDS: each 32x32 block goes to a wave-private [row][col]
   // slab and leaves as float4 rows (4 dwordx4 per lane instead of 16 dword
@@ -348,7 +356,9 @@ __global__ __launch_bounds__(256, 2) MIREC_NO_PK_F32 void gemm_nt_kernel(const f
       for (int q = 0; q < 4; ++q) {
         const int e = lane + 64 * q, rr = e >> 3, c4 = e & 7;
         const float4 v = ld4(sO + rr * kLdO + 4 * c4);
-        if (rbase + rr < n) st4(cb + (rbase + rr) * ldc + cc + 4 * c4, v);
+        // rows past n hold row n - 1's products (clamped loads): stored
+        // there as its own values, no branch
+        st4(cb + min(rbase + rr, n - 1) * ldc + cc + 4 * c4, v);
       }
       wave_sync();  // the slab is wave-private
     }
@@ -1080,16 +1090,23 @@ static int gemm_nt(const float *A, const float *A2, int32_t Ks, const float *Ama
     return MIREC_OK;
   }
   const bool bm64 = r64 < r128 || (r64 == r128 && t128 > slots);
-#define MIREC_NT_LAUNCH(BM, BKN)                                                               \
-  hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN>), dim3((unsigned)((n + BM - 1) / BM) * ncol), \
-                     dim3(256), 0, st, A, B, bias, C, n, (int)Kr, (int)No, fx)
+#define MIREC_NT_LAUNCH(BM, BKN, MASK)                                             \
+  hipLaunchKernelGGL((gemm_nt_kernel<BM, 1, BKN, MASK>),                           \
+                     dim3((unsigned)((n + BM - 1) / BM) * ncol), dim3(256), 0, st, A, B, bias, C, \
+                     n, (int)Kr, (int)No, fx)
+#define MIREC_NT_LAUNCH_M(BM, BKN)                        \
+  do {                                                    \
+    if (Amask != nullptr) MIREC_NT_LAUNCH(BM, BKN, true); \
+    else MIREC_NT_LAUNCH(BM, BKN, false);                 \
+  } while (0)
   if (bm64) {
-    if (bkn) MIREC_NT_LAUNCH(64, true);
-    else MIREC_NT_LAUNCH(64, false);
+    if (bkn) MIREC_NT_LAUNCH_M(64, true);
+    else MIREC_NT_LAUNCH_M(64, false);
   } else {
-    if (bkn) MIREC_NT_LAUNCH(128, true);
-    else MIREC_NT_LAUNCH(128, false);
+    if (bkn) MIREC_NT_LAUNCH_M(128, true);
+    else MIREC_NT_LAUNCH_M(128, false);
   }
+#undef MIREC_NT_LAUNCH_M
 #undef MIREC_NT_LAUNCH
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
