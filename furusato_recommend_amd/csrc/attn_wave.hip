@@ -126,7 +126,8 @@ struct Unit {
 // lengths and the longest units start first.
 __device__ __forceinline__ bool unit_of(const int32_t *offsets, const int32_t *order,
                                         int T_uniform, int H, int64_t n_units, Unit &u) {
-  const int64_t unit = (int64_t)blockIdx.x * kUnitsPerWG + (threadIdx.x >> 6);
+  const int64_t unit = (int64_t)blockIdx.x * kUnitsPerWG +
+                       __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
   if (unit >= n_units) return false;
   const int64_t b = order != nullptr ? (int64_t)order[unit / H] : unit / H;
   u.h = (int)(unit % H);
@@ -167,16 +168,21 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_e
   const int nb = (T + kBlk - 1) / kBlk;
   // every operand of the unit in flight at once (one round trip): Q, K in
   // the κ layout, V in the π layout, for the sequence's nb blocks
+  // rows past T load row T - 1 (unconditional loads, no exec-masked
+  // branches): their scores are masked to -inf and their P is 0, and the
+  // query rows past T are not stored; blocks past nb are not loaded
+  // (wave-uniform) and never read
   float qa[4][Q4], k[4][Q4], v[4][4][NCB];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
-    const int r = kBlk * b + j;
-    ld_kappa<Q4>(qb + (int64_t)r * rs, g, b < nb && r < T, qa[b]);
-    ld_kappa<Q4>(kb_ + (int64_t)r * rs, g, b < nb && r < T, k[b]);
+    if (b >= nb) break;
+    const int r = min(kBlk * b + j, T - 1);
+    ld_kappa<Q4>(qb + (int64_t)r * rs, g, true, qa[b]);
+    ld_kappa<Q4>(kb_ + (int64_t)r * rs, g, true, k[b]);
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
-      const int vr = kBlk * b + 4 * g + rr;
-      ld_pi<NCB>(vb + (int64_t)vr * rs, j, b < nb && vr < T, v[b][rr]);
+      const int vr = min(kBlk * b + 4 * g + rr, T - 1);
+      ld_pi<NCB>(vb + (int64_t)vr * rs, j, true, v[b][rr]);
     }
   }
 #pragma unroll
