@@ -418,8 +418,11 @@ __device__ __forceinline__ void ld_kappa_dh(const float *row, int g, int dh, boo
                                             float (&v)[Q4]) {
 #pragma unroll
   for (int c = 0; c < Q4 / 4; ++c) {
+    // unconditional load of a clamped dim, zero selected after (no
+    // exec-masked branch around the load)
     const int dim = 16 * c + 4 * g;
-    const float4 x = (ok && dim < dh) ? ld4(row + dim) : f4_zero();
+    float4 x = ld4(row + min(dim, dh - 4));
+    if (!(ok && dim < dh)) x = f4_zero();
     v[4 * c] = x.x;
     v[4 * c + 1] = x.y;
     v[4 * c + 2] = x.z;
@@ -538,19 +541,19 @@ __device__ __forceinline__ void load_pack(float *d0, float *d1, const float *qkv
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4, w = R / kB;
-    bool ok = w < ps.n && 4 * c < dh;
-    int64_t row = 0;
-    if (ok) {
-      int T, lo;
-      int64_t r0;
-      seq_of(ps, w, T, lo, r0);
-      const int loc = kB * (w - lo) + R % kB;
-      ok = loc < T;
-      row = r0 + loc;
-    }
-    const float *src = qkv + row * rs + coff + 4 * c;
-    v0[q] = ok ? ld4(src) : f4_zero();
-    v1[q] = ok ? ld4(src + rs / 3) : f4_zero();
+    // unconditional loads: a row past its sequence's length loads the
+    // sequence's last row (its score is masked to -inf, its P and dS are 0),
+    // a block past the pack's blocks loads a row of the pack (never read);
+    // only dims past dh must be zero (they would enter the contractions)
+    int T, lo;
+    int64_t r0;
+    seq_of(ps, w, T, lo, r0);
+    const int64_t row = r0 + min(kB * (w - lo) + R % kB, T - 1);
+    const float *src = qkv + row * rs + coff + 4 * min(c, dh / 4 - 1);
+    const float4 x0 = ld4(src), x1 = ld4(src + rs / 3);
+    const bool dim_ok = 4 * c < dh;
+    v0[q] = dim_ok ? x0 : f4_zero();
+    v1[q] = dim_ok ? x1 : f4_zero();
   }
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -603,13 +606,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   float *gbase = dqkv + row0 * rs + h * dh;
   const int ql = kB * (w - lo) + j;  // local query row of phase A
   const int qa = kB * w + j;         // its LDS row
-  const bool qvalid = act && ql < T;
   // q / dO rows in the κ layout: lane group g holds dims 16 c + 4 g + e
   // (float4 loads; the LDS operands are read the same way, as float4 —
   // conflict-free at the row stride ≡ 4 mod 32)
+  // (a query row past T loads the sequence's last row: its dQ is not
+  // stored, its P is 0 in phase B; an idle wave loads row 0, never used)
   float q[S::Q4], dov[S::Q4];
-  ld_kappa_dh<S::Q4>(base + (int64_t)ql * rs, g, dh, qvalid, q);
-  ld_kappa_dh<S::Q4>(dout + (row0 + ql) * d + h * dh, g, dh, qvalid, dov);
+  const int qlc = act ? min(ql, T - 1) : 0;
+  ld_kappa_dh<S::Q4>(base + (int64_t)qlc * rs, g, dh, true, q);
+  ld_kappa_dh<S::Q4>(dout + (row0 + qlc) * d + h * dh, g, dh, true, dov);
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
   float kr[S::Q4], vr[S::Q4];
