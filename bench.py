@@ -23,11 +23,19 @@ explicit form works too:
 --rehearse runs every rank on cuda:0 with gloo collectives (the N-rank code
 path on a one-GPU box; not a throughput measurement).
 
-Quality leg (--quality-steps S, default 3000 at N=1): a second C2-sized
-graph with community structure (kind='cluster'), S training steps of the
-same engine from random init, then Recall@20 / NDCG@20 with trainer.py /
-metric.py semantics — reported beside the throughput, which is measured on
-the structureless uniform graph where any recall is chance.
+Quality leg (--quality-steps S, default 3000): a second C2-sized graph with
+community structure (kind='cluster'), S training steps of the same engine
+from random init — with N > 1 through dist.DataParallel, every rank drawing B
+triples from its user shard — then rank 0 computes Recall@20 / NDCG@20 with
+trainer.py / metric.py semantics (the rank-0 evaluation of ddp_lgcn.py:
+678-743) — reported beside the throughput, which is measured on the
+structureless uniform graph where any recall is chance.
+
+Parity leg (--parity 1): at N = 1 one more GPU step against the CPU oracle
+from the same state; at N > 1 one more data-parallel step whose replicas must
+be bitwise equal (digests all-gathered) and whose table must match, at 1e-4,
+ONE single-process step of the union batch replayed on rank 0 from a snapshot
+(dp_union_parity).  A failed check fails the run.
 """
 from __future__ import annotations
 
@@ -57,9 +65,9 @@ PMC_FILE = os.path.join("profiles", "pmc_prop_kernel.json")
 # (the "HBM-honest" reference for counter bytes; the spec peak is above)
 HBM_STREAM_GBS = 6290.0
 PARITY_TOL = 1e-4  # north_star: output embeddings within 1e-4 rel fp32 of the CPU path
-# C5 (d = 256, 11.26 GB tables: no Infinity-Cache help) full launch, round 2
-C5_NO_CACHE = {"achieved_GBps": 6340.0, "frac_of_peak": 0.79,
-               "source": "profiles/round2_bench_c5_1gpu.json"}
+# C5 (d = 256, 11.26 GB tables: no Infinity-Cache help): the latest committed
+# full-size bench line, read at run time (no_cache_reference)
+C5_NO_CACHE_FILE = os.path.join("profiles", "round5_final_bench_c5_1gpu.json")
 
 
 def parse(argv=None):
@@ -76,8 +84,9 @@ def parse(argv=None):
     ap.add_argument("--kind", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--cpu-baseline", default="step", choices=["step", "forward", "off"])
     ap.add_argument("--cpu-k", type=int, default=3, help="timed CPU steps after 1 warm-up")
-    ap.add_argument("--quality-steps", type=int, default=-1,
-                    help="training steps of the Recall@20 leg (-1: 3000 at N=1, 0 at N>1)")
+    ap.add_argument("--quality-steps", type=int, default=3000,
+                    help="training steps of the Recall@20 leg (every rank, B triples each; "
+                         "with N > 1 through dist.DataParallel, rank 0 evaluates); 0: off")
     ap.add_argument("--quality-clusters", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=2020)
     ap.add_argument("--prune", type=int, default=1,
@@ -90,8 +99,10 @@ def parse(argv=None):
     ap.add_argument("--shard-chunks", type=int, default=4,
                     help="row blocks of the sharded last layer (all-gather overlap)")
     ap.add_argument("--parity", type=int, default=1,
-                    help="rank 0 at N=1: one more GPU step checked against the CPU oracle "
-                         "from the same table / Adam state / triples (the run fails above "
+                    help="N=1: one more GPU step checked against the CPU oracle from the "
+                         "same table / Adam state / triples; N>1: one more data-parallel "
+                         "step checked bitwise across the replicas and, on rank 0, against "
+                         "one single-process step on the union batch (the run fails above "
                          "1e-4)")
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
@@ -250,6 +261,107 @@ def oracle_parity(o, snap) -> dict:
     return r
 
 
+# ------------------------------------------------- data-parallel parity leg
+
+def _coll(t: torch.Tensor, backend: str, dev) -> torch.Tensor:
+    """A tensor in the place the backend's collectives take it (RCCL: the
+    device ``dev``; gloo: the host)."""
+    return t.to(dev) if backend == "nccl" else t.cpu()
+
+
+def replica_digest(*ts: torch.Tensor) -> torch.Tensor:
+    """16-byte BLAKE2b digest of the tensors' bytes (uint8 [16], host): two
+    replicas are bitwise equal iff their digests are (up to hash collision)."""
+    import hashlib
+    h = hashlib.blake2b(digest_size=16)
+    for t in ts:
+        h.update(t.detach().contiguous().cpu().view(torch.uint8).numpy().data)
+    return torch.frombuffer(bytearray(h.digest()), dtype=torch.uint8)
+
+
+def dp_union_parity(dp, emb: torch.Tensor, adam, users, pos, neg, decay: float, replay,
+                    tol: float = PARITY_TOL) -> dict:
+    """Proof that the N-rank step is the single-process step of the union
+    batch (the reference's intent: ddp_lgcn.py:669-673 steps every rank's
+    own batch through one shared model).  Collective: every rank calls it.
+
+    Every rank snapshots the table and the Adam state (in ``sharded`` mode
+    the moments are gathered first: each rank's are current on its own rows
+    only), then takes one ``dp.step`` on its own (u, p, n).  Afterwards
+      * every rank hashes its table and (gathered) Adam moments; the digests
+        are all-gathered and must be identical — the replicas are bitwise
+        one model;
+      * rank 0 gathers every rank's triples, and ``replay(snap, U, P, N) ->
+        (table, loss)`` takes ONE single-process step from the snapshot on
+        the concatenated union batch (rank-major order); its table must be
+        within ``tol`` (rel, max-abs) of the data-parallel table and its loss
+        of the mean of the ranks' losses.
+    Returns the record on rank 0 (``ok`` = all of it), a short one on the
+    others."""
+    world, rank = dp.world, dp.rank
+    backend = dist.get_backend(dp.group)
+    dev = emb.device
+    dp.gather_optimizer_state()  # (no-op unless sharded moments are stale)
+    snap = {"emb0": emb.detach().clone(), "exp_avg": adam.exp_avg.detach().clone(),
+            "exp_avg_sq": adam.exp_avg_sq.detach().clone(), "n_steps": int(adam.n_steps)}
+    trip = torch.stack([torch.as_tensor(x).to(torch.int32).reshape(-1)
+                        for x in (users, pos, neg)])  # [3, B]
+    allt = _coll(torch.empty(world * 3, trip.shape[1], dtype=torch.int32), backend, dev)
+    dist.all_gather_into_tensor(allt, _coll(trip, backend, dev), group=dp.group)
+    allt = allt.view(world, 3, -1)
+    loss = dp.step(users, pos, neg, decay)
+    dp.gather_optimizer_state()
+    lsum = _coll(torch.as_tensor(loss, dtype=torch.float32).detach().reshape(1).clone(),
+                 backend, dev)
+    dist.all_reduce(lsum, group=dp.group)
+    dig = torch.cat([replica_digest(emb), replica_digest(adam.exp_avg, adam.exp_avg_sq)])
+    digs = _coll(torch.empty(world * dig.numel(), dtype=torch.uint8), backend, dev)
+    dist.all_gather_into_tensor(digs, _coll(dig, backend, dev), group=dp.group)
+    digs = digs.cpu().view(world, -1)
+    tab_equal = bool((digs[:, :16] == digs[0, :16]).all())
+    mom_equal = bool((digs[:, 16:] == digs[0, 16:]).all())
+    r = {"world_size": world, "backend": backend, "mode": dp.mode,
+         "replicas_bitwise_equal": tab_equal, "moments_bitwise_equal": mom_equal,
+         "table_digest": digs[0, :16].numpy().tobytes().hex()}
+    if rank != 0:
+        return r
+    allt = allt.cpu()
+    U, P, N = (allt[:, k, :].reshape(-1) for k in range(3))
+    emb1, loss1 = replay(snap, U, P, N)
+    loss_dp = float(lsum.cpu()[0]) / world
+    r.update(rel_emb_step=rel_err(emb, emb1),
+             rel_loss=abs(loss_dp - float(loss1)) / max(abs(float(loss1)), 1e-30),
+             loss_dp=loss_dp, loss_union=float(loss1), union_batch=int(U.numel()),
+             rows=int(emb.shape[0]), tol=tol,
+             what=f"one {world}-rank data-parallel step ({dp.mode} exchange) vs ONE "
+                  f"single-process step on the union batch of all ranks' triples from the same "
+                  "table / Adam state (rank 0): rel = max|dp - union| / max|union| over the whole "
+                  "table; replicas' tables and Adam moments compared bitwise by digest")
+    r["ok"] = bool(tab_equal and mom_equal and r["rel_emb_step"] < tol and r["rel_loss"] < tol)
+    return r
+
+
+def engine_replay(graph, args, world: int, decay: float, adam_like):
+    """``replay`` for dp_union_parity on the GPU: a fresh PropagationEngine
+    sized for the union batch (world x B triples) takes one train_step from
+    the snapshot's table and Adam state."""
+    from furusato_recommend_amd.engine import AdamState, PropagationEngine
+
+    def replay(snap, U, P, N):
+        dev = graph.device
+        eng = PropagationEngine(graph, args.dim, args.layers, world * args.batch,
+                                prune=bool(args.prune))
+        e = snap["emb0"].to(dev).clone()
+        ad = AdamState(e, adam_like.lr, adam_like.betas, adam_like.eps)
+        ad.exp_avg.copy_(snap["exp_avg"])
+        ad.exp_avg_sq.copy_(snap["exp_avg_sq"])
+        ad.n_steps = snap["n_steps"]
+        loss = eng.train_step(e, ad, U.to(dev), P.to(dev), N.to(dev), decay)
+        torch.cuda.synchronize()
+        return e, float(loss.item())
+    return replay
+
+
 def cpu_baseline(ds, args, users, pos, neg, snap=None):
     """The CPU oracle (torch fp32) on a bounded sample of the same workload,
     timed per BASELINE.md §3: one warm-up training step, then the mean of K
@@ -335,7 +447,21 @@ def hbm_counter(traffic, avg_ms):
     rate = traffic / (avg_ms * 1e-3) / 1e9
     return {"counter_GBps": round(rate, 1), "frac_of_peak": round(rate / HBM_PEAK_GBS, 4),
             "stream_GBps": HBM_STREAM_GBS, "frac_of_stream": round(rate / HBM_STREAM_GBS, 4),
-            "no_cache_reference_c5": C5_NO_CACHE}
+            "no_cache_reference_c5": no_cache_reference()}
+
+
+def no_cache_reference(path: str = C5_NO_CACHE_FILE) -> dict | None:
+    """The HBM-honest roofline: C5's full launch (d = 256, 11.26 GB per
+    table, far beyond Infinity Cache) from the committed C5 bench line."""
+    try:
+        with open(os.path.join(ROOT, path)) as f:
+            j = next(json.loads(ln) for ln in f if ln.lstrip().startswith("{"))
+        r = j["roofline"]
+    except (OSError, StopIteration, KeyError, ValueError):
+        return None
+    return {"achieved_GBps": r["achieved"], "frac_of_peak": r["frac"],
+            "avg_launch_ms": r["avg_launch_ms"],
+            "algorithmic_bytes_per_launch": r["algorithmic_bytes_per_launch"], "source": path}
 
 
 def c2_workload(args) -> bool:
@@ -344,47 +470,87 @@ def c2_workload(args) -> bool:
 
 # ---------------------------------------------------------------- quality leg
 
-def quality_leg(args, dev, steps: int):
+def train_then_evaluate(step, steps: int, evaluate_fn, rank: int, world: int, sync=None,
+                        group=None):
+    """The quality leg's loop, rank-symmetric: ``steps`` calls of
+    ``step(i)`` on every rank (a data-parallel step when world > 1), then
+    rank 0 alone evaluates (``evaluate_fn()``) while the others wait at a
+    barrier — the reference's DDP loop with its rank-0 evaluation
+    (ddp_lgcn.py:669-743).  Returns (evaluation or None, train seconds)."""
+    sync = sync or (lambda: None)
+    sync()
+    t = time.perf_counter()
+    for i in range(steps):
+        step(i)
+        if (i + 1) % 500 == 0:
+            sync()
+            if rank == 0:
+                progress(f"quality leg: {i + 1}/{steps} training steps")
+    sync()
+    t = time.perf_counter() - t
+    res = None
+    if rank == 0:
+        progress("quality leg: evaluating Recall@20")
+        res = evaluate_fn()
+    if world > 1:
+        dist.barrier(group=group)
+    return res, t
+
+
+def quality_leg(args, dev, steps: int, rank: int = 0, world: int = 1, dp_mode: str = "sparse"):
     """Recall@20 that measures something: train the same engine on a
     C2-sized graph with community structure (items i % K == user u % K with
-    probability 0.9), `steps` steps of B triples from the on-device sampler,
-    then the evaluation path (trainer.py:115-187 semantics)."""
+    probability 0.9), `steps` steps of B triples per rank from the on-device
+    sampler (each rank from its user shard; with world > 1 through
+    dist.DataParallel in the exchange mode the throughput leg settled on),
+    then rank 0 runs the evaluation path (trainer.py:115-187 semantics).
+    Collective when world > 1; returns the record on rank 0, None elsewhere."""
     from furusato_recommend_amd import LightGCN, SyntheticBipartite
+    from furusato_recommend_amd.dist import DataParallel
     from furusato_recommend_amd.engine import sample_triples
     from furusato_recommend_amd.evaluate import evaluate
     t0 = time.perf_counter()
-    progress("quality leg: building the community graph")
+    if rank == 0:
+        progress("quality leg: building the community graph")
     ds = SyntheticBipartite(args.users, args.items, args.edges, seed=7, kind="cluster",
                             n_clusters=args.quality_clusters, p_in=0.9, test_frac=0.1)
-    progress("quality leg: graph built")
+    if rank == 0:
+        progress("quality leg: graph built")
     torch.manual_seed(args.seed)
     cfg = {"recdim": args.dim, "layer": args.layers, "lr": 1e-3, "decay": 1e-4,
            "device": str(dev), "bpr_batch_size": args.batch, "prune": bool(args.prune)}
     model = LightGCN(cfg, ds)
     eng, emb = model.engine, model.all_embedding.weight.data
+    dp = DataParallel(eng, emb, model.optim, mode=dp_mode,
+                      chunks=args.shard_chunks) if world > 1 else None
     B = args.batch
     u = torch.empty(B, dtype=torch.int32, device=dev)
     p, n = torch.empty_like(u), torch.empty_like(u)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    r0 = evaluate(model, ds.testDict, topks=(20,))
-    torch.cuda.synchronize()
-    t_train = time.perf_counter()
-    for i in range(steps):
-        sample_triples(model.graph, B, args.seed + 1, i * B, u, p, n, err, 0, 1)
-        eng.train_step(emb, model.optim, u, p, n, cfg["decay"])
-        if (i + 1) % 500 == 0:
-            torch.cuda.synchronize()
-            progress(f"quality leg: {i + 1}/{steps} training steps")
-    torch.cuda.synchronize()
-    t_train = time.perf_counter() - t_train
-    progress("quality leg: evaluating Recall@20")
-    r = evaluate(model, ds.testDict, topks=(10, 20))
+    r0 = evaluate(model, ds.testDict, topks=(20,)) if rank == 0 else None
+
+    def step(i):
+        sample_triples(model.graph, B, args.seed + 1, i * B, u, p, n, err, rank, world)
+        if dp is None:
+            eng.train_step(emb, model.optim, u, p, n, cfg["decay"])
+        else:
+            dp.step(u, p, n, cfg["decay"])
+    r, t_train = train_then_evaluate(step, steps,
+                                     lambda: evaluate(model, ds.testDict, topks=(10, 20)),
+                                     rank, world, sync=torch.cuda.synchronize)
+    if int(err.item()) != 0:
+        raise RuntimeError("sampler retry budget exhausted")
+    if rank != 0:
+        return None
     mean_deg = ds.trainDataSize / ds.n_users
     return {"recall@20": float(r["recall"][1]), "ndcg@20": float(r["ndcg"][1]),
             "recall@10": float(r["recall"][0]), "recall@20_at_init": float(r0["recall"][0]),
             "chance_recall@20": round(20.0 / (ds.m_items - mean_deg), 7),
-            "test_users": len(ds.testDict), "train_steps": steps, "batch": B, "lr": 1e-3,
-            "train_s": round(t_train, 2), "leg_s": round(time.perf_counter() - t0, 2),
+            "test_users": len(ds.testDict), "train_steps": steps, "batch_per_rank": B,
+            "global_batch": B * world, "ranks": world,
+            "trained_by": (f"dist.DataParallel ({dp.mode} exchange), {world} ranks, "
+                           "rank 0 evaluates" if dp is not None else "one engine"),
+            "lr": 1e-3, "train_s": round(t_train, 2), "leg_s": round(time.perf_counter() - t0, 2),
             "graph": f"cluster: {args.users} x {args.items} / {args.edges} edges, "
                      f"{args.quality_clusters} communities, p_in 0.9, seed 7"}
 
@@ -529,16 +695,27 @@ def main(argv=None):
     traffic, traffic_src = pmc_traffic(args)
 
     snap = None
+    dp_parity = None
     if rank == 0 and world == 1 and args.parity:
         progress("parity: GPU step from a host snapshot of the table and Adam state")
         snap = parity_snapshot(model, eng, emb, args, t_base + args.steps, rank, world)
+    elif world > 1 and args.parity:
+        if rank == 0:
+            progress("parity: one data-parallel step vs the union batch replayed on rank 0")
+        i = t_base + args.steps
+        sample_triples(model.graph, B, args.seed, i * B, u, p, n, err, rank, world)
+        dp_parity = dp_union_parity(dp, emb, model.optim, u, p, n, cfg["decay"],
+                                    engine_replay(model.graph, args, world, cfg["decay"],
+                                                  model.optim))
+        if rank == 0:
+            progress(f"parity: {dp_parity}")
 
-    qsteps = args.quality_steps if args.quality_steps >= 0 else (3000 if world == 1 else 0)
+    qsteps = max(0, args.quality_steps)
     recall = None
-    if qsteps > 0 and rank == 0:
+    if qsteps > 0:
         del model, eng, emb, dp
         torch.cuda.empty_cache()
-        recall = quality_leg(args, dev, qsteps)
+        recall = quality_leg(args, dev, qsteps, rank, world, dp_mode)
 
     cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline != "off":
@@ -550,6 +727,8 @@ def main(argv=None):
         o = OracleLightGCN(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, args.dim,
                            args.layers, 1e-3, 1e-4, emb=snap["emb0"])
         parity = oracle_parity(o, snap)
+    if dp_parity is not None:
+        parity = dp_parity
 
     if rank == 0:
         value = world * args.steps * B / dt
@@ -609,7 +788,7 @@ def main(argv=None):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if parity is not None and not parity["ok"]:
+    if parity is not None and not parity.get("ok", True):
         raise SystemExit(f"parity above {PARITY_TOL}: {parity}")
 
 

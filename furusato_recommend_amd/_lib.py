@@ -303,9 +303,18 @@ SIGNATURES = {
     "mirec_cpu_bpr_sample": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                      c_int64, c_uint64, c_uint64, c_int32, c_int32, c_void_p,
                                      c_void_p, c_void_p, c_void_p, c_int32]),
+    "mirec_cpu_bpr_sample_capped": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                            c_int64, c_int64, c_int32, c_uint64, c_uint64,
+                                            c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
     "mirec_cpu_bpr_step": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                    c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_float,
                                    c_void_p, c_void_p, c_int32]),
+    "mirec_cpu_bpr_grad": (c_int, [c_void_p, c_void_p, c_int64, c_int32, c_int64, c_void_p,
+                                   c_void_p, c_void_p, c_int64, c_float, c_float, c_void_p,
+                                   c_int32]),
+    "mirec_cpu_adam": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                               c_int32]),
 }
 
 

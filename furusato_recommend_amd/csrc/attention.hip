@@ -20,7 +20,7 @@
 //   causal mask, column softmax -> Pᵀ; Oᵀ = Σ_kb Vᵀ_kb Pᵀ_kb; store O rows.
 // Backward, phase A (wave w = query block w): recompute Pᵀ; dPᵀ = V dOᵀ;
 //   δ_q = Σ_k P dP; dSᵀ = Pᵀ ⊙ (dPᵀ − δ) / sqrt(dh); dQᵀ = Kᵀ dSᵀ -> store;
-//   the softmax statistics (max, 1/sum) and δ of each query -> LDS, the
+//   the softmax statistic (base-2 log-sum-exp) and δ of each query -> LDS, the
 //   wave's own K / V block -> registers.  Phase B (wave w = key block w), per
 //   query block qb >= w: S = Q_qb K_wᵀ and dP = dO_qb V_wᵀ (queries on the
 //   accumulator rows, keys on the lanes — the layout in which P and dS are
@@ -30,8 +30,11 @@
 //   the backward's LDS: more workgroups per CU hide the per-workgroup
 //   memory latency that bounds these small problems.
 // LDS (head dim padded to DPAD = 32 / 64): forward K, V (35 KB at DPAD 64,
-// 16 rows per block); backward K, V, later reused for Q, dO, plus 3 floats
-// per row of statistics (36 KB): 4 workgroups per CU either way.
+// 16 rows per block); backward K, V, later reused for Q, dO, plus 2 floats
+// per row of statistics (35 KB): 4 workgroups per CU either way.
+// Softmax in base 2 (common.h exp2_hw): scores are scaled by scale·log2(e),
+// every exponential is one v_exp_f32, and phase B's P = exp2(s·c − lse2)
+// needs one statistic per query (read as float4 per lane group).
 // q/k/v are read straight from the packed in-projection output (head h =
 // columns h*dh .. of each third); O / dQKV are written in the same layout.
 // Sequences come either as a uniform [B, T, 3d] batch or packed by offsets.
@@ -58,7 +61,7 @@ struct AttnShape {
   static constexpr int LDK = DPAD + 4;    // K / V, then Q / dO row stride (≡ 4 mod 32)
   static constexpr int fwd_lds = (int)sizeof(float) * 2 * TR * LDK;
   static constexpr int bwd_region = 2 * TR * LDK;
-  static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 3 * TR);
+  static constexpr int bwd_lds = (int)sizeof(float) * (bwd_region + 2 * TR);
 };
 
 __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
@@ -149,11 +152,12 @@ __device__ __forceinline__ void store4(float *row, int c, int dh, f32x4 x) {
 }
 
 // Pᵀ for query block w (key blocks 0..w) in registers: s[kb][r] =
-// P[query 16w + j][key 16kb + 4g + r] (j = lane & 15, g = lane >> 4).
+// P[query 16w + j][key 16kb + 4g + r] (j = lane & 15, g = lane >> 4), and the
+// query's lse2 = log2 Σ_k exp2(s_k · scale · log2 e) (base-2 log-sum-exp).
 template <int DPAD, int NB>
 __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)[DPAD / 4], int w,
-                                               int T, float scale, f32x4 (&s)[NB], float &m_out,
-                                               float &inv_out) {
+                                               int T, float scale, f32x4 (&s)[NB],
+                                               float &lse2_out) {
   using S = AttnShape<DPAD, NB>;
   const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -165,6 +169,7 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
       if (kb <= w) s[kb] = mfma16(sK[(kB * kb + j) * S::LDK + 4 * t + g], q[t], s[kb]);
   }
   const int qi = kB * w + j;
+  const float c2 = scale * kLog2e;
   float m = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < NB; ++kb) {
@@ -172,7 +177,7 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = kB * kb + 4 * g + r;
-      const float v = (key > qi || key >= T) ? -INFINITY : s[kb][r] * scale;
+      const float v = (key > qi || key >= T) ? -INFINITY : s[kb][r] * c2;
       s[kb][r] = v;
       m = fmaxf(m, v);
     }
@@ -185,7 +190,7 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float e = expf(s[kb][r] - m);
+      const float e = exp2_hw(s[kb][r] - m);
       s[kb][r] = e;
       sum += e;
     }
@@ -199,8 +204,7 @@ __device__ __forceinline__ void scores_softmax(const float *sK, const float (&q)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[kb][r] *= inv;
   }
-  m_out = m;
-  inv_out = inv;
+  lse2_out = m + log2_hw(sum);
 }
 
 // Sequence seq0 + blockIdx.x / H (or order[seq0 + blockIdx.x / H]), head
@@ -232,8 +236,8 @@ __global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restri
   __syncthreads();
   if (w >= nb) return;  // no barrier below
   f32x4 p[NB];
-  float m_, inv_;
-  scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, m_, inv_);
+  float lse2_;
+  scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, lse2_);
   f32x4 o[S::NCB];
 #pragma unroll
   for (int cb = 0; cb < S::NCB; ++cb) o[cb] = zero4();
@@ -268,7 +272,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
   float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
-  float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
+  float *sM = smem + S::bwd_region, *sD = sM + S::TR;  // per query: lse2, δ
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = lane & 15, g = lane >> 4;
   const int64_t b = order ? (int64_t)order[seq0 + blockIdx.x / H] : seq0 + blockIdx.x / H;
@@ -291,8 +295,8 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   float kr[S::Q4], vr[S::Q4];  // K / V rows 16w + j, dims 4t + g (phase B operands)
   if (w < nb) {
     f32x4 p[NB], dp[NB];
-    float m, inv;
-    scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, m, inv);
+    float lse2;
+    scores_softmax<DPAD, NB>(sK, q, w, T, scale, p, lse2);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
 #pragma unroll
@@ -311,8 +315,7 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
     delta += __shfl_xor(delta, 16);
     delta += __shfl_xor(delta, 32);
     if (g == 0) {
-      sM[qi] = m;
-      sL[qi] = inv;
+      sM[qi] = lse2;
       sD[qi] = delta;
     }
     // dSᵀ (in dp), then dQᵀ = Kᵀ dSᵀ
@@ -359,8 +362,12 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
       dv[cb] = zero4();
       dk[cb] = zero4();
     }
+    const float c2 = scale * kLog2e;
     for (int qb = w; qb < nb; ++qb) {
-      // S[query 16qb + 4g + r][key 16w + j] and dP likewise
+      // S[query 16qb + 4g + r][key 16w + j] and dP likewise; the four
+      // queries' statistics as one float4 each
+      const float4 l4 = ld4(sM + kB * qb + 4 * g), d4 = ld4(sD + kB * qb + 4 * g);
+      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
       f32x4 sc = zero4(), dpc = zero4();
       const float *qrow = sQ + (kB * qb + j) * S::LDK + g;
       const float *orow = sDO + (kB * qb + j) * S::LDK + g;
@@ -374,9 +381,9 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
       for (int r = 0; r < 4; ++r) {
         const int qq = kB * qb + 4 * g + r;
         const bool ok = key <= qq && qq < T;
-        const float pv = ok ? expf(sc[r] * scale - sM[qq]) * sL[qq] : 0.f;
+        const float pv = ok ? exp2_hw(fmaf(sc[r], c2, -lq[r])) : 0.f;
         pr[r] = pv;
-        dsr[r] = pv * (dpc[r] - sD[qq]) * scale;
+        dsr[r] = pv * (dpc[r] - dq4[r]) * scale;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -435,7 +442,7 @@ __device__ __forceinline__ void ld_kappa_dh(const float *row, int g, int dh, boo
 template <int DPAD, int NB>
 __device__ __forceinline__ void scores_softmax_kappa(const float *sK, const float (&q)[DPAD / 4],
                                                      int w, int T, float scale, f32x4 (&s)[NB],
-                                                     float &m_out, float &inv_out) {
+                                                     float &lse2_out) {
   using S = AttnShape<DPAD, NB>;
   const int lane = threadIdx.x & 63, j = lane & 15, g = lane >> 4;
 #pragma unroll
@@ -453,6 +460,7 @@ __device__ __forceinline__ void scores_softmax_kappa(const float *sK, const floa
       }
   }
   const int qi = kB * w + j;
+  const float c2 = scale * kLog2e;
   float m = -INFINITY;
 #pragma unroll
   for (int kb = 0; kb < NB; ++kb) {
@@ -460,7 +468,7 @@ __device__ __forceinline__ void scores_softmax_kappa(const float *sK, const floa
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int key = kB * kb + 4 * g + r;
-      const float v = (key > qi || key >= T) ? -INFINITY : s[kb][r] * scale;
+      const float v = (key > qi || key >= T) ? -INFINITY : s[kb][r] * c2;
       s[kb][r] = v;
       m = fmaxf(m, v);
     }
@@ -473,7 +481,7 @@ __device__ __forceinline__ void scores_softmax_kappa(const float *sK, const floa
     if (kb > w) break;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float e = expf(s[kb][r] - m);
+      const float e = exp2_hw(s[kb][r] - m);
       s[kb][r] = e;
       sum += e;
     }
@@ -487,8 +495,7 @@ __device__ __forceinline__ void scores_softmax_kappa(const float *sK, const floa
 #pragma unroll
     for (int r = 0; r < 4; ++r) s[kb][r] *= inv;
   }
-  m_out = m;
-  inv_out = inv;
+  lse2_out = m + log2_hw(sum);
 }
 
 struct PackSeqs {
@@ -575,7 +582,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
   float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
-  float *sM = smem + S::bwd_region, *sL = sM + S::TR, *sD = sL + S::TR;  // per query
+  float *sM = smem + S::bwd_region, *sD = sM + S::TR;  // per query: lse2, δ
   const int64_t pk = blockIdx.x / H;
   const int64_t busy = (int64_t)packs[0] * H;
   if ((int64_t)blockIdx.x >= busy) {
@@ -620,13 +627,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   float kr[S::Q4], vr[S::Q4];
   if (act) {
     f32x4 p[NB], dp[NB];
-    float m, inv;
+    float lse2;
     // local key blocks kb = 0..lw (LDS block lo + kb); the masks tell the
     // compiler lw, lo < 4 (as the plain kernel's w), which keeps the
     // unrolled block loops from holding every block's operands at once
     const int lw = (w - lo) & 3;
     const float *sKl = sK + kB * lo * S::LDK, *sVl = sV + kB * lo * S::LDK;  // lo < 4
-    scores_softmax_kappa<DPAD, NB>(sKl, q, lw, T, scale, p, m, inv);
+    scores_softmax_kappa<DPAD, NB>(sKl, q, lw, T, scale, p, lse2);
 #pragma unroll
     for (int kb = 0; kb < NB; ++kb) dp[kb] = zero4();
 #pragma unroll
@@ -651,8 +658,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     delta += __shfl_xor(delta, 16);
     delta += __shfl_xor(delta, 32);
     if (g == 0) {
-      sM[qa] = m;
-      sL[qa] = inv;
+      sM[qa] = lse2;
       sD[qa] = delta;
     }
     f32x4 dq[S::NCB];
@@ -711,10 +717,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     // local query blocks lw..nbs-1 of the sequence (LDS block lo + qb)
     const int lw = (w - lo) & 3, nbs = hi - lo, o = kB * (lo & 3);
     const float *sQl = sQ + o * S::LDK, *sDOl = sDO + o * S::LDK;
-    const float *sMl = sM + o, *sLl = sL + o, *sDl = sD + o;
-    (void)sMl, (void)sLl, (void)sDl;
+    const float *sMl = sM + o, *sDl = sD + o;
+    const float c2 = scale * kLog2e;
     for (int qb = lw; qb < nbs; ++qb) {
       float pr[4], dsr[4];
+      // the four queries' statistics of this lane group: one float4 each
+      const float4 l4 = ld4(sMl + kB * qb + 4 * g), d4 = ld4(sDl + kB * qb + 4 * g);
+      const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq4[4] = {d4.x, d4.y, d4.z, d4.w};
       f32x4 sc = zero4(), dpc = zero4();
       const float *qrow = sQl + (kB * qb + j) * S::LDK + 4 * g;
       const float *orow = sDOl + (kB * qb + j) * S::LDK + 4 * g;
@@ -734,9 +743,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
       for (int r = 0; r < 4; ++r) {
         const int qq = kB * qb + 4 * g + r;  // local query = its local LDS row
         const bool ok = key <= qq && qq < T;
-        const float pv = ok ? expf(sc[r] * scale - sMl[qq]) * sLl[qq] : 0.f;
+        const float pv = ok ? exp2_hw(fmaf(sc[r], c2, -lq[r])) : 0.f;
         pr[r] = pv;
-        dsr[r] = pv * (dpc[r] - sDl[qq]) * scale;
+        dsr[r] = pv * (dpc[r] - dq4[r]) * scale;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

@@ -29,10 +29,13 @@
 // Forward (per query block w):  Sᵀ_kb = K_kb Q_wᵀ (A = K κ, B = Q κ; keys on
 //   the accumulator rows, queries on the lanes), scale, causal mask, softmax
 //   over keys (per lane + two shuffles) -> Pᵀ; Oᵀ = Σ_kb Vᵀ_kb Pᵀ_kb (A = V π,
-//   B = Pᵀ as accumulated).  Also lse = max + log Σ per query (for backward).
+//   B = Pᵀ as accumulated).  Also lse2 = max + log2 Σ per query (for backward).
+// Softmax in base 2 (common.h exp2_hw): scores scaled by c2 = scale·log2(e),
+// so each exponential is one v_exp_f32 and the backward's P = exp2(s·c2 −
+// lse2) one fma + one v_exp_f32.
 // Backward, two launches (FlashAttention-2's split, without its dQ atomics):
 //   dq pass, per query block w:  δ = rowsum(dO ⊙ O); per kb <= w: Pᵀ =
-//     exp(Sᵀ·scale − lse), dPᵀ = V dOᵀ, dSᵀ = Pᵀ ⊙ (dPᵀ − δ)·scale, dQᵀ +=
+//     exp2(Sᵀ·c2 − lse2), dPᵀ = V dOᵀ, dSᵀ = Pᵀ ⊙ (dPᵀ − δ)·scale, dQᵀ +=
 //     Kᵀ dSᵀ (A = K π) -> store dQ rows and δ.
 //   dkdv pass, per key block kb: per w >= kb: S = Q_w K_kbᵀ (queries on the
 //     accumulator rows: A = Q κ, B = K κ), dP = dO V_kbᵀ, P and dS from lse /
@@ -189,6 +192,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_e
   for (int w = 0; w < 4; ++w) {
     if (w >= nb) break;
     const int qi = kBlk * w + j;
+    const float c2 = scale * kLog2e;
     f32x4 s[4];
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_e
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = kBlk * kb + 4 * g + r;
-        const float x = (key > qi || key >= T) ? -INFINITY : s[kb][r] * scale;
+        const float x = (key > qi || key >= T) ? -INFINITY : s[kb][r] * c2;
         s[kb][r] = x;
         m = fmaxf(m, x);
       }
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_e
       if (kb > w) break;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float e = expf(s[kb][r] - m);
+        const float e = exp2_hw(s[kb][r] - m);
         s[kb][r] = e;
         sum += e;
       }
@@ -241,7 +245,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) __attribute__((amdgpu_waves_per_e
     }
     if (qi < T) {
       st_out<NCB>(out + (u.row0 + qi) * d + u.h * DH, g, o);
-      if (g == 0 && lse != nullptr) lse[(u.row0 + qi) * H + u.h] = m + logf(sum);
+      if (g == 0 && lse != nullptr) lse[(u.row0 + qi) * H + u.h] = m + log2_hw(sum);
     }
   }
 }
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dq_kernel(
       for (int r = 0; r < 4; ++r) {
         const int key = kBlk * kb + 4 * g + r;
         const bool ok = key <= qi && qok;
-        const float p = ok ? expf(s[r] * scale - l) : 0.f;
+        const float p = ok ? exp2_hw(fmaf(s[r], scale * kLog2e, -l)) : 0.f;
         const float ds = p * (dp[r] - dl) * scale;
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) dq[cb] = mfma16(kp[r][cb], ds, dq[cb]);
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dkdv_kernel(
       for (int r = 0; r < 4; ++r) {
         const int qq = kBlk * w + 4 * g + r;
         const bool ok = key <= qq && qq < T;
-        const float p = ok ? expf(s[r] * scale - l[r]) : 0.f;
+        const float p = ok ? exp2_hw(fmaf(s[r], scale * kLog2e, -l[r])) : 0.f;
         const float ds = p * (dp[r] - dl[r]) * scale;
 #pragma unroll
         for (int cb = 0; cb < NCB; ++cb) {

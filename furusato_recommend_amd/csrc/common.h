@@ -97,6 +97,17 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
+// Softmax exponentials in the base-2 domain (attention.hip, attn_wave.hip):
+// scores are scaled by scale * log2(e) once, so every exponential is ONE
+// v_exp_f32 (libm expf without fast-math is a ~14-instruction range-reduced
+// sequence) and a log-sum-exp is kept as lse2 = max2 + log2(sum), one
+// v_log_f32.  exp2(-inf) = 0 keeps the causal mask; arguments are <= 0 and
+// an underflow to 0 (v_exp_f32 flushes results below 2^-126) is a
+// probability below 1e-38, zero in any f32 sum it enters.
+constexpr float kLog2e = 1.4426950408889634f;
+__device__ __forceinline__ float exp2_hw(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float log2_hw(float x) { return __builtin_amdgcn_logf(x); }
+
 // Kernels with no MFMA of their own that run on the SASRec / GraphSAGE
 // streams next to MFMA kernels are compiled without packed-f32 VALU ops:
 // a v_pk_*_f32 whose op_sel feeds a pair's HIGH dword to the low lane

@@ -17,6 +17,9 @@
 // The gradient is accumulated in batch order on one thread (deterministic);
 // the dense Adam and the gradient clear run on n_threads threads over row
 // blocks.  The Adam arithmetic is the device kernels' (adam1, common.h).
+// mirec_cpu_bpr_step = mirec_cpu_bpr_grad + mirec_cpu_adam; the two halves
+// are exported for the host data-parallel step (dist.HostDataParallel: the
+// gradient is all-reduced between them).
 #include <algorithm>
 #include <cmath>
 #include <thread>
@@ -45,13 +48,12 @@ void parallel_rows(int64_t n, int n_threads, F &&f) {
 
 }  // namespace
 
-extern "C" int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_sq, float *grad,
-                                  int64_t n_rows, int32_t dim, int64_t item_offset,
-                                  const int32_t *users, const int32_t *pos, const int32_t *neg,
-                                  int64_t batch, float decay, const mirec_adam_hparams_t *h,
-                                  float *loss_out, int32_t n_threads) {
-  if (!table || !exp_avg || !exp_avg_sq || !grad || !h || n_rows <= 0 || dim <= 0 ||
-      item_offset < 0 || item_offset > n_rows || batch <= 0 || !users || !pos || !neg)
+extern "C" int mirec_cpu_bpr_grad(const float *table, float *grad, int64_t n_rows, int32_t dim,
+                                  int64_t item_offset, const int32_t *users, const int32_t *pos,
+                                  const int32_t *neg, int64_t batch, float decay,
+                                  float grad_scale, float *loss_out, int32_t n_threads) {
+  if (!table || !grad || n_rows <= 0 || dim <= 0 || item_offset < 0 || item_offset > n_rows ||
+      batch <= 0 || !users || !pos || !neg)
     return MIREC_ERR_ARG;
   const int64_t d = dim;
   for (int64_t b = 0; b < batch; ++b) {
@@ -62,7 +64,7 @@ extern "C" int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_s
   parallel_rows(n_rows * d, n_threads, [&](int64_t a, int64_t b) {
     std::fill(grad + a, grad + b, 0.f);
   });
-  const float inv_b = 1.f / (float)batch;
+  const float inv_b = 1.f / (float)batch * grad_scale;
   const float rc = decay * inv_b;
   double loss = 0.0, reg = 0.0;
   for (int64_t b = 0; b < batch; ++b) {
@@ -91,10 +93,28 @@ extern "C" int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_s
       gn[c] += cs * uc + rc * qc;
     }
   }
-  parallel_rows(n_rows * d, n_threads, [&](int64_t a, int64_t b) {
-    for (int64_t i = a; i < b; ++i) adam_host(table[i], exp_avg[i], exp_avg_sq[i], grad[i], *h);
-  });
   if (loss_out)
     *loss_out = (float)(loss / (double)batch + (double)decay * 0.5 * reg / (double)batch);
   return MIREC_OK;
+}
+
+extern "C" int mirec_cpu_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq,
+                              int64_t n, const mirec_adam_hparams_t *h, int32_t n_threads) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || !h || n < 0) return MIREC_ERR_ARG;
+  parallel_rows(n, n_threads, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) adam_host(param[i], exp_avg[i], exp_avg_sq[i], grad[i], *h);
+  });
+  return MIREC_OK;
+}
+
+extern "C" int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_sq, float *grad,
+                                  int64_t n_rows, int32_t dim, int64_t item_offset,
+                                  const int32_t *users, const int32_t *pos, const int32_t *neg,
+                                  int64_t batch, float decay, const mirec_adam_hparams_t *h,
+                                  float *loss_out, int32_t n_threads) {
+  if (!exp_avg || !exp_avg_sq || !h) return MIREC_ERR_ARG;
+  const int rc = mirec_cpu_bpr_grad(table, grad, n_rows, dim, item_offset, users, pos, neg, batch,
+                                    decay, 1.f, loss_out, n_threads);
+  if (rc != MIREC_OK) return rc;
+  return mirec_cpu_adam(table, grad, exp_avg, exp_avg_sq, n_rows * (int64_t)dim, h, n_threads);
 }

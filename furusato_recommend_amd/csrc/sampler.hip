@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256) void bpr_sample_kernel(
 // (exclusive sum) and only the kept candidates draw their negative.
 struct CandRng {
   XorShift64Star rng;
-  __device__ CandRng(uint64_t seed, uint64_t offset, int32_t shard, int64_t t) {
+  __host__ __device__ CandRng(uint64_t seed, uint64_t offset, int32_t shard, int64_t t) {
     const uint64_t key = splitmix64(seed + 0xD1B54A32D192ED03ull * (uint64_t)shard);
     rng.s = splitmix64(key ^ (offset + (uint64_t)t));
     if (rng.s == 0) rng.s = 0x853C49E6748FEA9Bull;
@@ -169,7 +169,7 @@ struct CandRng {
 };
 
 // candidate t: user u (its shard), positive item p or -1 (no positives)
-__device__ __forceinline__ void draw_candidate(CandRng &c, const int64_t *__restrict__ rowptr,
+__host__ __device__ __forceinline__ void draw_candidate(CandRng &c, const int64_t *__restrict__ rowptr,
                                                const int32_t *__restrict__ col,
                                                const float *__restrict__ pos_cdf, int64_t n_users,
                                                int32_t shard, int32_t n_shards, int64_t &u,
@@ -220,6 +220,30 @@ __global__ __launch_bounds__(256) void cand_keep_kernel(const int32_t *__restric
   flag[vals[i]] = (keys[i] < m_items && i - run[i] < cap) ? 1 : 0;
 }
 
+// A kept candidate t redraws its stream (same u, p), then draws its negative,
+// and writes the triple at output position o; false if the negative draw
+// exhausted its retry budget.
+__host__ __device__ __forceinline__ bool emit_candidate(
+    const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
+    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    int64_t m_items, int64_t t, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
+    int64_t o, int32_t *users, int32_t *pos, int32_t *neg) {
+  CandRng c(seed, offset, shard, t);  // the same stream: same u, p, then n
+  int64_t u, p, beg, deg;
+  draw_candidate(c, rowptr, col, pos_cdf, n_users, shard, n_shards, u, p, beg, deg);
+  int64_t ng = 0;
+  bool ok = false;
+  const int64_t base = rowptr[0];
+  for (int k = 0; k < kMaxNegTries && !ok; ++k) {
+    ng = c.rng.below(m_items);
+    ok = !row_has(col, sorted, base, beg, deg, (int32_t)(n_users + ng));
+  }
+  users[o] = (int32_t)u;
+  pos[o] = (int32_t)p;
+  neg[o] = (int32_t)ng;
+  return ok;
+}
+
 __global__ __launch_bounds__(256) void cand_emit_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
     const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
@@ -231,21 +255,9 @@ __global__ __launch_bounds__(256) void cand_emit_kernel(
   if (t >= n) return;
   if (t == n - 1) count[0] = at[t] + flag[t];
   if (!flag[t]) return;
-  CandRng c(seed, offset, shard, t);  // the same stream: same u, p, then n
-  int64_t u, p, beg, deg;
-  draw_candidate(c, rowptr, col, pos_cdf, n_users, shard, n_shards, u, p, beg, deg);
-  int64_t ng = 0;
-  bool ok = false;
-  const int64_t base = rowptr[0];
-  for (int k = 0; k < kMaxNegTries && !ok; ++k) {
-    ng = c.rng.below(m_items);
-    ok = !row_has(col, sorted, base, beg, deg, (int32_t)(n_users + ng));
-  }
-  if (!ok) err[0] = 1;
-  const int32_t o = at[t];
-  users[o] = (int32_t)u;
-  pos[o] = (int32_t)p;
-  neg[o] = (int32_t)ng;
+  if (!emit_candidate(rowptr, col, sorted, pos_cdf, n_users, m_items, t, seed, offset, shard,
+                      n_shards, at[t], users, pos, neg))
+    err[0] = 1;
 }
 
 struct MaxOp {
@@ -426,6 +438,68 @@ extern "C" int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col,
   for (int w = 1; w < nt; ++w) th.emplace_back(work, w);
   work(0);
   for (auto &x : th) x.join();
+  for (int w = 0; w < nt; ++w)
+    if (bad[w]) err[0] = 1;
+  return MIREC_OK;
+}
+
+// The capped epoch sampler on the host (a CPU model under train_dp /
+// Trainer(sampler="ddp_capped")): the device sampler's candidate streams, so
+// the kept triples equal mirec_bpr_sample_capped_ex's bit for bit.  The
+// candidates are drawn on n_threads threads, the keep decision is the
+// reference's own sequential count per item (ddp_lgcn.py:571-572), and the
+// kept candidates draw their negatives on the threads again.
+extern "C" int mirec_cpu_bpr_sample_capped(const int64_t *rowptr, const int32_t *col,
+                                           const int32_t *col_sorted, const float *pos_cdf,
+                                           int64_t n_users, int64_t m_items,
+                                           int64_t n_candidates, int32_t cap, uint64_t seed,
+                                           uint64_t offset, int32_t shard, int32_t n_shards,
+                                           int32_t *users, int32_t *pos, int32_t *neg,
+                                           int32_t *count, int32_t *err, int32_t *cand_u,
+                                           int32_t *cand_p, int32_t n_threads) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(rowptr && col && users && pos && neg && count && err);
+  MIREC_CHECK_ARG(n_users > 0 && m_items > 0 && cap >= 0 && n_candidates >= 0);
+  MIREC_CHECK_ARG(n_candidates < ((int64_t)1 << 31));
+  MIREC_CHECK_ARG(n_shards >= 1 && shard >= 0 && shard < n_shards && shard < n_users);
+  const int64_t n = n_candidates;
+  const int nt = (int)std::max<int64_t>(
+      1, std::min<int64_t>(std::min<int64_t>(n_threads > 0 ? n_threads : 1, 64), (n + 4095) / 4096));
+  auto parallel = [&](auto &&f) {
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w) th.emplace_back([&, w] { f(n * w / nt, n * (w + 1) / nt, w); });
+    f(0, n / nt, 0);
+    for (auto &x : th) x.join();
+  };
+  std::vector<int32_t> item(n);
+  parallel([&](int64_t a, int64_t b, int) {
+    for (int64_t t = a; t < b; ++t) {
+      CandRng c(seed, offset, shard, t);
+      int64_t u, p, beg, deg;
+      draw_candidate(c, rowptr, col, pos_cdf, n_users, shard, n_shards, u, p, beg, deg);
+      item[t] = (int32_t)p;
+      if (cand_u) cand_u[t] = (int32_t)u;
+      if (cand_p) cand_p[t] = (int32_t)p;
+    }
+  });
+  // kept iff fewer than cap earlier candidates with the same item were kept;
+  // at[t] = the output position of a kept candidate, -1 otherwise
+  std::vector<int32_t> seen(m_items, 0);
+  std::vector<int64_t> at(n);
+  int64_t k = 0;
+  for (int64_t t = 0; t < n; ++t) {
+    const int32_t p = item[t];
+    at[t] = (p >= 0 && seen[p] < cap) ? k++ : -1;
+    if (p >= 0 && seen[p] < cap) ++seen[p];
+  }
+  std::vector<int> bad(nt, 0);
+  parallel([&](int64_t a, int64_t b, int w) {
+    for (int64_t t = a; t < b; ++t)
+      if (at[t] >= 0 && !emit_candidate(rowptr, col, col_sorted, pos_cdf, n_users, m_items, t,
+                                        seed, offset, shard, n_shards, at[t], users, pos, neg))
+        bad[w] = 1;
+  });
+  count[0] = (int32_t)k;
   for (int w = 0; w < nt; ++w)
     if (bad[w]) err[0] = 1;
   return MIREC_OK;

@@ -410,6 +410,44 @@ class DataParallel:
         return self.calibration
 
 
+class HostDataParallel:
+    """Data parallelism for a model trained on the host (MF with
+    device="cpu", configuration C1, under train_dp --device cpu; the
+    reference's DDP over gloo).  The model exposes the two halves of its
+    fused host step: ``host_grad(u, p, n, grad_scale)`` (the dense gradient
+    into ``host_grad_buffer``) and ``host_adam()``.  Every rank computes its
+    own batch's gradient scaled by 1/world_size, the gradients are SUM
+    all-reduced, and every rank applies the same Adam step: the union
+    batch's update, replicas bit-identical.  The initial table is broadcast
+    from rank 0."""
+
+    accumulates_loss = True  # step() adds the loss into the caller's accumulator
+
+    def __init__(self, model, group=None):
+        self.model = model
+        self.group = group
+        self.distributed = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.distributed else 1
+        self.rank = dist.get_rank(group) if self.distributed else 0
+        self.comm_events = None
+        if self.world > 1:
+            for p in model.parameters():
+                dist.broadcast(p.data, src=0, group=group)
+
+    def step(self, users, pos, neg, decay: float | None = None, loss_accum=None):
+        m = self.model
+        loss = m.host_grad(users, pos, neg, grad_scale=1.0 / self.world)
+        if self.distributed and self.world > 1:
+            dist.all_reduce(m.host_grad_buffer, op=dist.ReduceOp.SUM, group=self.group)
+        m.host_adam()
+        if loss_accum is not None:
+            loss_accum += loss
+        return loss
+
+    def gather_optimizer_state(self):
+        """Nothing is sharded: every rank holds the whole state."""
+
+
 def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, group=None):
     """all_to_all_single; CUDA tensors under gloo (CPU tests, one-GPU
     rehearsals) travel through host copies."""

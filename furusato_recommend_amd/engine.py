@@ -34,6 +34,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -740,13 +741,16 @@ def sample_triples(graph: Graph, batch: int, seed: int, offset: int, users, pos,
 
 
 def sample_epoch_capped(graph: Graph, n_candidates: int, cap: int, seed: int, offset: int = 0,
-                        shard: int = 0, n_shards: int = 1, return_candidates: bool = False):
+                        shard: int = 0, n_shards: int = 1, return_candidates: bool = False,
+                        n_threads: int | None = None):
     """The ddp_lgcn.py epoch sampler on device (ddp_lgcn.py:33-35, 541-582):
     ``n_candidates`` (= TRAIN_ITERATIVE x trainDataSize) uniform users, a
     positive each, kept while the positive item was kept fewer than ``cap``
     (POSITIVE_NUM_LIMIT) times before in draw order.  Returns int32 device
     (users, pos, neg) of the kept triples in draw order (+ every candidate's
-    user and positive, -1 = skipped user, with ``return_candidates``)."""
+    user and positive, -1 = skipped user, with ``return_candidates``).  A
+    graph on the host (a CPU model) runs mirec_cpu_bpr_sample_capped: the same
+    streams, the same triples, on ``n_threads`` threads."""
     dev = graph.device
     n = int(n_candidates)
     i32 = dict(dtype=torch.int32, device=dev)
@@ -755,6 +759,19 @@ def sample_epoch_capped(graph: Graph, n_candidates: int, cap: int, seed: int, of
     err = torch.zeros(1, **i32)
     cu = torch.empty(max(n, 1), **i32) if return_candidates else None
     cp = torch.empty(max(n, 1), **i32) if return_candidates else None
+    if dev.type == "cpu":  # a host model (C1): the same streams on CPU threads
+        check(lib.mirec_cpu_bpr_sample_capped(
+            graph.rowptr_host.ctypes.data, graph.col_host.ctypes.data, ptr(graph.col_sorted),
+            ptr(getattr(graph, "pos_cdf", None)), graph.n_users, graph.m_items, n, int(cap),
+            ctypes.c_uint64(seed & (2**64 - 1)), ctypes.c_uint64(offset & (2**64 - 1)),
+            int(shard), int(n_shards), users.data_ptr(), pos.data_ptr(), neg.data_ptr(),
+            count.data_ptr(), err.data_ptr(), ptr(cu), ptr(cp),
+            int(n_threads or os.cpu_count() or 1)), "cpu_bpr_sample_capped")
+        k = int(count.item())
+        if int(err.item()) != 0:
+            raise RuntimeError("sampler: a user has every item as a positive")
+        out = (users[:k], pos[:k], neg[:k])
+        return out + (cu[:n], cp[:n]) if return_candidates else out
     nb = ctypes.c_size_t(0)
     check(lib.mirec_bpr_sample_capped_workspace(n, graph.m_items, ctypes.byref(nb)),
           "bpr_sample_capped_workspace")

@@ -157,6 +157,32 @@ class MF(nn.Module):
             loss_accum += loss
         return loss
 
+    def host_grad(self, u, p, n, grad_scale: float = 1.0):
+        """The gradient half of the host step (mirec_cpu_bpr_grad): dLoss/dtable
+        of one batch x ``grad_scale`` into ``self.host_grad_buffer``; returns
+        the (unscaled) loss.  With host_adam: dist.HostDataParallel's step."""
+        u, p, n = self._as_i32(u), self._as_i32(p), self._as_i32(n)
+        out = ctypes.c_float(0.0)
+        check(lib.mirec_cpu_bpr_grad(self._table.data_ptr(), self._grad_ws.data_ptr(),
+                                     self._table.shape[0], self.latent_dim, self.num_users,
+                                     u.data_ptr(), p.data_ptr(), n.data_ptr(), u.numel(),
+                                     float(self.config["decay"]), float(grad_scale),
+                                     ctypes.byref(out), self.n_threads), "cpu_bpr_grad")
+        return torch.tensor(out.value, dtype=torch.float32)
+
+    @property
+    def host_grad_buffer(self) -> torch.Tensor:
+        return self._grad_ws
+
+    def host_adam(self):
+        """Adam over the whole table from ``host_grad_buffer`` (mirec_cpu_adam)."""
+        hp = self.optim.next_hparams()
+        st = self.optim
+        check(lib.mirec_cpu_adam(self._table.data_ptr(), self._grad_ws.data_ptr(),
+                                 st.exp_avg.data_ptr(), st.exp_avg_sq.data_ptr(),
+                                 self._table.numel(), ctypes.byref(hp), self.n_threads),
+              "cpu_adam")
+
     @torch.no_grad()
     def OneEpoch(self, user, pos, neg):
         B = int(self.config["bpr_batch_size"])

@@ -97,10 +97,16 @@ def wrap(model, group=None, mode: str | None = None, **kw):
     fused engine (LightGCN; ``mode`` = its gradient exchange) or
     ``DenseGradDataParallel`` for the autograd models (``mode`` = the id
     table's exchange)."""
-    from .dist import DataParallel, DenseGradDataParallel
+    from .dist import DataParallel, DenseGradDataParallel, HostDataParallel
     if hasattr(model, "engine") and hasattr(model, "all_embedding"):
         return DataParallel(model.engine, model.all_embedding.weight.data, model.optim,
                             group=group, mode=mode or "auto", **kw)
+    if hasattr(model, "host_grad") and getattr(model, "on_host", False):
+        return HostDataParallel(model, group=group)  # MF on the host (C1)
+    if hasattr(model, "engine") and hasattr(model, "_table"):
+        # MF on the GPU: the fused engine with no propagation layers
+        return DataParallel(model.engine, model._table, model.optim, group=group,
+                            mode=mode or "sparse", **kw)
     return DenseGradDataParallel(model, group=group, table_exchange=mode, **kw)
 
 
@@ -176,9 +182,10 @@ class DPTrainer:
 
     # ------------------------------------------------------------- training
     def _accumulates(self) -> bool:
-        """DataParallel (the fused engine) sums the loss on the device; the
-        autograd wrappers return each step's loss."""
-        return hasattr(self.dp, "engine")
+        """DataParallel (the fused engine) sums the loss on the device and
+        HostDataParallel on the host; the autograd wrappers return each
+        step's loss."""
+        return bool(getattr(self.dp, "accumulates_loss", hasattr(self.dp, "engine")))
 
     def _step(self, u, p, n, acc):
         if self._accumulates():

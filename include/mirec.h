@@ -728,8 +728,9 @@ int mirec_attention_ordered_bwd(const float *qkv, const float *dout, const int32
  * every operand loaded straight into its MFMA lane layout; head_dim 16, 32
  * or 64 (mirec_attention_wave_supported).  offsets == NULL: uniform batch
  * [batch, T, ...] (1 <= T <= 64); else packed as in the varlen form.  The
- * forward also writes lse [n_rows, heads] (log-sum-exp of each query's scaled
- * scores); the backward takes out and lse from it and writes dqkv and delta
+ * forward also writes lse [n_rows, heads] (BASE-2 log-sum-exp of each query's
+ * scaled scores: log2 sum_k 2^(s_k * scale * log2 e), i.e. the natural lse times
+ * log2 e); the backward takes out and lse from it and writes dqkv and delta
  * [n_rows, heads] (rowsum(dout ⊙ out), scratch), in two launches.  order
  * (optional, packed form): the sequences in the order their units run, from
  * mirec_attention_length_order (longest first, device int32 [batch]; the
@@ -1011,6 +1012,19 @@ int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col, const int32_
                          int32_t *users, int32_t *pos, int32_t *neg, int32_t *err,
                          int32_t n_threads);
 
+/* mirec_bpr_sample_capped_ex on the host (the ddp_lgcn.py epoch sampler for
+ * a CPU model): the same candidate streams, so users / pos / neg (capacity
+ * n_candidates), *count and the optional cand_u / cand_p equal the device
+ * sampler's bit for bit; the keep decision is the reference's sequential
+ * per-item count (ddp_lgcn.py:571-572).  *err = 1 if a negative draw
+ * exhausted its retries.  No workspace. */
+int mirec_cpu_bpr_sample_capped(const int64_t *rowptr, const int32_t *col,
+                                const int32_t *col_sorted, const float *pos_cdf, int64_t n_users,
+                                int64_t m_items, int64_t n_candidates, int32_t cap, uint64_t seed,
+                                uint64_t offset, int32_t shard, int32_t n_shards, int32_t *users,
+                                int32_t *pos, int32_t *neg, int32_t *count, int32_t *err,
+                                int32_t *cand_u, int32_t *cand_p, int32_t n_threads);
+
 /* One MF stageOne (model/MF.py:62-94: BPR loss + decay x reg, backward,
  * torch.optim.Adam over the whole table) on a [n_rows, dim] host table whose
  * item rows start at item_offset (= n_users): grad is a [n_rows, dim]
@@ -1020,6 +1034,17 @@ int mirec_cpu_bpr_step(float *table, float *exp_avg, float *exp_avg_sq, float *g
                        int64_t n_rows, int32_t dim, int64_t item_offset, const int32_t *users,
                        const int32_t *pos, const int32_t *neg, int64_t batch, float decay,
                        const mirec_adam_hparams_t *h, float *loss_out, int32_t n_threads);
+
+/* The two halves of mirec_cpu_bpr_step (bitwise the same arithmetic): the
+ * dense gradient of one batch's loss + decay reg, multiplied by grad_scale
+ * (1 / world_size under data parallelism; 1 = the step's), into grad
+ * (*loss_out unscaled); then torch.optim.Adam over n elements. */
+int mirec_cpu_bpr_grad(const float *table, float *grad, int64_t n_rows, int32_t dim,
+                       int64_t item_offset, const int32_t *users, const int32_t *pos,
+                       const int32_t *neg, int64_t batch, float decay, float grad_scale,
+                       float *loss_out, int32_t n_threads);
+int mirec_cpu_adam(float *param, const float *grad, float *exp_avg, float *exp_avg_sq, int64_t n,
+                   const mirec_adam_hparams_t *h, int32_t n_threads);
 
 #ifdef __cplusplus
 }

@@ -3570,6 +3570,29 @@ def test_host_sampler_equals_device_sampler(golden):
                 assert torch.equal(a.cpu(), b), (weighted, shard)
 
 
+def test_host_capped_sampler_equals_device_sampler():
+    """mirec_cpu_bpr_sample_capped (a CPU model's epoch sampler) draws the
+    device capped sampler's kept triples, count and candidates bit for bit:
+    uniform and weighted positives, sharded."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.engine import sample_epoch_capped
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(5000, 300, 200_000, seed=6, kind="zipf", test_frac=0)
+    gd = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cuda:0")
+    gh = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cpu")
+    rng = np.random.default_rng(1)
+    probs = [rng.random(int(d)) + 0.01 for d in np.diff(gh.rowptr_host[: ds.n_users + 1])]
+    for weighted in (False, True):
+        for g in (gd, gh):
+            g.set_positive_probs(probs if weighted else None)
+        for shard, n_shards in ((0, 1), (2, 3)):
+            kw = dict(seed=5, offset=123, shard=shard, n_shards=n_shards, return_candidates=True)
+            dev = sample_epoch_capped(gd, 150_000, 200, **kw)
+            host = sample_epoch_capped(gh, 150_000, 200, n_threads=8, **kw)
+            for a, b in zip(dev, host):
+                assert torch.equal(a.cpu(), b), (weighted, shard)
+
+
 def test_sampler_binary_search_equals_scan():
     """With the sorted user rows (csr.col_sorted) the negative rejection is a
     binary search; the triples equal the row-scan ones draw for draw."""

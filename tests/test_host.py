@@ -143,7 +143,7 @@ class OracleEngine:
         self._d = out.grad * grad_scale / (o.L + 1)
         self._e = e.grad * grad_scale
         self._N = N
-        return loss.detach()
+        return (loss + decay * reg).detach()  # what the HIP bpr reports (stageOne's loss)
 
     def export_seeds(self):
         rows = torch.nonzero((self._d != 0).any(1) | (self._e != 0).any(1)).flatten()
@@ -757,6 +757,118 @@ def test_bench_oracle_parity_leg():
     assert not r["ok"] and r["rel_emb_step"] > 1e-4 and r["rel_out"] == 0.0
 
 
+class _StepView(_OptimView):
+    """_OptimView with the AdamState fields the parity leg snapshots."""
+
+    def __init__(self, o, lr):
+        super().__init__(o)
+        self.lr, self.betas, self.eps = lr, (0.9, 0.999), 1e-8
+
+    @property
+    def n_steps(self):
+        return int(self.o.optim.state[self.o.emb]["step"])
+
+
+def _bench_dp_legs_worker(rank, world, port, fpath, q, mode, tamper):
+    """One rank of bench.py's N > 1 legs over gloo with the oracle engine:
+    two ordinary data-parallel steps, the parity leg (dp_union_parity, rank 0
+    replaying the union batch on a fresh oracle), then the quality loop
+    (train_then_evaluate: every rank steps, rank 0 evaluates)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from furusato_recommend_amd.dist import DataParallel
+    f = dict(np.load(fpath))
+    nu, mi, lr, decay = int(f["n_users"]), int(f["m_items"]), float(f["lr"]), float(f["decay"])
+    o = O.OracleLightGCN(f["train_user"], f["train_item"], nu, mi, 64, 3, lr, decay,
+                         emb=torch.from_numpy(f["emb0"]))
+    t = f["triples"]
+    per = len(t) // world
+    dp = DataParallel(OracleEngine(o, per), o.emb.data, None, mode=mode, chunks=2)
+    view = _StepView(o, lr)
+    dp.adam = view
+
+    def batch(i):
+        b = np.roll(t, 7 * i, axis=0)[rank * per:(rank + 1) * per]
+        return b[:, 0], b[:, 1], b[:, 2]
+    for i in range(2):
+        dp.step(*batch(i), decay)
+    if tamper == "replica" and rank == 1:
+        with torch.no_grad():
+            o.emb[3, 5] += 1e-3  # this replica drifts: the digests must disagree
+
+    def replay(snap, U, P, N):
+        r = O.OracleLightGCN(f["train_user"], f["train_item"], nu, mi, 64, 3, lr, decay,
+                             emb=snap["emb0"])
+        r.optim.state[r.emb] = {"step": torch.tensor(float(snap["n_steps"])),
+                                "exp_avg": snap["exp_avg"].clone(),
+                                "exp_avg_sq": snap["exp_avg_sq"].clone()}
+        loss = r.stageOne(U.numpy(), P.numpy(), N.numpy())
+        e = r.emb.detach()
+        if tamper == "replay":
+            e = e + 1e-3 * e.abs().max()
+        return e, loss
+    par = bench.dp_union_parity(dp, o.emb.data, view, *batch(2), decay, replay)
+    seen = []
+
+    def step(i):
+        seen.append(i)
+        dp.step(*batch(3 + i), decay)
+    ev, _ = bench.train_then_evaluate(step, 3, lambda: {"emb": o.emb.detach().numpy().copy()},
+                                      rank, world)
+    q.put((rank, par, ev, seen, o.emb.detach().numpy().copy()))
+    dist.destroy_process_group()
+
+
+def _run_dp_legs(mode, tamper=None, world=2):
+    from tests.conftest import GOLDEN
+    fpath = os.path.join(GOLDEN, "lgcn_d64_L3.npz")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_dp_legs_worker,
+                         args=(r, world, port, fpath, q, mode, tamper)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: rest for r, *rest in (q.get(timeout=240) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+@pytest.mark.parametrize("mode", ["sparse", "sharded"])
+def test_bench_dp_parity_and_quality_legs_gloo(mode):
+    """bench.py at N > 1 proves itself: after ordinary
+    data-parallel steps, one more step leaves bitwise-equal replicas (table
+    and gathered Adam moments, compared by all-gathered digests) and rank 0's
+    replay of ONE single-process step on the union batch from the snapshot
+    matches the data-parallel table at 1e-4; the quality loop steps every rank
+    and evaluates on rank 0 only."""
+    res = _run_dp_legs(mode)
+    par0, ev0, seen0, emb0 = res[0]
+    par1, ev1, seen1, emb1 = res[1]
+    assert par0["ok"], par0
+    assert par0["replicas_bitwise_equal"] and par0["moments_bitwise_equal"]
+    assert par0["rel_emb_step"] < 2e-5 and par0["rel_loss"] < 1e-5
+    assert par0["union_batch"] == 64 and par0["mode"] == mode
+    assert par1["table_digest"] == par0["table_digest"] and "ok" not in par1
+    assert seen0 == seen1 == [0, 1, 2]
+    assert ev1 is None and np.array_equal(ev0["emb"], emb0)
+    assert np.array_equal(emb0, emb1)
+
+
+@pytest.mark.parametrize("tamper", ["replica", "replay"])
+def test_bench_dp_parity_leg_detects_divergence(tamper):
+    """A drifted replica fails the bitwise digest check; a union replay that
+    disagrees fails the 1e-4 bar."""
+    par0 = _run_dp_legs("sparse", tamper)[0][0]
+    assert not par0["ok"]
+    if tamper == "replica":
+        assert not par0["replicas_bitwise_equal"]
+    else:
+        assert par0["replicas_bitwise_equal"] and par0["rel_emb_step"] > 1e-4
+
+
 def test_host_threads_bounded():
     import bench
     n = bench.host_threads()
@@ -1015,3 +1127,98 @@ def test_mf_cpu_c1_epochs_and_evaluation_vs_oracle():
     ref = O.evaluate(o.user.detach(), o.item.detach(), ds.testDict, allpos, topks=(10, 20))
     for k in ("recall", "precision", "ndcg"):
         assert np.allclose(res[k], ref[k], atol=2e-4), (k, res[k], ref[k])
+
+
+def test_host_capped_sampler_matches_sequential_rule():
+    """mirec_cpu_bpr_sample_capped (the ddp_lgcn.py epoch sampler for a CPU
+    model) == the reference's loop (ddp_lgcn.py:541-582) on the
+    same candidate stream: users without positives skipped, a candidate kept
+    iff its positive was kept < cap times before it, kept triples in draw
+    order, negatives never positives; sharded streams stay in the shard."""
+    from furusato_recommend_amd import SyntheticBipartite
+    from furusato_recommend_amd.engine import sample_epoch_capped
+    from furusato_recommend_amd.graph import Graph
+    ds = SyntheticBipartite(3000, 400, 30_000, seed=4, kind="zipf", test_frac=0)
+    g = Graph.from_interactions(ds.trainUser, ds.trainItem, ds.n_users, ds.m_items, "cpu")
+    cap = 40
+    for shard, n_shards in ((0, 1), (1, 3)):
+        u, p, n, cu, cp = sample_epoch_capped(g, 3 * 30_000, cap, seed=9, shard=shard,
+                                              n_shards=n_shards, return_candidates=True,
+                                              n_threads=4)
+        assert u.device.type == "cpu"
+        cu, cp = cu.numpy(), cp.numpy()
+        cnt, kept = {}, []
+        for t in range(len(cp)):
+            if cp[t] < 0 or cnt.get(int(cp[t]), 0) >= cap:
+                continue
+            cnt[int(cp[t])] = cnt.get(int(cp[t]), 0) + 1
+            kept.append(t)
+        kept = np.array(kept)
+        assert len(kept) == u.numel() and len(kept) < len(cp)  # the cap bit
+        assert np.array_equal(u.numpy(), cu[kept]) and np.array_equal(p.numpy(), cp[kept])
+        assert (u.numpy() % n_shards == shard).all()
+        rp, col = g.rowptr_host, g.col_host
+        uu, pp, nn = u.numpy(), p.numpy(), n.numpy()
+        for k in range(0, len(uu), 97):
+            row = col[rp[uu[k]]:rp[uu[k] + 1]] - g.n_users
+            assert pp[k] in row and nn[k] not in row
+        # thread count does not change the draw
+        u1, p1, n1 = sample_epoch_capped(g, 3 * 30_000, cap, seed=9, shard=shard,
+                                         n_shards=n_shards, n_threads=1)
+        assert torch.equal(u1, u) and torch.equal(p1, p) and torch.equal(n1, n)
+
+
+def test_mf_host_grad_adam_equals_fused_host_step(golden):
+    """mirec_cpu_bpr_grad + mirec_cpu_adam (HostDataParallel's halves) are
+    bitwise mirec_cpu_bpr_step; grad_scale multiplies the gradient only."""
+    from furusato_recommend_amd import MF
+    f = golden("mf_d32.npz")
+    cfg = {"latent_dim_rec": 32, "lr": float(f["lr"]), "decay": float(f["decay"]),
+           "device": "cpu", "bpr_batch_size": 64}
+    ds = _DS(f["train_user"], f["train_item"], f["n_users"], f["m_items"])
+    a, b = MF(cfg, ds), MF(cfg, ds)
+    t = torch.from_numpy(f["triples"])
+    for m in (a, b):
+        m.load_table(torch.from_numpy(f["user_w0"]), torch.from_numpy(f["item_w0"]))
+    for _ in range(3):
+        la = a.stageOne(t[:, 0], t[:, 1], t[:, 2])
+        lb = b.host_grad(t[:, 0], t[:, 1], t[:, 2])
+        b.host_adam()
+        assert float(la) == float(lb)
+        assert torch.equal(a._table, b._table)
+        assert torch.equal(a.optim.exp_avg_sq, b.optim.exp_avg_sq)
+    g1 = b.host_grad(t[:, 0], t[:, 1], t[:, 2]).clone()
+    full = b.host_grad_buffer.clone()
+    b.host_grad(t[:, 0], t[:, 1], t[:, 2], grad_scale=0.5)
+    assert torch.allclose(b.host_grad_buffer, 0.5 * full, rtol=1e-6, atol=0)
+    assert float(g1) == float(b.host_grad(t[:, 0], t[:, 1], t[:, 2]))
+
+
+def test_train_dp_cli_mf_cpu_registry_two_ranks(golden, tmp_path):
+    """``train_dp --model mf --device cpu --gpus 2`` through the model
+    registry (no --factory): the host capped sampler, the host
+    data-parallel step (gradients all-reduced over gloo), rank-0 evaluation
+    and the checkpoint — no HIP call anywhere."""
+    import json
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    _write_split(golden, tmp_path / "data")
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["PYTHONPATH"] = ROOT
+    env["HIP_VISIBLE_DEVICES"] = ""  # a host without a GPU
+    ck = tmp_path / "ck"
+    cmd = [sys.executable, "-m", "furusato_recommend_amd.train_dp", "--model", "mf",
+           "--gpus", "2", "--device", "cpu", "--data", str(tmp_path / "data"),
+           "--recdim", "16", "--bpr_batch", "16", "--test_span", "1", "--epochs", "2",
+           "--path", str(ck)]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert [x["epoch"] for x in recs] == [0, 1] and recs[0]["world"] == 2
+    assert recs[0]["triples_per_rank"] > 0 and all(np.isfinite(x["loss"]) for x in recs)
+    assert recs[1]["loss"] < recs[0]["loss"] + 1e-3
+    for k in ("recall", "ndcg"):
+        assert all(np.isfinite(recs[1]["metrics"][k]))
+    assert (ck / "ddp_mf_all.pth").exists()

@@ -19,6 +19,8 @@
 #   c3 / c4    GraphSAGE C3 / SASRec C4 lines with CPU baselines -> bench_c3.log, bench_c4.log
 #   c3prof / c4prof   kernel stats of the C3 step / the captured C4 step
 #   zipf       the C2 Zipf-popularity graph: line + kernel stats
+#   rehearse2 / rehearse8   bench.py --gpus N --rehearse (N ranks on one GPU,
+#              gloo): the DP parity and Recall@20 legs   -> bench_c2_rehearse_dpN.log
 #   c5         LightGCN-3 d=256 10 M x 1 M / 200 M on one GPU   -> bench_c5.log
 #   pmc_tg     FETCH / WRITE of the C3 table-gradient sum vs its algorithmic
 #              bytes (tools/tg_sum_bytes.py)                     -> pmc_tg_sum.json
@@ -91,6 +93,13 @@ for leg in $LEGS; do
       lines $E/bench_c2_zipf.log
       run 300 $E/zipf.log rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0
       find $E/zipf -name "*kernel_trace.csv" -delete ;;
+    rehearse2|rehearse8)
+      # the N-rank bench on one GPU (gloo): parity leg (bitwise replicas +
+      # union-batch replay on rank 0) and the DataParallel Recall@20 leg
+      N=${leg#rehearse}
+      Q=$([ "$N" = 8 ] && echo 1000 || echo 3000)
+      run 700 $E/bench_c2_rehearse_dp$N.log python bench.py --gpus $N --rehearse --steps 5 --warmup 2 --quality-steps $Q
+      lines $E/bench_c2_rehearse_dp$N.log 600 ;;
     c5)
       run 900 $E/bench_c5.log python bench.py --users 10000000 --items 1000000 --edges 200000000 --dim 256 --steps 5 --warmup 2 --cpu-baseline off --quality-steps 0 --parity 0
       lines $E/bench_c5.log ;;
