@@ -44,7 +44,6 @@ import json
 import math
 import os
 import platform
-import socket
 import subprocess
 import sys
 import time
@@ -112,20 +111,14 @@ def parse(argv=None):
 
 # ---------------------------------------------------------------- launcher
 
-def free_port() -> int:
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def launch_command(n: int, argv: list[str], port: int) -> list[str]:
+def launch_command(n: int, argv: list[str]) -> list[str]:
     """The child command that starts n ranks of this script (one process
-    per GPU) with the same arguments."""
+    per GPU) with the same arguments.  The rendezvous store binds its own
+    port (c10d endpoint 127.0.0.1:0): no port is picked here and handed
+    over, so no other process can take it in between."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-            f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
-            "--master-port", str(port), os.path.abspath(__file__), *argv]
+            f"--nproc-per-node={n}", "--rdzv-backend=c10d", "--rdzv-endpoint=127.0.0.1:0",
+            "--local-addr=127.0.0.1", os.path.abspath(__file__), *argv]
 
 
 def needs_launch(args, env=os.environ) -> bool:
@@ -138,7 +131,7 @@ def launch(args, argv: list[str], runner=subprocess.run) -> int:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", str(max(1, host_threads() // args.gpus)))
-    r = runner(launch_command(args.gpus, argv, free_port()), env=env)
+    r = runner(launch_command(args.gpus, argv), env=env)
     return int(r.returncode)
 
 

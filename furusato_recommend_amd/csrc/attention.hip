@@ -219,7 +219,10 @@ __global__ __launch_bounds__(64 * NB) void attn_fwd_kernel(const float *__restri
   using S = AttnShape<DPAD, NB>;
   __shared__ __attribute__((aligned(16))) float sK[S::TR * S::LDK];
   __shared__ __attribute__((aligned(16))) float sV[S::TR * S::LDK];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index, wave-uniform in an SGPR (the compiler cannot prove
+  // threadIdx.x >> 6 uniform): every block loop and bound derived from it
+  // becomes a scalar branch instead of an exec-masked one
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const int64_t b = order ? (int64_t)order[seq0 + blockIdx.x / H] : seq0 + blockIdx.x / H;
   const int h = blockIdx.x % H;
@@ -273,7 +276,10 @@ __global__ __launch_bounds__(64 * NB) __attribute__((amdgpu_waves_per_eu(4))) vo
   float *sK = smem, *sV = smem + S::TR * S::LDK;   // phase A
   float *sQ = smem, *sDO = smem + S::TR * S::LDK;  // phase B (same region)
   float *sM = smem + S::bwd_region, *sD = sM + S::TR;  // per query: lse2, δ
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index, wave-uniform in an SGPR (the compiler cannot prove
+  // threadIdx.x >> 6 uniform): every block loop and bound derived from it
+  // becomes a scalar branch instead of an exec-masked one
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const int64_t b = order ? (int64_t)order[seq0 + blockIdx.x / H] : seq0 + blockIdx.x / H;
   const int h = blockIdx.x % H;
@@ -538,13 +544,21 @@ __device__ __forceinline__ void seq_of(const PackSeqs &ps, int w, int &T, int &l
     }
 }
 
-// K / V rows of every block of the pack into LDS (rows past a sequence's
-// length and dims past dh zero), all loads issued before the first store.
-template <int DPAD, int LD>
-__device__ __forceinline__ void load_pack(float *d0, float *d1, const float *qkv, int64_t rs,
-                                          int coff, const PackSeqs &ps, int dh) {
-  constexpr int C4 = DPAD / 4, TR = 4 * kB, PER = TR * C4 / 256;
+// K / V rows of every block of the pack (rows past a sequence's length and
+// dims past dh zero): load_pack_regs issues the loads into registers,
+// store_pack puts them into LDS — the caller issues its own row loads in
+// between, so all of a workgroup's global loads share one round trip.
+template <int DPAD>
+struct PackRegs {
+  static constexpr int PER = 4 * kB * (DPAD / 4) / 256;
   float4 v0[PER], v1[PER];
+};
+
+template <int DPAD>
+__device__ __forceinline__ void load_pack_regs(PackRegs<DPAD> &pr, const float *qkv, int64_t rs,
+                                               int coff, const PackSeqs &ps, int dh) {
+  constexpr int C4 = DPAD / 4, PER = PackRegs<DPAD>::PER;
+  float4 *v0 = pr.v0, *v1 = pr.v1;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4, w = R / kB;
@@ -562,11 +576,16 @@ __device__ __forceinline__ void load_pack(float *d0, float *d1, const float *qkv
     v0[q] = dim_ok ? x0 : f4_zero();
     v1[q] = dim_ok ? x1 : f4_zero();
   }
+}
+
+template <int DPAD, int LD>
+__device__ __forceinline__ void store_pack(float *d0, float *d1, const PackRegs<DPAD> &pr) {
+  constexpr int C4 = DPAD / 4, PER = PackRegs<DPAD>::PER;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4;
-    st4(d0 + R * LD + 4 * c, v0[q]);
-    st4(d1 + R * LD + 4 * c, v1[q]);
+    st4(d0 + R * LD + 4 * c, pr.v0[q]);
+    st4(d1 + R * LD + 4 * c, pr.v1[q]);
   }
 }
 
@@ -595,13 +614,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
     return;
   }
   const int h = blockIdx.x % H;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the wave index, wave-uniform in an SGPR (the compiler cannot prove
+  // threadIdx.x >> 6 uniform): every block loop and bound derived from it
+  // becomes a scalar branch instead of an exec-masked one
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, g = lane >> 4;
   const int d = H * dh;
   const int64_t rs = 3 * (int64_t)d;
   PackSeqs ps;
   read_pack(packs, pk, ps);
-  load_pack<DPAD, S::LDK>(sK, sV, qkv, rs, d + h * dh, ps, dh);
+  PackRegs<DPAD> kv;
+  load_pack_regs<DPAD>(kv, qkv, rs, d + h * dh, ps, dh);
   // this wave's sequence
   const bool act = w < ps.n;
   int T = 0, lo = 0;
@@ -622,6 +645,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   const int qlc = act ? min(ql, T - 1) : 0;
   ld_kappa_dh<S::Q4>(base + (int64_t)qlc * rs, g, dh, true, q);
   ld_kappa_dh<S::Q4>(dout + (row0 + qlc) * d + h * dh, g, dh, true, dov);
+  store_pack<DPAD, S::LDK>(sK, sV, kv);  // (waits for the K / V loads only)
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
   float kr[S::Q4], vr[S::Q4];

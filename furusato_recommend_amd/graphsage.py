@@ -468,6 +468,11 @@ class _ChunkTrees:
         return len(self._trees)
 
     def __getitem__(self, k: int):
+        n = len(self._trees)
+        if k < 0:
+            k += n
+        if not 0 <= k < n:
+            raise IndexError(f"micro-batch tree {k} of {n}")
         for j in range(k + 1):
             if self._trees[j] is None:
                 self._trees[j] = self._sample(j)

@@ -404,29 +404,28 @@ def needs_launch(args, env=os.environ) -> bool:
     return args.gpus > 1 and "WORLD_SIZE" not in env
 
 
-def launch_command(args, argv: list, port: int) -> list:
+def launch_command(args, argv: list) -> list:
+    """torch.distributed.run with a c10d rendezvous whose store binds its own
+    port (endpoint 127.0.0.1:0): no free port is picked here and handed over
+    (another process could take it in between)."""
     import sys
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
-            "--master-port", str(port), "-m", "furusato_recommend_amd.train_dp", *argv]
+            f"--nproc-per-node={args.gpus}", "--rdzv-backend=c10d",
+            "--rdzv-endpoint=127.0.0.1:0", "--local-addr=127.0.0.1",
+            "-m", "furusato_recommend_amd.train_dp", *argv]
 
 
 def launch(args, argv: list, runner=None) -> int:
     """Start the ranks as a child process tree (nothing here initialises
     HIP) and return their exit status."""
-    import socket
     import subprocess
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env["PYTHONPATH"] = os.pathsep.join(p for p in (root, env.get("PYTHONPATH")) if p)
     if "OMP_NUM_THREADS" not in env:
         env["OMP_NUM_THREADS"] = str(max(1, min(os.cpu_count() or 1, 64) // args.gpus))
-    r = (runner or subprocess.run)(launch_command(args, argv, port), env=env)
+    r = (runner or subprocess.run)(launch_command(args, argv), env=env)
     return int(r.returncode)
 
 

@@ -508,7 +508,10 @@ def test_train_dp_cli_launch_command():
     cmd = seen["cmd"]
     assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=8" in cmd
     assert cmd[cmd.index("-m", 3):][:2] == ["-m", "furusato_recommend_amd.train_dp"]
-    assert cmd[-4:] == ["--model", "sage", "--gpus", "8"] and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--model", "sage", "--gpus", "8"]
+    # the rendezvous store binds its own port: no port picked and handed over
+    assert "--rdzv-endpoint=127.0.0.1:0" in cmd and "--local-addr=127.0.0.1" in cmd
+    assert "--master-port" not in cmd
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
     cfg = T.build_config(T.parse_args(["--model", "sage", "--suffix", "x", "--path", "/c"]), "cuda:0")
     assert cfg["checkpoint_path"] == "/c/ddp_sage_x.pth" and cfg["topks"] == (10, 20)
@@ -705,7 +708,8 @@ def test_bench_launcher_command():
     assert bench.launch(a, ["--gpus", "4", "--steps", "3"], runner=runner) == 7
     cmd = seen["cmd"]
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
-    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert "--nproc-per-node=4" in cmd and "--rdzv-endpoint=127.0.0.1:0" in cmd
+    assert "--local-addr=127.0.0.1" in cmd and "--master-port" not in cmd
     assert cmd[-3:] == ["--gpus", "4", "--steps", "3"][-3:] and cmd[-4] == "--gpus"
     assert seen["env"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
 
@@ -867,6 +871,19 @@ def test_bench_dp_parity_leg_detects_divergence(tamper):
         assert not par0["replicas_bitwise_equal"]
     else:
         assert par0["replicas_bitwise_equal"] and par0["rel_emb_step"] > 1e-4
+
+
+def test_chunk_trees_negative_index():
+    """_ChunkTrees[-1] is the last micro-batch tree (sampling the earlier
+    ones first); out of range raises."""
+    from furusato_recommend_amd.graphsage import _ChunkTrees
+    seen = []
+    t = _ChunkTrees(lambda j: seen.append(j) or f"t{j}", 3)
+    assert t[-1] == "t2" and seen == [0, 1, 2]
+    assert t[-3] == "t0" and list(t) == ["t0", "t1", "t2"]
+    for k in (3, -4):
+        with pytest.raises(IndexError):
+            t[k]
 
 
 def test_host_threads_bounded():
