@@ -216,6 +216,9 @@ SIGNATURES = {
                                              c_int64, c_int32, c_void_p]),
     "mirec_attention_packed_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                            c_int32, c_int32, c_void_p, c_int64, c_void_p]),
+    "mirec_attention_packed_bwd_lse": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_int64, c_int32, c_int32, c_void_p,
+                                               c_int64, c_void_p]),
     "mirec_attention_wave_fwd": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32,
                                          c_int32, c_void_p, c_void_p, c_int64, c_void_p]),
     "mirec_attention_wave_bwd": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -591,11 +591,17 @@ __device__ __forceinline__ void store_pack(float *d0, float *d1, const PackRegs<
 
 // waves_per_eu(4): at most 128 registers, so four workgroups (the LDS
 // limit) fit per CU.  dh % 4 == 0.
-template <int DPAD>
+// FWD_STATS: the forward's lse2 [n_rows, H] (the wave forward's base-2
+// log-sum-exp) is given, so phase A's P = exp2(S·c2 − lse2) directly: no
+// max and sum reductions, no normalisation pass; δ = Σ_k P dP as before.
+// (δ = rowsum(dO ⊙ O), FlashAttention-2's form, was measured slower here:
+// it reads O, 29 MB more per C4 launch, for VALU this kernel is not bound by.)
+template <int DPAD, bool FWD_STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_bwd_packed_kernel(
     const float *__restrict__ qkv, const float *__restrict__ dout, float *__restrict__ dqkv,
     int H, int dh, float scale, const int32_t *__restrict__ offsets,
-    const int32_t *__restrict__ packs, int64_t batch, int64_t n_rows) {
+    const int32_t *__restrict__ packs, int64_t batch, int64_t n_rows,
+    const float *__restrict__ fwd_lse2) {
   constexpr int NB = 4;
   using S = AttnShape<DPAD, NB>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -645,11 +651,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   const int qlc = act ? min(ql, T - 1) : 0;
   ld_kappa_dh<S::Q4>(base + (int64_t)qlc * rs, g, dh, true, q);
   ld_kappa_dh<S::Q4>(dout + (row0 + qlc) * d + h * dh, g, dh, true, dov);
+  float lq = 0.f;
+  if constexpr (FWD_STATS) lq = fwd_lse2[(row0 + qlc) * H + h];
   store_pack<DPAD, S::LDK>(sK, sV, kv);  // (waits for the K / V loads only)
   __syncthreads();
   // ---------------------------------------------------- phase A: query block w
   float kr[S::Q4], vr[S::Q4];
-  if (act) {
+  if (FWD_STATS && act) {
+    // P from the forward's lse2 (no max / sum passes); δ = Σ_k P dP
+    const int lw = (w - lo) & 3;
+    const float *sKl = sK + kB * lo * S::LDK, *sVl = sV + kB * lo * S::LDK;
+    const float c2 = scale * kLog2e, nl = -lq;
+    f32x4 p[NB], dp[NB];
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      p[kb] = zero4();
+      dp[kb] = zero4();
+    }
+#pragma unroll
+    for (int c = 0; c < S::Q4 / 4; ++c) {
+#pragma unroll
+      for (int kb = 0; kb < NB; ++kb)
+        if (kb <= lw) {
+          const float4 k4 = ld4(sKl + (kB * kb + j) * S::LDK + 16 * c + 4 * g);
+          const float4 v4 = ld4(sVl + (kB * kb + j) * S::LDK + 16 * c + 4 * g);
+          p[kb] = mfma16(k4.x, q[4 * c], p[kb]);
+          dp[kb] = mfma16(v4.x, dov[4 * c], dp[kb]);
+          p[kb] = mfma16(k4.y, q[4 * c + 1], p[kb]);
+          dp[kb] = mfma16(v4.y, dov[4 * c + 1], dp[kb]);
+          p[kb] = mfma16(k4.z, q[4 * c + 2], p[kb]);
+          dp[kb] = mfma16(v4.z, dov[4 * c + 2], dp[kb]);
+          p[kb] = mfma16(k4.w, q[4 * c + 3], p[kb]);
+          dp[kb] = mfma16(v4.w, dov[4 * c + 3], dp[kb]);
+        }
+    }
+    float delta = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb > lw) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kB * kb + 4 * g + r;
+        const float pv = (key <= ql && key < T) ? exp2_hw(fmaf(p[kb][r], c2, nl)) : 0.f;
+        p[kb][r] = pv;
+        delta = fmaf(pv, dp[kb][r], delta);
+      }
+    }
+    delta += __shfl_xor(delta, 16);
+    delta += __shfl_xor(delta, 32);
+    if (g == 0) {
+      sM[qa] = lq;
+      sD[qa] = delta;
+    }
+    f32x4 dq[S::NCB];
+#pragma unroll
+    for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = zero4();
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) {
+      if (kb > lw) break;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ds = p[kb][r] * (dp[kb][r] - delta) * scale;
+        const float *krow = sKl + (kB * kb + 4 * g + r) * S::LDK + j;
+#pragma unroll
+        for (int cb = 0; cb < S::NCB; ++cb) dq[cb] = mfma16(krow[kB * cb], ds, dq[cb]);
+      }
+    }
+    if (ql < T) {
+      float *row = gbase + (int64_t)ql * rs;
+#pragma unroll
+      for (int cb = 0; cb < S::NCB; ++cb) store4(row, kB * cb + 4 * g, dh, dq[cb]);
+    }
+#pragma unroll
+    for (int c = 0; c < S::Q4 / 4; ++c) {
+      const float4 k4 = ld4(sK + qa * S::LDK + 16 * c + 4 * g);
+      const float4 v4 = ld4(sV + qa * S::LDK + 16 * c + 4 * g);
+      kr[4 * c] = k4.x;
+      kr[4 * c + 1] = k4.y;
+      kr[4 * c + 2] = k4.z;
+      kr[4 * c + 3] = k4.w;
+      vr[4 * c] = v4.x;
+      vr[4 * c + 1] = v4.y;
+      vr[4 * c + 2] = v4.z;
+      vr[4 * c + 3] = v4.w;
+    }
+  } else if (!FWD_STATS && act) {
     f32x4 p[NB], dp[NB];
     float lse2;
     // local key blocks kb = 0..lw (LDS block lo + kb); the masks tell the
@@ -794,20 +880,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void a
   }
 }
 
-template <int DPAD>
+template <int DPAD, bool FWD_STATS>
 static int launch_packed_bwd(const float *qkv, const float *dout, const int32_t *offsets,
                              const int32_t *packs, int64_t batch, int heads, int dh, float *dqkv,
-                             int64_t n_rows, hipStream_t st) {
+                             int64_t n_rows, const float *fwd_lse2, hipStream_t st) {
   constexpr int lds = AttnShape<DPAD, 4>::bwd_lds;
   static int rc = -1;
   if (rc < 0)
-    rc = hipFuncSetAttribute((const void *)attn_bwd_packed_kernel<DPAD>,
+    rc = hipFuncSetAttribute((const void *)attn_bwd_packed_kernel<DPAD, FWD_STATS>,
                              hipFuncAttributeMaxDynamicSharedMemorySize, lds) == hipSuccess ? 0 : 1;
   if (rc != 0) return MIREC_ERR_HIP;
   // at most batch packs per head, plus spare workgroups for the padding rows
-  hipLaunchKernelGGL((attn_bwd_packed_kernel<DPAD>), dim3((unsigned)(batch * heads + 256)),
-                     dim3(256), lds, st, qkv, dout, dqkv, heads, dh, 1.f / sqrtf((float)dh),
-                     offsets, packs, batch, n_rows);
+  hipLaunchKernelGGL((attn_bwd_packed_kernel<DPAD, FWD_STATS>),
+                     dim3((unsigned)(batch * heads + 256)), dim3(256), lds, st, qkv, dout, dqkv,
+                     heads, dh, 1.f / sqrtf((float)dh), offsets, packs, batch, n_rows, fwd_lse2);
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }
@@ -990,8 +1076,27 @@ extern "C" int mirec_attention_packed_bwd(const float *qkv, const float *dout,
   MIREC_CHECK_ARG(((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   return head_dim <= 32
-             ? launch_packed_bwd<32>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv,
-                                     n_rows, st)
-             : launch_packed_bwd<64>(qkv, dout, offsets, packs, batch, heads, head_dim, dqkv,
-                                     n_rows, st);
+             ? launch_packed_bwd<32, false>(qkv, dout, offsets, packs, batch, heads, head_dim,
+                                            dqkv, n_rows, nullptr, st)
+             : launch_packed_bwd<64, false>(qkv, dout, offsets, packs, batch, heads, head_dim,
+                                            dqkv, n_rows, nullptr, st);
+}
+
+extern "C" int mirec_attention_packed_bwd_lse(const float *qkv, const float *lse,
+                                              const float *dout, const int32_t *offsets,
+                                              const int32_t *packs, int64_t batch, int32_t heads,
+                                              int32_t head_dim, float *dqkv, int64_t n_rows,
+                                              mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(batch >= 0 && heads >= 1 && head_dim >= 4 && head_dim <= 64 &&
+                  head_dim % 4 == 0 && n_rows >= 0);
+  if (batch == 0) return MIREC_OK;
+  MIREC_CHECK_ARG(qkv && lse && dout && offsets && packs && dqkv && (uintptr_t)packs % 16 == 0);
+  MIREC_CHECK_ARG(((uintptr_t)qkv | (uintptr_t)dout | (uintptr_t)dqkv) % 16 == 0);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  return head_dim <= 32
+             ? launch_packed_bwd<32, true>(qkv, dout, offsets, packs, batch, heads, head_dim,
+                                           dqkv, n_rows, lse, st)
+             : launch_packed_bwd<64, true>(qkv, dout, offsets, packs, batch, heads, head_dim,
+                                           dqkv, n_rows, lse, st);
 }

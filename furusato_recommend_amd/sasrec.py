@@ -232,16 +232,15 @@ class _CausalAttentionVarlen(torch.autograd.Function):
                 if ctx.padded:
                     _zero_tail(dqkv, offsets)
                 _wave_bwd(qkv, out, lse, order, dout, offsets, B, 0, ctx.heads, dh, dqkv)
-            else:  # sequences packed into workgroups, longest first; its spare
-                # workgroups zero the capacity padding rows
+            else:  # sequences packed into workgroups, longest first, from the
+                # forward's lse (no softmax reductions); its spare workgroups
+                # zero the capacity padding rows
                 _timed("bwd", (B, -1, ctx.heads, dh), lambda: check(
-                    lib.mirec_attention_packed_bwd(qkv.data_ptr(), dout.data_ptr(),
-                                                   offsets.data_ptr(),
-                                                   order[-(-B // 4) * 4:].data_ptr(), B,
-                                                   ctx.heads, dh, dqkv.data_ptr(),
-                                                   n if ctx.padded else 0,
-                                                   _lib.stream_handle()),
-                    "attention_packed_bwd"), offsets)
+                    lib.mirec_attention_packed_bwd_lse(
+                        qkv.data_ptr(), lse.data_ptr(), dout.data_ptr(), offsets.data_ptr(),
+                        order[-(-B // 4) * 4:].data_ptr(), B, ctx.heads, dh, dqkv.data_ptr(),
+                        n if ctx.padded else 0, _lib.stream_handle()),
+                    "attention_packed_bwd_lse"), offsets)
             return dqkv, None, None, None, None
         if ctx.padded:
             _zero_tail(dqkv, offsets)

@@ -714,6 +714,14 @@ int mirec_attention_packed_bwd(const float *qkv, const float *dout, const int32_
                                const int32_t *packs, int64_t batch, int32_t heads,
                                int32_t head_dim, float *dqkv, int64_t n_rows,
                                mirec_stream_t stream);
+/* The packed backward given the forward's statistic: lse [n, heads] as
+ * mirec_attention_wave_fwd wrote it (base 2).  P = exp2(S scale log2 e -
+ * lse) directly, with no max / sum reductions in the kernel.  Same packs,
+ * layout and padding rows as mirec_attention_packed_bwd. */
+int mirec_attention_packed_bwd_lse(const float *qkv, const float *lse, const float *dout,
+                                   const int32_t *offsets, const int32_t *packs, int64_t batch,
+                                   int32_t heads, int32_t head_dim, float *dqkv, int64_t n_rows,
+                                   mirec_stream_t stream);
 
 /* Packed form with the workgroups in a given sequence order (device int32
  * [batch], e.g. mirec_attention_length_order: longest first). */

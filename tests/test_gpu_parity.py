@@ -1335,6 +1335,51 @@ def test_attention_wave_matches_block_and_repeats(monkeypatch):
             assert rel(res[impl][1], res["block"][1]) < TOL, (impl, heads, dh)
 
 
+@pytest.mark.parametrize("heads,dh", [(2, 64), (4, 32), (8, 16)])
+def test_packed_bwd_from_forward_lse_equals_recomputed(heads, dh):
+    """mirec_attention_packed_bwd_lse (phase A's P from the wave forward's
+    base-2 lse: no max / sum reductions) ==
+    mirec_attention_packed_bwd (softmax statistics recomputed in the kernel)
+    on packed sequences at every block edge, capacity padding rows zero in
+    both; reruns bitwise equal."""
+    from furusato_recommend_amd import _lib
+    from furusato_recommend_amd.sasrec import _length_order
+    lib, st = _lib.lib, _lib.stream_handle()
+    torch.manual_seed(11)
+    lens = torch.tensor([0, 1, 16, 17, 32, 33, 48, 49, 64, 5, 50, 40, 23, 9, 2, 3, 4, 31])
+    B, n = len(lens), int(lens.sum())
+    cap = n + 300
+    d = heads * dh
+    offs = torch.zeros(B + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(lens, 0)
+    offs = offs.cuda()
+    qkv = torch.randn(cap, 3 * d, device="cuda")
+    dout = torch.randn(cap, d, device="cuda")
+    out = torch.empty(cap, d, device="cuda")
+    lse = torch.empty(cap, heads, device="cuda")
+    order = _length_order(offs, B)
+    packs = order[-(-B // 4) * 4:]
+    _lib.check(lib.mirec_attention_wave_fwd(qkv.data_ptr(), offs.data_ptr(), order.data_ptr(), B,
+                                            0, heads, dh, out.data_ptr(), lse.data_ptr(), cap,
+                                            st), "wave_fwd")
+    res = []
+    for stats in (False, True, True):
+        g = torch.full_like(qkv, float("nan"))
+        if stats:
+            rc = lib.mirec_attention_packed_bwd_lse(
+                qkv.data_ptr(), lse.data_ptr(), dout.data_ptr(), offs.data_ptr(),
+                packs.data_ptr(), B, heads, dh, g.data_ptr(), cap, st)
+        else:
+            rc = lib.mirec_attention_packed_bwd(qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(),
+                                                packs.data_ptr(), B, heads, dh, g.data_ptr(), cap,
+                                                st)
+        _lib.check(rc, "packed_bwd")
+        assert torch.isfinite(g).all() and float(g[n:].abs().max()) == 0.0
+        res.append(g)
+    assert torch.equal(res[1], res[2])
+    assert rel(res[1][:n], res[0][:n]) < 1e-5
+
+
 def test_attention_capacity_padding_rows_zero(attn_impl):
     """A capacity-padded packed batch (the captured step's form): the rows
     past the last sequence come out zero in the output and in dqkv, even when

@@ -89,10 +89,13 @@ def main():
                 "packed_bwd": lambda: chk(lib.mirec_attention_packed_bwd(
                     qkv.data_ptr(), dout.data_ptr(), offs.data_ptr(), order[bp:].data_ptr(), B, H,
                     dh, dqkv.data_ptr(), n, st), "packed_bwd"),
+                "packed_lse_bwd": lambda: chk(lib.mirec_attention_packed_bwd_lse(
+                    qkv.data_ptr(), lse.data_ptr(), dout.data_ptr(), offs.data_ptr(),
+                    order[bp:].data_ptr(), B, H, dh, dqkv.data_ptr(), n, st), "packed_lse_bwd"),
             }
             for name, fn in runs.items():
-                if name == "wave_bwd":
-                    runs["wave_fwd"]()
+                if name in ("wave_bwd", "packed_lse_bwd"):
+                    runs["wave_fwd"]()  # the forward's out / lse
                 us = timed(fn, a.reps)
                 by = by_b if name.endswith("bwd") else by_f
                 print(json.dumps({"kernel": name, "order": a.order, "mix": mix, "B": B, "n_tok": n, "us": round(us, 1),
