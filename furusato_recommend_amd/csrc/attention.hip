@@ -561,7 +561,13 @@ __device__ __forceinline__ void load_pack_regs(PackRegs<DPAD> &pr, const float *
   float4 *v0 = pr.v0, *v1 = pr.v1;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
-    const int e = threadIdx.x + q * 256, R = e / C4, c = e % C4, w = R / kB;
+    // thread t covers row R = t / C4 + q·(256 / C4) (16-row block w, row
+    // R % 16 in it), dims 4c..; the block is the same for a whole wave
+    // (DPAD 64: w = q; DPAD 32: t / 128 + 2q), so the sequence lookup runs
+    // on scalars
+    const int c = threadIdx.x % C4, rr = (threadIdx.x / C4) % kB;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / C4) / kB) +
+                  q * (256 / C4 / kB);
     // unconditional loads: a row past its sequence's length loads the
     // sequence's last row (its score is masked to -inf, its P and dS are 0),
     // a block past the pack's blocks loads a row of the pack (never read);
@@ -569,12 +575,18 @@ __device__ __forceinline__ void load_pack_regs(PackRegs<DPAD> &pr, const float *
     int T, lo;
     int64_t r0;
     seq_of(ps, w, T, lo, r0);
-    const int64_t row = r0 + min(kB * (w - lo) + R % kB, T - 1);
+    const int64_t row = r0 + min(kB * (w - lo) + rr, T - 1);
     const float *src = qkv + row * rs + coff + 4 * min(c, dh / 4 - 1);
-    const float4 x0 = ld4(src), x1 = ld4(src + rs / 3);
-    const bool dim_ok = 4 * c < dh;
-    v0[q] = dim_ok ? x0 : f4_zero();
-    v1[q] = dim_ok ? x1 : f4_zero();
+    v0[q] = ld4(src);
+    v1[q] = ld4(src + rs / 3);
+  }
+  if (dh < DPAD) {  // (wave-uniform) dims past dh read as zero
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const bool dim_ok = 4 * (int)(threadIdx.x % C4) < dh;
+      v0[q] = dim_ok ? v0[q] : f4_zero();
+      v1[q] = dim_ok ? v1[q] : f4_zero();
+    }
   }
 }
 

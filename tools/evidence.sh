@@ -14,11 +14,15 @@
 #   smoke      __graft_entry__.smoke()                           -> smoke.log
 #   c2         the headline bench line (bench.py defaults: roofline, CPU
 #              baseline, oracle parity leg, Recall@20)           -> bench_c2.log
+#   c2quick    the C2 line without the CPU baseline and Recall legs (oracle parity kept)
 #   prof       C2 rocprofv3 passes: kernel stats, FETCH_SIZE, WRITE_SIZE of
 #              prop_kernel (tools/profile.sh), summarised        -> prof/, summary.json
+#   c2prof     kernel stats of 13 C2 steps (no CPU / parity / Recall legs)
 #   c3 / c4    GraphSAGE C3 / SASRec C4 lines with CPU baselines -> bench_c3.log, bench_c4.log
 #   c3prof / c4prof   kernel stats of the C3 step / the captured C4 step
 #   zipf       the C2 Zipf-popularity graph: line + kernel stats
+#   c4nodes    the captured C4 step's HIP graph by node kind (memcpy / memset /
+#              kernels; tools/c4_graph_nodes.py)                -> c4_graph_nodes.log
 #   rehearse2 / rehearse8   bench.py --gpus N --rehearse (N ranks on one GPU,
 #              gloo): the DP parity and Recall@20 legs   -> bench_c2_rehearse_dpN.log
 #   c5         LightGCN-3 d=256 10 M x 1 M / 200 M on one GPU   -> bench_c5.log
@@ -29,6 +33,7 @@
 #   trace_c3   device timeline of one simulated pipelined C3 step (W = 8, C = 2):
 #              rocprofv3 --kernel-trace + tools/trace_step.py  -> trace_c3_step.txt
 #   world_c2   rank 0's C2 step at W = 1..8 (sparse / sharded)
+#   world_c5   rank 0's C5 step (10 M x 1 M / 200 M, d = 256) at W = 1..8 (sparse / sharded)
 #   eval       streamed evaluation at C2 with the float64 near-tie check
 #   eval_d256  the streamed evaluation at d = 256 (2 M x 1 M, the D > 128 path)
 #   attn       attention kernels at the C4 length mix
@@ -72,6 +77,9 @@ for leg in $LEGS; do
     c2)
       run 700 $E/bench_c2.log python bench.py
       lines $E/bench_c2.log 600 ;;
+    c2quick)
+      run 400 $E/bench_c2_quick.log python bench.py --cpu-baseline off --quality-steps 0
+      lines $E/bench_c2_quick.log 600 ;;
     prof)
       PROF_OUT=$E/prof bash tools/profile.sh || exit 1
       find $E/prof -name "*kernel_trace.csv" -delete
@@ -82,6 +90,9 @@ for leg in $LEGS; do
     c4)
       run 400 $E/bench_c4.log python tools/bench_sasrec.py --steps 100
       lines $E/bench_c4.log ;;
+    c2prof)
+      run 300 $E/c2prof.log rocprofv3 --kernel-trace --stats -d $E/c2 -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0
+      find $E/c2 -name "*kernel_trace.csv" -delete ;;
     c3prof)
       run 300 $E/c3prof.log rocprofv3 --kernel-trace --stats -d $E/c3 -o run --output-format csv -- python3 tools/bench_sage.py --steps 10 --warmup 3 --cpu-baseline 0
       find $E/c3 -name "*kernel_trace.csv" -delete ;;
@@ -93,6 +104,9 @@ for leg in $LEGS; do
       lines $E/bench_c2_zipf.log
       run 300 $E/zipf.log rocprofv3 --kernel-trace --stats -d $E/zipf -o run --output-format csv -- python3 bench.py --kind zipf --steps 10 --warmup 3 --cpu-baseline off --quality-steps 0 --parity 0
       find $E/zipf -name "*kernel_trace.csv" -delete ;;
+    c4nodes)
+      run 300 $E/c4_graph_nodes.log python tools/c4_graph_nodes.py --out $E/c4_graph.dot
+      lines $E/c4_graph_nodes.log 3000 ;;
     rehearse2|rehearse8)
       # the N-rank bench on one GPU (gloo): parity leg (bitwise replicas +
       # union-batch replay on rank 0) and the DataParallel Recall@20 leg
@@ -122,6 +136,9 @@ for leg in $LEGS; do
     world_c2)
       timeout -k 10 900 python -u tools/bench_world_sim.py --modes sparse,sharded > $E/world_sim_c2.jsonl 2> $E/world_sim_c2.log || { echo "world sim rc=$?"; tail $E/world_sim_c2.log; exit 1; }
       lines $E/world_sim_c2.jsonl 300 ;;
+    world_c5)
+      timeout -k 10 1000 python -u tools/bench_world_sim.py --users 10000000 --items 1000000 --edges 200000000 --dim 256 --modes sparse,sharded --steps 5 --warmup 2 > $E/world_sim_c5.jsonl 2> $E/world_sim_c5.log || { echo "world sim rc=$?"; tail $E/world_sim_c5.log; exit 1; }
+      lines $E/world_sim_c5.jsonl 300 ;;
     eval)
       run 600 $E/eval_c2.log python -u tools/eval_bench.py --reps 10
       lines $E/eval_c2.log 300 ;;
