@@ -167,10 +167,12 @@ extern "C" int mirec_csr_sort_rows(const int64_t *rowptr, const int32_t *col, in
 // e of its user row (rows 0 .. n_users - 1, the allPos order), each row's
 // probabilities non-negative with a positive sum; cdf[e - rowptr[0]] = the
 // inclusive cumulative sum in float64 divided by the row total (numpy's
-// choice normalises the same way), rounded to float, the row's last entry
-// exactly 1.  Empty rows are skipped.
+// choice normalises the same way), kept in float64 — an entry of
+// probability 1e-12 after a row mass of 0.5 stays its own CDF step (a float
+// CDF would merge it into its neighbour) — the row's last entry exactly 1.
+// Empty rows are skipped.
 extern "C" int mirec_pos_cdf_build(const int64_t *rowptr, int64_t n_users, const double *probs,
-                                   float *cdf) {
+                                   double *cdf) {
   if (rowptr == nullptr || n_users < 0) return MIREC_ERR_ARG;
   const int64_t base = rowptr[0], total = rowptr[n_users] - base;
   if (total > 0 && (probs == nullptr || cdf == nullptr)) return MIREC_ERR_ARG;
@@ -184,16 +186,15 @@ extern "C" int mirec_pos_cdf_build(const int64_t *rowptr, int64_t n_users, const
       s += probs[e];
     }
     if (!(s > 0.0)) return MIREC_ERR_ARG;
-    double c = 0.0;
-    float prev = 0.f;
+    double c = 0.0, prev = 0.0;
     for (int64_t e = a; e < b; ++e) {
       c += probs[e];
-      float v = (float)(c / s);
-      v = v < prev ? prev : (v > 1.f ? 1.f : v);
+      double v = c / s;
+      v = v < prev ? prev : (v > 1.0 ? 1.0 : v);
       cdf[e] = v;
       prev = v;
     }
-    cdf[b - 1] = 1.f;
+    cdf[b - 1] = 1.0;
   }
   return MIREC_OK;
 }

@@ -47,9 +47,9 @@ struct XorShift64Star {
     return (int64_t)(uint64_t)(((unsigned __int128)next() * (uint64_t)n) >> 64);
 #endif
   }
-  // Uniform float in [0, 1) on the 2^-24 grid (exactly representable).
-  __host__ __device__ __forceinline__ float unit() {
-    return (float)(uint32_t)(next() >> 40) * 0x1p-24f;
+  // Uniform double in [0, 1) on the 2^-53 grid (exactly representable).
+  __host__ __device__ __forceinline__ double unit() {
+    return (double)(next() >> 11) * 0x1p-53;
   }
 };
 
@@ -58,11 +58,11 @@ struct XorShift64Star {
 // e within its row, the row's last entry 1) the first entry whose cumulative
 // probability exceeds a uniform draw in [0, 1) — an entry of zero
 // probability is never chosen.
-__host__ __device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const float *__restrict__ cdf,
+__host__ __device__ __forceinline__ int64_t draw_positive(XorShift64Star &rng, const double *__restrict__ cdf,
                                                  int64_t base, int64_t beg, int64_t deg) {
   if (cdf == nullptr) return rng.below(deg);
-  const float r = rng.unit();
-  const float *c = cdf + (beg - base);
+  const double r = rng.unit();
+  const double *c = cdf + (beg - base);
   int64_t lo = 0, hi = deg - 1;  // the last entry (cdf 1 > r) always qualifies
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
@@ -100,7 +100,7 @@ constexpr int kMaxNegTries = 1 << 16;
 // if a draw exhausted its retry budget.
 __host__ __device__ __forceinline__ bool bpr_sample_one(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    const int32_t *__restrict__ sorted, const double *__restrict__ pos_cdf, int64_t n_users,
     int64_t m_items, int64_t t, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
     int32_t *users, int32_t *pos, int32_t *neg) {
   XorShift64Star rng;
@@ -138,7 +138,7 @@ __host__ __device__ __forceinline__ bool bpr_sample_one(
 
 __global__ __launch_bounds__(256) void bpr_sample_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    const int32_t *__restrict__ sorted, const double *__restrict__ pos_cdf, int64_t n_users,
     int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset, int32_t shard,
     int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg, int32_t *err) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -171,7 +171,7 @@ struct CandRng {
 // candidate t: user u (its shard), positive item p or -1 (no positives)
 __host__ __device__ __forceinline__ void draw_candidate(CandRng &c, const int64_t *__restrict__ rowptr,
                                                const int32_t *__restrict__ col,
-                                               const float *__restrict__ pos_cdf, int64_t n_users,
+                                               const double *__restrict__ pos_cdf, int64_t n_users,
                                                int32_t shard, int32_t n_shards, int64_t &u,
                                                int64_t &p, int64_t &beg, int64_t &deg) {
   const int64_t n_local = (n_users - shard + n_shards - 1) / n_shards;
@@ -184,7 +184,7 @@ __host__ __device__ __forceinline__ void draw_candidate(CandRng &c, const int64_
 
 __global__ __launch_bounds__(256) void cand_kernel(const int64_t *__restrict__ rowptr,
                                                    const int32_t *__restrict__ col,
-                                                   const float *__restrict__ pos_cdf,
+                                                   const double *__restrict__ pos_cdf,
                                                    int64_t n_users, int64_t m_items, int64_t n,
                                                    uint64_t seed, uint64_t offset, int32_t shard,
                                                    int32_t n_shards, int32_t *__restrict__ keys,
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(256) void cand_keep_kernel(const int32_t *__restric
 // exhausted its retry budget.
 __host__ __device__ __forceinline__ bool emit_candidate(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    const int32_t *__restrict__ sorted, const double *__restrict__ pos_cdf, int64_t n_users,
     int64_t m_items, int64_t t, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
     int64_t o, int32_t *users, int32_t *pos, int32_t *neg) {
   CandRng c(seed, offset, shard, t);  // the same stream: same u, p, then n
@@ -246,7 +246,7 @@ __host__ __device__ __forceinline__ bool emit_candidate(
 
 __global__ __launch_bounds__(256) void cand_emit_kernel(
     const int64_t *__restrict__ rowptr, const int32_t *__restrict__ col,
-    const int32_t *__restrict__ sorted, const float *__restrict__ pos_cdf, int64_t n_users,
+    const int32_t *__restrict__ sorted, const double *__restrict__ pos_cdf, int64_t n_users,
     int64_t m_items, int64_t n, uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
     const int32_t *__restrict__ flag, const int32_t *__restrict__ at, int32_t *__restrict__ users,
     int32_t *__restrict__ pos, int32_t *__restrict__ neg, int32_t *__restrict__ count,
@@ -311,7 +311,7 @@ extern "C" int mirec_bpr_sample_capped_workspace(int64_t n_candidates, int64_t m
   return MIREC_OK;
 }
 
-extern "C" int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const float *pos_cdf,
+extern "C" int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const double *pos_cdf,
                                           int64_t n_users, int64_t m_items,
                                        int64_t n_candidates, int32_t cap, uint64_t seed,
                                        uint64_t offset, int32_t shard, int32_t n_shards,
@@ -382,7 +382,7 @@ extern "C" int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, 
                                     cand_p, workspace, workspace_bytes, stream);
 }
 
-extern "C" int mirec_bpr_sample_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+extern "C" int mirec_bpr_sample_ex(const mirec_csr_t *csr, const double *pos_cdf, int64_t n_users,
                                    int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset,
                                    int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
                                    int32_t *neg, int32_t *err, mirec_stream_t stream) {
@@ -413,7 +413,7 @@ extern "C" int mirec_bpr_sample(const mirec_csr_t *csr, int64_t n_users, int64_t
 // streams, so the triples equal mirec_bpr_sample's bit for bit.  Threads
 // take contiguous blocks of triples.
 extern "C" int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col,
-                                    const int32_t *col_sorted, const float *pos_cdf,
+                                    const int32_t *col_sorted, const double *pos_cdf,
                                     int64_t n_users, int64_t m_items, int64_t batch,
                                     uint64_t seed, uint64_t offset, int32_t shard,
                                     int32_t n_shards, int32_t *users, int32_t *pos, int32_t *neg,
@@ -450,7 +450,7 @@ extern "C" int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col,
 // reference's own sequential count per item (ddp_lgcn.py:571-572), and the
 // kept candidates draw their negatives on the threads again.
 extern "C" int mirec_cpu_bpr_sample_capped(const int64_t *rowptr, const int32_t *col,
-                                           const int32_t *col_sorted, const float *pos_cdf,
+                                           const int32_t *col_sorted, const double *pos_cdf,
                                            int64_t n_users, int64_t m_items,
                                            int64_t n_candidates, int32_t cap, uint64_t seed,
                                            uint64_t offset, int32_t shard, int32_t n_shards,

@@ -163,7 +163,7 @@ class Graph:
             flat = np.concatenate(parts) if parts else np.zeros(0)
         if flat.size != n:
             raise ValueError(f"probs: {flat.size} entries for {n} user-row entries")
-        cdf = np.empty(max(n, 1), np.float32)
+        cdf = np.empty(max(n, 1), np.float64)
         check(lib.mirec_pos_cdf_build(self.rowptr_host.ctypes.data, nu, flat.ctypes.data,
                                       cdf.ctypes.data), "pos_cdf_build")
         self.pos_cdf = torch.from_numpy(cdf).to(self.device)

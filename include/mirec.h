@@ -458,17 +458,18 @@ int mirec_bpr_sample_capped_workspace(int64_t n_candidates, int64_t m_items, siz
  * np.random.choice(len(allPos[u]), p=probs[u])): pos_cdf[e - rowptr[0]]
  * is the inclusive cumulative probability of entry e within its user row
  * (rows 0 .. n_users - 1 of the CSR, i.e. the allPos order), non-decreasing
- * in the row, its last entry exactly 1.0f (mirec_pos_cdf_build makes it on
- * the host).  The positive is the first entry whose cumulative probability
- * exceeds a uniform draw on the 2^-24 grid (numpy's searchsorted 'right');
+ * in the row, its last entry exactly 1.0, in float64 (mirec_pos_cdf_build makes
+ * it on the host).  The positive is the first entry whose cumulative
+ * probability exceeds a uniform draw on the 2^-53 grid (numpy's searchsorted
+ * 'right' over its float64 CDF);
  * with pos_cdf = NULL they are the functions above (bit for bit). */
 /* Host: cdf from probs[e - rowptr[0]] (float64, per user-row entry, each
  * non-empty row non-negative with a positive sum; normalised per row in
  * float64 as numpy's choice does).  MIREC_ERR_ARG on a negative / NaN entry
  * or a zero row. */
 int mirec_pos_cdf_build(const int64_t *rowptr, int64_t n_users, const double *probs,
-                        float *cdf);
-int mirec_bpr_sample_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+                        double *cdf);
+int mirec_bpr_sample_ex(const mirec_csr_t *csr, const double *pos_cdf, int64_t n_users,
                         int64_t m_items, int64_t batch, uint64_t seed, uint64_t offset,
                         int32_t shard, int32_t n_shards, int32_t *users, int32_t *pos,
                         int32_t *neg, int32_t *err, mirec_stream_t stream);
@@ -478,7 +479,7 @@ int mirec_bpr_sample_capped(const mirec_csr_t *csr, int64_t n_users, int64_t m_i
                             int32_t *neg, int32_t *count, int32_t *err, int32_t *cand_u,
                             int32_t *cand_p, void *workspace, size_t workspace_bytes,
                             mirec_stream_t stream);
-int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const float *pos_cdf, int64_t n_users,
+int mirec_bpr_sample_capped_ex(const mirec_csr_t *csr, const double *pos_cdf, int64_t n_users,
                                int64_t m_items, int64_t n_candidates, int32_t cap,
                                uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
                                int32_t *users, int32_t *pos, int32_t *neg, int32_t *count,
@@ -1015,7 +1016,7 @@ int mirec_score_topk(const float *user_emb, int64_t n_eval, const float *item_em
  * mirec_csr_t / mirec_bpr_sample_ex).  Replaces UniformSample,
  * negative_sample.py:98-134, for a CPU model. */
 int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col, const int32_t *col_sorted,
-                         const float *pos_cdf, int64_t n_users, int64_t m_items, int64_t batch,
+                         const double *pos_cdf, int64_t n_users, int64_t m_items, int64_t batch,
                          uint64_t seed, uint64_t offset, int32_t shard, int32_t n_shards,
                          int32_t *users, int32_t *pos, int32_t *neg, int32_t *err,
                          int32_t n_threads);
@@ -1027,7 +1028,7 @@ int mirec_cpu_bpr_sample(const int64_t *rowptr, const int32_t *col, const int32_
  * per-item count (ddp_lgcn.py:571-572).  *err = 1 if a negative draw
  * exhausted its retries.  No workspace. */
 int mirec_cpu_bpr_sample_capped(const int64_t *rowptr, const int32_t *col,
-                                const int32_t *col_sorted, const float *pos_cdf, int64_t n_users,
+                                const int32_t *col_sorted, const double *pos_cdf, int64_t n_users,
                                 int64_t m_items, int64_t n_candidates, int32_t cap, uint64_t seed,
                                 uint64_t offset, int32_t shard, int32_t n_shards, int32_t *users,
                                 int32_t *pos, int32_t *neg, int32_t *count, int32_t *err,

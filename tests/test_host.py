@@ -455,8 +455,10 @@ def test_train_dp_cli_two_ranks_gloo(golden, tmp_path):
 
 def test_pos_cdf_build_matches_numpy_choice(golden):
     """mirec_pos_cdf_build (host, libmirec) == numpy choice's normalised
-    cumulative probabilities per user row (oracle.pos_cdf), rounded to
-    float32, each row ending at exactly 1; bad rows rejected."""
+    cumulative probabilities per user row (oracle.pos_cdf), in float64 —
+    exactly, each row ending at exactly 1; bad rows rejected; a long tail of
+    tiny probabilities keeps one CDF step per entry (a float CDF
+    merged entries below ~2^-24 of the row mass into their neighbours)."""
     import ctypes
 
     from furusato_recommend_amd import Graph
@@ -470,10 +472,10 @@ def test_pos_cdf_build_matches_numpy_choice(golden):
     rp = g.rowptr_host
     # the CSR's user rows are the allPos order
     assert all(np.array_equal(g.col_host[rp[k]:rp[k + 1]] - nu, all_pos[k]) for k in range(nu))
-    cdf = np.empty(len(flat), np.float32)
+    cdf = np.empty(len(flat), np.float64)
     assert lib.mirec_pos_cdf_build(rp.ctypes.data, nu, flat.ctypes.data, cdf.ctypes.data) == 0
     ref = O.pos_cdf(all_pos, probs)
-    assert np.max(np.abs(cdf - ref)) <= 2 ** -24
+    assert np.array_equal(cdf, ref)
     ends = rp[1:nu + 1] - rp[0] - 1
     assert np.all(cdf[ends[np.diff(rp[:nu + 1]) > 0]] == 1.0)
     for k in range(nu):
@@ -490,6 +492,14 @@ def test_pos_cdf_build_matches_numpy_choice(golden):
     assert np.array_equal(g.pos_cdf.numpy(), cdf)
     with pytest.raises(ValueError):
         g.set_positive_probs(probs[:-1])
+    # the long tail: 1e-12 entries between two halves stay distinct steps
+    tail = np.array([0.5] + [1e-12] * 6 + [0.5])
+    trp = np.array([0, len(tail)], dtype=np.int64)
+    tc = np.empty(len(tail), np.float64)
+    assert lib.mirec_pos_cdf_build(trp.ctypes.data, 1, tail.ctypes.data, tc.ctypes.data) == 0
+    assert np.all(np.diff(tc) > 0) and tc[-1] == 1.0
+    assert np.array_equal(tc, np.cumsum(tail) / np.cumsum(tail)[-1])
+    assert np.any(np.diff(tc.astype(np.float32)) == 0)  # what a float CDF would have merged
     _ = ctypes
 
 

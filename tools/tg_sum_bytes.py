@@ -53,6 +53,7 @@ def counts(B=2048, fan=(25, 10), dim=128):
         else:  # targets with at least one valid child
             rows_once += int(((ids.view(nt, k) >= 0).any(1)).sum())
     distinct = int(torch.unique(valid).numel())
+    reuse = reuse_windows(groups)
     rb = dim * 4
     alg = 8 * n_ent + 4 * n_tgt + rb * rows_once + (rb + 4) * distinct
     return {"entries": n_ent, "valid_entries": int(valid.numel()), "targets": n_tgt,
@@ -60,7 +61,42 @@ def counts(B=2048, fan=(25, 10), dim=128):
             "groups": [(int(ids.numel()), nt, k) for ids, nt, k in groups],
             "algorithmic_bytes": alg,
             "pull_read_bytes": 8 * n_ent + 4 * n_tgt + rb * int(valid.numel()),
-            "write_bytes": (rb + 4) * distinct}
+            "write_bytes": (rb + 4) * distinct, "reuse": reuse}
+
+
+def reuse_windows(groups, windows=(8, 64, 512, 4096, 32768)):
+    """How much of the pull form's gradient-row re-reading a window of sorted
+    entries could absorb: the entries in sort order (row id, entry order),
+    each tagged with the gradient row it reads (its target's g_out row for a
+    fanout group, its own row for a k = 1 group); per window of W consecutive
+    sorted entries, the distinct gradient rows it reads.  distinct / entries
+    = the fraction of row reads a perfect W-entry reuse (LDS or cache) would
+    still issue; 1.0 = no reuse at that scale.  The VERDICT r5 variant (a
+    fanout group's entries ordered by (row, target)) changes only the order
+    inside a run of equal row ids, i.e. windows of one run."""
+    import torch
+    keys, src, base = [], [], 0
+    for ids, nt, k in groups:
+        ids = ids.view(-1)
+        e = torch.arange(ids.numel(), device=ids.device)
+        tgt = (e // k + base) if k > 1 else (e + base)
+        base += nt if k > 1 else ids.numel()
+        ok = ids >= 0
+        keys.append(ids[ok].long())
+        src.append(tgt[ok])
+    keys, src = torch.cat(keys), torch.cat(src)
+    order = torch.sort(keys, stable=True).indices
+    s = src[order]
+    k_sorted = keys[order]
+    runs = int(torch.unique_consecutive(k_sorted).numel())
+    out = {"valid_entries": int(s.numel()), "runs": runs,
+           "mean_run": round(s.numel() / max(runs, 1), 3)}
+    for W in windows:
+        m = s.numel() // W * W
+        blk = torch.sort(s[:m].view(-1, W), dim=1).values
+        d = int((blk[:, 1:] != blk[:, :-1]).sum()) + blk.shape[0]
+        out[f"distinct_per_entry_W{W}"] = round(d / max(m, 1), 4)
+    return out
 
 
 def pmc(dirname, counter, kernel="tg_sum_kernel"):
