@@ -122,6 +122,10 @@ SIGNATURES = {
                                 c_size_t, c_void_p, c_void_p]),
     "mirec_gather_rows_counted": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32,
                                           c_void_p, c_void_p]),
+    "mirec_route_pack": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int32, c_int64,
+                                 c_void_p, c_void_p]),
+    "mirec_gather_rows_routed": (c_int, [c_void_p, c_int64, c_void_p, c_int32, c_int32, c_int64,
+                                         c_int32, c_void_p, c_void_p]),
     "mirec_bpr_forward": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int32, c_int64,
                                   c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p,
                                   c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -354,6 +354,86 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(const float4 *__restr
     if (id[k] >= 0) dst[(int64_t)id[k] * d4 + c] = x[k];
 }
 
+// ------------------------------------------ capacity-bounded read-set routing
+// A micro-batch's read set (ascending ids, its count on the device) as one
+// fixed-capacity block per owner: block q at blocks + q·stride holds
+// [count_q, the ids of owner block q, unused up to cap].  The id all-to-all
+// then runs with equal splits and the counts travel in-band, so the planner
+// of the pipelined fetch exchange (dist.DenseGradDataParallel._plan_fetch)
+// enqueues every micro-batch's routing without reading a count on the host.
+constexpr int kRouteMaxParts = 256;
+
+__global__ __launch_bounds__(256) void rp_pack_kernel(const int32_t *__restrict__ ids,
+                                                      const int32_t *__restrict__ count,
+                                                      int64_t n_rows, int32_t parts, int32_t cap,
+                                                      int64_t stride, int32_t *__restrict__ blocks) {
+  __shared__ int32_t start[kRouteMaxParts + 1];
+  const int32_t n = count[0];
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x;
+  if (blockIdx.x > 0 && i0 >= n) return;  // (whole block: no barrier below is reached)
+  const int64_t per = n_rows / parts;
+  for (int q = threadIdx.x; q <= parts; q += blockDim.x)
+    start[q] = q == parts ? n : sr_lower_bound(ids, n, q * per);
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int q = threadIdx.x; q < parts; q += blockDim.x) blocks[q * stride] = start[q + 1] - start[q];
+  for (int64_t i = i0 + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t id = ids[i];
+    const int q = (int)min<int64_t>(id / per, parts - 1);
+    const int64_t pos = i - start[q];
+    if (pos < cap) blocks[q * stride + 1 + pos] = id;
+  }
+}
+
+// The owner side: out = the rows of table for the ids of the received
+// blocks, in source order (block q's rows at Σ_{p<q} min(count_p, cap)), on
+// a grid sized for the capacity; rows past the total, and ids outside
+// [0, n_rows) (zeros written), touch no table memory.
+__global__ __launch_bounds__(256) void rp_gather_kernel(const float4 *__restrict__ table,
+                                                        int64_t n_rows,
+                                                        const int32_t *__restrict__ blocks,
+                                                        int32_t parts, int32_t cap, int64_t stride,
+                                                        int32_t d4, int32_t lg,
+                                                        float4 *__restrict__ out) {
+  __shared__ int32_t off[kRouteMaxParts + 1];
+  if (threadIdx.x == 0) {
+    int32_t s = 0;
+    for (int q = 0; q < parts; ++q) {
+      off[q] = s;
+      s += min(max(blocks[q * stride], 0), cap);
+    }
+    off[parts] = s;
+  }
+  __syncthreads();
+  const int64_t total = off[parts];
+  const int per = 256 >> lg;
+  const int c = threadIdx.x & ((1 << lg) - 1);
+  const int64_t r0 = (int64_t)blockIdx.x * per * kRowRounds + (threadIdx.x >> lg);
+  if (r0 >= total || c >= d4) return;
+  int32_t id[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k) {
+    const int64_t r = r0 + k * per;
+    id[k] = -1;
+    if (r < total) {
+      int a = 0, b = parts;  // the last q with off[q] <= r
+      while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (off[m] <= r) a = m;
+        else b = m;
+      }
+      const int32_t v = blocks[a * stride + 1 + (r - off[a])];
+      id[k] = v >= 0 && v < n_rows ? v : -2;
+    }
+  }
+  float4 x[kRowRounds];
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k) x[k] = id[k] >= 0 ? table[(int64_t)id[k] * d4 + c] : f4_zero();
+#pragma unroll
+  for (int k = 0; k < kRowRounds; ++k)
+    if (id[k] != -1) out[(r0 + k * per) * d4 + c] = x[k];
+}
+
 }  // namespace mirec
 
 extern "C" int64_t mirec_distinct_rows_workspace(int64_t n_rows) {
@@ -452,6 +532,41 @@ extern "C" int mirec_gather_rows_counted(const float *src, const int32_t *rows,
   hipLaunchKernelGGL(gather_counted_kernel, dim3((unsigned)row_blocks(capacity, lg)), dim3(256), 0,
                      st, reinterpret_cast<const float4 *>(src), rows, count, dim / 4, lg,
                      reinterpret_cast<float4 *>(out));
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_route_pack(const int32_t *ids, const int32_t *count, int64_t capacity,
+                                int64_t n_rows, int32_t parts, int32_t cap, int64_t stride,
+                                int32_t *blocks, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(count && blocks && capacity >= 0 && n_rows >= 0 && cap >= 0);
+  MIREC_CHECK_ARG(capacity == 0 || ids);
+  MIREC_CHECK_ARG(parts >= 1 && parts <= kRouteMaxParts && stride >= (int64_t)cap + 1);
+  MIREC_CHECK_ARG(n_rows >= parts);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int64_t nb = std::min<int64_t>(std::max<int64_t>((capacity + 255) / 256, 1), 4096);
+  hipLaunchKernelGGL(rp_pack_kernel, dim3((unsigned)nb), dim3(256), 0, st, ids, count, n_rows,
+                     parts, cap, stride, blocks);
+  MIREC_LAUNCH_CHECK();
+  return MIREC_OK;
+}
+
+extern "C" int mirec_gather_rows_routed(const float *table, int64_t n_rows, const int32_t *blocks,
+                                        int32_t parts, int32_t cap, int64_t stride, int32_t dim,
+                                        float *out, mirec_stream_t stream) {
+  using namespace mirec;
+  MIREC_CHECK_ARG(table && blocks && out && n_rows >= 0 && cap >= 0 && dim > 0 && dim % 4 == 0);
+  MIREC_CHECK_ARG(parts >= 1 && parts <= kRouteMaxParts && stride >= (int64_t)cap + 1);
+  MIREC_CHECK_ARG(((uintptr_t)table & 15u) == 0 && ((uintptr_t)out & 15u) == 0);
+  const int64_t slots = (int64_t)parts * cap;
+  if (slots == 0) return MIREC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int lg = row_lg(dim / 4);
+  MIREC_CHECK_ARG(lg <= 8);
+  hipLaunchKernelGGL(rp_gather_kernel, dim3((unsigned)row_blocks(slots, lg)), dim3(256), 0, st,
+                     reinterpret_cast<const float4 *>(table), n_rows, blocks, parts, cap, stride,
+                     dim / 4, lg, reinterpret_cast<float4 *>(out));
   MIREC_LAUNCH_CHECK();
   return MIREC_OK;
 }

@@ -460,12 +460,14 @@ def _a2a(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None, 
 
 
 def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0,
-                  have: torch.Tensor | None = None) -> torch.Tensor:
+                  have: torch.Tensor | None = None, sync: bool = True):
     """Ascending distinct ids of the int32 device tensor ``ids`` in [0,
     n_rows) outside [lo, hi) (mirec_distinct_rows: byte map, block counts,
     ordered writes — no sort); one host sync for the count.  ``have`` (bool
     / uint8 [n_rows]): ids marked there are skipped, and the ids returned are
-    marked (mirec_distinct_rows_unseen)."""
+    marked (mirec_distinct_rows_unseen).  ``sync=False``: no host sync —
+    returns (the n_rows-long output buffer, the count int32 [1] on the
+    device)."""
     from . import _lib
     from ._lib import check, lib
     ids = ids.to(torch.int32).contiguous()
@@ -485,7 +487,42 @@ def distinct_rows(ids: torch.Tensor, n_rows: int, lo: int = 0, hi: int = 0,
                                              int(hi), have.data_ptr(), out.data_ptr(),
                                              cnt.data_ptr(), ws.data_ptr(), ws.numel(),
                                              _lib.stream_handle()), "distinct_rows_unseen")
+    if not sync:
+        return out, cnt
     return out[: int(cnt.item())]
+
+
+def route_pack(ids: torch.Tensor, count: torch.Tensor, n_rows: int, parts: int, cap: int,
+               blocks: torch.Tensor, stride: int) -> None:
+    """The ascending ids (``count`` int32 [1] of them valid, on the device)
+    as one block per owner at blocks[q·stride:]: [count_q, owner q's ids, ...
+    up to cap] — an all-to-all with equal splits moves them and the counts
+    travel in-band (mirec_route_pack; no host sync)."""
+    from . import _lib
+    from ._lib import check, lib
+    if blocks.dtype != torch.int32 or not blocks.is_contiguous() or \
+            blocks.numel() < (parts - 1) * stride + cap + 1:
+        raise ValueError("blocks: contiguous int32 holding parts blocks of stride words")
+    check(lib.mirec_route_pack(ids.data_ptr(), count.data_ptr(), ids.numel(), int(n_rows),
+                               int(parts), int(cap), int(stride), blocks.data_ptr(),
+                               _lib.stream_handle()), "route_pack")
+
+
+def gather_rows_routed(table: torch.Tensor, blocks: torch.Tensor, parts: int, cap: int,
+                       stride: int, out: torch.Tensor) -> None:
+    """The owner side of route_pack's blocks (received from every source):
+    out[...] = table rows of their ids in source order, the counts read on
+    the device (mirec_gather_rows_routed); ``out`` holds parts·cap rows."""
+    from . import _lib
+    from ._lib import check, lib
+    d = table.shape[1]
+    if out.shape[0] < parts * cap or out.shape[1] != d or not out.is_contiguous():
+        raise ValueError("out: contiguous [parts * cap, d]")
+    if blocks.numel() < (parts - 1) * stride + cap + 1:
+        raise ValueError("blocks shorter than parts blocks of stride words")
+    check(lib.mirec_gather_rows_routed(table.data_ptr(), table.shape[0], blocks.data_ptr(),
+                                       int(parts), int(cap), int(stride), d, out.data_ptr(),
+                                       _lib.stream_handle()), "gather_rows_routed")
 
 
 def export_stamped(tg, parts: int, ws: torch.Tensor | None = None):
@@ -735,6 +772,8 @@ class DenseGradDataParallel:
         # same ranks — dist.new_group must run on every process), else the
         # fetches share ``group`` (same results, no overlap).
         self._fetch_group = fetch_group
+        self._counts_host = None  # pipelined fetch: the planner's pinned counts
+        self._fetch_side = None  # pipelined fetch: the fetched rows' stream
         self._have = None  # pipelined fetch: rows fetched for an earlier micro-batch
         if (fetch_group is None and group is None and self.distributed and self.world > 1
                 and table_exchange == "fetch"):
@@ -965,6 +1004,20 @@ class DenseGradDataParallel:
 
     @torch.no_grad()
     def _plan_fetch(self, trees, st):
+        """Route every micro-batch's read set with no host round trip in the
+        planning: each read set (distinct rows outside the own block, rows
+        of earlier micro-batches skipped) is packed into fixed-capacity
+        blocks per owner with its count in-band (route_pack; capacity = the
+        smaller of the tree's row count and the largest owner block, so no
+        count can exceed it), an all-to-all with equal splits moves the
+        blocks, the owners gather the requested rows reading the counts on
+        the device (gather_rows_routed), and the send / receive counts go to
+        pinned host memory behind an event.  The host reads micro-batch k's
+        counts only when it issues k's rows (the uneven all-to-all needs its
+        splits): micro-batch 0's at the end of the planning, while the
+        device still plans the later micro-batches; the rows leave on a
+        stream of their own that waits only for their gather
+        (_fetch_issue)."""
         m = self.model
         if self._norms_next is not None:
             m._norm_cache = (self._norms_next, m._norm_token())
@@ -974,7 +1027,8 @@ class DenseGradDataParallel:
             return
         p = m._table_state.param
         N, d = p.shape
-        n_own = N // self.world
+        W, C = self.world, len(trees)
+        n_own = N // W
         lo = self.rank * n_own
         # the micro-batches' fetched-rows map: kept, cleared per step (a
         # 1-byte fill of the kept buffer: ~4 us against ~16 for torch.zeros)
@@ -983,40 +1037,92 @@ class DenseGradDataParallel:
         have = self._have
         have.zero_()
         a = self._event()
+        if self._counts_host is None or len(self._counts_host) < C or \
+                self._counts_host[0].shape != (2, W):
+            self._counts_host = [torch.empty(2, W, dtype=torch.int32, pin_memory=p.is_cuda)
+                                 for _ in range(max(C, 1))]
         for k, tree in enumerate(trees):
-            # rows fetched for an earlier micro-batch are skipped (and marked)
-            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, lo, lo + n_own,
-                                 have=have if len(trees) > 1 else None)
-            req, rc, sc = route_ids(need, N, self.group)
-            rows = gather_rows(p.data, req)  # owner side: the current rows
-            st["fetch"].append({"need": need, "rows": rows, "rc": rc, "sc": sc})
-            self.last_exchange_bytes += need.numel() * d * p.element_size() + \
-                (sum(rc) - rc[self.rank]) * 4
-            if k == 0:
-                # micro-batch 0's rows leave now (own communicator): they
-                # travel while the later read sets are planned
-                self._fetch_issue(0, st)
+            ids = torch.cat([g for g, _ in tree.groups])
+            cap = max(1, min(N - (W - 1) * n_own, ids.numel()))
+            seg = 1 + cap
+            buf, cnt = distinct_rows(ids, N, lo, lo + n_own, have=have if C > 1 else None,
+                                     sync=False)
+            send = torch.empty(W * seg, dtype=torch.int32, device=p.device)
+            route_pack(buf, cnt, N, W, cap, send, seg)
+            recv = torch.empty_like(send)
+            _a2a(recv, send, group=self.group)  # equal splits: one block of cap + 1 words a peer
+            host = self._counts_host[k]
+            host.copy_(torch.stack((send.view(W, seg)[:, 0], recv.view(W, seg)[:, 0])),
+                       non_blocking=True)
+            counted = torch.cuda.Event() if p.is_cuda else None
+            if counted is not None:
+                counted.record()
+            out = torch.empty(W * cap, d, dtype=p.dtype, device=p.device)
+            gather_rows_routed(p.data, recv, W, cap, seg, out)  # owner side: the current rows
+            gathered = torch.cuda.Event() if p.is_cuda else None
+            if gathered is not None:
+                gathered.record()
+            st["fetch"].append({"buf": buf, "out": out, "cap": cap, "host": host,
+                                "counted": counted, "gathered": gathered, "work": None})
+            self.last_exchange_bytes += (W - 1) * seg * 4
+        self._fetch_issue(0, st)
         self._note(a, self._event())
 
-    def _fetch_issue(self, k, st):
+    def _fetch_stream(self):
+        if self._fetch_side is None:
+            self._fetch_side = torch.cuda.Stream(device=self.model._table_state.param.device)
+        return self._fetch_side
+
+    def _fetch_issue(self, k, st, block=True):
+        """Send micro-batch k's requested rows (own communicator): read its
+        counts (``block=False``: only if they are on the host already) and
+        issue the uneven all-to-all on the fetch stream, which waits only
+        for k's gather.  Returns whether k's rows are in flight."""
         f = st["fetch"][k]
+        if f is None or "got" in f:
+            return True
+        if f["counted"] is not None:
+            if not block and not f["counted"].query():
+                return False
+            f["counted"].synchronize()
+        sc, rc = f["host"][0].tolist(), f["host"][1].tolist()
+        if max(sc + rc) > f["cap"]:
+            raise RuntimeError("read-set routing: an owner count above the block capacity")
         p = self.model._table_state.param
+        f["need"] = f["buf"][:sum(sc)]
+        rows = f["out"][:sum(rc)]
         f["got"] = torch.empty(f["need"].numel(), p.shape[1], dtype=p.dtype, device=p.device)
-        f["work"] = self._a2a_async(f["got"], f["rows"], f["sc"], f["rc"],
-                                    group=self._fetch_group)
+        self.last_exchange_bytes += f["need"].numel() * p.shape[1] * p.element_size()
+        if f["gathered"] is None:  # (host tensors: no streams)
+            f["work"] = self._a2a_async(f["got"], rows, sc, rc, group=self._fetch_group)
+            return True
+        side = self._fetch_stream()
+        with torch.cuda.stream(side):
+            side.wait_event(f["gathered"])
+            f["work"] = self._a2a_async(f["got"], rows, sc, rc, group=self._fetch_group)
+        rows.record_stream(side)
+        f["got"].record_stream(side)
+        return True
 
     @torch.no_grad()
     def _fetch_wait(self, k, st):
+        """Before micro-batch k's forward: its rows installed (the current
+        stream waits for their transfer), and k + 1's rows sent if their
+        counts are on the host already (else after k's backward is issued,
+        _route_chunk — the host never waits while the device idles)."""
         if not st["fetch"]:
             return
         f = st["fetch"][k]
+        self._fetch_issue(k, st)  # (issued by now but for a count read that was not ready)
         a = self._event()
         if f["work"] is not None:
             f["work"].wait()
+        if f["gathered"] is not None:
+            torch.cuda.current_stream().wait_stream(self._fetch_stream())
         self._note(a, self._event())
         scatter_rows(self.model._table_state.param.data, f["need"], f["got"])
         if k + 1 < len(st["fetch"]):
-            self._fetch_issue(k + 1, st)  # in flight while micro-batch k computes
+            self._fetch_issue(k + 1, st, block=False)  # in flight while micro-batch k computes
         st["fetch"][k] = None
 
     @torch.no_grad()
@@ -1025,6 +1131,8 @@ class DenseGradDataParallel:
         the device (no host sync, export_stamped), then send micro-batch
         k - 1's — whose counts are ready by now, while k computes — so the
         host never waits for the micro-batch it has just issued."""
+        if st["fetch"] and k + 1 < len(st["fetch"]):
+            self._fetch_issue(k + 1, st)  # (if _fetch_wait(k) found its counts not ready)
         tg = self.model._tg
         rows, vals, counts, self._sr_ws = export_stamped(tg, self.world, self._sr_ws)
         ev = torch.cuda.Event()

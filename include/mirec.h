@@ -317,6 +317,25 @@ int mirec_gather_rows_counted(const float *src, const int32_t *rows, const int32
                               int64_t capacity, int32_t dim, float *out,
                               mirec_stream_t stream);
 
+/* Capacity-bounded routing of a read set (the pipelined fetch exchange's
+ * planner; replaces the per-read-set count read of ddp_sage.py:800-806's
+ * exchange).  mirec_route_pack: ids ascending int32, *count (device) of them
+ * valid, capacity = the ids buffer's length; writes one block per owner q
+ * (contiguous row blocks of n_rows / parts, the last to n_rows) at
+ * blocks + q*stride: blocks[q*stride] = the count of owner q's ids, then up
+ * to cap of them (stride >= cap + 1; a count above cap is written as it is,
+ * its ids past cap dropped: the host checks counts <= cap).  parts <= 256.
+ * mirec_gather_rows_routed: the owner side over received blocks of that
+ * layout: out[Σ_{p<q} min(c_p, cap) + j, :] = table[id_{q,j}, :], in source
+ * order; out holds parts*cap rows of dim floats (ids outside [0, n_rows)
+ * give zero rows). */
+int mirec_route_pack(const int32_t *ids, const int32_t *count, int64_t capacity, int64_t n_rows,
+                     int32_t parts, int32_t cap, int64_t stride, int32_t *blocks,
+                     mirec_stream_t stream);
+int mirec_gather_rows_routed(const float *table, int64_t n_rows, const int32_t *blocks,
+                             int32_t parts, int32_t cap, int64_t stride, int32_t dim, float *out,
+                             mirec_stream_t stream);
+
 /* ------------------------------------------------------------------------ */
 /* BPR (model/lgcn.py:98-133)                                                */
 /* ------------------------------------------------------------------------ */

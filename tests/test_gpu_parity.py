@@ -3996,6 +3996,46 @@ def test_distinct_rows_unseen_excludes_earlier_sets(n_rows, n):
         assert torch.equal(have, seen)
 
 
+@pytest.mark.parametrize("n_rows,n,parts,cap", [(1_100_000, 880_000, 8, 137_500),
+                                                (4097, 10_000, 2, 2049), (8, 3, 8, 1),
+                                                (70_001, 0, 1, 5), (5000, 5000, 3, 700),
+                                                (1000, 900, 4, 300)])
+def test_route_pack_and_routed_gather(n_rows, n, parts, cap):
+    """The pipelined planner's capacity-bounded routing: route_pack writes
+    per owner block q (contiguous n_rows / parts rows, the last to n_rows)
+    its count in-band and its ids (up to cap: (5000, 3, 700) and (1000, 4,
+    300) overflow some blocks — the count stays the true one, the ids past
+    cap are dropped), with no host read of the device count; gather_rows_
+    routed over those blocks == the table rows of the kept ids in block
+    order, past the total nothing written."""
+    from furusato_recommend_amd.dist import distinct_rows, gather_rows_routed, route_pack
+    g = torch.Generator(device="cuda").manual_seed(n_rows + n + parts)
+    ids = torch.randint(0, n_rows, (n,), device="cuda", generator=g, dtype=torch.int32)
+    buf, cnt = distinct_rows(ids, n_rows, sync=False)
+    u = torch.unique(ids.long()).cpu().numpy()
+    stride = cap + 3  # (blocks need not be packed)
+    blocks = torch.full((parts * stride,), -7, dtype=torch.int32, device="cuda")
+    route_pack(buf, cnt, n_rows, parts, cap, blocks, stride)
+    b = blocks.cpu().numpy()
+    per = n_rows // parts
+    owner = np.minimum(u // per, parts - 1)
+    kept = []
+    for q in range(parts):
+        mine = u[owner == q]
+        assert b[q * stride] == mine.size, q
+        k = min(mine.size, cap)
+        assert np.array_equal(b[q * stride + 1: q * stride + 1 + k], mine[:k]), q
+        assert (b[q * stride + 1 + k: (q + 1) * stride] == -7).all()
+        kept.append(mine[:k])
+    kept = np.concatenate(kept)
+    table = torch.randn(n_rows, 16, device="cuda", generator=g)
+    out = torch.full((parts * cap, 16), 5.0, device="cuda")
+    gather_rows_routed(table, blocks, parts, cap, stride, out)
+    got = out.cpu()
+    assert torch.equal(got[:kept.size], table.cpu()[torch.from_numpy(kept).long()])
+    assert bool((got[kept.size:] == 5.0).all())
+
+
 @pytest.mark.parametrize("n_rows,n,parts", [(1_100_000, 880_000, 8), (4097, 10_000, 2),
                                             (8, 3, 8), (70_001, 0, 1), (5000, 5000, 3)])
 def test_export_stamped_matches_nonzero(n_rows, n, parts):

@@ -57,6 +57,9 @@ def main():
                     help="sage: table exchanges to simulate")
     ap.add_argument("--rates", default="100,200,300,400",
                     help="sage: link rates (GB/s of received bytes per rank) to project at")
+    ap.add_argument("--no-step-sync", action="store_true",
+                    help="pipelined C3: no synchronisation after each timed step (rounds 4-6 "
+                         "synchronise, to read the step's events)")
     ap.add_argument("--microbatches", default="1",
                     help="sage fetch: comma list of micro-batch counts C (the pipelined "
                          "exchange; C = 1 is the unpipelined step)")
@@ -279,7 +282,7 @@ def sage_pipelined(args, m, W, C, base, rates):
     micro-batch k - 1's routed rows overlap micro-batch k's compute (HIP
     events around it), the last micro-batch's routed rows are exposed."""
     from furusato_recommend_amd.dist import (DenseGradDataParallel, distinct_rows, export_stamped,
-                                             gather_rows, scatter_rows)
+                                             gather_rows_routed, route_pack, scatter_rows)
     dev = torch.device("cuda:0")
     side = torch.cuda.Stream(device=dev)
     B = args.batch
@@ -314,20 +317,51 @@ def sage_pipelined(args, m, W, C, base, rates):
             m._norm_cache = (rec.pop("norms"), m._norm_token())
         have = rec.setdefault("have", torch.empty(N, dtype=torch.uint8, device=dev))
         have.zero_()  # (as dist._plan_fetch: a kept map)
-        rec["need"], rec["fetch_rows"], rec["plan_ev"] = [], [], []
-        for tree in trees:
-            need = distinct_rows(torch.cat([g for g, _ in tree.groups]), N, 0, n_own, have=have)
-            # the owners' gather of the requested rows (rank 0 serves a share of
-            # the same size) and the install after the transfer
-            rec["need"].append((need.long(), gather_rows(m._table.data, need)))
-            rec["fetch_rows"].append(need.numel())
+        # as dist._plan_fetch: every read set packed into capacity-bounded
+        # owner blocks with in-band counts, the owners' gathers reading the
+        # counts on the device (rank 0 serves requests of the same size as
+        # its own: its own blocks stand in for the received ones — the id
+        # all-to-all's bytes are projected), the counts to pinned memory
+        # behind an event; the host reads micro-batch 0's at the end of the
+        # planning (the device still plans the later ones), k's before k
+        hosts = rec.setdefault("hosts", [torch.empty(W, dtype=torch.int32, pin_memory=True)
+                                         for _ in range(C)])
+        rec["plan"], rec["plan_ev"], rec["fetch_rows"] = [], [], []
+        rec["id_bytes"] = []
+        for k, tree in enumerate(trees):
+            ids = torch.cat([g for g, _ in tree.groups])
+            cap = max(1, min(N - (W - 1) * n_own, ids.numel()))
+            seg = 1 + cap
+            rec["id_bytes"].append((W - 1) * seg * 4)
+            buf, cnt = distinct_rows(ids, N, 0, n_own, have=have, sync=False)
+            send = torch.empty(W * seg, dtype=torch.int32, device=dev)
+            route_pack(buf, cnt, N, W, cap, send, seg)
+            hosts[k].copy_(send.view(W, seg)[:, 0], non_blocking=True)
+            counted = torch.cuda.Event()
+            counted.record()
+            out = torch.empty(W * cap, d, device=dev)
+            gather_rows_routed(m._table.data, send, W, cap, seg, out)
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            rec["plan_ev"].append(e)  # micro-batch 0's fetch leaves at the first
+            rec["plan_ev"].append(e)  # micro-batch 0's rows leave at the first
+            rec["plan"].append((buf, out, hosts[k], counted))
+        rec["need"] = [None] * C
+        read(0)
         rec["ev"] = []
+
+    def read(k):
+        buf, out, host, counted = rec["plan"][k]
+        counted.synchronize()
+        n = int(host.sum())
+        # the install after the transfer: the fetched rows (rank 0's own
+        # gather output stands in for them: same count)
+        rec["need"][k] = (buf[:n], out[:n])
+        rec["fetch_rows"].append(n)
 
     def chunk_hook(k, phase):
         if phase == "pre":
+            if rec["need"][k] is None:
+                read(k)
             need, rows = rec["need"][k]
             scatter_rows(m._table.data, need, rows)
             e = torch.cuda.Event(enable_timing=True)
@@ -388,27 +422,33 @@ def sage_pipelined(args, m, W, C, base, rates):
     chunk_ms = [0.0] * C
     fetch_rows = [0] * C
     plan_rest_ms = 0.0  # planning of micro-batches 1.. (device), after micro-batch 0's fetch left
+    kept = []  # each step's events, read after the timed loop
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        torch.cuda.synchronize()
-        for k in range(C):
-            chunk_ms[k] += rec["ev"][k][0].elapsed_time(rec["ev"][k][1]) / args.steps
-            fetch_rows[k] += rec["fetch_rows"][k] / args.steps
-        pe = rec["plan_ev"]
-        plan_rest_ms += pe[0].elapsed_time(pe[-1]) / args.steps
+        kept.append((rec["ev"], rec["plan_ev"], rec["fetch_rows"]))
+        if not args.no_step_sync:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / args.steps * 1e3
+    for ev, pe, fr in kept:
+        for k in range(C):
+            chunk_ms[k] += ev[k][0].elapsed_time(ev[k][1]) / args.steps
+            fetch_rows[k] += fr[k] / args.steps
+        plan_rest_ms += pe[0].elapsed_time(pe[-1]) / args.steps
     small_b = sum(q.numel() for q in m.parameters() if q is not m._table) * 4
     fetch_b = [f * row_b for f in fetch_rows]
     route_b = route_other / C  # the other ranks' routed rows, per micro-batch
-    recv = sum(fetch_b) + route_other + 2 * (W - 1) * small_b // W
+    id_b = rec["id_bytes"]  # the capacity-bounded id blocks (equal-split all-to-alls)
+    recv = sum(id_b) + sum(fetch_b) + route_other + 2 * (W - 1) * small_b // W
     proj = {}
     for r in rates:
         rate = r * 1e6  # bytes per ms
-        # micro-batch 0's rows (own communicator, dist._plan_fetch) travel
-        # while the later micro-batches' read sets are planned
-        exposed = max(0.0, fetch_b[0] / rate - plan_rest_ms) + route_b / rate + \
-            2 * (W - 1) * small_b / W / rate
+        # micro-batch 0's id blocks precede its gather (exposed); its rows
+        # (own communicator, dist._plan_fetch) travel, with the later
+        # micro-batches' id blocks, while those are planned
+        exposed = id_b[0] / rate + max(0.0, (fetch_b[0] + sum(id_b[1:])) / rate - plan_rest_ms) + \
+            route_b / rate + 2 * (W - 1) * small_b / W / rate
         for k in range(C):
             hidden = ((fetch_b[k + 1] if k + 1 < C else 0.0) + (route_b if k > 0 else 0.0)) / rate
             exposed += max(0.0, hidden - chunk_ms[k])
@@ -422,9 +462,11 @@ def sage_pipelined(args, m, W, C, base, rates):
                       "fetched_rows_per_chunk": [int(x) for x in fetch_rows],
                       "routed_rows_from_others": int(route_other // row_b),
                       "recv_bytes_per_rank": int(recv),
-                      "projection": "compute (measured, no transfers) + what of the first "
-                                    "micro-batch's rows exceeds the later micro-batches' "
-                                    "planning + the last's routed rows + the "
+                      "id_block_bytes": [int(x) for x in id_b],
+                      "projection": "compute (measured, no transfers) + micro-batch 0's id "
+                                    "blocks + what of its rows and the later id blocks "
+                                    "exceeds the later micro-batches' planning + the last's "
+                                    "routed rows + the "
                                     "small bucket + whatever of micro-batch k+1's rows and "
                                     "k-1's routed rows exceeds micro-batch k's compute",
                       "projected": proj}), flush=True)
