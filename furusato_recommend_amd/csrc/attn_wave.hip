@@ -391,9 +391,11 @@ __global__ __launch_bounds__(64 * kUnitsPerWG) void attnw_bwd_dkdv_kernel(
 // packs[5 + 8p + 2s] = (first row, length) of the sequence in slot s of pack
 // p, (0, 0) for an empty slot — the descriptor the backward workgroup reads
 // with two 16-byte loads, no dependent load of the offsets.  Over the same
-// order, each sequence of 49-64 or 33-48 positions (4 / 3 blocks of 16) is a
-// pack of its own, those of 17-32 go two to a pack and those of 1-16 four to
-// a pack (empty sequences in none): mirec_attention_packed_bwd's workgroups.
+// order, each sequence of 49-64 positions (4 blocks of 16) is a pack of its
+// own; each of 33-48 (3 blocks) takes a sequence of 1-16 (1 block) into its
+// fourth wave while there are any (the longest of each); those of 17-32 go
+// two to a pack and the remaining 1-16 four to a pack (empty sequences in
+// none): mirec_attention_packed_bwd's workgroups, longest first.
 __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__restrict__ offsets,
                                                            int64_t batch,
                                                            int32_t *__restrict__ order,
@@ -409,7 +411,7 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
     return;
   }
   __shared__ int cnt[kMaxT + 1], start[kMaxT + 1];
-  __shared__ int cls_start[5], cls_count[5], pack_base[5];
+  __shared__ int cls_start[5], cls_count[5], pack_base[5], n31;
   for (int i = threadIdx.x; i <= kMaxT; i += blockDim.x) cnt[i] = 0;
   __syncthreads();
   for (int64_t b = threadIdx.x; b < batch; b += blockDim.x)
@@ -424,13 +426,16 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
     // classes by block count k = ceil(L / 16), contiguous in the order
     for (int k = 0; k <= 4; ++k) cls_count[k] = 0;
     for (int L = 0; L <= kMaxT; ++L) cls_count[(L + kBlk - 1) / kBlk] += cnt[L];
+    // 3-block sequences carry a 1-block one in their idle fourth wave
+    n31 = min(cls_count[3], cls_count[1]);
     int pos = 0, pb = 0;
     for (int k = 4; k >= 1; --k) {
       const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
+      const int alone = k == 1 ? cls_count[1] - n31 : cls_count[k];  // in packs of class k
       cls_start[k] = pos;
       pack_base[k] = pb;
       pos += cls_count[k];
-      pb += (cls_count[k] + per - 1) / per;
+      pb += (alone + per - 1) / per;
     }
     cls_start[0] = pos;
     pack_base[0] = pb;  // = the pack count
@@ -446,7 +451,10 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
       int k = 4;
       while (k > 1 && p >= pack_base[k - 1]) --k;
       const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
-      const int used = min(per, cls_count[k] - (p - pack_base[k]) * per);
+      const int i = p - pack_base[k];
+      const int used = k == 3   ? 1 + (i < n31 ? 1 : 0)
+                       : k == 1 ? min(per, cls_count[1] - n31 - i * per)
+                                : min(per, cls_count[k] - i * per);
       for (int sl = used; sl < 4; ++sl) {
         packs[4 + 8 * (int64_t)p + 2 * sl] = 0;
         packs[5 + 8 * (int64_t)p + 2 * sl] = 0;
@@ -461,7 +469,13 @@ __global__ __launch_bounds__(1024) void length_order_kernel(const int32_t *__res
     if (packs != nullptr && k > 0) {
       const int per = k >= 3 ? 1 : (k == 2 ? 2 : 4);
       const int i = pos - cls_start[k];
-      const int64_t slot = 4 + 8 * (int64_t)(pack_base[k] + i / per) + 2 * (i % per);
+      int64_t slot;
+      if (k == 1 && i < n31)  // slot 1 of the i-th 3-block pack (blocks 3)
+        slot = 4 + 8 * (int64_t)(pack_base[3] + i) + 2;
+      else {
+        const int ia = k == 1 ? i - n31 : i;
+        slot = 4 + 8 * (int64_t)(pack_base[k] + ia / per) + 2 * (ia % per);
+      }
       packs[slot] = offsets[b];
       packs[slot + 1] = L;
     }
