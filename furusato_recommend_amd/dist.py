@@ -1091,17 +1091,21 @@ class DenseGradDataParallel:
         p = self.model._table_state.param
         f["need"] = f["buf"][:sum(sc)]
         rows = f["out"][:sum(rc)]
-        f["got"] = torch.empty(f["need"].numel(), p.shape[1], dtype=p.dtype, device=p.device)
+        shape = (f["need"].numel(), p.shape[1])
         self.last_exchange_bytes += f["need"].numel() * p.shape[1] * p.element_size()
         if f["gathered"] is None:  # (host tensors: no streams)
+            f["got"] = torch.empty(shape, dtype=p.dtype, device=p.device)
             f["work"] = self._a2a_async(f["got"], rows, sc, rc, group=self._fetch_group)
             return True
         side = self._fetch_stream()
         with torch.cuda.stream(side):
             side.wait_event(f["gathered"])
+            # allocated on the fetch stream: a block the current stream
+            # freed may still be in use by its queued kernels, which this
+            # stream does not wait for
+            f["got"] = torch.empty(shape, dtype=p.dtype, device=p.device)
             f["work"] = self._a2a_async(f["got"], rows, sc, rc, group=self._fetch_group)
         rows.record_stream(side)
-        f["got"].record_stream(side)
         return True
 
     @torch.no_grad()
@@ -1121,6 +1125,8 @@ class DenseGradDataParallel:
             torch.cuda.current_stream().wait_stream(self._fetch_stream())
         self._note(a, self._event())
         scatter_rows(self.model._table_state.param.data, f["need"], f["got"])
+        if f["gathered"] is not None:  # (read here, allocated on the fetch stream)
+            f["got"].record_stream(torch.cuda.current_stream())
         if k + 1 < len(st["fetch"]):
             self._fetch_issue(k + 1, st, block=False)  # in flight while micro-batch k computes
         st["fetch"][k] = None
