@@ -183,9 +183,6 @@ SIGNATURES = {
     "mirec_table_grad_sorted_rows": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
                                              c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                              c_size_t, c_void_p]),
-    "mirec_key_sort_workspace": (c_int, [c_int64, c_int32, POINTER(c_size_t)]),
-    "mirec_key_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
-                                     c_int32, c_void_p, c_size_t, c_void_p]),
     "mirec_table_grad_atomic": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                         c_int32, c_void_p]),
     "mirec_table_grad_dense": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32,

@@ -140,32 +140,3 @@ def gather_rows_norm(table: torch.Tensor, ids: torch.Tensor, split: int | None =
         return a.view(*ids.shape, table.shape[1]), norm
     return a, b, norm
 
-
-def key_sort_pairs(keys: torch.Tensor, n_keys: int, vals: torch.Tensor | None = None,
-                   offsets: bool = False):
-    """Stable sort of int32 (key, value) pairs by key for keys in [0, n_keys)
-    (mirec_key_sort_pairs, a counting sort): returns (keys_sorted,
-    vals_sorted) — equal keys in input order; vals None = the positions —
-    and, with ``offsets``, the [n_keys + 1] bucket starts.  The table-
-    gradient sums sort their entries this way (tablegrad.hip)."""
-    import ctypes
-    keys = keys.reshape(-1).to(torch.int32).contiguous()
-    if not keys.is_cuda:
-        raise ValueError("key_sort_pairs: device keys")
-    n = keys.numel()
-    if vals is not None:
-        vals = vals.reshape(-1).to(torch.int32).contiguous()
-        if vals.numel() != n:
-            raise ValueError("key_sort_pairs: vals and keys differ in length")
-    ko = torch.empty_like(keys)
-    vo = torch.empty_like(keys)
-    off = torch.empty(n_keys + 1, dtype=torch.int32, device=keys.device) if offsets else None
-    nb = ctypes.c_size_t()
-    check(lib.mirec_key_sort_workspace(n, n_keys, ctypes.byref(nb)), "key_sort_workspace")
-    ws = torch.empty(max(nb.value, 1), dtype=torch.uint8, device=keys.device)
-    check(lib.mirec_key_sort_pairs(keys.data_ptr(), vals.data_ptr() if vals is not None else None,
-                                   ko.data_ptr(), vo.data_ptr(),
-                                   off.data_ptr() if off is not None else None, n, n_keys,
-                                   ws.data_ptr(), nb.value, _lib.stream_handle()),
-          "key_sort_pairs")
-    return (ko, vo, off) if offsets else (ko, vo)

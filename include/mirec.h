@@ -632,22 +632,6 @@ int mirec_table_grad_sorted_rows(const mirec_row_grad_group_t *groups, int32_t n
                                  float *vals, int32_t *counts, void *workspace,
                                  size_t workspace_bytes, mirec_stream_t stream);
 
-/* Stable sort of n (int32 key, int32 value) pairs by key, keys dense ids in
- * [0, nk) (a key outside is sorted as nk - 1): keys_out / vals_out = the
- * pairs in ascending key order, equal keys in input order — bit for bit a
- * stable radix sort's result.  vals_in NULL = the identity (value i for pair
- * i); offsets (optional, [nk + 1]) = each key's first position, offsets[nk] =
- * n.  A counting sort (keysort.hip): bucket counts summed per tile in LDS,
- * one scatter, the order inside each bucket restored deterministically —
- * the table-gradient key sorts of mirec_table_grad_sorted use it.  n <=
- * 2^27; no host synchronisation; workspace: mirec_key_sort_workspace bytes.
- * Replaces the device-library radix sort behind the GraphSAGE / SASRec
- * embedding-gradient sums (reference: graphsage.py:311-324, sasrec.py:437-474). */
-int mirec_key_sort_workspace(int64_t n, int32_t nk, size_t *bytes);
-int mirec_key_sort_pairs(const int32_t *keys_in, const int32_t *vals_in, int32_t *keys_out,
-                         int32_t *vals_out, int32_t *offsets, int64_t n, int32_t nk,
-                         void *workspace, size_t workspace_bytes, mirec_stream_t stream);
-
 /* The same S in the atomic form, for plain groups only (k = 1, mean = 0,
  * dropout_p = 0): touched rows stamped and zeroed, then every gradient row
  * added with float atomics — two launches, no workspace; the summation
