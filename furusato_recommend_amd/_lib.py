@@ -183,16 +183,6 @@ SIGNATURES = {
     "mirec_table_grad_sorted_rows": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
                                              c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
                                              c_size_t, c_void_p]),
-    "mirec_table_grad_sorted_pull": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
-                                             c_void_p, c_void_p, c_int32, c_void_p, c_void_p,
-                                             c_size_t, c_void_p]),
-    "mirec_table_grad_resolve": (c_int, [POINTER(RowGradGroup), c_int32, c_int32, c_int32,
-                                         c_void_p, c_void_p, c_int32, c_void_p, c_size_t,
-                                         c_void_p]),
-    "mirec_adam_table_pull": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
-                                      c_void_p, c_int32, c_int64, c_int32, POINTER(AdamH),
-                                      c_void_p, c_void_p, c_void_p, POINTER(RowGradGroup),
-                                      c_int32, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mirec_table_grad_atomic": (c_int, [c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p,
                                         c_int32, c_void_p]),
     "mirec_table_grad_dense": (c_int, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_int32,

@@ -179,7 +179,7 @@ __device__ __forceinline__ int grp_bcast(int x, int base, int u) {
 // only the rows stay live during the loads).  Only entries lo <= u < hi load
 // (the others were not decoded: their addresses are null).
 template <int LPR>
-__device__ __forceinline__ void tg_rows(int base, int col, bool act, unsigned want, uint64_t am,
+__device__ __forceinline__ void tg_rows(int base, int col, bool act, int lo, int hi, uint64_t am,
                                         uint64_t hm, uint32_t thm, float wm,
                                         float4 (&x)[kCh]) {
   const uint32_t am_lo = (uint32_t)am, am_hi = (uint32_t)(am >> 32);
@@ -188,7 +188,7 @@ __device__ __forceinline__ void tg_rows(int base, int col, bool act, unsigned wa
   for (int u = 0; u < kCh; ++u) {
     const uint64_t a = (uint64_t)(uint32_t)grp_bcast<LPR>((int)am_lo, base, u) |
                        ((uint64_t)(uint32_t)grp_bcast<LPR>((int)am_hi, base, u) << 32);
-    x[u] = (act && ((want >> u) & 1u)) ? ldg4(reinterpret_cast<const float *>(a) + col) : f4_zero();
+    x[u] = (act && u >= lo && u < hi) ? ldg4(reinterpret_cast<const float *>(a) + col) : f4_zero();
   }
 #pragma unroll
   for (int u = 0; u < kCh; ++u) {
@@ -247,16 +247,11 @@ __device__ __forceinline__ void tg_load_raw(const int32_t *__restrict__ keys,
 }
 
 // One chunk of pass 1 from its loaded keys / indices (see below).
-// Which runs a pass-1 launch sums (the pull form of the fused Adam,
-// mirec_table_grad_sorted_pull, splits them): all, only the LONG runs' segments
-// (partial slots; pass 2 finishes them), or only the SHORT runs (final rows).
-enum TgMode { kTgAll = 0, kTgLong = 1, kTgShort = 2 };
-
 template <int LPR>
 __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t d, int32_t n_rows,
                                          const TgOut &o, float *__restrict__ part,
                                          int64_t chunk, int sub,
-                                         int base, const TgRaw &r, int mode) {
+                                         int base, const TgRaw &r) {
   const int64_t beg = chunk * kCh;
   const int64_t end = beg + kCh < n ? beg + kCh : n;
   const int64_t xend = end + kCh < n ? end + kCh : n;  // the window after the chunk
@@ -284,9 +279,8 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
   const bool last_from_before = cont_in && klast == kprev;  // the run covers the chunk
   const unsigned long long diff_out = (__ballot(in_win && kx != klast) >> base) & kmask;
   const bool out_short = cont_out && !last_from_before && (diff_out != 0 || xend < end + kCh);
-  const int n_ext = (out_short && mode != kTgLong)
-                        ? (diff_out != 0 ? (int)__builtin_ctzll(diff_out) : (int)(xend - end))
-                        : 0;
+  const int n_ext =
+      out_short ? (diff_out != 0 ? (int)__builtin_ctzll(diff_out) : (int)(xend - end)) : 0;
   uint64_t am = 0, hm = 0, am2 = 0, hm2 = 0;
   uint32_t thm = 0, thm2 = 0;
   float wm = 0.f, wm2 = 0.f;
@@ -295,25 +289,6 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
   // valid entries of the chunk: up to the first invalid id (they sort last)
   const unsigned long long bad = (__ballot(in_chunk && km >= n_rows) >> base) & kmask;
   const int nval = bad != 0 ? (int)__builtin_ctzll(bad) : nin;
-  const unsigned span = ((1u << nval) - 1u) & ~((1u << skip) - 1u);  // entries [skip, nval)
-  unsigned want = span;
-  if (mode != kTgAll) {
-    // the entries of long-run segments: the run entering the chunk when it is
-    // long (its entries before the first id change), the run leaving it when
-    // it is long (from the last id change on)
-    unsigned lmask = 0;
-    if (cont_in && !in_short)
-      lmask |= diff_in != 0 ? (1u << __builtin_ctzll(diff_in)) - 1u : (1u << nin) - 1u;
-    if (cont_out && !out_short) {
-      const int32_t kl = __shfl(km, base + (sub > 0 ? sub - 1 : 0));
-      const unsigned long long bnd =
-          (__ballot(in_chunk && sub > 0 && km != kl) >> base) & kmask;
-      const int last_start = bnd != 0 ? 63 - __builtin_clzll(bnd) : 0;
-      lmask |= ((1u << nval) - 1u) & ~((1u << last_start) - 1u);
-    }
-    want = mode == kTgLong ? (span & lmask) : (span & ~lmask);
-    if (want == 0 && n_ext == 0) return;  // (group-uniform) nothing of this mode here
-  }
   for (int c0 = 0; c0 < d; c0 += 4 * LPR) {
     const int col = c0 + 4 * sub;
     const bool act = col < d;
@@ -321,7 +296,7 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
     // both at once measured slower — 127 VGPRs, four waves per SIMD instead
     // of five: pass 1 263 vs 226 us at C3, profiles/round4_tg_bench.jsonl)
     float4 x[kCh];
-    tg_rows<LPR>(base, col, act, want, am, hm, thm, wm, x);
+    tg_rows<LPR>(base, col, act, skip, nval, am, hm, thm, wm, x);
     int32_t cur = -1;
     int64_t seg_beg = 0;
     float4 acc = f4_zero();
@@ -330,8 +305,6 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
     auto close = [&](int64_t pos) {
       const bool cont_prev = seg_beg == beg && cont_in && !in_short;
       const bool cont_next = pos == end && cont_out && !out_short;
-      const bool partial = cont_prev || cont_next;
-      if ((mode == kTgLong && !partial) || (mode == kTgShort && partial)) return;
       float *dst;
       if (!cont_prev && !cont_next) {
         if (o.slot != nullptr) {  // a final row starts at its run's head: seg_beg
@@ -364,7 +337,7 @@ __device__ __forceinline__ void tg_chunk(const GroupArgs &ga, int64_t n, int32_t
       }
     }
     if (n_ext > 0) {  // the rest of the last run (id klast == cur), in order
-      tg_rows<LPR>(base, col, act, (1u << n_ext) - 1u, am2, hm2, thm2, wm2, x);
+      tg_rows<LPR>(base, col, act, 0, n_ext, am2, hm2, thm2, wm2, x);
 #pragma unroll
       for (int u = 0; u < kCh; ++u)
         if (u < n_ext) acc = f4_add(acc, x[u]);
@@ -380,7 +353,7 @@ template <int LPR>
 __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t *__restrict__ keys,
                                                      const int2 *__restrict__ plan, int64_t n,
                                                      int32_t d, int32_t n_rows, TgOut o,
-                                                     float *__restrict__ part, int mode) {
+                                                     float *__restrict__ part) {
   static_assert(LPR >= kCh, "chunk layout: one entry per lane");
   const int lane = threadIdx.x & 63;
   const int sub = lane & (LPR - 1);
@@ -390,7 +363,7 @@ __global__ __launch_bounds__(256) void tg_sum_kernel(GroupArgs ga, const int32_t
   if (group >= n_chunks) return;  // the whole group leaves together
   TgRaw r;
   tg_load_raw(keys, plan, o.slot, n, group, sub, r);
-  tg_chunk<LPR>(ga, n, d, n_rows, o, part, group, sub, base, r, mode);
+  tg_chunk<LPR>(ga, n, d, n_rows, o, part, group, sub, base, r);
 }
 
 // Pass 2a: block sums of long runs.  Block b = chunks [G b, G b + G) lies
@@ -661,106 +634,6 @@ __global__ __launch_bounds__(256) void tg_adam_kernel(float *__restrict__ param,
     if ((int)threadIdx.x < s) {
       red[0][threadIdx.x] += red[0][threadIdx.x + s];
       red[1][threadIdx.x] += red[1][threadIdx.x + s];
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    sumsq[2 * blockIdx.x] = red[0][0];
-    sumsq[2 * blockIdx.x + 1] = red[1][0];
-  }
-}
-
-// S of a short run in the pull form: its entries' rows weighted / masked
-// and added in entry order from zero — tg_rows and tg_chunk's adds exactly
-// (the same row loads, the same drop4_hq / f4_scale, the same f4_add chain),
-// so the sum is bitwise pass 1's.  Eight rows in flight per batch; the
-// entry's plan is decoded again after the loads instead of being held.
-__device__ __forceinline__ float4 tg_pull(const GroupArgs &ga, const int2 *__restrict__ plan,
-                                          int32_t beg, int len, int32_t d, int col) {
-  float4 acc = f4_zero();
-  for (int u0 = 0; u0 < len; u0 += kCh) {
-    int2 pl[kCh];
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) pl[u] = u0 + u < len ? plan[beg + u0 + u] : make_int2(0, 0);
-    float4 x[kCh];
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      x[u] = f4_zero();
-      if (u0 + u < len) {
-        uint64_t am, hm;
-        uint32_t thm;
-        float wm;
-        tg_decode(ga, pl[u], d, am, hm, thm, wm);
-        x[u] = ldg4(reinterpret_cast<const float *>(am) + col);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      if (u0 + u < len) {
-        uint64_t am, hm;
-        uint32_t thm;
-        float wm;
-        tg_decode(ga, pl[u], d, am, hm, thm, wm);
-        const float4 y = thm != 0u ? drop4_hq(x[u], hm + (uint64_t)(col >> 2), thm, wm)
-                                   : f4_scale(wm, x[u]);
-        acc = f4_add(acc, y);
-      }
-    }
-  }
-  return acc;
-}
-
-// tg_adam_kernel in the pull form (mirec_adam_table_pull): row r's S is
-// acc[r] when stamp[r] == gen (a long run, summed by passes 1 + 2), else its
-// short run summed here (runs[r] of this generation: tg_runs_kernel), else
-// 0.  The table-gradient pass then never writes the short runs' rows and
-// this pass never reads them back: the ~0.26 GB round trip of the C3 step
-// goes, and the pass's gathers (Infinity-Cache hits) overlap this kernel's
-// HBM stream.  Same element mapping, the same G = fma(c, W, S) and block
-// partials as tg_adam_kernel: bitwise its result.
-__global__ __launch_bounds__(256) void tg_adam_pull_kernel(
-    GroupArgs ga, const int2 *__restrict__ plan, const int2 *__restrict__ runs,
-    float *__restrict__ param, float *__restrict__ m, float *__restrict__ v,
-    const float *__restrict__ coef, int64_t n_user, const float *__restrict__ acc,
-    const int32_t *__restrict__ stamp, int32_t gen, int64_t n_rows, int32_t d4, int32_t shift,
-    mirec_adam_hparams_t h_arg, const mirec_adam_hparams_t *__restrict__ h_dev,
-    float *__restrict__ sumsq) {
-  __shared__ float red[2][256];
-  const mirec_adam_hparams_t h = h_dev != nullptr ? *h_dev : h_arg;
-  const float cu = coef ? coef[0] : 0.f, ci = coef ? coef[1] : 0.f;
-  const int64_t n4 = n_rows * d4;
-  float su = 0.f, si = 0.f;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    float4 p = adam_ld4(param + 4 * i), a = adam_ld4(m + 4 * i), b = adam_ld4(v + 4 * i);
-    const int64_t r = row_of(i, d4, shift);
-    const int32_t sr = stamp[r];
-    const int2 ru = runs[r];
-    float4 s = f4_zero();
-    if (sr == gen) s = ld4(acc + 4 * i);
-    else if ((ru.y >> 4) == gen) s = tg_pull(ga, plan, ru.x, ru.y & 15, 4 * d4, (int)(4 * (i - r * d4)));
-    const float cc = r < n_user ? cu : ci;
-    const float4 g = make_float4(fmaf(cc, p.x, s.x), fmaf(cc, p.y, s.y), fmaf(cc, p.z, s.z),
-                                 fmaf(cc, p.w, s.w));
-    adam1(p.x, a.x, b.x, g.x, h);
-    adam1(p.y, a.y, b.y, g.y, h);
-    adam1(p.z, a.z, b.z, g.z, h);
-    adam1(p.w, a.w, b.w, g.w, h);
-    st4(param + 4 * i, p);
-    st4(m + 4 * i, a);
-    st4(v + 4 * i, b);
-    const float q = p.x * p.x + p.y * p.y + p.z * p.z + p.w * p.w;
-    if (r < n_user) su += q;
-    else si += q;
-  }
-  if (sumsq == nullptr) return;
-  red[0][threadIdx.x] = su;
-  red[1][threadIdx.x] = si;
-  __syncthreads();
-  for (int q = 128; q > 0; q >>= 1) {
-    if ((int)threadIdx.x < q) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + q];
-      red[1][threadIdx.x] += red[1][threadIdx.x + q];
     }
     __syncthreads();
   }
@@ -1095,8 +968,22 @@ extern "C" int mirec_table_grad_atomic(const mirec_row_grad_group_t *groups, int
   return MIREC_OK;
 }
 
-static int make_group_args(const mirec_row_grad_group_t *groups, int32_t n_groups, GroupArgs &ga) {
-  ga = GroupArgs{};
+// The sorted accumulate into `o` (dense or compact; compact: also the
+// counts [1 + parts]).
+static int tg_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups, int32_t n_rows,
+                     int32_t dim, TgOut o, int32_t parts, int32_t *counts, void *workspace,
+                     size_t workspace_bytes, mirec_stream_t stream) {
+  TgLayout L;
+  const int rc = tg_layout(groups, n_groups, n_rows, dim, &L);
+  if (rc != MIREC_OK) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (L.n_ent == 0) {
+    if (counts != nullptr) MIREC_HIP(hipMemsetAsync(counts, 0, 4 * (size_t)(1 + parts), st));
+    return MIREC_OK;
+  }
+  MIREC_CHECK_ARG(workspace);
+  if (workspace_bytes < L.total) return MIREC_ERR_WORKSPACE;
+  GroupArgs ga = {};
   ga.n_groups = n_groups;
   for (int g = 0; g < kMaxGroups; ++g) {
     const bool real = g < n_groups;
@@ -1118,51 +1005,6 @@ static int make_group_args(const mirec_row_grad_group_t *groups, int32_t n_group
     ga.thresh[g] = th;
     ga.scale[g] = sc;
   }
-  return MIREC_OK;
-}
-
-// Pull form: the run of every row touched this step whose entries pass 1
-// sums whole (a SHORT run, TgMode) — runs[r] = (first sorted entry, gen << 4
-// | length), length 1..15 — so that the fused Adam can sum it itself
-// (tg_adam_pull_kernel).  A run is short iff it ends before the end of the
-// chunk after its head's chunk, or the array ends there (tg_chunk's
-// in_short / out_short, from the run's own side).  Long runs are not
-// listed: pass 1 + pass 2 store them into acc / stamp as before.
-__global__ __launch_bounds__(256) void tg_runs_kernel(const int32_t *__restrict__ keys, int64_t n,
-                                                      int32_t n_rows, int32_t gen,
-                                                      int2 *__restrict__ runs) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const int32_t k = keys[e];
-  if (k >= n_rows || (e > 0 && keys[e - 1] == k)) return;
-  const int64_t w = (e / kCh) * kCh + 2 * kCh;  // end of the window after the head's chunk
-  const int64_t lim = w < n ? w : n;
-  int64_t E = e + 1;
-  while (E < lim && keys[E] == k) ++E;
-  if (E == w && w <= n) return;  // reached the window's end: long
-  runs[k] = make_int2((int32_t)e, (gen << 4) | (int32_t)(E - e));
-}
-
-// The sorted accumulate into `o` (dense or compact; compact: also the
-// counts [1 + parts]).  mode kTgLong (pull form, dense output only) also
-// lists the short runs in `runs`; kTgShort sums only those (resolve).
-static int tg_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups, int32_t n_rows,
-                     int32_t dim, TgOut o, int32_t parts, int32_t *counts, void *workspace,
-                     size_t workspace_bytes, mirec_stream_t stream, int mode = kTgAll,
-                     int2 *runs = nullptr) {
-  TgLayout L;
-  const int rc = tg_layout(groups, n_groups, n_rows, dim, &L);
-  if (rc != MIREC_OK) return rc;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (L.n_ent == 0) {
-    if (counts != nullptr) MIREC_HIP(hipMemsetAsync(counts, 0, 4 * (size_t)(1 + parts), st));
-    return MIREC_OK;
-  }
-  MIREC_CHECK_ARG(workspace);
-  if (workspace_bytes < L.total) return MIREC_ERR_WORKSPACE;
-  GroupArgs ga;
-  const int rg = make_group_args(groups, n_groups, ga);
-  if (rg != MIREC_OK) return rg;
   char *ws = static_cast<char *>(workspace);
   int32_t *keys_in = reinterpret_cast<int32_t *>(ws + L.keys_in);
   int32_t *keys_out = reinterpret_cast<int32_t *>(ws + L.keys_out);
@@ -1172,23 +1014,16 @@ static int tg_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups, int
   int2 *plan = reinterpret_cast<int2 *>(ws + L.plan);
   float *part = reinterpret_cast<float *>(ws + L.part);
   float *bsum = reinterpret_cast<float *>(ws + L.bsum);
-  if (mode != kTgShort) {  // (resolve: the sort and plan of the pull form's call are reused)
-    const int64_t nprep = std::max(L.n_ent, L.n_tgt);
-    hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
-                       L.n_ent, L.n_tgt, n_rows, keys_in, vals_in, wt);
-    MIREC_LAUNCH_CHECK();
-    size_t sort_bytes = L.sort_bytes;
-    MIREC_HIP(tg_sort(ws + L.sort, sort_bytes, keys_in, keys_out, vals_in, vals_out, (int)L.n_ent,
-                      L.end_bit, st));
-    hipLaunchKernelGGL(tg_plan_kernel, dim3((unsigned)((L.n_ent + 255) / 256)), dim3(256), 0, st,
-                       ga, vals_out, wt, L.n_ent, plan);
-    MIREC_LAUNCH_CHECK();
-  }
-  if (mode == kTgLong) {
-    hipLaunchKernelGGL(tg_runs_kernel, dim3((unsigned)((L.n_ent + 255) / 256)), dim3(256), 0, st,
-                       keys_out, L.n_ent, n_rows, o.gen, runs);
-    MIREC_LAUNCH_CHECK();
-  }
+  const int64_t nprep = std::max(L.n_ent, L.n_tgt);
+  hipLaunchKernelGGL(tg_prep_kernel, dim3((unsigned)((nprep + 255) / 256)), dim3(256), 0, st, ga,
+                     L.n_ent, L.n_tgt, n_rows, keys_in, vals_in, wt);
+  MIREC_LAUNCH_CHECK();
+  size_t sort_bytes = L.sort_bytes;
+  MIREC_HIP(tg_sort(ws + L.sort, sort_bytes, keys_in, keys_out, vals_in, vals_out, (int)L.n_ent,
+                    L.end_bit, st));
+  hipLaunchKernelGGL(tg_plan_kernel, dim3((unsigned)((L.n_ent + 255) / 256)), dim3(256), 0, st,
+                     ga, vals_out, wt, L.n_ent, plan);
+  MIREC_LAUNCH_CHECK();
   int32_t *slot = reinterpret_cast<int32_t *>(ws + L.slot);
   if (o.vals != nullptr) {  // compact: the run heads' slots
     size_t sb = L.scan_bytes;
@@ -1206,9 +1041,8 @@ static int tg_sorted(const mirec_row_grad_group_t *groups, int32_t n_groups, int
 #define MIREC_TG_LAUNCH(LP)                                                                   \
   case LP:                                                                                   \
     hipLaunchKernelGGL(tg_sum_kernel<LP>, grid, dim3(256), 0, st, ga,        \
-                       keys_out, plan, L.n_ent, dim, n_rows, o, part, mode);                  \
+                       keys_out, plan, L.n_ent, dim, n_rows, o, part);                        \
     MIREC_LAUNCH_CHECK();                                                                    \
-    if (mode == kTgShort) break;                                                             \
     if (n_blocks > 0) {                                                                      \
       hipLaunchKernelGGL(tg_block_kernel<LP>, dim3((unsigned)((n_blocks * LP + 255) / 256)),  \
                          dim3(256), 0, st, keys_out, L.n_ent, dim, n_rows, part, bsum);       \
@@ -1242,26 +1076,6 @@ extern "C" int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int
   MIREC_CHECK_ARG(acc && stamp);
   return tg_sorted(groups, n_groups, n_rows, dim, TgOut{acc, stamp, gen, nullptr, nullptr, nullptr},
                    1, nullptr, workspace, workspace_bytes, stream);
-}
-
-extern "C" int mirec_table_grad_sorted_pull(const mirec_row_grad_group_t *groups, int32_t n_groups,
-                                            int32_t n_rows, int32_t dim, float *acc,
-                                            int32_t *stamp, int32_t gen, int32_t *runs,
-                                            void *workspace, size_t workspace_bytes,
-                                            mirec_stream_t stream) {
-  MIREC_CHECK_ARG(acc && stamp && runs && gen > 0 && gen < (1 << 27));
-  return tg_sorted(groups, n_groups, n_rows, dim, TgOut{acc, stamp, gen, nullptr, nullptr, nullptr},
-                   1, nullptr, workspace, workspace_bytes, stream, kTgLong,
-                   reinterpret_cast<int2 *>(runs));
-}
-
-extern "C" int mirec_table_grad_resolve(const mirec_row_grad_group_t *groups, int32_t n_groups,
-                                        int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
-                                        int32_t gen, void *workspace, size_t workspace_bytes,
-                                        mirec_stream_t stream) {
-  MIREC_CHECK_ARG(acc && stamp && gen > 0);
-  return tg_sorted(groups, n_groups, n_rows, dim, TgOut{acc, stamp, gen, nullptr, nullptr, nullptr},
-                   1, nullptr, workspace, workspace_bytes, stream, kTgShort);
 }
 
 extern "C" int mirec_table_grad_sorted_rows(const mirec_row_grad_group_t *groups,
@@ -1324,46 +1138,6 @@ static int adam_table(float *param, float *exp_avg, float *exp_avg_sq, const flo
   hipLaunchKernelGGL(tg_adam_kernel, dim3(blocks), dim3(256), 0, st, param, exp_avg, exp_avg_sq,
                      coef, n_user, acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4), h0,
                      h ? nullptr : h_dev, sumsq);
-  MIREC_LAUNCH_CHECK();
-  if (norms) {
-    hipLaunchKernelGGL(tg_norm_final_kernel, dim3(1), dim3(1024), 0, st, sumsq, (int64_t)blocks,
-                       norms);
-    MIREC_LAUNCH_CHECK();
-  }
-  return MIREC_OK;
-}
-
-extern "C" int mirec_adam_table_pull(float *param, float *exp_avg, float *exp_avg_sq,
-                                     const float *coef, int64_t n_user, const float *acc,
-                                     const int32_t *stamp, int32_t gen, int64_t n_rows,
-                                     int32_t dim, const mirec_adam_hparams_t *h,
-                                     const mirec_adam_hparams_t *h_device, float *sumsq,
-                                     float *norms, const mirec_row_grad_group_t *groups,
-                                     int32_t n_groups, const int32_t *runs,
-                                     const void *workspace, size_t workspace_bytes,
-                                     mirec_stream_t stream) {
-  MIREC_CHECK_ARG(param && exp_avg && exp_avg_sq && acc && stamp && runs && workspace &&
-                  ((h != nullptr) != (h_device != nullptr)) && n_rows >= 0 && dim > 0 &&
-                  dim % 4 == 0 && n_user >= 0 && n_user <= n_rows);
-  MIREC_CHECK_ARG(((uintptr_t)param | (uintptr_t)exp_avg | (uintptr_t)exp_avg_sq |
-                   (uintptr_t)acc) % 16 == 0);
-  MIREC_CHECK_ARG((sumsq == nullptr) == (norms == nullptr));
-  TgLayout L;
-  const int rc = tg_layout(groups, n_groups, (int32_t)n_rows, dim, &L);
-  if (rc != MIREC_OK) return rc;
-  if (workspace_bytes < L.total) return MIREC_ERR_WORKSPACE;
-  GroupArgs ga;
-  const int rg = make_group_args(groups, n_groups, ga);
-  if (rg != MIREC_OK) return rg;
-  if (n_rows == 0) return MIREC_OK;
-  hipStream_t st = (hipStream_t)stream;
-  const int64_t n4 = n_rows * (dim / 4);
-  const unsigned blocks = tg_blocks(n4);
-  const mirec_adam_hparams_t h0 = h ? *h : mirec_adam_hparams_t{};
-  const int2 *plan = reinterpret_cast<const int2 *>(static_cast<const char *>(workspace) + L.plan);
-  hipLaunchKernelGGL(tg_adam_pull_kernel, dim3(blocks), dim3(256), 0, st, ga, plan,
-                     reinterpret_cast<const int2 *>(runs), param, exp_avg, exp_avg_sq, coef, n_user,
-                     acc, stamp, gen, n_rows, dim / 4, pow2_shift(dim / 4), h0, h_device, sumsq);
   MIREC_LAUNCH_CHECK();
   if (norms) {
     hipLaunchKernelGGL(tg_norm_final_kernel, dim3(1), dim3(1024), 0, st, sumsq, (int64_t)blocks,

@@ -543,8 +543,6 @@ def export_stamped(tg, parts: int, ws: torch.Tensor | None = None):
         if counts.numel() != 1 + parts:
             raise ValueError("table gradient exported for another world size")
         return rows, vals, counts, ws
-    if hasattr(tg, "resolve"):
-        tg.resolve()  # a pull-form accumulate: the short runs into acc / stamp first
     N, d, dev = tg.n_rows, tg.dim, tg.acc.device
     nb = max(int(lib.mirec_distinct_rows_workspace(N)), 16)
     if ws is None or ws.numel() < nb:
@@ -757,12 +755,6 @@ class DenseGradDataParallel:
             if self.world > 1 or table_exchange != "dense":
                 tg.dense = table_exchange == "dense"
             model._tg_routed = table_exchange != "dense"
-            # S exported / exchanged (or a captured split step that replays the
-            # accumulate without the host state a pull form needs): the plain
-            # sorted sum; a lone process with the dense exchange (its hook does
-            # nothing) keeps the single-GPU pull form
-            if self.distributed or table_exchange != "dense":
-                tg.pull = False
         self._norms_next = None  # fetch: the table's slice norms after the last update
         self._sharded = set()  # ids of the parameters whose Adam runs sharded
         self._ones = None      # the routed Adam's all-stamped shard
@@ -849,7 +841,6 @@ class DenseGradDataParallel:
         """This rank's touched table rows (ascending int32) and their rows of
         S, the sparse term of the table gradient (a host sync: the count)."""
         tg = self.model._tg
-        tg.resolve()
         rows = torch.nonzero(tg.stamp == tg.gen).view(-1).to(torch.int32)
         return rows, tg.acc.index_select(0, rows.long())
 

@@ -91,15 +91,6 @@ class TableGrad:
         # sees S = 0, never stale rows)
         self.rows_parts = None
         self.export = None
-        # pull form (single GPU, S consumed by adam()): the accumulate sums only
-        # the long runs into acc / stamp and lists the short ones in ``runs``;
-        # the fused Adam sums those itself (mirec_adam_table_pull, bitwise the
-        # same S).  Anything else that reads acc / stamp calls resolve() first.
-        self.pull = True
-        self.runs = torch.zeros(n_rows, 2, dtype=torch.int32, device=device)
-        self._pull = None  # (groups array, n, kept gradient tensors) of a pending pull
-        self.last_adam_pull = False
-        self.targets = 0
 
     def accumulate(self, groups):
         """groups: [(ids int32, grad_out [n_t, d], k, mean, dropout p, seed)]."""
@@ -107,7 +98,6 @@ class TableGrad:
         if not 1 <= n <= _lib.TABLE_GRAD_MAX_GROUPS:
             raise ValueError("table gradient: 1..8 row groups")
         self.entries = sum(int(g[0].numel()) for g in groups)  # bounds the rows stamped
-        self.targets = sum(int(g[0].numel()) // int(g[2]) for g in groups)  # gradient rows
         arr = (_lib.RowGradGroup * n)()
         keep = []
         for a, (ids, g, k, mean, p, seed) in zip(arr, groups):
@@ -143,40 +133,15 @@ class TableGrad:
             self.export = (rows, vals, counts)
             self.pending = True
             return
-        if self.pull and not self.dense and self.gen < (1 << 27):
-            check(lib.mirec_table_grad_sorted_pull(arr, n, self.n_rows, self.dim,
-                                                   self.acc.data_ptr(), self.stamp.data_ptr(),
-                                                   self.gen, self.runs.data_ptr(),
-                                                   self._ws.data_ptr(), self._ws.numel(),
-                                                   _lib.stream_handle()), "table_grad_sorted_pull")
-            self._pull = (arr, n, keep)  # the gradient rows the Adam will read
-            self.pending = True
-            return
         check(lib.mirec_table_grad_sorted(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
                                           self.stamp.data_ptr(), self.gen, self._ws.data_ptr(),
                                           self._ws.numel(), _lib.stream_handle()),
               "table_grad_sorted")
         self.pending = True
 
-    def resolve(self):
-        """Store the short runs of a pending pull-form accumulate into acc /
-        stamp (a no-op otherwise): acc / stamp then hold all of S, bit for
-        bit what the plain sorted accumulate stores."""
-        if self._pull is None:
-            return
-        arr, n, _ = self._pull
-        check(lib.mirec_table_grad_resolve(arr, n, self.n_rows, self.dim, self.acc.data_ptr(),
-                                           self.stamp.data_ptr(), self.gen, self._ws.data_ptr(),
-                                           self._ws.numel(), _lib.stream_handle()),
-              "table_grad_resolve")
-        self._pull = None
-
     def _next_gen(self):
-        self._pull = None
         if self.static:
             self.stamp.zero_()
-            if self.pull:
-                self.runs.zero_()
             self.gen = 1
         else:
             self.gen += 1
@@ -190,7 +155,6 @@ class TableGrad:
 
     def materialize(self, table: torch.Tensor) -> torch.Tensor:
         """G as a dense [N, d] tensor."""
-        self.resolve()
         grad = torch.empty_like(table)
         check(lib.mirec_table_grad_dense(table.data_ptr(), self.coef.data_ptr(), self.n_user,
                                          self.acc.data_ptr(), self.stamp.data_ptr(), self.gen,
@@ -216,19 +180,7 @@ class TableGrad:
         if ev is not None:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-        self.last_adam_pull = False
-        if self._pull is not None:
-            arr, n, _ = self._pull
-            hp = state.next_hparams() if h_dev is None else None
-            check(lib.mirec_adam_table_pull(*args, ctypes.byref(hp) if hp is not None else None,
-                                            h_dev.data_ptr() if h_dev is not None else None,
-                                            _lib.ptr(sumsq), _lib.ptr(norms), arr, n,
-                                            self.runs.data_ptr(), self._ws.data_ptr(),
-                                            self._ws.numel(), _lib.stream_handle()),
-                  "adam_table_pull")
-            self._pull = None
-            self.last_adam_pull = True
-        elif h_dev is None:
+        if h_dev is None:
             hp = state.next_hparams()
             check(lib.mirec_adam_table(*args, ctypes.byref(hp), _lib.ptr(sumsq), _lib.ptr(norms),
                                        _lib.stream_handle()), "adam_table")

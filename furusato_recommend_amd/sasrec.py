@@ -1333,11 +1333,6 @@ class _CapturedStep:
         self.turn = 0
         if model._tg is not None:
             model._tg.static = True  # the generation is baked into the graph
-            if split is not None:
-                # the host hook between the two graphs may read S (materialize)
-                # on every replay, which the pull form's host-side state does
-                # not follow: the plain sorted sum in a split step
-                model._tg.pull = False
         pool = model.__dict__.setdefault("_graph_pool", torch.cuda.graph_pool_handle())
         params = list(model.parameters())
         snap = [p.detach().clone() for p in params]

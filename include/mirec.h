@@ -618,26 +618,6 @@ int mirec_table_grad_sorted(const mirec_row_grad_group_t *groups, int32_t n_grou
                             int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
                             void *workspace, size_t workspace_bytes, mirec_stream_t stream);
 
-/* Pull form (the single-GPU fused Adam): the same sort, but pass 1 sums only
- * the LONG runs (hub ids, through the partial slots and pass 2) into acc /
- * stamp; every SHORT run (<= 15 entries, ending before the end of the chunk
- * after its head's — nearly all of them) is listed instead: runs[2 r] = its
- * first sorted entry, runs[2 r + 1] = gen << 4 | its length (runs [n_rows, 2]
- * int32, zero-initialised, never cleared; gen < 2^27).
- * mirec_adam_table_pull then sums each short run itself, bitwise as pass 1
- * would, so those rows of S are never written or read back.  The workspace
- * (sorted keys, the entries' plans) and the groups' gradient rows must stay
- * unchanged until that Adam (or mirec_table_grad_resolve) has run.
- * mirec_table_grad_resolve stores the short runs too (acc / stamp then equal
- * mirec_table_grad_sorted's, bit for bit), for a consumer that reads S. */
-int mirec_table_grad_sorted_pull(const mirec_row_grad_group_t *groups, int32_t n_groups,
-                                 int32_t n_rows, int32_t dim, float *acc, int32_t *stamp,
-                                 int32_t gen, int32_t *runs, void *workspace,
-                                 size_t workspace_bytes, mirec_stream_t stream);
-int mirec_table_grad_resolve(const mirec_row_grad_group_t *groups, int32_t n_groups,
-                             int32_t n_rows, int32_t dim, float *acc, int32_t *stamp, int32_t gen,
-                             void *workspace, size_t workspace_bytes, mirec_stream_t stream);
-
 /* The same S packed (the data-parallel exchanges' export): rows[j] = the
  * j-th touched row id ascending and vals[j] its row of S, j < counts[0];
  * counts[1 + p] = the touched rows in owner block p (rows [p N/P, (p + 1)
@@ -696,19 +676,6 @@ int mirec_adam_table_dev(float *param, float *exp_avg, float *exp_avg_sq, const 
                          int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
                          int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h_device,
                          float *sumsq, float *norms, mirec_stream_t stream);
-
-/* mirec_adam_table in the pull form: S of the short runs of the last
- * mirec_table_grad_sorted_pull (same groups, workspace and runs) summed in
- * the kernel; the long runs' rows from acc / stamp.  Exactly one of h (host
- * hyper-parameters) and h_device (read when the kernel runs) is given.
- * Bitwise mirec_adam_table after mirec_table_grad_sorted. */
-int mirec_adam_table_pull(float *param, float *exp_avg, float *exp_avg_sq, const float *coef,
-                          int64_t n_user, const float *acc, const int32_t *stamp, int32_t gen,
-                          int64_t n_rows, int32_t dim, const mirec_adam_hparams_t *h,
-                          const mirec_adam_hparams_t *h_device, float *sumsq, float *norms,
-                          const mirec_row_grad_group_t *groups, int32_t n_groups,
-                          const int32_t *runs, const void *workspace, size_t workspace_bytes,
-                          mirec_stream_t stream);
 
 /* coef[i] = norm[i*norm_stride] > 0 ? g[i*g_stride] / norm[i*norm_stride] : 0
  * for i < n (<= 1024): a table gradient's norm-term coefficients. */

@@ -3427,7 +3427,6 @@ def test_table_grad_runs_of_every_length_and_alignment(d):
         gr = torch.randn(q.numel() // k, d, generator=g)
         groups.append((q.int().cuda(), gr.cuda(), k, mean, p, sd))
     tg = TableGrad(n_rows, 2000, d, "cuda")
-    tg.pull = False  # the plain sorted sum (the pull form: test_table_grad_pull_*)
     tg.accumulate(groups)
     a1, st = tg.acc.clone(), tg.stamp.clone()
     tg.accumulate(groups)
@@ -3465,7 +3464,6 @@ def test_table_grad_sorted_matches_fp64_and_repeats(d, hub):
     n_rows = 5000
     groups = _tg_groups(n_rows, d, seed=d + hub, hub_count=hub)
     tg = TableGrad(n_rows, 2000, d, "cuda")
-    tg.pull = False
     tg.accumulate(groups)
     a1 = tg.acc.clone()
     st = tg.stamp.clone()
@@ -3498,7 +3496,6 @@ def test_table_grad_packed_rows_equal_dense_form(d, hub, parts):
     n_rows = 5000
     groups = _tg_groups(n_rows, d, seed=d + hub + 1, hub_count=hub)
     tg = TableGrad(n_rows, 2000, d, "cuda")
-    tg.pull = False
     tg.accumulate(groups)
     rows_ref = torch.nonzero(tg.stamp == tg.gen).view(-1).int()
     vals_ref = tg.acc[rows_ref.long()].clone()
@@ -3517,93 +3514,6 @@ def test_table_grad_packed_rows_equal_dense_form(d, hub, parts):
     hi = torch.cat([lo[1:], torch.tensor([n_rows], device="cuda")])
     ref_counts = ((rows_ref[None, :] >= lo[:, None]) & (rows_ref[None, :] < hi[:, None])).sum(1)
     assert torch.equal(counts[1:].long(), ref_counts)
-
-
-def _tg_groups_runs(d, seed=0, n_rows=6000):
-    """Row groups whose sorted runs take every length 1..40 plus 100 / 300 /
-    1000 (long runs through the partials) and 7..17 (the short / long edge
-    of the chunk window), invalid ids among them; an inner and a dropout
-    mean leaf group."""
-    g = torch.Generator().manual_seed(d + seed)
-    lens = torch.randint(1, 41, (1500,), generator=g)
-    lens = torch.cat([lens, torch.tensor([100, 300, 1000, 17, 9, 8, 7, 16, 15])])
-    ids = torch.repeat_interleave(torch.randperm(n_rows, generator=g)[:lens.numel()], lens)
-    ids = ids[torch.randperm(ids.numel(), generator=g)]
-    ids[::53] = -1
-    n_inner = (ids.numel() // 3) // 10 * 10
-    inner, leaf = ids[:n_inner], ids[n_inner:]
-    leaf = leaf[: leaf.numel() // 10 * 10]
-    out = []
-    for q, k, mean, p, sd in ((inner, 1, 0, 0.0, 0), (leaf, 10, 1, 0.2, 21)):
-        gr = torch.randn(q.numel() // k, d, generator=g)
-        out.append((q.int().cuda(), gr.cuda(), k, mean, p, sd))
-    return out
-
-
-@pytest.mark.parametrize("d", [16, 128, 256])
-@pytest.mark.parametrize("kind", ["runs", "hub", "plain"])
-def test_table_grad_pull_adam_equals_sorted_adam(d, kind):
-    """The pull form (mirec_table_grad_sorted_pull: long runs only, the short
-    runs listed; mirec_adam_table_pull sums them in the kernel) == the sorted
-    sum + mirec_adam_table, bitwise — table, both moments and the slice
-    norms, over three steps; and resolve() leaves acc / stamp bitwise the
-    plain sorted sum's (touched rows, stamps)."""
-    from furusato_recommend_amd.engine import AdamState
-    from furusato_recommend_amd.graphsage import TableGrad
-    n_rows, nu = (6000, 2500) if kind == "runs" else (5000, 2000)
-    if kind == "runs":
-        groups = _tg_groups_runs(d)
-    else:
-        groups = _tg_groups(n_rows, d, seed=d + 5, hub_count=200_000 if kind == "hub" else 0)
-    torch.manual_seed(1)
-    w0 = torch.randn(n_rows, d, device="cuda") * 0.1
-    ta, tb = TableGrad(n_rows, nu, d, "cuda"), TableGrad(n_rows, nu, d, "cuda")
-    ta.pull = False
-    for t in (ta, tb):
-        t.coef.copy_(torch.tensor([1e-3, -2e-3]))
-    wa, wb = w0.clone(), w0.clone()
-    sa, sb = AdamState(wa, 1e-3), AdamState(wb, 1e-3)
-    for it in range(3):
-        ta.accumulate(groups)
-        tb.accumulate(groups)
-        assert tb._pull is not None and ta._pull is None
-        na, nb = torch.empty(2, device="cuda"), torch.empty(2, device="cuda")
-        ta.adam(sa, na)
-        tb.adam(sb, nb)
-        for x, y in ((wa, wb), (sa.exp_avg, sb.exp_avg), (sa.exp_avg_sq, sb.exp_avg_sq),
-                     (na, nb)):
-            assert torch.equal(x, y), (it, int((x != y).sum()))
-    # resolve: the short runs stored too -> the plain sum's acc / stamp
-    ta.accumulate(groups)
-    tb.accumulate(groups)
-    tb.resolve()
-    sa_, sb_ = ta.stamp == ta.gen, tb.stamp == tb.gen
-    assert torch.equal(sa_, sb_)
-    assert torch.equal(ta.acc[sa_], tb.acc[sb_])
-    assert tb._pull is None
-
-
-def test_table_grad_pull_static_generations():
-    """A static TableGrad (the captured SASRec step: stamps and runs cleared,
-    generation 1 every step) in the pull form, alternating two row-group
-    sets: every step's Adam == the plain sorted form's, bitwise (no stale
-    run of the other set is ever pulled)."""
-    from furusato_recommend_amd.engine import AdamState
-    from furusato_recommend_amd.graphsage import TableGrad
-    n_rows, nu, d = 6000, 2500, 128
-    sets = [_tg_groups_runs(d, seed=1), _tg_groups_runs(d, seed=2)]
-    w0 = torch.randn(n_rows, d, device="cuda") * 0.1
-    ta, tb = TableGrad(n_rows, nu, d, "cuda"), TableGrad(n_rows, nu, d, "cuda")
-    ta.pull = False
-    ta.static = tb.static = True
-    wa, wb = w0.clone(), w0.clone()
-    sa, sb = AdamState(wa, 1e-3), AdamState(wb, 1e-3)
-    for it in range(4):
-        ta.accumulate(sets[it % 2])
-        tb.accumulate(sets[it % 2])
-        ta.adam(sa)
-        tb.adam(sb)
-        assert torch.equal(wa, wb) and torch.equal(sa.exp_avg_sq, sb.exp_avg_sq), it
 
 
 def test_fused_table_adam_equals_dense_adam():

@@ -149,19 +149,10 @@ def main():
         ms = sum(a.elapsed_time(b) for a, b in tg.adam_events) / len(tg.adam_events)
         touched = int((tg.stamp == tg.gen).sum())
         nbytes = 6 * tg.n_rows * tg.dim * 4 + tg.n_rows * 4 + touched * tg.dim * 4
-        kname = "tg_adam_kernel (fused table Adam)"
-        if tg.last_adam_pull:
-            # pull form: + the runs map (8 B per row), each gradient row of the
-            # tree read once (its target rows: sum of n_targets, the distinct
-            # rows the short runs gather) and each pulled entry's 8-B plan;
-            # `touched` (stamp == gen) is now the long runs' rows only
-            nbytes += tg.n_rows * 8 + tg.targets * tg.dim * 4 + tg.entries * 8
-            kname = "tg_adam_pull_kernel (fused table Adam + short-run sums)"
-        roof = {"bound": "hbm", "kernel": kname,
+        roof = {"bound": "hbm", "kernel": "tg_adam_kernel (fused table Adam)",
                 "achieved": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(nbytes / (ms * 1e-3) / 1e9 / 8000.0, 4),
-                "traffic": None if tg.last_adam_pull else 3660805737,
-                "traffic_source": None if tg.last_adam_pull else "profiles/round3d_pmc_tg_adam.json",
+                "traffic": 3660805737, "traffic_source": "profiles/round3d_pmc_tg_adam.json",
                 "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
                 "launches_per_step": round(len(tg.adam_events) / args.steps, 2)}
         tg.adam_events = None

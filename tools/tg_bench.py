@@ -20,9 +20,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--batch", type=int, default=2048)
-    ap.add_argument("--pull", type=int, default=0,
-                    help="1: the pull form's accumulate (long runs only; resolve() outside "
-                         "the timed loop before hashing)")
     a = ap.parse_args()
     import torch
 
@@ -44,7 +41,6 @@ def main():
     torch.cuda.synchronize()
     G.TableGrad.accumulate = orig
     tg, groups = seen[-1]
-    tg.pull = bool(a.pull)
     for _ in range(3):
         tg.accumulate(groups)
     torch.cuda.synchronize()
@@ -55,12 +51,11 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / a.reps
-    tg.resolve()
     rows = (tg.stamp == tg.gen).nonzero().squeeze(1)
     s = tg.acc[rows].contiguous()
     h = hashlib.sha1(s.cpu().numpy().tobytes() + rows.cpu().numpy().tobytes()).hexdigest()[:16]
     print(json.dumps({"lib": os.path.basename(os.environ.get("MIREC_LIB", "libmirec.so")),
-                      "ms_per_accumulate": round(ms, 4), "reps": a.reps, "pull": bool(a.pull),
+                      "ms_per_accumulate": round(ms, 4), "reps": a.reps,
                       "entries": sum(int(g[0].numel()) for g in groups),
                       "stamped_rows": int(rows.numel()), "sum_f64": float(s.double().sum()),
                       "abs_f64": float(s.double().abs().sum()), "hash": h}), flush=True)
