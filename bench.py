@@ -97,6 +97,10 @@ def parse(argv=None):
                     help="timed warm-up steps per exchange mode for --dp-mode auto")
     ap.add_argument("--shard-chunks", type=int, default=4,
                     help="row blocks of the sharded last layer (all-gather overlap)")
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="HIP timing events (propagation launches, collectives) on every "
+                         "k-th timed step only: each event record leaves the GPU idle ~5 us, "
+                         "so events on every step would add ~1 %% to the timed step")
     ap.add_argument("--parity", type=int, default=1,
                     help="N=1: one more GPU step checked against the CPU oracle from the "
                          "same table / Adam state / triples; N>1: one more data-parallel "
@@ -616,24 +620,33 @@ def main(argv=None):
     ag_ms = dp.time_table_allgather() if (dp is not None and calib is None
                                           and dp.mode == "sharded") else None
     torch.cuda.synchronize()
-    eng.prop_events = []
-    if dp is not None:
-        dp.comm_events = []
+    # the live launch timing: HIP events on the launch stream around every
+    # propagation launch (and collective) of every k-th timed step — an event
+    # record idles the GPU for ~5 us (round-6 trace: ~50 us per C2 step with
+    # events on all 12 records), so the other steps run without them
+    every = max(1, args.event_every)
+    prop_ev, comm_ev = [], []
+    sampled = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(t_base, t_base + args.steps):
+    for j, i in enumerate(range(t_base, t_base + args.steps)):
+        on = j % every == every - 1 or (args.steps < every and j == args.steps - 1)
+        sampled += int(on)
+        eng.prop_events = prop_ev if on else None
+        if dp is not None:
+            dp.comm_events = comm_ev if on else None
         step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    events, eng.prop_events = eng.prop_events, None
+    events, eng.prop_events = prop_ev, None
     comm = None
     if dp is not None:
         from furusato_recommend_amd.dist import _elapsed_ms
-        comm_ms = dp._max_over_ranks(_elapsed_ms(dp.comm_events) / args.steps)
+        comm_ms = dp._max_over_ranks(_elapsed_ms(comm_ev) / sampled)
         dp.comm_events = None
         xb = dp.exchange_bytes_per_rank(B)
         table = emb.numel() * emb.element_size()
@@ -680,7 +693,7 @@ def main(argv=None):
         d[0] += 1
         d[1] += ms
         d[2] += nbytes
-    t_prop = sum(v[1] for v in per_kind.values()) / args.steps
+    t_prop = sum(v[1] for v in per_kind.values()) / sampled
     dom = per_kind.get((0, False, False), [1, 1.0, 0])
     avg_ms = dom[1] / dom[0]
     avg_bytes = dom[2] / dom[0]
@@ -760,12 +773,13 @@ def main(argv=None):
                          "traffic_source": traffic_src,
                          "avg_launch_ms": round(avg_ms, 4),
                          "algorithmic_bytes_per_launch": int(avg_bytes),
-                         "launches_per_step": round(dom[0] / args.steps, 2)},
+                         "launches_per_step": round(dom[0] / sampled, 2),
+                         "timed_steps_sampled": sampled},
             "roofline_hbm_counter": hbm_counter(traffic, avg_ms),
             "propagation_ms_per_step": round(t_prop, 3),
             "per_launch_kind": {
                 f"{KIND_NAMES[k[0]]}{'+inmask' if k[1] else ''}{'+rowmask' if k[2] else ''}":
-                {"launches_per_step": round(v[0] / args.steps, 2), "avg_ms": round(v[1] / v[0], 4)}
+                {"launches_per_step": round(v[0] / sampled, 2), "avg_ms": round(v[1] / v[0], 4)}
                 for k, v in sorted(per_kind.items())},
             "prune": bool(args.prune),
             "frontier_F1_rows": f1_rows,

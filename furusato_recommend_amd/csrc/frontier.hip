@@ -15,6 +15,8 @@
 // one wave per segment, so a hot item does not serialise the launch.
 // mirec_mask_compact turns a byte map (F1) into a row list for the masked
 // propagation launches.
+#include <algorithm>
+
 #include "common.h"
 
 namespace mirec {
@@ -79,6 +81,19 @@ __global__ __launch_bounds__(256) void frontier_self_kernel(
   if (valid) bm_hop[node] = 1;
   const int32_t off = block_reserve(first ? 1 : 0, self_count);
   if (first) self_list[off] = (int32_t)node;
+}
+
+// The step's clears in one launch: both byte maps (uint4 stores), the S
+// count and the row-list counters the following mask_compact calls fill
+// (four memset launches before, ~5 us each on the C2 step).
+__global__ __launch_bounds__(256) void frontier_clear_kernel(uint4 *__restrict__ maps, int64_t n16,
+                                                             int32_t *__restrict__ self_count,
+                                                             int32_t *__restrict__ zero,
+                                                             int32_t n_zero) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t j = i; j < n16; j += (int64_t)gridDim.x * blockDim.x) maps[j] = make_uint4(0, 0, 0, 0);
+  if (i == 0 && self_count != nullptr) *self_count = 0;
+  if (i < n_zero) zero[i] = 0;
 }
 
 // One wave per S node: its CSR row's neighbours into bm_hop with plain byte
@@ -575,24 +590,34 @@ extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t
                               const int32_t *users, const int32_t *pos, const int32_t *neg,
                               int64_t batch, int64_t n_users, uint8_t *bm_self,
                               uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
+                              int32_t *zero_counts, int32_t n_zero_counts,
                               mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(c && c->rowptr && c->col && bm_self && bm_hop);
   MIREC_CHECK_ARG(keys != nullptr || (users && pos && neg && batch >= 0 && n_users >= 0));
   MIREC_CHECK_ARG(self_list == nullptr || self_count != nullptr);
+  MIREC_CHECK_ARG(n_zero_counts >= 0 && n_zero_counts <= 256 &&
+                  (n_zero_counts == 0 || zero_counts != nullptr));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const size_t bytes = (size_t)((c->n_rows + 3) / 4) * 4;  // whole words (test_and_set)
   const size_t bytes16 = (bytes + 15) / 16 * 16;
-  if (bm_hop == bm_self + bytes16) {  // adjacent maps (16-B row stride): one clear
-    MIREC_HIP(hipMemsetAsync(bm_self, 0, 2 * bytes16, st));
+  int32_t *sc = self_list != nullptr ? self_count : nullptr;
+  if (bm_hop == bm_self + bytes16 && ((uintptr_t)bm_self & 15u) == 0) {
+    // adjacent, 16-B aligned maps: everything cleared by one launch
+    const int64_t n16 = (int64_t)(2 * bytes16 / 16);
+    const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n16 + 255) / 256, 1024));
+    hipLaunchKernelGGL(frontier_clear_kernel, dim3(blocks), dim3(256), 0, st,
+                       reinterpret_cast<uint4 *>(bm_self), n16, sc, zero_counts, n_zero_counts);
+    MIREC_LAUNCH_CHECK();
   } else {
     MIREC_HIP(hipMemsetAsync(bm_self, 0, bytes, st));
     MIREC_HIP(hipMemsetAsync(bm_hop, 0, bytes, st));
+    if (sc != nullptr) MIREC_HIP(hipMemsetAsync(sc, 0, 4, st));
+    if (n_zero_counts > 0) MIREC_HIP(hipMemsetAsync(zero_counts, 0, 4 * (size_t)n_zero_counts, st));
   }
   const int64_t n = keys != nullptr ? n_keys : 3 * batch;
   const int32_t split = c->n_seg > 0 ? c->split : 0;
   if (self_list != nullptr) {
-    MIREC_HIP(hipMemsetAsync(self_count, 0, 4, st));
     if (n > 0) {
       hipLaunchKernelGGL(frontier_self_kernel, dim3((n + 255) / 256), dim3(256), 0, st, c->n_rows,
                          keys, n_keys, users, pos, neg, batch, n_users, bm_self, bm_hop,
@@ -619,13 +644,16 @@ extern "C" int mirec_frontier(const mirec_csr_t *c, const int32_t *keys, int64_t
 
 extern "C" int mirec_mask_compact(const mirec_csr_t *c, const uint8_t *bm, int32_t narrow_max,
                                   int32_t *list, int32_t *count, int32_t *wide_list,
-                                  int32_t *wide_count, mirec_stream_t stream) {
+                                  int32_t *wide_count, int32_t counts_zeroed,
+                                  mirec_stream_t stream) {
   using namespace mirec;
   MIREC_CHECK_ARG(c && c->rowptr && bm && list && count && c->n_rows >= 0);
   MIREC_CHECK_ARG(wide_list == nullptr || wide_count != nullptr);
   MIREC_CHECK_ARG(((uintptr_t)bm & 15u) == 0);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (wide_count == count + 1) {  // adjacent counters: one clear
+  if (counts_zeroed) {
+    // (cleared by the caller on this stream, e.g. mirec_frontier's zero_counts)
+  } else if (wide_count == count + 1) {  // adjacent counters: one clear
     MIREC_HIP(hipMemsetAsync(count, 0, 8, st));
   } else {
     MIREC_HIP(hipMemsetAsync(count, 0, 4, st));

@@ -383,6 +383,10 @@ class PropagationEngine:
         """bm_self = S, bm_hop = S ∪ N(S) for a triple batch or a key list;
         self_list = S deduplicated, hop_list = F1 as a row list (pruning)."""
         g = self.g
+        # the row-list counters of the mask_compact calls below are cleared by
+        # the frontier's clear launch (one launch for maps, S count, counters)
+        lists = self.prune and self.use_hop_list
+        zc, nz = (self.list_counts.data_ptr(), 4) if lists else (None, 0)
         if keys is not None:
             n = int(n_keys)
             if self.self_list.shape[0] < n:
@@ -390,7 +394,7 @@ class PropagationEngine:
             check(lib.mirec_frontier(g.csr_ptr(), keys.data_ptr(), n, None, None, None,
                                      0, g.n_users, self.bm_self.data_ptr(),
                                      self.bm_hop.data_ptr(), self.self_list.data_ptr(),
-                                     self.self_count.data_ptr(), _lib.stream_handle()),
+                                     self.self_count.data_ptr(), zc, nz, _lib.stream_handle()),
                   "frontier")
             self._self_cap = n
         else:
@@ -401,15 +405,15 @@ class PropagationEngine:
                                      neg.data_ptr(), B, g.n_users,
                                      self.bm_self.data_ptr(), self.bm_hop.data_ptr(),
                                      self.self_list.data_ptr(), self.self_count.data_ptr(),
-                                     _lib.stream_handle()), "frontier")
+                                     zc, nz, _lib.stream_handle()), "frontier")
             self._self_cap = 3 * B
-        if self.prune and self.use_hop_list:
+        if lists:
             c = self.list_counts
             for k, (bm, (nl, wl)) in enumerate(((self.bm_self, self.s_lists),
                                                 (self.bm_hop, self.hop_lists))):
                 check(lib.mirec_mask_compact(g.csr_ptr(), bm.data_ptr(), int(self.narrow_max),
                                              nl.data_ptr(), c[2 * k].data_ptr(),
-                                             wl.data_ptr(), c[2 * k + 1].data_ptr(),
+                                             wl.data_ptr(), c[2 * k + 1].data_ptr(), 1,
                                              _lib.stream_handle()), "mask_compact")
         self._masks_ready = True
 
@@ -451,7 +455,7 @@ class PropagationEngine:
         cnt = torch.zeros(2, dtype=torch.int32, device=dev)
         check(lib.mirec_mask_compact(g.csr_ptr(), bm.data_ptr(), int(self.narrow_max),
                                      nl.data_ptr(), cnt[0].data_ptr(), wl.data_ptr(),
-                                     cnt[1].data_ptr(), _lib.stream_handle()), "mask_compact")
+                                     cnt[1].data_ptr(), 0, _lib.stream_handle()), "mask_compact")
         return dict(row_mask=bm, row_list=nl, row_count=cnt[0], row_list_cap=N,
                     wide_list=wl, wide_count=cnt[1])
 

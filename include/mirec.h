@@ -236,12 +236,15 @@ int mirec_shard_unpack(const float *stage, int64_t n_rows, int32_t dim, int32_t 
  * (with one memset when bm_hop starts right after bm_self's 16-byte-rounded
  * size).  If self_list
  * is given it receives the distinct nodes of S (in no particular order) and
- * *self_count their number (capacity: n_keys or 3*batch). */
+ * *self_count their number (capacity: n_keys or 3*batch).  zero_counts[0 ..
+ * n_zero_counts) (<= 256, may be NULL / 0) are set to 0 with the maps — the
+ * counters of the mirec_mask_compact calls that follow (counts_zeroed = 1):
+ * adjacent, 16-byte aligned maps, S count and counters clear in one launch. */
 int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    const int32_t *users, const int32_t *pos, const int32_t *neg,
                    int64_t batch, int64_t n_users, uint8_t *bm_self,
                    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
-                   mirec_stream_t stream);
+                   int32_t *zero_counts, int32_t n_zero_counts, mirec_stream_t stream);
 
 /* Row lists of the nodes whose byte in the byte map bm[csr->n_rows] is
  * non-zero (16-byte aligned map): nodes of degree <= narrow_max (or all, if
@@ -249,10 +252,11 @@ int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
  * wide_list[0 .. *wide_count); each list is ascending within runs of 4096
  * nodes, runs in no particular order (the result of a propagation does not
  * depend on list order).  Capacity: n_rows each.  Feeds the row_list /
- * wide_list of mirec_prop_t for the frontier-pruned launches. */
+ * wide_list of mirec_prop_t for the frontier-pruned launches.  The counts
+ * are cleared first unless counts_zeroed (already 0 on this stream). */
 int mirec_mask_compact(const mirec_csr_t *csr, const uint8_t *bm,
                        int32_t narrow_max, int32_t *list, int32_t *count,
-                       int32_t *wide_list, int32_t *wide_count,
+                       int32_t *wide_list, int32_t *wide_count, int32_t counts_zeroed,
                        mirec_stream_t stream);
 
 /* The ascending distinct ids of ids[0 .. n) that lie in [0, n_rows) and
