@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
+#include "smallsort.h"
 
 namespace mirec {
 
@@ -263,7 +264,15 @@ static int end_bit_for(int64_t n_nodes) {
 
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// The (node, occurrence) sorts: up to kSmallSortMax pairs the library's own
+// one / two-launch sort (smallsort.hip: the C2 step's 6 144 seeds in one
+// launch instead of the radix sort's six), above it the device library's
+// radix sort; both return the stable order.
 static int sort_temp_bytes(int64_t n3, int64_t n_nodes, size_t *bytes) {
+  if (n3 <= kSmallSortMax) {
+    *bytes = small_sort_workspace(n3);
+    return MIREC_OK;
+  }
   size_t tb = 0;
   hipError_t e = hipcub::DeviceRadixSort::SortPairs(
       nullptr, tb, (const int32_t *)nullptr, (int32_t *)nullptr, (const int32_t *)nullptr,
@@ -274,6 +283,15 @@ static int sort_temp_bytes(int64_t n3, int64_t n_nodes, size_t *bytes) {
   }
   *bytes = tb;
   return MIREC_OK;
+}
+
+static hipError_t sort_pairs(void *ws, size_t tb, const int32_t *keys, int32_t *keys_sorted,
+                             const int32_t *vals, int32_t *vals_sorted, int64_t n,
+                             int64_t n_nodes, hipStream_t st) {
+  if (n <= kSmallSortMax)
+    return small_sort_pairs(ws, tb, keys, keys_sorted, vals, vals_sorted, n, st);
+  return hipcub::DeviceRadixSort::SortPairs(ws, tb, keys, keys_sorted, vals, vals_sorted, (int)n,
+                                            0, end_bit_for(n_nodes), st);
 }
 
 template <int D>
@@ -374,8 +392,7 @@ extern "C" int mirec_bpr_seed(const float *out, const float *emb, int64_t n_node
   int32_t *vals_sorted = reinterpret_cast<int32_t *>(ws + align_up(tb));
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   size_t tb2 = tb;
-  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws, tb2, keys, keys_sorted, vals, vals_sorted,
-                                               (int)n3, 0, end_bit_for(n_nodes), st));
+  MIREC_HIP(sort_pairs(ws, tb2, keys, keys_sorted, vals, vals_sorted, n3, n_nodes, st));
   hipLaunchKernelGGL(seed_heads_kernel, dim3((n3 + 255) / 256), dim3(256), 0, st, keys_sorted, n3,
                      slot);
   MIREC_LAUNCH_CHECK();
@@ -456,9 +473,7 @@ extern "C" int mirec_seed_merge(const int32_t *keys_packed, const float *rows_p,
   hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, idx_in, n);
   MIREC_LAUNCH_CHECK();
   size_t tb2 = tb;
-  MIREC_HIP(hipcub::DeviceRadixSort::SortPairs(ws, tb2, keys_packed, keys_sorted, idx_in,
-                                               idx_sorted, (int)n, 0, end_bit_for(n_nodes + 1),
-                                               st));
+  MIREC_HIP(sort_pairs(ws, tb2, keys_packed, keys_sorted, idx_in, idx_sorted, n, n_nodes + 1, st));
   hipLaunchKernelGGL(merge_heads_kernel, dim3((n + 255) / 256), dim3(256), 0, st, keys_sorted, n,
                      (int32_t)n_nodes, slot);
   MIREC_LAUNCH_CHECK();

@@ -37,6 +37,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
+#include "smallsort.h"
 
 namespace mirec {
 
@@ -806,6 +807,15 @@ __global__ __launch_bounds__(256) void os_adam_kernel(OsBlocks b, const int32_t 
 // -> 0.367 ms, same order, bitwise equal sums).
 static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *ko, const int32_t *vi,
                           int32_t *vo, int n, int end_bit, hipStream_t st) {
+  // up to 8 K entries the library's own two-launch sort (smallsort.hip)
+  // instead of the radix sort's block sort + merge passes; the same order
+  if (n <= kSmallSortMax) {
+    if (tmp == nullptr) {
+      bytes = small_sort_workspace(n);
+      return hipSuccess;
+    }
+    return small_sort_pairs(tmp, bytes, ki, ko, vi, vo, n, st);
+  }
   using Onesweep = rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>,
                                                        rocprim::kernel_config<1024, 8>, 11,
                                                        rocprim::block_radix_rank_algorithm::match>;

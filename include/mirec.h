@@ -246,6 +246,19 @@ int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
                    int32_t *zero_counts, int32_t n_zero_counts, mirec_stream_t stream);
 
+/* Stable sort of n <= 8 192 (int32 key >= 0, int32 value) pairs: ascending
+ * keys, equal keys in input order — bit for bit a stable radix sort's
+ * result; vals_in NULL = the identity.  Two launches: every (key, index)
+ * composite's rank counted over a grid of 256-entry blocks x 256-entry
+ * chunks, then each pair written at its rank.  The sort of the BPR seed
+ * grouping (mirec_bpr_seed: 3B node keys) and of small table-gradient
+ * steps (mirec_table_grad_sorted); workspace: mirec_small_sort_workspace
+ * bytes (ceil(n / 256) x n int32). */
+int mirec_small_sort_workspace(int64_t n, size_t *bytes);
+int mirec_small_sort_pairs(const int32_t *keys_in, const int32_t *vals_in, int32_t *keys_out,
+                           int32_t *vals_out, int64_t n, void *workspace, size_t workspace_bytes,
+                           mirec_stream_t stream);
+
 /* Row lists of the nodes whose byte in the byte map bm[csr->n_rows] is
  * non-zero (16-byte aligned map): nodes of degree <= narrow_max (or all, if
  * wide_list is NULL) go to list[0 .. *count), the others to
