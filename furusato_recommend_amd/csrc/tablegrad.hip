@@ -828,10 +828,15 @@ static hipError_t tg_sort(void *tmp, size_t &bytes, const int32_t *ki, int32_t *
   return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, ki, ko, vi, vo, (size_t)n, 0, end_bit, st);
 }
 
+// Lanes per chunk group: one entry per lane (kCh) up to 16, wider rows in a
+// column loop.  Groups of 32 (d = 128: a whole row per group) repeated the
+// chunk's key / plan bookkeeping in 24 lanes that carry no entry; 16-lane
+// groups with a two-pass column loop: C3 accumulate 0.357 -> 0.345 ms, the
+// same sums bit for bit (profiles/round6_tg_lanes.jsonl).
 static int lanes_per_row(int32_t d) {
   const int d4 = (d + 3) / 4;
   int l = kCh;  // pass 1: one entry per lane of a group
-  while (l < d4 && l < 64) l <<= 1;
+  while (l < d4 && l < 16) l <<= 1;
   return l;
 }
 
