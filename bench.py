@@ -110,7 +110,10 @@ def parse(argv=None):
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
     ap.add_argument("--launch-selftest", action="store_true", help=argparse.SUPPRESS)
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.steps < 1:
+        ap.error("--steps must be >= 1")
+    return args
 
 
 # ---------------------------------------------------------------- launcher

@@ -82,6 +82,8 @@ def main():
     ap.add_argument("--rehearse", action="store_true",
                     help="all ranks on cuda:0, gloo collectives (N-rank path on one GPU)")
     args = ap.parse_args()
+    if args.steps < 1:
+        ap.error("--steps must be >= 1")
     from furusato_recommend_amd import graphsage as _gs
     _gs.SORTED_LEAF_BACKWARD = args.leaf_bwd == "sorted"
     if args.blas:
