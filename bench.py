@@ -66,7 +66,7 @@ HBM_STREAM_GBS = 6290.0
 PARITY_TOL = 1e-4  # north_star: output embeddings within 1e-4 rel fp32 of the CPU path
 # C5 (d = 256, 11.26 GB tables: no Infinity-Cache help): the latest committed
 # full-size bench line, read at run time (no_cache_reference)
-C5_NO_CACHE_FILE = os.path.join("profiles", "round5_final_bench_c5_1gpu.json")
+C5_NO_CACHE_FILE = os.path.join("profiles", "round6_final_bench_c5_1gpu.json")
 
 
 def parse(argv=None):
