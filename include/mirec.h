@@ -383,7 +383,8 @@ int mirec_bpr_loss(const float *softplus, const float *reg, int64_t batch,
 int mirec_bpr_seed_workspace(int64_t batch, int64_t n_nodes, size_t *bytes);
 
 /* Gradient seeds of the backward pass.  Sorts the 3B (node, occurrence)
- * pairs (stable radix sort), marks the first position q of every distinct
+ * pairs stably (mirec_small_sort_pairs up to 8 192 pairs, the device
+ * library's radix sort above), marks the first position q of every distinct
  * node in `slot` (slot[node] = q; slot must be all -1 on entry) and writes
  *   seed_p[q] = (sum over the node's occurrences of dLoss/d out_node) / (L+1)
  *   seed_e[q] = decay * (#occurrences) * emb[node] / B   (reg term)
@@ -622,8 +623,9 @@ typedef struct mirec_row_grad_group {
 /* sizeof(mirec_row_grad_group_t), for FFI struct-mirror checks. */
 int64_t mirec_row_grad_group_size(void);
 
-/* S for every touched row: the entries of all groups radix-sorted by row id
- * (stable), each id's contributions summed in entry order (runs longer than
+/* S for every touched row: the entries of all groups sorted by row id
+ * (stable: mirec_small_sort_pairs up to 8 192 entries, the device library's
+ * radix sort above), each id's contributions summed in entry order (runs longer than
  * a 64-entry chunk: per-chunk partials added in chunk order) — no float
  * atomics, bitwise repeatable.  Writes acc[r] = S[r] and stamp[r] = gen for
  * the touched rows only (nothing is cleared: a row belongs to this step iff
