@@ -107,6 +107,8 @@ SIGNATURES = {
     "mirec_frontier": (c_int, [POINTER(CSR), c_void_p, c_int64, c_void_p, c_void_p, c_void_p,
                                c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_int32, c_void_p]),
+    "mirec_mask_compact_pair": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_void_p, c_void_p]),
     "mirec_small_sort_workspace": (c_int, [c_int64, POINTER(c_size_t)]),
     "mirec_small_sort_pairs": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
                                        c_size_t, c_void_p]),

@@ -408,14 +408,37 @@ class PropagationEngine:
                                      zc, nz, _lib.stream_handle()), "frontier")
             self._self_cap = 3 * B
         if lists:
-            c = self.list_counts
-            for k, (bm, (nl, wl)) in enumerate(((self.bm_self, self.s_lists),
-                                                (self.bm_hop, self.hop_lists))):
-                check(lib.mirec_mask_compact(g.csr_ptr(), bm.data_ptr(), int(self.narrow_max),
-                                             nl.data_ptr(), c[2 * k].data_ptr(),
-                                             wl.data_ptr(), c[2 * k + 1].data_ptr(), 1,
-                                             _lib.stream_handle()), "mask_compact")
+            # S and F1 compacted in one launch, the degree split from a static
+            # bitmap (mirec_mask_compact_pair; counters zeroed by the frontier)
+            check(lib.mirec_mask_compact_pair(self.bm_self.data_ptr(), self.bm_hop.data_ptr(),
+                                              self._wide_bits().data_ptr(), g.n_nodes,
+                                              self.s_lists[0].data_ptr(),
+                                              self.s_lists[1].data_ptr(),
+                                              self.hop_lists[0].data_ptr(),
+                                              self.hop_lists[1].data_ptr(),
+                                              self.list_counts.data_ptr(), _lib.stream_handle()),
+                  "mask_compact_pair")
         self._masks_ready = True
+
+    def _wide_bits(self) -> torch.Tensor:
+        """Bit v of word v // 32: node v's degree > narrow_max (the row lists'
+        narrow / wide split), built once per graph and narrow_max."""
+        key = int(self.narrow_max)
+        wb = getattr(self, "_wide_bits_cache", None)
+        if wb is not None and wb[0] == key:
+            return wb[1]
+        g = self.g
+        rp = g.rowptr
+        n = g.n_nodes
+        wide = (rp[1:n + 1] - rp[:n]) > key
+        words = (n + 31) // 32
+        bits = torch.zeros(words * 32, dtype=torch.int64, device=wide.device)
+        bits[:n] = wide.to(torch.int64)
+        shifts = torch.arange(32, dtype=torch.int64, device=wide.device)
+        w = (bits.view(words, 32) << shifts).sum(1)        # < 2^32
+        w = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+        self._wide_bits_cache = (key, w.contiguous())
+        return self._wide_bits_cache[1]
 
     def _lists(self, k, bm, lists, cap):
         if not self.use_hop_list:

@@ -246,6 +246,17 @@ int mirec_frontier(const mirec_csr_t *csr, const int32_t *keys, int64_t n_keys,
                    uint8_t *bm_hop, int32_t *self_list, int32_t *self_count,
                    int32_t *zero_counts, int32_t n_zero_counts, mirec_stream_t stream);
 
+/* mirec_mask_compact of two byte maps in one launch (the step's S and F1 =
+ * S ∪ N(S)), the degree split read from wide_bits (bit v of word v / 32:
+ * degree of node v > narrow_max; built once per graph) instead of rowptr:
+ * list_a / wide_a get map a's narrow / wide nodes, list_b / wide_b map b's;
+ * counts[0..3] = their lengths (a narrow, a wide, b narrow, b wide), which
+ * must be 0 on entry (mirec_frontier's zero_counts).  Lists ascending
+ * within runs of 8 192 nodes; 16-byte aligned maps of >= n_rows bytes. */
+int mirec_mask_compact_pair(const uint8_t *bm_a, const uint8_t *bm_b, const uint32_t *wide_bits,
+                            int64_t n_rows, int32_t *list_a, int32_t *wide_a, int32_t *list_b,
+                            int32_t *wide_b, int32_t *counts, mirec_stream_t stream);
+
 /* Stable sort of n <= 8 192 (int32 key >= 0, int32 value) pairs: ascending
  * keys, equal keys in input order — bit for bit a stable radix sort's
  * result; vals_in NULL = the identity.  Two launches: every (key, index)
