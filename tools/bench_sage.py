@@ -161,7 +161,7 @@ def main():
         roof = {"bound": "hbm", "kernel": "tg_adam_kernel (fused table Adam)",
                 "achieved": round(nbytes / (ms * 1e-3) / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
                 "frac": round(nbytes / (ms * 1e-3) / 1e9 / 8000.0, 4),
-                "traffic": 3660805737, "traffic_source": "profiles/round3d_pmc_tg_adam.json",
+                "traffic": 3660651465, "traffic_source": "profiles/round6_final_pmc_tg_adam.json",
                 "avg_launch_ms": round(ms, 4), "algorithmic_bytes_per_launch": nbytes,
                 "launches_per_step": round(len(tg.adam_events) / sampled, 2),
                 "timed_steps_sampled": sampled}

@@ -121,7 +121,7 @@ if __name__ == "__main__":
         fs, ws = pmc(a.fetch, "FETCH_SIZE"), pmc(a.write, "WRITE_SIZE")
         rd = 2 * 1024 * sum(fs) / max(len(fs), 1)  # gfx950: 2 x FETCH_SIZE x 1 KiB
         wr = 1024 * sum(ws) / max(len(ws), 1)
-        res = dict(c, kernel="tg_sum_kernel<32> (C3 sorted table-gradient sum, pass 1)",
+        res = dict(c, kernel="tg_sum_kernel (C3 sorted table-gradient sum, pass 1)",
                    launches=[len(fs), len(ws)], read_bytes=rd, write_bytes_counter=wr,
                    hbm_bytes_per_launch=rd + wr,
                    counter_over_algorithmic=round((rd + wr) / c["algorithmic_bytes"], 3),
