@@ -370,7 +370,11 @@ __device__ __forceinline__ void wave_row(const PropK &a, int32_t row) {
   if (lane < LPR) row_epilogue<D>(a, row, s, lane % LPR);
 }
 
-constexpr int64_t kListBlocks = 4096;  // 2 x the waves resident at 8/SIMD
+// Grid of the list launches (their row counts live on the device): 4x the
+// waves resident at 8 per SIMD.  4096 -> 8192: the row-masked launches
+// 0.366 -> 0.357 ms, the SPARSE one 0.224 -> 0.208 ms, C2 4.666 -> 4.630
+// ms per step (profiles/round6_ab_list_blocks.txt; 2048: 4.79, 16384: 4.63).
+constexpr int64_t kListBlocks = 8192;
 
 // Occupancy floor (waves per SIMD): keeps the register allocator at <= 72
 // VGPRs so 7-8 waves per SIMD keep enough gathers in flight.
